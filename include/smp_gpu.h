@@ -1,0 +1,152 @@
+/* smp_gpu.h -- C ABI of the MI355X BiRRT* sampling / collision hot path.
+ *
+ * Drop-in boundary for the planner core that squirrel_8dof_planner drives
+ * (tpatten/squirrel_motion_planner).  Each entry point replaces one interface of the reference:
+ *
+ *   smp_robot_create_json      KDLRobotModel + CollisionChecker construction
+ *                              (birrt_star.cpp:61-73, kdl_kuka_model.cpp:12-236, collision_checker.hpp:65-74)
+ *   smp_robot_create_urdf      the same from robot_description / SRDF text (collision_checker.hpp:176-393)
+ *   smp_scene_from_keys        BiRRTstarPlanner::setOctree -> CollisionChecker::setOcTree
+ *                              (birrt_star.cpp:1621-1624, collision_checker.hpp:76-88) for occupied leaf keys
+ *   smp_scene_from_bt          the same from an octomap binary (.bt / binary octomap_msgs payload), with the
+ *                              node's floor insertion (squirrel_8dof_planner.cpp:862-917)
+ *   smp_planner_create         BiRRTstarPlanner::initialize (birrt_star.cpp:11-326) on one GPU
+ *   smp_planner_set_scene      BiRRTstarPlanner::setOctree (copies; caller keeps ownership)
+ *   smp_set_disabled_map_links BiRRTstarPlanner::setDisabledLinkMapCollisions (birrt_star.cpp:6916-6919)
+ *   smp_plan                   reset_planner_and_config + setPlanningSceneInfo + init_planner + run_planner
+ *                              + getJointTrajectoryRef (squirrel_8dof_planner.cpp:1221-1248,
+ *                              birrt_star.cpp:335-536, 983-1407, 1688-1691)
+ *   smp_plan_batch             independent queries against one scene (one workgroup each)
+ *   smp_check_configs          batched isConfigValid (birrt_star.cpp:6897-6908) -> valid flags
+ *   smp_is_config_valid        BiRRTstarPlanner::isConfigValid for one configuration
+ *   smp_result_free            releases library-owned result buffers
+ *   smp_strerror               text of a status code
+ *
+ * Conventions: the caller owns every input buffer; results are library-allocated and released with
+ * smp_result_free.  Every function returns SMP_OK (0) or a negative status.  One smp_planner per host
+ * thread (the reference planner is not thread-safe either, squirrel_8dof_planner_node.cpp:12).
+ * Configurations are 8 fp64 values in chain order [x, y, theta, arm1..arm5].
+ */
+#ifndef SMP_GPU_H
+#define SMP_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  SMP_OK = 0,
+  SMP_ERR_ARG = -1,           /* bad argument / dimension mismatch (birrt_star.cpp:338-342) */
+  SMP_ERR_START_INVALID = -2, /* start configuration in collision (birrt_star.cpp:353-357) */
+  SMP_ERR_GOAL_INVALID = -3,  /* goal configuration in collision (birrt_star.cpp:358-362) */
+  SMP_ERR_NO_SOLUTION = -4,   /* budget exhausted without a path (birrt_star.cpp:1405) */
+  SMP_ERR_HIP = -5,           /* HIP runtime error */
+  SMP_ERR_PARSE = -6,         /* model / octomap parse error */
+  SMP_ERR_CAPACITY = -7,      /* tree capacity exceeded (raise smp_params.node_capacity) */
+  SMP_ERR_NO_DEVICE = -8      /* no usable GPU: the library never falls back to the CPU */
+};
+
+typedef struct smp_robot smp_robot;
+typedef struct smp_scene smp_scene;
+typedef struct smp_planner smp_planner;
+
+typedef struct smp_scene_opts {
+  double resolution;      /* metres per voxel (used by smp_scene_from_keys) */
+  double z_offset;        /* octree transform z (collision_checker.hpp:87: -0.02) */
+  int insert_floor;       /* 1: insert the node's floor square (squirrel_8dof_planner.cpp:889-902) */
+  double floor_center[2]; /* robot x, y at planning time */
+  double floor_distance;  /* floor_collision_distance (parameters.yaml:24: 3.0) */
+} smp_scene_opts;
+
+typedef struct smp_params {
+  double near_threshold;   /* near_threshold_interpolation (birrt_star.cpp:183, default 4.0) */
+  double step_factor;      /* unconstraint_extend_step_factor (birrt_star.cpp:189, default 0.5) */
+  int num_traj_segments;   /* num_traj_segments_interp (birrt_star.cpp:186, default 20) */
+  int max_near_nodes;      /* max_near_nodes (birrt_star.cpp:195, default 20) */
+  double path_optimality_threshold; /* birrt_star.cpp:201 (default 1.0) */
+  int tree_optimization;   /* m_tree_optimization_active (default 1) */
+  int informed_sampling;   /* m_informed_sampling_active (default 1) */
+  int64_t node_capacity;   /* per-tree node capacity on the device (0: derived from the budget) */
+} smp_params;
+
+typedef struct smp_query {
+  double start[8];
+  double goal[8];
+  double env_x[2];         /* setPlanningSceneInfo size_x (0,0 = unconfined) */
+  double env_y[2];
+  int check_self;
+  int check_map;
+  int budget_is_time;      /* 0: max iterations (flag_iter_or_time = 0), 1: max seconds */
+  double budget;           /* iterations or seconds */
+  uint64_t seed;
+  uint32_t query_id;       /* RNG stream of this query */
+} smp_query;
+
+typedef struct smp_stats {
+  int64_t iterations;
+  int64_t first_solution_iter;   /* -1 if none */
+  int64_t last_solution_iter;
+  int64_t configs_checked;       /* isInCollision calls of the reference semantics */
+  int64_t configs_valid;         /* ... of which collision free */
+  double time_first_solution;    /* seconds from planning start (device clock) */
+  double time_total;             /* seconds of the planning loop (device clock) */
+  double cost_best[3];           /* total, revolute, prismatic */
+  double cost_theoretical[3];
+  int64_t nodes_start, nodes_goal, edges_start, edges_goal, rewires_start, rewires_goal;
+  int32_t connected_tree_is_start;
+  int32_t conn_node_b, conn_node_a;
+} smp_stats;
+
+typedef struct smp_result {
+  int status;               /* SMP_OK or a negative code */
+  int64_t n_waypoints;
+  double* waypoints;        /* n_waypoints x 8, row-major (library-owned) */
+  smp_stats stats;
+  int64_t n_cost_rows;
+  double* cost_rows;        /* n_cost_rows x 5: [iteration, time, c_best, c_rev, c_prism] (birrt_star.cpp:1325-1331) */
+} smp_result;
+
+void smp_params_default(smp_params* p);
+void smp_scene_opts_default(smp_scene_opts* o);
+
+int smp_robot_create_json(const char* model_json, smp_robot** out);
+int smp_robot_create_urdf(const char* urdf_xml, const char* srdf_xml, const char* spheres_json, smp_robot** out);
+void smp_robot_destroy(smp_robot* r);
+int smp_robot_num_links(const smp_robot* r);
+const char* smp_robot_link_name(const smp_robot* r, int i);
+
+int smp_scene_from_keys(const uint16_t* keys_xyz, int64_t n, const smp_scene_opts* opts, smp_scene** out);
+int smp_scene_from_bt(const uint8_t* data, size_t size, const smp_scene_opts* opts, smp_scene** out);
+void smp_scene_destroy(smp_scene* s);
+/* Grid geometry of a scene: dims[3], origin[3], resolution; bitset/d2 copies for inspection (may be NULL). */
+int smp_scene_info(const smp_scene* s, int dims[3], double origin[3], double* resolution,
+                   int64_t* n_occupied, double bbox_min[3], double bbox_max[3]);
+int smp_scene_export(const smp_scene* s, uint64_t* bits, uint16_t* d2);
+
+int smp_planner_create(int device, const smp_robot* robot, const smp_params* params, smp_planner** out);
+void smp_planner_destroy(smp_planner* p);
+int smp_planner_set_scene(smp_planner* p, const smp_scene* s);
+int smp_set_disabled_map_links(smp_planner* p, const char* const* link_names, int n);
+
+int smp_plan(smp_planner* p, const smp_query* q, smp_result* out);
+int smp_plan_batch(smp_planner* p, const smp_query* q, int n, smp_result* out);
+void smp_result_free(smp_result* r);
+
+/* Tree dump of the last smp_plan (which: 0 start tree, 1 goal tree) for parity checks; arrays may be NULL. */
+int64_t smp_get_tree(smp_planner* p, int which, int32_t* parent, double* conf, double* cost);
+
+int smp_check_configs(smp_planner* p, const double* q_soa, int64_t n, int check_self, int check_map, uint8_t* valid);
+int smp_is_config_valid(smp_planner* p, const double q[8], int check_self, int check_map, int* valid);
+
+/* Kernel timing of the last smp_check_configs / smp_plan call: milliseconds on the launch stream. */
+int smp_last_kernel_ms(const smp_planner* p, double* check_ms, double* plan_ms, int64_t* plan_launches);
+
+const char* smp_strerror(int status);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SMP_GPU_H */

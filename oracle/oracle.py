@@ -77,6 +77,8 @@ def lib():
         L.orc_check_configs.argtypes = [ctypes.c_void_p, _pd, _i, _i, _i, ctypes.c_void_p]
         L.orc_fk.argtypes = [ctypes.c_void_p, _pd, _i, _pd, _pd]
         L.orc_sincos.argtypes = [_pd, _i, _pd, _pd]
+        L.orc_body_fk.argtypes = [ctypes.c_void_p, _pd, _i, _pd]
+        L.orc_philox.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         L.orc_u01.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p, _i, _pd]
         L.orc_plan.argtypes = [ctypes.c_void_p, _pd, _pd, ctypes.POINTER(Params), ctypes.POINTER(Result)]
         L.orc_get_path.argtypes = [ctypes.c_void_p, _pd]
@@ -275,6 +277,12 @@ class Oracle:
         lib().orc_fk(self.h, _p(q, _d), len(q), _p(fr, _d), _p(z, _d))
         return fr, z
 
+    def body_fk(self, q):
+        q = np.ascontiguousarray(q, np.float64).reshape(-1, 8)
+        fr = np.zeros((len(q), self.robot.n_body, 12))
+        lib().orc_body_fk(self.h, _p(q, _d), len(q), _p(fr, _d))
+        return fr
+
     def plan(self, start, goal, **kw):
         p = dict(DEFAULT_PARAMS)
         p.update(kw)
@@ -322,4 +330,13 @@ def u01(seed, query, ctr):
     ctr = np.ascontiguousarray(ctr, np.uint32).reshape(-1, 4)
     out = np.zeros(len(ctr))
     lib().orc_u01(seed, query, ctr.ctypes.data_as(ctypes.c_void_p), len(ctr), _p(out, _d))
+    return out
+
+
+def philox(ctr, key):
+    c = np.ascontiguousarray(ctr, np.uint32)
+    k = np.ascontiguousarray(key, np.uint32)
+    out = np.zeros(4, np.uint32)
+    lib().orc_philox(c.ctypes.data_as(ctypes.c_void_p), k.ctypes.data_as(ctypes.c_void_p),
+                     out.ctypes.data_as(ctypes.c_void_p))
     return out

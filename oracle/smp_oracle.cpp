@@ -1110,6 +1110,26 @@ void orc_fk(void* hp, const double* q, int n, double* frames, double* eez) {
   }
 }
 
+// Body frames (n x n_body x 12) of the collision model.
+void orc_body_fk(void* hp, const double* q, int n, double* frames) {
+  orc_handle* h = (orc_handle*)hp;
+  std::vector<orc::Frame> B(h->rb->n_body);
+  for (int i = 0; i < n; ++i) {
+    orc::body_frames(*h->rb, q + 8 * i, B.data());
+    for (int b = 0; b < h->rb->n_body; ++b) {
+      std::memcpy(frames + ((size_t)i * h->rb->n_body + b) * 12, B[b].R, 9 * sizeof(double));
+      std::memcpy(frames + ((size_t)i * h->rb->n_body + b) * 12 + 9, B[b].p, 3 * sizeof(double));
+    }
+  }
+}
+
+// Raw Philox4x32-10 block (known-answer tests).
+void orc_philox(const uint32_t* ctr, const uint32_t* key, uint32_t* out) {
+  uint32_t c[4] = {ctr[0], ctr[1], ctr[2], ctr[3]};
+  orc::philox(c, key[0], key[1]);
+  for (int i = 0; i < 4; ++i) out[i] = c[i];
+}
+
 void orc_sincos(const double* x, int n, double* s, double* c) {
   for (int i = 0; i < n; ++i) orc::psincos(x[i], s + i, c + i);
 }

@@ -1,0 +1,737 @@
+// C ABI implementation (include/smp_gpu.h): device memory, launches, result assembly.
+// No CPU fallback: without a usable GPU every compute entry point returns SMP_ERR_NO_DEVICE.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <set>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/smp_gpu.h"
+#include "smp_host.h"
+#include "smp_math.h"
+#include "smp_plan.h"
+#include "smp_types.h"
+
+namespace smp {
+__global__ void check_kernel(const RobotDev* rb, SceneDev sc, const MapCfg* mc, const double* q, long long n, int self,
+                             int map, uint8_t* valid);
+__global__ void plan_kernel(const RobotDev* rb, SceneDev sc, const MapCfg* mc, QueryDev* qs, int iters);
+__global__ void path_kernel(QueryDev* qs, int* counts);
+__global__ void sincos_kernel(const double* x, int n, double* s, double* c);
+__global__ void u01_kernel(unsigned long long seed, unsigned query, const uint32_t* ctr, int n, double* out);
+__global__ void fk_kernel(const RobotDev* rb, const double* q, int n, double* frames, double* eez);
+__global__ void sqrt_div_kernel(const double* a, const double* b, int n, double* sq, double* dv);
+}  // namespace smp
+
+using namespace smp;
+
+struct smp_robot {
+  RobotHost h;
+};
+
+struct smp_scene {
+  SceneHost h;
+};
+
+namespace {
+
+#define HIPCHK(x)                                                                         \
+  do {                                                                                    \
+    hipError_t e_ = (x);                                                                  \
+    if (e_ != hipSuccess) {                                                               \
+      fprintf(stderr, "smp_gpu: HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); \
+      return SMP_ERR_HIP;                                                                 \
+    }                                                                                     \
+  } while (0)
+
+template <typename T>
+struct DBuf {  // device buffer that only grows
+  T* p = nullptr;
+  size_t n = 0;
+  hipError_t reserve(size_t want) {
+    if (want <= n) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+    hipError_t e = hipMalloc(&p, std::max<size_t>(want, 1) * sizeof(T));
+    if (e == hipSuccess) n = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
+struct QueryBuffers {
+  DBuf<QState> st;
+  DBuf<double> q, cost, e_start, e_target, rows;
+  DBuf<int> parent, first_child, next_sib, prev_sib, stack, path_nodes;
+  DBuf<ViaNode> via;
+  size_t cap = 0;
+  void release() {
+    st.release(); q.release(); cost.release(); e_start.release(); e_target.release(); rows.release();
+    parent.release(); first_child.release(); next_sib.release(); prev_sib.release(); stack.release();
+    path_nodes.release(); via.release();
+    cap = 0;
+  }
+};
+
+}  // namespace
+
+struct smp_planner {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  RobotHost robot;
+  smp_params params;
+  RobotDev* d_rb = nullptr;
+  MapCfg mc_host;
+  MapCfg* d_mc = nullptr;
+  DBuf<uint64_t> d_bits;
+  DBuf<uint16_t> d_d2;
+  SceneDev sc{};
+  bool have_scene = false;
+  double scene_res = 0.05;
+  std::set<std::string> disabled;
+  std::vector<QueryBuffers> qb;
+  DBuf<QueryDev> d_qdev;
+  DBuf<int> d_counts;
+  DBuf<double> d_cq;
+  DBuf<uint8_t> d_valid;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  double last_check_ms = 0, last_plan_ms = 0;
+  int64_t last_plan_launches = 0;
+  double wall_rate_hz = 1e8;
+  // last plan (query 0) bookkeeping for smp_get_tree
+  int last_n[2] = {0, 0};
+};
+
+static int update_mapcfg(smp_planner* p) {
+  const RobotDev& d = p->robot.dev;
+  std::memset(&p->mc_host, 0, sizeof(MapCfg));
+  p->mc_host.has_map = p->have_scene ? 1 : 0;
+  for (int s = 0; s < d.n_sph; ++s) {
+    p->mc_host.T[s] = p->have_scene ? sphere_threshold(d.sph_r[s], p->scene_res) : 0;
+    int link = d.cl_link[d.sph_clink[s]];
+    p->mc_host.map_on[s] = p->disabled.count(p->robot.link_names[link]) ? 0 : 1;
+  }
+  HIPCHK(hipMemcpyAsync(p->d_mc, &p->mc_host, sizeof(MapCfg), hipMemcpyHostToDevice, p->stream));
+  HIPCHK(hipStreamSynchronize(p->stream));
+  return SMP_OK;
+}
+
+extern "C" {
+
+void smp_params_default(smp_params* p) {
+  p->near_threshold = 4.0;
+  p->step_factor = 0.5;
+  p->num_traj_segments = 20;
+  p->max_near_nodes = 20;
+  p->path_optimality_threshold = 1.0;
+  p->tree_optimization = 1;
+  p->informed_sampling = 1;
+  p->node_capacity = 0;
+}
+
+void smp_scene_opts_default(smp_scene_opts* o) {
+  o->resolution = 0.05;
+  o->z_offset = -0.02;
+  o->insert_floor = 0;
+  o->floor_center[0] = o->floor_center[1] = 0.0;
+  o->floor_distance = 3.0;
+}
+
+const char* smp_strerror(int s) {
+  switch (s) {
+    case SMP_OK: return "ok";
+    case SMP_ERR_ARG: return "invalid argument";
+    case SMP_ERR_START_INVALID: return "start configuration is invalid";
+    case SMP_ERR_GOAL_INVALID: return "goal configuration is invalid";
+    case SMP_ERR_NO_SOLUTION: return "no solution found within the budget";
+    case SMP_ERR_HIP: return "HIP runtime error";
+    case SMP_ERR_PARSE: return "parse error";
+    case SMP_ERR_CAPACITY: return "tree capacity exceeded";
+    case SMP_ERR_NO_DEVICE: return "no usable GPU (the library has no CPU fallback)";
+    default: return "unknown status";
+  }
+}
+
+int smp_robot_create_json(const char* model_json, smp_robot** out) {
+  if (!model_json || !out) return SMP_ERR_ARG;
+  smp_robot* r = new smp_robot();
+  try {
+    robot_from_json(model_json, &r->h);
+  } catch (const std::exception& e) {
+    fprintf(stderr, "smp_gpu: %s\n", e.what());
+    delete r;
+    return SMP_ERR_PARSE;
+  }
+  *out = r;
+  return SMP_OK;
+}
+
+int smp_robot_create_urdf(const char* urdf_xml, const char* srdf_xml, const char* spheres_json, smp_robot** out) {
+  if (!urdf_xml || !srdf_xml || !spheres_json || !out) return SMP_ERR_ARG;
+  smp_robot* r = new smp_robot();
+  try {
+    robot_from_urdf(urdf_xml, srdf_xml, spheres_json, &r->h);
+  } catch (const std::exception& e) {
+    fprintf(stderr, "smp_gpu: %s\n", e.what());
+    delete r;
+    return SMP_ERR_PARSE;
+  }
+  *out = r;
+  return SMP_OK;
+}
+
+void smp_robot_destroy(smp_robot* r) { delete r; }
+int smp_robot_num_links(const smp_robot* r) { return r ? (int)r->h.link_names.size() : 0; }
+const char* smp_robot_link_name(const smp_robot* r, int i) {
+  if (!r || i < 0 || i >= (int)r->h.link_names.size()) return nullptr;
+  return r->h.link_names[i].c_str();
+}
+
+int smp_scene_from_keys(const uint16_t* keys, int64_t n, const smp_scene_opts* o, smp_scene** out) {
+  if (!o || !out || (n > 0 && !keys) || !(o->resolution > 0)) return SMP_ERR_ARG;
+  std::vector<uint16_t> k(keys, keys + 3 * std::max<int64_t>(n, 0));
+  if (o->insert_floor) floor_keys(o->floor_center[0], o->floor_center[1], o->resolution, o->floor_distance, &k);
+  smp_scene* s = new smp_scene();
+  scene_from_keys(k.data(), (int64_t)k.size() / 3, o->resolution, o->z_offset, &s->h);
+  *out = s;
+  return SMP_OK;
+}
+
+int smp_scene_from_bt(const uint8_t* data, size_t size, const smp_scene_opts* o, smp_scene** out) {
+  if (!data || !o || !out) return SMP_ERR_ARG;
+  std::vector<uint16_t> k;
+  double res = 0;
+  try {
+    octomap_bt_keys(data, size, &res, &k);
+  } catch (const std::exception& e) {
+    fprintf(stderr, "smp_gpu: %s\n", e.what());
+    return SMP_ERR_PARSE;
+  }
+  if (o->insert_floor) floor_keys(o->floor_center[0], o->floor_center[1], res, o->floor_distance, &k);
+  smp_scene* s = new smp_scene();
+  scene_from_keys(k.data(), (int64_t)k.size() / 3, res, o->z_offset, &s->h);
+  *out = s;
+  return SMP_OK;
+}
+
+void smp_scene_destroy(smp_scene* s) { delete s; }
+
+int smp_scene_info(const smp_scene* s, int dims[3], double origin[3], double* resolution, int64_t* n_occupied,
+                   double bbox_min[3], double bbox_max[3]) {
+  if (!s) return SMP_ERR_ARG;
+  if (dims) { dims[0] = s->h.nx; dims[1] = s->h.ny; dims[2] = s->h.nz; }
+  if (origin) { origin[0] = s->h.ox; origin[1] = s->h.oy; origin[2] = s->h.oz; }
+  if (resolution) *resolution = s->h.res;
+  if (n_occupied) *n_occupied = s->h.n_occupied;
+  for (int d = 0; d < 3; ++d) {
+    if (bbox_min) bbox_min[d] = s->h.bbox_min[d];
+    if (bbox_max) bbox_max[d] = s->h.bbox_max[d];
+  }
+  return SMP_OK;
+}
+
+int smp_scene_export(const smp_scene* s, uint64_t* bits, uint16_t* d2) {
+  if (!s) return SMP_ERR_ARG;
+  if (bits) std::memcpy(bits, s->h.bits.data(), s->h.bits.size() * sizeof(uint64_t));
+  if (d2) std::memcpy(d2, s->h.d2.data(), s->h.d2.size() * sizeof(uint16_t));
+  return SMP_OK;
+}
+
+int smp_planner_create(int device, const smp_robot* robot, const smp_params* params, smp_planner** out) {
+  if (!robot || !out) return SMP_ERR_ARG;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || device < 0 || device >= ndev) return SMP_ERR_NO_DEVICE;
+  HIPCHK(hipSetDevice(device));
+  smp_planner* p = new smp_planner();
+  p->device = device;
+  p->robot = robot->h;
+  if (params) p->params = *params; else smp_params_default(&p->params);
+  if (p->params.max_near_nodes > 20 || p->params.max_near_nodes < 1 || p->params.num_traj_segments < 1 ||
+      p->params.num_traj_segments > MAX_PTS) {
+    delete p;
+    return SMP_ERR_ARG;
+  }
+  HIPCHK(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
+  HIPCHK(hipMalloc(&p->d_rb, sizeof(RobotDev)));
+  HIPCHK(hipMalloc(&p->d_mc, sizeof(MapCfg)));
+  HIPCHK(hipMemcpy(p->d_rb, &p->robot.dev, sizeof(RobotDev), hipMemcpyHostToDevice));
+  HIPCHK(hipEventCreate(&p->ev0));
+  HIPCHK(hipEventCreate(&p->ev1));
+  int khz = 0;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) == hipSuccess && khz > 0)
+    p->wall_rate_hz = khz * 1000.0;
+  std::memset(&p->sc, 0, sizeof(p->sc));
+  int st = update_mapcfg(p);
+  if (st) { delete p; return st; }
+  *out = p;
+  return SMP_OK;
+}
+
+void smp_planner_destroy(smp_planner* p) {
+  if (!p) return;
+  (void)hipSetDevice(p->device);
+  (void)hipStreamSynchronize(p->stream);
+  for (auto& q : p->qb) q.release();
+  p->d_qdev.release(); p->d_counts.release(); p->d_cq.release(); p->d_valid.release();
+  p->d_bits.release(); p->d_d2.release();
+  if (p->d_rb) (void)hipFree(p->d_rb);
+  if (p->d_mc) (void)hipFree(p->d_mc);
+  if (p->ev0) (void)hipEventDestroy(p->ev0);
+  if (p->ev1) (void)hipEventDestroy(p->ev1);
+  if (p->stream) (void)hipStreamDestroy(p->stream);
+  delete p;
+}
+
+int smp_planner_set_scene(smp_planner* p, const smp_scene* s) {
+  if (!p || !s) return SMP_ERR_ARG;
+  HIPCHK(hipSetDevice(p->device));
+  HIPCHK(p->d_bits.reserve(s->h.bits.size()));
+  HIPCHK(p->d_d2.reserve(s->h.d2.size()));
+  HIPCHK(hipMemcpyAsync(p->d_bits.p, s->h.bits.data(), s->h.bits.size() * sizeof(uint64_t), hipMemcpyHostToDevice, p->stream));
+  HIPCHK(hipMemcpyAsync(p->d_d2.p, s->h.d2.data(), s->h.d2.size() * sizeof(uint16_t), hipMemcpyHostToDevice, p->stream));
+  p->sc.nx = s->h.nx; p->sc.ny = s->h.ny; p->sc.nz = s->h.nz; p->sc.wx = s->h.wx;
+  p->sc.ox = s->h.ox; p->sc.oy = s->h.oy; p->sc.oz = s->h.oz; p->sc.res = s->h.res;
+  p->sc.bits = p->d_bits.p;
+  p->sc.d2 = p->d_d2.p;
+  p->have_scene = true;
+  p->scene_res = s->h.res;
+  return update_mapcfg(p);
+}
+
+int smp_set_disabled_map_links(smp_planner* p, const char* const* names, int n) {
+  if (!p || (n > 0 && !names)) return SMP_ERR_ARG;
+  HIPCHK(hipSetDevice(p->device));
+  p->disabled.clear();
+  for (int i = 0; i < n; ++i) if (names[i]) p->disabled.insert(names[i]);
+  return update_mapcfg(p);
+}
+
+int smp_check_configs(smp_planner* p, const double* q_soa, int64_t n, int check_self, int check_map, uint8_t* valid) {
+  if (!p || n < 0 || (n > 0 && (!q_soa || !valid))) return SMP_ERR_ARG;
+  if (n == 0) return SMP_OK;
+  HIPCHK(hipSetDevice(p->device));
+  HIPCHK(p->d_cq.reserve((size_t)n * NJ));
+  HIPCHK(p->d_valid.reserve((size_t)n));
+  HIPCHK(hipMemcpyAsync(p->d_cq.p, q_soa, (size_t)n * NJ * sizeof(double), hipMemcpyHostToDevice, p->stream));
+  long long tiles = (n + 15) / 16;
+  int grid = (int)std::min<long long>(tiles, 256 * 8);
+  HIPCHK(hipEventRecord(p->ev0, p->stream));
+  hipLaunchKernelGGL(check_kernel, dim3(grid), dim3(256), 0, p->stream, p->d_rb, p->sc, p->d_mc, p->d_cq.p, (long long)n,
+                     check_self, check_map && p->have_scene, p->d_valid.p);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(p->ev1, p->stream));
+  HIPCHK(hipMemcpyAsync(valid, p->d_valid.p, (size_t)n, hipMemcpyDeviceToHost, p->stream));
+  HIPCHK(hipStreamSynchronize(p->stream));
+  float ms = 0;
+  HIPCHK(hipEventElapsedTime(&ms, p->ev0, p->ev1));
+  p->last_check_ms = ms;
+  return SMP_OK;
+}
+
+int smp_is_config_valid(smp_planner* p, const double q[8], int check_self, int check_map, int* valid) {
+  if (!p || !q || !valid) return SMP_ERR_ARG;
+  double soa[8];
+  for (int j = 0; j < 8; ++j) soa[j] = q[j];
+  uint8_t v = 0;
+  int st = smp_check_configs(p, soa, 1, check_self, check_map, &v);
+  *valid = v;
+  return st;
+}
+
+int smp_last_kernel_ms(const smp_planner* p, double* check_ms, double* plan_ms, int64_t* plan_launches) {
+  if (!p) return SMP_ERR_ARG;
+  if (check_ms) *check_ms = p->last_check_ms;
+  if (plan_ms) *plan_ms = p->last_plan_ms;
+  if (plan_launches) *plan_launches = p->last_plan_launches;
+  return SMP_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------------------------------ planning
+// C = H * diag(1, .., 1, det H), H = I - 2 v v^T / v^T v, v = e1 - a (DESIGN.md "Informed sampling");
+// a non-finite direction (start == goal in a block) falls back to a = e1 (the reference divides by zero).
+static void householder_C(const double* a_in, int n, double* C) {
+  double a[6], v[6], vv = 0.0;
+  bool fin = true;
+  for (int i = 0; i < n; ++i) { a[i] = a_in[i]; if (!std::isfinite(a[i])) fin = false; }
+  if (!fin) for (int i = 0; i < n; ++i) a[i] = (i == 0) ? 1.0 : 0.0;
+  for (int i = 0; i < n; ++i) { v[i] = (i == 0 ? 1.0 : 0.0) - a[i]; vv += v[i] * v[i]; }
+  double det = vv == 0.0 ? 1.0 : -1.0;
+  for (int i = 0; i < n; ++i)
+    for (int k = 0; k < n; ++k) {
+      double h = (i == k ? 1.0 : 0.0) - (vv == 0.0 ? 0.0 : 2.0 * v[i] * v[k] / vv);
+      C[i * n + k] = (k == n - 1) ? h * det : h;
+    }
+}
+
+static void init_qstate(const smp_planner* p, const smp_query& q, int64_t cap, int via_cap, QState* S) {
+  std::memset(S, 0, sizeof(QState));
+  const RobotDev& rb = p->robot.dev;
+  S->status = 0;
+  S->phase = 0;
+  S->A = 0;
+  S->n[0] = S->n[1] = 1;
+  S->cap = (int)cap;
+  S->via_cap = via_cap;
+  S->max_iter = q.budget_is_time ? (long long)1 << 62 : (long long)q.budget;
+  S->first_iter = -1;
+  S->last_iter = -1;
+  S->cbest[0] = S->cbest[1] = S->cbest[2] = 10000.0;
+  double a = 0, r = 0, pp = 0;  // distance_heuristics.cpp:160-217
+  for (int j = 0; j < NJ; ++j) {
+    double d = q.goal[j] - q.start[j];
+    a += d * d;
+    if (rb.rev[j]) r += d * d; else pp += d * d;
+  }
+  S->h0[0] = std::sqrt(a); S->h0[1] = std::sqrt(r); S->h0[2] = std::sqrt(pp);
+  for (int j = 0; j < NJ; ++j) { S->qs[j] = q.start[j]; S->qg[j] = q.goal[j]; }
+  double arev[6], apr[2];
+  int ir = 0, ip = 0;
+  for (int j = 0; j < NJ; ++j) {  // jointConfigEllipseInitialization (birrt_star.cpp:3472-3604)
+    if (rb.rev[j]) { S->ctr_rev[ir] = (q.start[j] + q.goal[j]) / 2.0; arev[ir++] = (q.goal[j] - q.start[j]) / S->h0[1]; }
+    else { S->ctr_pr[ip] = (q.start[j] + q.goal[j]) / 2.0; apr[ip++] = (q.goal[j] - q.start[j]) / S->h0[2]; }
+  }
+  householder_C(arev, 6, S->Crev);
+  householder_C(apr, 2, S->Cpr);
+  S->env_x[0] = q.env_x[0]; S->env_x[1] = q.env_x[1];
+  S->env_y[0] = q.env_y[0]; S->env_y[1] = q.env_y[1];
+  S->near_r = p->params.near_threshold;
+  S->step = p->params.step_factor;
+  S->opt_thresh = p->params.path_optimality_threshold;
+  S->n_pts = p->params.num_traj_segments;
+  S->max_near = p->params.max_near_nodes;
+  S->tree_opt = p->params.tree_optimization;
+  S->informed = p->params.informed_sampling;
+  S->self = q.check_self;
+  S->map = q.check_map && p->have_scene;
+  S->seed = q.seed;
+  S->query = q.query_id;
+}
+
+static hipError_t alloc_query(QueryBuffers& b, size_t cap, int via_cap, long long rows) {
+  hipError_t e;
+  if ((e = b.st.reserve(1))) return e;
+  if ((e = b.q.reserve(cap * NJ * 2))) return e;
+  if ((e = b.cost.reserve(cap * 3 * 2))) return e;
+  if ((e = b.e_start.reserve(cap * NJ * 2))) return e;
+  if ((e = b.e_target.reserve(cap * NJ * 2))) return e;
+  if ((e = b.parent.reserve(cap * 2))) return e;
+  if ((e = b.first_child.reserve(cap * 2))) return e;
+  if ((e = b.next_sib.reserve(cap * 2))) return e;
+  if ((e = b.prev_sib.reserve(cap * 2))) return e;
+  if ((e = b.stack.reserve(cap))) return e;
+  if ((e = b.path_nodes.reserve(cap * 2))) return e;
+  if ((e = b.via.reserve(via_cap))) return e;
+  if ((e = b.rows.reserve(std::max<long long>(rows, 1) * 5))) return e;
+  b.cap = cap;
+  return hipSuccess;
+}
+
+static QueryDev make_qdev(QueryBuffers& b, size_t cap, long long rows) {
+  QueryDev d;
+  d.st = b.st.p;
+  for (int t = 0; t < 2; ++t) {
+    TreeDev& T = d.tr[t];
+    T.q = b.q.p + (size_t)t * cap * NJ;
+    T.cost = b.cost.p + (size_t)t * cap * 3;
+    T.e_start = b.e_start.p + (size_t)t * cap * NJ;
+    T.e_target = b.e_target.p + (size_t)t * cap * NJ;
+    T.parent = b.parent.p + (size_t)t * cap;
+    T.first_child = b.first_child.p + (size_t)t * cap;
+    T.next_sib = b.next_sib.p + (size_t)t * cap;
+    T.prev_sib = b.prev_sib.p + (size_t)t * cap;
+  }
+  d.via = b.via.p;
+  d.stack = b.stack.p;
+  d.rows = b.rows.p;
+  d.rows_cap = rows;
+  d.path_nodes = b.path_nodes.p;
+  return d;
+}
+
+static int upload_roots(smp_planner* p, QueryBuffers& b, const QueryDev& d, const smp_query& q, size_t cap) {
+  for (int t = 0; t < 2; ++t) {
+    const double* root = t == 0 ? q.start : q.goal;
+    double col[NJ];
+    for (int j = 0; j < NJ; ++j) col[j] = root[j];
+    for (int j = 0; j < NJ; ++j)
+      HIPCHK(hipMemcpyAsync(d.tr[t].q + (size_t)j * cap, &col[j], sizeof(double), hipMemcpyHostToDevice, p->stream));
+    double zero = 0.0;
+    for (int k = 0; k < 3; ++k)
+      HIPCHK(hipMemcpyAsync(d.tr[t].cost + (size_t)k * cap, &zero, sizeof(double), hipMemcpyHostToDevice, p->stream));
+    int z = 0, m1 = -1;
+    HIPCHK(hipMemcpyAsync(d.tr[t].parent, &z, sizeof(int), hipMemcpyHostToDevice, p->stream));
+    HIPCHK(hipMemcpyAsync(d.tr[t].first_child, &m1, sizeof(int), hipMemcpyHostToDevice, p->stream));
+    HIPCHK(hipMemcpyAsync(d.tr[t].next_sib, &m1, sizeof(int), hipMemcpyHostToDevice, p->stream));
+    HIPCHK(hipMemcpyAsync(d.tr[t].prev_sib, &m1, sizeof(int), hipMemcpyHostToDevice, p->stream));
+  }
+  (void)b;
+  return SMP_OK;
+}
+
+extern "C" int smp_plan_batch(smp_planner* p, const smp_query* qs, int nq, smp_result* out) {
+  if (!p || !qs || nq <= 0 || !out) return SMP_ERR_ARG;
+  HIPCHK(hipSetDevice(p->device));
+  for (int i = 0; i < nq; ++i) { std::memset(&out[i], 0, sizeof(smp_result)); }
+  // init_planner validity of start and goal (birrt_star.cpp:350-362)
+  std::vector<int> status(nq, SMP_OK);
+  {
+    // per-query self/map flags may differ: check each query's pair with its own flags
+    for (int i = 0; i < nq; ++i) {
+      double pair[NJ * 2];
+      for (int j = 0; j < NJ; ++j) { pair[j * 2] = qs[i].start[j]; pair[j * 2 + 1] = qs[i].goal[j]; }
+      uint8_t v[2];
+      int st = smp_check_configs(p, pair, 2, qs[i].check_self, qs[i].check_map, v);
+      if (st) return st;
+      if (!v[0]) status[i] = SMP_ERR_START_INVALID;
+      else if (!v[1]) status[i] = SMP_ERR_GOAL_INVALID;
+      if (!(qs[i].budget >= 0)) status[i] = SMP_ERR_ARG;
+    }
+  }
+  if ((int)p->qb.size() < nq) p->qb.resize(nq);
+  std::vector<QueryDev> qdev(nq);
+  std::vector<QState> S(nq);
+  std::vector<long long> rows_cap(nq, 0);
+  for (int i = 0; i < nq; ++i) {
+    const smp_query& q = qs[i];
+    int64_t cap = p->params.node_capacity;
+    long long iters = q.budget_is_time ? 0 : (long long)q.budget;
+    if (cap <= 0) cap = q.budget_is_time ? (int64_t)4 << 20 : std::min<int64_t>(1024 + 16 * iters, (int64_t)1 << 27);
+    rows_cap[i] = q.budget_is_time ? 1 << 20 : std::max<long long>(iters, 1);
+    int via_cap = 4096;
+    HIPCHK(alloc_query(p->qb[i], (size_t)cap, via_cap, rows_cap[i]));
+    qdev[i] = make_qdev(p->qb[i], (size_t)cap, rows_cap[i]);
+    init_qstate(p, q, cap, via_cap, &S[i]);
+    if (status[i] != SMP_OK) { S[i].status = status[i]; S[i].phase = 2; }
+    if (!q.budget_is_time && iters <= 0 && S[i].phase == 0) S[i].max_iter = 0;
+    int st = upload_roots(p, p->qb[i], qdev[i], q, (size_t)cap);
+    if (st) return st;
+    HIPCHK(hipMemcpyAsync(qdev[i].st, &S[i], sizeof(QState), hipMemcpyHostToDevice, p->stream));
+  }
+  HIPCHK(p->d_qdev.reserve(nq));
+  HIPCHK(p->d_counts.reserve(2 * nq));
+  HIPCHK(hipMemcpyAsync(p->d_qdev.p, qdev.data(), nq * sizeof(QueryDev), hipMemcpyHostToDevice, p->stream));
+  HIPCHK(hipStreamSynchronize(p->stream));
+
+  // launch loop: each launch advances every query by `chunk` iterations; time budgets use a device deadline
+  double tmax = 0;
+  for (int i = 0; i < nq; ++i) if (qs[i].budget_is_time) tmax = std::max(tmax, qs[i].budget);
+  auto t_begin = std::chrono::steady_clock::now();
+  int chunk = 256;
+  float total_ms = 0;
+  int64_t launches = 0;
+  bool deadline_set = false;
+  long long max_iters = 0;
+  for (int i = 0; i < nq; ++i) max_iters = std::max(max_iters, qs[i].budget_is_time ? 0LL : (long long)qs[i].budget);
+  for (;;) {
+    if (tmax == 0 && launches > max_iters / 256 + 64) return SMP_ERR_HIP;  // no progress: never spin forever
+    if (tmax > 0 && std::chrono::duration<double>(std::chrono::steady_clock::now() - t_begin).count() > tmax * 4 + 60)
+      return SMP_ERR_HIP;
+    HIPCHK(hipEventRecord(p->ev0, p->stream));
+    hipLaunchKernelGGL(plan_kernel, dim3(nq), dim3(256), 0, p->stream, p->d_rb, p->sc, p->d_mc, p->d_qdev.p, chunk);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(p->ev1, p->stream));
+    launches++;
+    for (int i = 0; i < nq; ++i)
+      HIPCHK(hipMemcpyAsync(&S[i], qdev[i].st, sizeof(QState), hipMemcpyDeviceToHost, p->stream));
+    HIPCHK(hipStreamSynchronize(p->stream));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, p->ev0, p->ev1));
+    total_ms += ms;
+    bool all_done = true;
+    for (int i = 0; i < nq; ++i) all_done &= (S[i].phase == 2 || S[i].status != 0);
+    if (all_done) break;
+    if (tmax > 0 && !deadline_set) {
+      // convert the wall-clock budget into a device-clock deadline per timed query
+      for (int i = 0; i < nq; ++i) {
+        if (!qs[i].budget_is_time || S[i].phase == 2) continue;
+        S[i].deadline = S[i].t0 + (unsigned long long)(qs[i].budget * p->wall_rate_hz);
+        HIPCHK(hipMemcpyAsync(&qdev[i].st->deadline, &S[i].deadline, sizeof(unsigned long long), hipMemcpyHostToDevice, p->stream));
+      }
+      deadline_set = true;
+    }
+    if (chunk < 4096) chunk *= 2;
+    double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_begin).count();
+    (void)el;
+  }
+  p->last_plan_ms = total_ms;
+  p->last_plan_launches = launches;
+
+  // path extraction
+  hipLaunchKernelGGL(path_kernel, dim3(nq), dim3(64), 0, p->stream, p->d_qdev.p, p->d_counts.p);
+  HIPCHK(hipGetLastError());
+  std::vector<int> counts(2 * nq);
+  HIPCHK(hipMemcpyAsync(counts.data(), p->d_counts.p, 2 * nq * sizeof(int), hipMemcpyDeviceToHost, p->stream));
+  HIPCHK(hipStreamSynchronize(p->stream));
+  int rc = SMP_OK;
+  for (int i = 0; i < nq; ++i) {
+    QState& s = S[i];
+    smp_result& r = out[i];
+    size_t cap = p->qb[i].cap;
+    r.status = s.status != 0 ? s.status : (s.have_sol ? SMP_OK : SMP_ERR_NO_SOLUTION);
+    smp_stats& st = r.stats;
+    st.iterations = s.iter;
+    st.first_solution_iter = s.first_iter;
+    st.last_solution_iter = s.last_iter;
+    st.configs_checked = s.checked;
+    st.configs_valid = s.valid;
+    st.time_first_solution = s.have_sol && s.t_first >= s.t0 ? (double)(s.t_first - s.t0) / p->wall_rate_hz : -1.0;
+    st.time_total = s.t_end >= s.t0 ? (double)(s.t_end - s.t0) / p->wall_rate_hz : 0.0;
+    for (int k = 0; k < 3; ++k) { st.cost_best[k] = s.cbest[k]; st.cost_theoretical[k] = s.h0[k]; }
+    st.nodes_start = s.n[0]; st.nodes_goal = s.n[1];
+    st.edges_start = s.edges[0]; st.edges_goal = s.edges[1];
+    st.rewires_start = s.rewires[0]; st.rewires_goal = s.rewires[1];
+    st.connected_tree_is_start = s.conn_start;
+    st.conn_node_b = s.nB.id; st.conn_node_a = s.nA.id;
+    if (i == 0) { p->last_n[0] = s.n[0]; p->last_n[1] = s.n[1]; }
+    // cost rows
+    r.n_cost_rows = s.n_rows;
+    if (s.n_rows > 0) {
+      r.cost_rows = (double*)malloc(sizeof(double) * 5 * s.n_rows);
+      HIPCHK(hipMemcpy(r.cost_rows, p->qb[i].rows.p, sizeof(double) * 5 * s.n_rows, hipMemcpyDeviceToHost));
+      for (int64_t k = 0; k < s.n_rows; ++k) r.cost_rows[k * 5 + 1] /= p->wall_rate_hz;
+    }
+    if (r.status != SMP_OK) continue;
+    int ns = counts[2 * i], ng = counts[2 * i + 1];
+    std::vector<int> ids(ns + ng);
+    if (ns) HIPCHK(hipMemcpy(ids.data(), qdev[i].path_nodes, ns * sizeof(int), hipMemcpyDeviceToHost));
+    if (ng) HIPCHK(hipMemcpy(ids.data() + ns, qdev[i].path_nodes + cap, ng * sizeof(int), hipMemcpyDeviceToHost));
+    const int np = p->params.num_traj_segments;
+    std::vector<double> wp;
+    auto edge_of = [&](int t, int id, double* st8, double* tg8) -> int {
+      for (int j = 0; j < NJ; ++j) {
+        HIPCHK(hipMemcpy(&st8[j], qdev[i].tr[t].e_start + (size_t)j * cap + id, sizeof(double), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(&tg8[j], qdev[i].tr[t].e_target + (size_t)j * cap + id, sizeof(double), hipMemcpyDeviceToHost));
+      }
+      return SMP_OK;
+    };
+    for (int k = 0; k < ns; ++k) {  // start-tree edges contribute points 0 .. np-1
+      double a[NJ], b[NJ], stp[NJ];
+      if (edge_of(0, ids[k], a, b)) return SMP_ERR_HIP;
+      for (int j = 0; j < NJ; ++j) stp[j] = (b[j] - a[j]) / double(np);
+      for (int inc = 0; inc < np; ++inc)
+        for (int j = 0; j < NJ; ++j) wp.push_back(a[j] + inc * stp[j]);
+    }
+    for (int k = 0; k < ng; ++k) {  // goal-tree edges reversed: points np .. 1, then point 0 of the last
+      double a[NJ], b[NJ], stp[NJ];
+      if (edge_of(1, ids[ns + k], a, b)) return SMP_ERR_HIP;
+      for (int j = 0; j < NJ; ++j) stp[j] = (b[j] - a[j]) / double(np);
+      for (int inc = np; inc > 0; --inc)
+        for (int j = 0; j < NJ; ++j) wp.push_back(a[j] + inc * stp[j]);
+      if (k == ng - 1)
+        for (int j = 0; j < NJ; ++j) wp.push_back(a[j] + 0 * stp[j]);
+    }
+    r.n_waypoints = (int64_t)(wp.size() / NJ);
+    if (!wp.empty()) {
+      r.waypoints = (double*)malloc(sizeof(double) * wp.size());
+      std::memcpy(r.waypoints, wp.data(), sizeof(double) * wp.size());
+    }
+  }
+  for (int i = 0; i < nq; ++i) if (out[i].status != SMP_OK && rc == SMP_OK) rc = out[i].status;
+  return rc;
+}
+
+extern "C" int smp_plan(smp_planner* p, const smp_query* q, smp_result* out) { return smp_plan_batch(p, q, 1, out); }
+
+extern "C" void smp_result_free(smp_result* r) {
+  if (!r) return;
+  free(r->waypoints);
+  free(r->cost_rows);
+  r->waypoints = nullptr;
+  r->cost_rows = nullptr;
+  r->n_waypoints = r->n_cost_rows = 0;
+}
+
+extern "C" int64_t smp_get_tree(smp_planner* p, int which, int32_t* parent, double* conf, double* cost) {
+  if (!p || p->qb.empty() || which < 0 || which > 1) return -1;
+  if (hipSetDevice(p->device) != hipSuccess) return -1;
+  QueryBuffers& b = p->qb[0];
+  size_t cap = b.cap;
+  int n = p->last_n[which];
+  if (parent && hipMemcpy(parent, b.parent.p + (size_t)which * cap, n * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  std::vector<double> tmp((size_t)n);
+  if (conf)
+    for (int j = 0; j < NJ; ++j) {
+      if (hipMemcpy(tmp.data(), b.q.p + (size_t)which * cap * NJ + (size_t)j * cap, n * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+      for (int i = 0; i < n; ++i) conf[(size_t)i * NJ + j] = tmp[i];
+    }
+  if (cost)
+    for (int k = 0; k < 3; ++k) {
+      if (hipMemcpy(tmp.data(), b.cost.p + (size_t)which * cap * 3 + (size_t)k * cap, n * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+      for (int i = 0; i < n; ++i) cost[(size_t)i * 3 + k] = tmp[i];
+    }
+  return n;
+}
+
+// ------------------------------------------------------------------------------------------ parity probes
+// Device evaluations of the shared arithmetic (tests only): portable sin/cos, the Philox draw, body FK,
+// end-effector z and the fp64 sqrt / division used throughout.
+extern "C" int smp_probe_sincos(int device, const double* x, int n, double* s, double* c) {
+  if (hipSetDevice(device) != hipSuccess) return SMP_ERR_NO_DEVICE;
+  double *dx, *ds, *dc;
+  HIPCHK(hipMalloc(&dx, n * sizeof(double))); HIPCHK(hipMalloc(&ds, n * sizeof(double))); HIPCHK(hipMalloc(&dc, n * sizeof(double)));
+  HIPCHK(hipMemcpy(dx, x, n * sizeof(double), hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(sincos_kernel, dim3((n + 255) / 256), dim3(256), 0, 0, dx, n, ds, dc);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpy(s, ds, n * sizeof(double), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(c, dc, n * sizeof(double), hipMemcpyDeviceToHost));
+  (void)hipFree(dx); (void)hipFree(ds); (void)hipFree(dc);
+  return SMP_OK;
+}
+
+extern "C" int smp_probe_u01(int device, uint64_t seed, uint32_t query, const uint32_t* ctr, int n, double* out) {
+  if (hipSetDevice(device) != hipSuccess) return SMP_ERR_NO_DEVICE;
+  uint32_t* dc;
+  double* d;
+  HIPCHK(hipMalloc(&dc, 4 * n * sizeof(uint32_t))); HIPCHK(hipMalloc(&d, n * sizeof(double)));
+  HIPCHK(hipMemcpy(dc, ctr, 4 * n * sizeof(uint32_t), hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(u01_kernel, dim3((n + 255) / 256), dim3(256), 0, 0, (unsigned long long)seed, query, dc, n, d);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpy(out, d, n * sizeof(double), hipMemcpyDeviceToHost));
+  (void)hipFree(dc); (void)hipFree(d);
+  return SMP_OK;
+}
+
+extern "C" int smp_probe_fk(smp_planner* p, const double* q, int n, double* frames, double* eez) {
+  if (!p) return SMP_ERR_ARG;
+  HIPCHK(hipSetDevice(p->device));
+  int nb = p->robot.dev.n_body;
+  double *dq, *df, *dz;
+  HIPCHK(hipMalloc(&dq, (size_t)n * NJ * sizeof(double)));
+  HIPCHK(hipMalloc(&df, (size_t)n * nb * 12 * sizeof(double)));
+  HIPCHK(hipMalloc(&dz, (size_t)n * sizeof(double)));
+  HIPCHK(hipMemcpy(dq, q, (size_t)n * NJ * sizeof(double), hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(fk_kernel, dim3((n + 127) / 128), dim3(128), 0, 0, p->d_rb, dq, n, df, dz);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpy(frames, df, (size_t)n * nb * 12 * sizeof(double), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(eez, dz, (size_t)n * sizeof(double), hipMemcpyDeviceToHost));
+  (void)hipFree(dq); (void)hipFree(df); (void)hipFree(dz);
+  return SMP_OK;
+}
+
+extern "C" int smp_probe_sqrt_div(int device, const double* a, const double* b, int n, double* sq, double* dv) {
+  if (hipSetDevice(device) != hipSuccess) return SMP_ERR_NO_DEVICE;
+  double *da, *db, *ds, *dd;
+  HIPCHK(hipMalloc(&da, n * sizeof(double))); HIPCHK(hipMalloc(&db, n * sizeof(double)));
+  HIPCHK(hipMalloc(&ds, n * sizeof(double))); HIPCHK(hipMalloc(&dd, n * sizeof(double)));
+  HIPCHK(hipMemcpy(da, a, n * sizeof(double), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(db, b, n * sizeof(double), hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(sqrt_div_kernel, dim3((n + 255) / 256), dim3(256), 0, 0, da, db, n, ds, dd);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpy(sq, ds, n * sizeof(double), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(dv, dd, n * sizeof(double), hipMemcpyDeviceToHost));
+  (void)hipFree(da); (void)hipFree(db); (void)hipFree(ds); (void)hipFree(dd);
+  return SMP_OK;
+}

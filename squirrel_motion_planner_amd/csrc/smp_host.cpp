@@ -1,0 +1,302 @@
+// Host-side builders of the device model and scene.  See smp_host.h.
+#include "smp_host.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <map>
+#include <stdexcept>
+
+#include "smp_json.h"
+
+namespace smp {
+
+static int type_code(const std::string& t) {
+  if (t == "RotAxis") return 1;
+  if (t == "TransAxis") return 2;
+  return 0;
+}
+
+static void copy3(const json::Value& v, double* o, int n = 3) {
+  if (v.size() != (size_t)n) throw std::runtime_error("model: bad vector length");
+  for (int i = 0; i < n; ++i) o[i] = v[i].d();
+}
+
+// Robot model JSON (tools/gen_robot_model.py).  Mirrors KDLRobotModel + CollisionChecker construction.
+void robot_from_json(const std::string& text, RobotHost* out) {
+  json::Value m = json::parse(text.c_str());
+  RobotDev& d = out->dev;
+  std::memset(&d, 0, sizeof(d));
+  d.root_z = m["root_z"].d();
+  const json::Value& links = m["links"];
+  out->link_names.clear();
+  for (size_t i = 0; i < links.size(); ++i) out->link_names.push_back(links[i]["name"].s());
+  const json::Value& bc = m["body_chain"];
+  d.n_chain = (int)bc.size();
+  if (d.n_chain > MAX_CHAIN) throw std::runtime_error("model: body chain too long");
+  for (int k = 0; k < d.n_chain; ++k) {
+    const json::Value& e = bc[k];
+    d.ch_type[k] = type_code(e["type"].s());
+    d.ch_joint[k] = e["joint"].i();
+    d.ch_body[k] = e["body"].i();
+    copy3(e["axis"], &d.ch_axis[k * 3]);
+    copy3(e["origin"], &d.ch_origin[k * 3]);
+    copy3(e["R"], &d.ch_R[k * 9], 9);
+    copy3(e["p"], &d.ch_p[k * 3]);
+  }
+  d.n_body = (int)m["bodies"].size();
+  if (d.n_body > MAX_BODY) throw std::runtime_error("model: too many bodies");
+  const json::Value& ch = m["chain"];
+  d.n_seg = (int)ch.size();
+  if (d.n_seg > MAX_SEG) throw std::runtime_error("model: chain too long");
+  for (int s = 0; s < d.n_seg; ++s) {
+    const json::Value& e = ch[s];
+    d.seg_type[s] = type_code(e["type"].s());
+    d.seg_joint[s] = e["joint"].i();
+    copy3(e["axis"], &d.seg_axis[s * 3]);
+    copy3(e["origin"], &d.seg_origin[s * 3]);
+    copy3(e["ftip_R"], &d.seg_R[s * 9], 9);
+    copy3(e["ftip_p"], &d.seg_p[s * 3]);
+  }
+  // collision links -> compact slots (order of link_bounds)
+  const json::Value& lb = m["link_bounds"];
+  d.n_clink = (int)lb.size();
+  if (d.n_clink > MAX_CLINK) throw std::runtime_error("model: too many collision links");
+  out->clink_of_link.assign(links.size(), -1);
+  for (int c = 0; c < d.n_clink; ++c) {
+    int li = lb[c]["link"].i();
+    out->clink_of_link[li] = c;
+    d.cl_link[c] = li;
+    d.cl_body[c] = lb[c]["body"].i();
+    copy3(lb[c]["cb"], &d.cl_cb[c * 3]);
+    d.cl_r[c] = lb[c]["r"].d();
+  }
+  // spheres sorted by clink slot (stable)
+  const json::Value& S = m["spheres"];
+  d.n_sph = (int)S.size();
+  if (d.n_sph > MAX_SPH) throw std::runtime_error("model: too many spheres");
+  std::vector<int> order(d.n_sph);
+  for (int i = 0; i < d.n_sph; ++i) order[i] = i;
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+    return out->clink_of_link[S[a]["link"].i()] < out->clink_of_link[S[b]["link"].i()];
+  });
+  for (int c = 0; c < d.n_clink; ++c) { d.cl_sph0[c] = 0; d.cl_nsph[c] = 0; }
+  for (int k = 0; k < d.n_sph; ++k) {
+    const json::Value& s = S[order[k]];
+    int c = out->clink_of_link[s["link"].i()];
+    if (c < 0) throw std::runtime_error("model: sphere on a link without bounds");
+    d.sph_clink[k] = c;
+    d.sph_body[k] = s["body"].i();
+    copy3(s["cb"], &d.sph_cb[k * 3]);
+    d.sph_r[k] = s["r"].d();
+    if (d.cl_nsph[c] == 0) d.cl_sph0[c] = k;
+    d.cl_nsph[c]++;
+  }
+  const json::Value& P = m["self_pairs"];
+  d.n_pairs = (int)P.size();
+  if (d.n_pairs > MAX_PAIRS) throw std::runtime_error("model: too many pairs");
+  for (int p = 0; p < d.n_pairs; ++p) {
+    d.pair_a[p] = out->clink_of_link[P[p][0].i()];
+    d.pair_b[p] = out->clink_of_link[P[p][1].i()];
+    if (d.pair_a[p] < 0 || d.pair_b[p] < 0) throw std::runtime_error("model: pair on a link without geometry");
+  }
+  for (int j = 0; j < NJ; ++j) {
+    d.q_min[j] = m["q_min"][j].d();
+    d.q_max[j] = m["q_max"][j].d();
+    d.rev[j] = m["joint_is_revolute"][j].i();
+  }
+}
+
+// ------------------------------------------------------------------------------------------ scene
+int grid_pad_cells(double res) { return (int)std::ceil(0.30 / res) + 2; }
+
+uint32_t sphere_threshold(double r, double res) {
+  double a = r / res + 1.7320508075688772 + 1e-3;
+  return (uint32_t)std::ceil(a * a);
+}
+
+// 1-D squared distance transform of f (Felzenszwalb & Huttenlocher 2012), in place.
+static void dt1d(double* f, int n, int stride, std::vector<double>& tmp, std::vector<int>& v, std::vector<double>& z) {
+  const double INF = std::numeric_limits<double>::infinity();
+  tmp.resize(n);
+  v.resize(n);
+  z.resize(n + 1);
+  for (int i = 0; i < n; ++i) tmp[i] = f[(size_t)i * stride];
+  int k = -1;
+  for (int q = 0; q < n; ++q) {
+    if (tmp[q] == INF) continue;
+    double s = 0.0;
+    while (k >= 0) {  // z[0] = -inf, so the first parabola is never popped
+      int vk = v[k];
+      s = ((tmp[q] + (double)q * q) - (tmp[vk] + (double)vk * vk)) / (2.0 * q - 2.0 * vk);
+      if (s <= z[k]) --k; else break;
+    }
+    if (k < 0) { k = 0; v[0] = q; z[0] = -INF; z[1] = INF; continue; }
+    ++k;
+    v[k] = q;
+    z[k] = s;
+    z[k + 1] = INF;
+  }
+  if (k < 0) return;  // all infinite: unchanged
+  int j = 0;
+  for (int q = 0; q < n; ++q) {
+    while (z[j + 1] < q) ++j;
+    double dq = (double)(q - v[j]);
+    f[(size_t)q * stride] = dq * dq + tmp[v[j]];
+  }
+}
+
+void edt_squared(const std::vector<uint8_t>& occ, int nx, int ny, int nz, std::vector<uint16_t>* d2) {
+  const double INF = std::numeric_limits<double>::infinity();
+  size_t n = (size_t)nx * ny * nz;
+  std::vector<double> f(n);
+  bool any = false;
+  for (size_t i = 0; i < n; ++i) { f[i] = occ[i] ? 0.0 : INF; any |= occ[i] != 0; }
+  d2->assign(n, 65535);
+  if (!any) return;
+  std::vector<double> tmp, z;
+  std::vector<int> v;
+  for (int k = 0; k < nz; ++k)
+    for (int j = 0; j < ny; ++j) dt1d(&f[((size_t)k * ny + j) * nx], nx, 1, tmp, v, z);
+  for (int k = 0; k < nz; ++k)
+    for (int i = 0; i < nx; ++i) dt1d(&f[(size_t)k * ny * nx + i], ny, nx, tmp, v, z);
+  for (int j = 0; j < ny; ++j)
+    for (int i = 0; i < nx; ++i) dt1d(&f[(size_t)j * nx + i], nz, nx * ny, tmp, v, z);
+  for (size_t i = 0; i < n; ++i) (*d2)[i] = f[i] >= 65535.0 ? 65535 : (uint16_t)f[i];
+}
+
+void scene_from_keys(const uint16_t* keys, int64_t n, double res, double z_offset, SceneHost* out) {
+  out->res = res;
+  out->n_occupied = 0;
+  if (n <= 0) {
+    out->nx = out->ny = out->nz = 1;
+    out->wx = 1;
+    out->ox = out->oy = 0.0;
+    out->oz = 0.0 + z_offset;
+    out->bits.assign(1, 0);
+    out->d2.assign(1, 65535);
+    for (int d = 0; d < 3; ++d) out->bbox_min[d] = out->bbox_max[d] = 0.0;
+    return;
+  }
+  int kmin[3] = {1 << 30, 1 << 30, 1 << 30}, kmax[3] = {-1, -1, -1};
+  for (int64_t i = 0; i < n; ++i)
+    for (int d = 0; d < 3; ++d) {
+      int k = keys[i * 3 + d];
+      kmin[d] = std::min(kmin[d], k);
+      kmax[d] = std::max(kmax[d], k);
+    }
+  int pad = grid_pad_cells(res);
+  for (int d = 0; d < 3; ++d) {
+    out->bbox_min[d] = (double)(kmin[d] - KEY_OFFSET) * res;
+    out->bbox_max[d] = (double)(kmax[d] - KEY_OFFSET + 1) * res;
+    kmin[d] -= pad;
+    kmax[d] += pad;
+  }
+  out->nx = kmax[0] - kmin[0] + 1;
+  out->ny = kmax[1] - kmin[1] + 1;
+  out->nz = kmax[2] - kmin[2] + 1;
+  out->wx = (out->nx + 63) / 64;
+  out->ox = (double)(kmin[0] - KEY_OFFSET) * res;
+  out->oy = (double)(kmin[1] - KEY_OFFSET) * res;
+  out->oz = (double)(kmin[2] - KEY_OFFSET) * res + z_offset;
+  size_t ncell = (size_t)out->nx * out->ny * out->nz;
+  std::vector<uint8_t> occ(ncell, 0);
+  out->bits.assign((size_t)out->wx * out->ny * out->nz, 0);
+  for (int64_t i = 0; i < n; ++i) {
+    int x = keys[i * 3] - kmin[0], y = keys[i * 3 + 1] - kmin[1], z = keys[i * 3 + 2] - kmin[2];
+    size_t c = ((size_t)z * out->ny + y) * out->nx + x;
+    if (!occ[c]) {
+      occ[c] = 1;
+      out->n_occupied++;
+      out->bits[((size_t)z * out->ny + y) * out->wx + (x >> 6)] |= 1ull << (x & 63);
+    }
+  }
+  edt_squared(occ, out->nx, out->ny, out->nz, &out->d2);
+}
+
+void floor_keys(double cx, double cy, double res, double distance, std::vector<uint16_t>* keys) {
+  // octree->coordToKey(x, y, -res/2): key = floor(coord / res) + 32768 (octomap OcTreeBaseImpl::coordToKey)
+  int kx = (int)std::floor(cx / res) + KEY_OFFSET;
+  int ky = (int)std::floor(cy / res) + KEY_OFFSET;
+  int kz = (int)std::floor((-res * 0.5) / res) + KEY_OFFSET;
+  int nd = (int)(distance / res);
+  for (int x = kx - nd; x <= kx + nd; ++x)
+    for (int y = ky - nd; y <= ky + nd; ++y) {
+      keys->push_back((uint16_t)x);
+      keys->push_back((uint16_t)y);
+      keys->push_back((uint16_t)kz);
+    }
+}
+
+// Octomap binary format (OcTreeBase::writeBinaryNode): per inner node two bytes, 2 bits per child
+// (00 unknown, 01 occupied leaf, 10 free leaf, 11 inner), then the inner children recursively.
+namespace {
+struct BtReader {
+  const uint8_t* p;
+  const uint8_t* end;
+  std::vector<uint16_t>* keys;
+  void node(int depth, int kx, int ky, int kz) {
+    if (end - p < 2) throw std::runtime_error("octomap: truncated binary stream");
+    uint8_t c14 = *p++, c58 = *p++;
+    int half = 32768 >> (depth + 1);  // center offset of the children
+    int inner[8];
+    for (int i = 0; i < 8; ++i) {
+      uint8_t byte = i < 4 ? c14 : c58;
+      int b = (i & 3) * 2;
+      int b0 = (byte >> b) & 1, b1 = (byte >> (b + 1)) & 1;
+      inner[i] = (b0 && b1);
+      int cx = kx + ((i & 1) ? half : -half - (half ? 0 : 1));
+      int cy = ky + ((i & 2) ? half : -half - (half ? 0 : 1));
+      int cz = kz + ((i & 4) ? half : -half - (half ? 0 : 1));
+      if (!b0 && b1) emit(depth + 1, cx, cy, cz);
+    }
+    for (int i = 0; i < 8; ++i) {
+      if (!inner[i]) continue;
+      if (depth + 1 >= 16) throw std::runtime_error("octomap: inner node below max depth");
+      int cx = kx + ((i & 1) ? half : -half - (half ? 0 : 1));
+      int cy = ky + ((i & 2) ? half : -half - (half ? 0 : 1));
+      int cz = kz + ((i & 4) ? half : -half - (half ? 0 : 1));
+      node(depth + 1, cx, cy, cz);
+    }
+  }
+  void emit(int depth, int kx, int ky, int kz) {
+    if (depth >= 16) {
+      keys->push_back((uint16_t)kx); keys->push_back((uint16_t)ky); keys->push_back((uint16_t)kz);
+      return;
+    }
+    int h = 32768 >> depth;  // pruned leaf covers [k - h, k + h - 1]
+    for (int z = kz - h; z < kz + h; ++z)
+      for (int y = ky - h; y < ky + h; ++y)
+        for (int x = kx - h; x < kx + h; ++x) {
+          keys->push_back((uint16_t)x); keys->push_back((uint16_t)y); keys->push_back((uint16_t)z);
+        }
+  }
+};
+}  // namespace
+
+void octomap_bt_keys(const uint8_t* data, size_t size, double* res, std::vector<uint16_t>* keys) {
+  const uint8_t* p = data;
+  const uint8_t* end = data + size;
+  bool have_res = false, in_header = true;
+  std::string id;
+  long long nodes = -1;
+  while (in_header) {
+    const uint8_t* nl = (const uint8_t*)memchr(p, '\n', end - p);
+    if (!nl) throw std::runtime_error("octomap: header not terminated");
+    std::string line((const char*)p, nl - p);
+    p = nl + 1;
+    if (!line.empty() && line.back() == '\r') line.pop_back();
+    if (line.empty() || line[0] == '#') continue;
+    if (line.rfind("id ", 0) == 0) id = line.substr(3);
+    else if (line.rfind("size ", 0) == 0) nodes = atoll(line.c_str() + 5);
+    else if (line.rfind("res ", 0) == 0) { *res = strtod(line.c_str() + 4, nullptr); have_res = true; }
+    else if (line == "data") in_header = false;
+  }
+  if (!have_res || (id != "OcTree" && !id.empty())) throw std::runtime_error("octomap: unsupported header");
+  if (nodes == 0) return;
+  BtReader r{p, end, keys};
+  r.node(0, 32768, 32768, 32768);
+}
+
+}  // namespace smp

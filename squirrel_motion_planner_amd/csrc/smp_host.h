@@ -1,0 +1,42 @@
+// Host-side builders: robot model (JSON / URDF+SRDF), occupancy scene (keys / octomap .bt), squared EDT.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "smp_types.h"
+
+namespace smp {
+
+struct RobotHost {
+  RobotDev dev;
+  std::vector<std::string> link_names;  // all tree links
+  std::vector<int> clink_of_link;       // -1 if the link has no collision geometry
+};
+
+struct SceneHost {
+  int nx = 1, ny = 1, nz = 1, wx = 1;
+  double ox = 0, oy = 0, oz = 0, res = 0.05;
+  std::vector<uint64_t> bits;
+  std::vector<uint16_t> d2;
+  int64_t n_occupied = 0;
+  double bbox_min[3] = {0, 0, 0}, bbox_max[3] = {0, 0, 0};  // metric bbox of the occupied keys (octree frame)
+};
+
+// Throws std::runtime_error on malformed input.
+void robot_from_json(const std::string& text, RobotHost* out);
+void robot_from_urdf(const std::string& urdf, const std::string& srdf, const std::string& spheres_json, RobotHost* out);
+
+constexpr int KEY_OFFSET = 32768;  // octomap tree_max_val
+
+int grid_pad_cells(double res);
+void scene_from_keys(const uint16_t* keys, int64_t n, double res, double z_offset, SceneHost* out);
+// Octomap binary stream (.bt file or octomap_msgs binary payload) -> occupied leaf keys (expanded to depth 16).
+void octomap_bt_keys(const uint8_t* data, size_t size, double* res, std::vector<uint16_t>* keys);
+// squirrel_8dof_planner.cpp:889-902 floor square around (cx, cy) at the key of z = -res/2.
+void floor_keys(double cx, double cy, double res, double distance, std::vector<uint16_t>* keys);
+// Exact squared Euclidean distance transform (voxel units) of a dense occupancy mask (x fastest).
+void edt_squared(const std::vector<uint8_t>& occ, int nx, int ny, int nz, std::vector<uint16_t>* d2);
+uint32_t sphere_threshold(double r, double res);
+
+}  // namespace smp

@@ -1,0 +1,1007 @@
+// HIP kernels for gfx950: batched configuration validity and the device-resident BiRRT* planner.
+//
+// Design: one 256-thread workgroup owns one planning query for its whole run_planner loop
+// (birrt_star.cpp:983-1407).  The sequential decisions of the reference are taken by one lane and broadcast
+// through LDS; the data-parallel parts run on the whole workgroup:
+//   * nearest-neighbour argmin and radius-near selection over SoA node arrays (birrt_star.cpp:4076-4133,
+//     4272-4324) -- coalesced fp64 streams, wave shuffles + LDS reduction, lowest-index tie break;
+//   * edge validity (isEdgeValid, birrt_star.cpp:6864-6895) as 32-configuration collision tiles in LDS;
+//   * candidate edges of choose-parent / rewire / connect evaluated speculatively in one batch and then
+//     committed in the reference's sequential order, so trees are identical to the sequential planner.
+// Several queries (C3/C5) run as several workgroups of one launch; each launch advances every query by a
+// bounded number of iterations and persists the state (QState) in HBM.
+#include <hip/hip_runtime.h>
+
+#include "smp_collide.h"
+#include "smp_math.h"
+#include "smp_plan.h"
+#include "smp_types.h"
+
+namespace smp {
+
+// ============================================================================================ batch check
+// valid[i] = !isInCollision(q_i) for n configurations given as SoA q[j*n + i].
+constexpr int CHECK_CT = 16;
+
+__global__ void __launch_bounds__(BLOCK) check_kernel(const RobotDev* __restrict__ rb, SceneDev sc,
+                                                      const MapCfg* __restrict__ mc, const double* __restrict__ q,
+                                                      long long n, int self, int map, uint8_t* __restrict__ valid) {
+  __shared__ TileLds<CHECK_CT> L;
+  __shared__ double ql[CHECK_CT][NJ];
+  const long long ntiles = (n + CHECK_CT - 1) / CHECK_CT;
+  for (long long t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    long long base = t * CHECK_CT;
+    int nc = (int)min((long long)CHECK_CT, n - base);
+    if (threadIdx.x < nc * NJ) {
+      int c = threadIdx.x / NJ, j = threadIdx.x - c * NJ;
+      ql[c][j] = q[(long long)j * n + base + c];
+    }
+    __syncthreads();
+    collide_tile<CHECK_CT>(rb, sc, mc, nc, ql, self, map, L);
+    if (threadIdx.x < nc) valid[base + threadIdx.x] = L.coll[threadIdx.x] ? 0 : 1;
+    __syncthreads();
+  }
+}
+
+// ============================================================================================ parity kernels
+__global__ void sincos_kernel(const double* x, int n, double* s, double* c) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) psincos(x[i], s + i, c + i);
+}
+
+__global__ void u01_kernel(unsigned long long seed, unsigned query, const uint32_t* ctr, int n, double* out) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = u01(seed, query, ctr[4 * i], ctr[4 * i + 1], ctr[4 * i + 2], ctr[4 * i + 3]);
+}
+
+// body frames (n x n_body x 12) and end-effector z of n configurations (row-major q).
+__global__ void fk_kernel(const RobotDev* __restrict__ rb, const double* q, int n, double* frames, double* eez) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double qq[NJ];
+  for (int j = 0; j < NJ; ++j) qq[j] = q[i * NJ + j];
+  Frame B[MAX_BODY];
+  body_frames(rb, qq, B);
+  for (int b = 0; b < rb->n_body; ++b) {
+    for (int k = 0; k < 9; ++k) frames[((size_t)i * rb->n_body + b) * 12 + k] = B[b].R[k];
+    for (int k = 0; k < 3; ++k) frames[((size_t)i * rb->n_body + b) * 12 + 9 + k] = B[b].p[k];
+  }
+  eez[i] = ee_z(rb, qq);
+}
+
+__global__ void sqrt_div_kernel(const double* a, const double* b, int n, double* sq, double* dv) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) { sq[i] = sqrt(a[i]); dv[i] = a[i] / b[i]; }
+}
+
+// ============================================================================================ planner
+struct PlanLds {
+  QState S;
+  union {
+    struct {
+      TileLds<32> T;
+      double tq[32][NJ];
+    } tile;
+    double seg[MAXE][MAX_PTS][3];
+    struct {
+      double rd[BLOCK / 64];
+      int ri[BLOCK / 64];
+      double rc2[BLOCK / 64];
+      int ri2[BLOCK / 64];
+    } red;
+  } u;
+  // edge batch
+  double eg_start[MAXE][NJ], eg_target[MAXE][NJ], eg_step[MAXE][NJ], eg_end[MAXE][NJ];
+  double eg_base[MAXE][3], eg_cost[MAXE][3];
+  int eg_first[MAXE], eg_need[MAXE], eg_near[MAXE];
+  // near lists (ascending (cost,id) for the first max_near; last max_near in ascending order)
+  int nk;
+  int lo_i[MAX_NEAR], hi_i[MAX_NEAR];
+  double lo_c[MAX_NEAR], hi_c[MAX_NEAR];
+  int n_lo, n_hi;
+  // working nodes
+  NodeRef nn, xn, xc, cur, g;
+  double xr[NJ], ext[NJ], ox[NJ];
+  double en_start[NJ], en_target[NJ];
+  int ext_nn, ext_bp, flag, found, nn_id, cnt;
+  int reached;
+  // via list (connectGraphs / choose_parent): count, tree-local next id
+  int n_via, nn_t, tree_expand;
+  NodeRef sel;
+  double sel_start[NJ], sel_target[NJ];
+  double csp[3], best_nv;
+  double sol[3];
+  // wave reductions
+  double wd[BLOCK / 64];
+  int wi[BLOCK / 64];
+  long long wcount[BLOCK / 64];
+};
+
+struct Ctx {
+  const RobotDev* __restrict__ rb;
+  SceneDev sc;
+  const MapCfg* __restrict__ mc;
+  QueryDev Q;
+};
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+__device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
+
+// --------------------------------------------------------------------------------------- node access
+__device__ __forceinline__ void load_node(const Ctx& C, int t, int id, NodeRef* o) {
+  const TreeDev& T = C.Q.tr[t];
+  int cap = C.Q.st->cap;
+  for (int j = 0; j < NJ; ++j) o->q[j] = T.q[(size_t)j * cap + id];
+  for (int k = 0; k < 3; ++k) o->c[k] = T.cost[(size_t)k * cap + id];
+  o->id = id;
+  o->parent = T.parent[id];
+}
+
+// insertNode (birrt_star.cpp:3298-3322), single lane.  Appends at index n[t] (== node id).
+__device__ void insert_node(const Ctx& C, PlanLds& L, int t, const double* e_start, const double* e_target, const NodeRef& x) {
+  QState& S = L.S;
+  int i = S.n[t];
+  if (i >= S.cap || x.id != i) { S.status = -7; S.phase = 2; return; }
+  const TreeDev& T = C.Q.tr[t];
+  int cap = S.cap;
+  for (int j = 0; j < NJ; ++j) {
+    T.q[(size_t)j * cap + i] = x.q[j];
+    T.e_start[(size_t)j * cap + i] = e_start[j];
+    T.e_target[(size_t)j * cap + i] = e_target[j];
+  }
+  for (int k = 0; k < 3; ++k) T.cost[(size_t)k * cap + i] = x.c[k];
+  T.parent[i] = x.parent;
+  T.first_child[i] = -1;
+  int p = x.parent;
+  int f = T.first_child[p];
+  T.next_sib[i] = f;
+  T.prev_sib[i] = -1;
+  if (f >= 0) T.prev_sib[f] = i;
+  T.first_child[p] = i;
+  S.n[t] = i + 1;
+  S.edges[t]++;
+}
+
+// --------------------------------------------------------------------------------------- scans
+// Block argmin of (d, i): smallest d, then smallest i; d >= 10000 never wins (birrt_star.cpp:4090,4122).
+__device__ int block_argmin(PlanLds& L, double d, int i) {
+  for (int off = 32; off > 0; off >>= 1) {
+    double od = __shfl_xor(d, off);
+    int oi = __shfl_xor(i, off);
+    if (od < d || (od == d && oi < i)) { d = od; i = oi; }
+  }
+  if (lane_id() == 0) { L.wd[wave_id()] = d; L.wi[wave_id()] = i; }
+  __syncthreads();
+  double bd = L.wd[0];
+  int bi = L.wi[0];
+  for (int w = 1; w < BLOCK / 64; ++w)
+    if (L.wd[w] < bd || (L.wd[w] == bd && L.wi[w] < bi)) { bd = L.wd[w]; bi = L.wi[w]; }
+  __syncthreads();
+  return bd < 10000.0 ? bi : 0;
+}
+
+// find_nearest_neighbour_interpolation: first strict minimum of the Euclidean joint distance (DH:128-156).
+__device__ int nearest(const Ctx& C, PlanLds& L, int t, const double* q) {
+  const TreeDev& T = C.Q.tr[t];
+  const int n = L.S.n[t], cap = L.S.cap;
+  double qq[NJ];
+  for (int j = 0; j < NJ; ++j) qq[j] = q[j];
+  double best = 10000.0;
+  int bid = 0x7fffffff;
+  for (int i = threadIdx.x; i < n; i += BLOCK) {
+    double s = 0.0;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      double d = qq[j] - T.q[(size_t)j * cap + i];
+      s += d * d;
+    }
+    double dist = sqrt(s);
+    if (dist < best) { best = dist; bid = i; }
+  }
+  return block_argmin(L, best, bid);
+}
+
+// (cost,id) lexicographic order of the near list (std::sort order made total).
+__device__ __forceinline__ bool ci_less(double ca, int ia, double cb, int ib) {
+  return ca < cb || (ca == cb && ia < ib);
+}
+
+// find_near_vertices_interpolation (birrt_star.cpp:4272-4324): count k, the first MAX_NEAR and the last
+// MAX_NEAR entries of the (cost,id)-sorted near list.  Per-thread register lists + 20-round block merge.
+template <int K>
+__device__ void near_set(const Ctx& C, PlanLds& L, int t, const double* q, int excl) {
+  const TreeDev& T = C.Q.tr[t];
+  const int n = L.S.n[t], cap = L.S.cap;
+  const double r = L.S.near_r;
+  double qq[NJ];
+  for (int j = 0; j < NJ; ++j) qq[j] = q[j];
+  double lc[K], hc[K];
+  int li[K], hi[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) { lc[k] = __builtin_inf(); li[k] = 0x7fffffff; hc[k] = -__builtin_inf(); hi[k] = -1; }
+  long long cnt = 0;
+  for (int i = threadIdx.x; i < n; i += BLOCK) {
+    double s = 0.0;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      double d = qq[j] - T.q[(size_t)j * cap + i];
+      s += d * d;
+    }
+    double dist = sqrt(s);
+    if (dist < r && i != excl) {
+      cnt++;
+      double c = T.cost[i];
+      if (ci_less(c, i, lc[K - 1], li[K - 1])) {
+        double cc = c;
+        int ii = i;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          bool sw = ci_less(cc, ii, lc[k], li[k]);
+          double tc = lc[k];
+          int ti = li[k];
+          lc[k] = sw ? cc : lc[k];
+          li[k] = sw ? ii : li[k];
+          cc = sw ? tc : cc;
+          ii = sw ? ti : ii;
+        }
+      }
+      if (ci_less(hc[K - 1], hi[K - 1], c, i)) {
+        double cc = c;
+        int ii = i;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          bool sw = ci_less(hc[k], hi[k], cc, ii);
+          double tc = hc[k];
+          int ti = hi[k];
+          hc[k] = sw ? cc : hc[k];
+          hi[k] = sw ? ii : hi[k];
+          cc = sw ? tc : cc;
+          ii = sw ? ti : ii;
+        }
+      }
+    }
+  }
+  // total count
+  for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
+  if (lane_id() == 0) L.wcount[wave_id()] = cnt;
+  __syncthreads();
+  long long total = 0;
+  for (int w = 0; w < BLOCK / 64; ++w) total += L.wcount[w];
+  const int take = (int)min((long long)K, total);
+  // merge: `take` rounds of block-wide min (lo) and max (hi) over list heads
+  for (int rnd = 0; rnd < take; ++rnd) {
+    double dl = lc[0], dh = hc[0];
+    int il = li[0], ih = hi[0];
+    for (int off = 32; off > 0; off >>= 1) {
+      double odl = __shfl_xor(dl, off), odh = __shfl_xor(dh, off);
+      int oil = __shfl_xor(il, off), oih = __shfl_xor(ih, off);
+      if (ci_less(odl, oil, dl, il)) { dl = odl; il = oil; }
+      if (ci_less(dh, ih, odh, oih)) { dh = odh; ih = oih; }
+    }
+    if (lane_id() == 0) { L.u.red.rd[wave_id()] = dl; L.u.red.ri[wave_id()] = il; L.u.red.rc2[wave_id()] = dh; L.u.red.ri2[wave_id()] = ih; }
+    __syncthreads();
+    dl = L.u.red.rd[0]; il = L.u.red.ri[0]; dh = L.u.red.rc2[0]; ih = L.u.red.ri2[0];
+    for (int w = 1; w < BLOCK / 64; ++w) {
+      if (ci_less(L.u.red.rd[w], L.u.red.ri[w], dl, il)) { dl = L.u.red.rd[w]; il = L.u.red.ri[w]; }
+      if (ci_less(dh, ih, L.u.red.rc2[w], L.u.red.ri2[w])) { dh = L.u.red.rc2[w]; ih = L.u.red.ri2[w]; }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) { L.lo_c[rnd] = dl; L.lo_i[rnd] = il; L.hi_c[take - 1 - rnd] = dh; L.hi_i[take - 1 - rnd] = ih; }
+    // pop the winners' heads (ids are unique: exactly one thread owns each)
+    if (li[0] == il) {
+#pragma unroll
+      for (int k = 0; k < K - 1; ++k) { lc[k] = lc[k + 1]; li[k] = li[k + 1]; }
+      lc[K - 1] = __builtin_inf(); li[K - 1] = 0x7fffffff;
+    }
+    if (hi[0] == ih) {
+#pragma unroll
+      for (int k = 0; k < K - 1; ++k) { hc[k] = hc[k + 1]; hi[k] = hi[k + 1]; }
+      hc[K - 1] = -__builtin_inf(); hi[K - 1] = -1;
+    }
+  }
+  if (threadIdx.x == 0) { L.nk = (int)total; L.n_lo = take; L.n_hi = take; }
+  __syncthreads();
+}
+
+// --------------------------------------------------------------------------------------- edges
+// connectNodesInterpolation + compute_edge_cost_interpolation (birrt_star.cpp:4380-4440, 4443-4526,
+// 4162-4242) for E <= MAXE edges eg_start -> eg_target, base costs eg_base.  Segment norms in parallel,
+// ordered sums per edge.  Fills eg_step, eg_end (the child configuration) and eg_cost.
+__device__ void edge_costs(const Ctx& C, PlanLds& L, int E) {
+  const int np = L.S.n_pts;
+  const RobotDev* rb = C.rb;
+  if (threadIdx.x < E * NJ) {
+    int e = threadIdx.x / NJ, j = threadIdx.x - e * NJ;
+    double st = (L.eg_target[e][j] - L.eg_start[e][j]) / double(np);
+    L.eg_step[e][j] = st;
+    L.eg_end[e][j] = L.eg_start[e][j] + np * st;
+  }
+  __syncthreads();
+  for (int it = threadIdx.x; it < E * np; it += BLOCK) {
+    int e = it / np, s = it - e * np;
+    double t = 0.0, r = 0.0, p = 0.0;
+    for (int j = 0; j < NJ; ++j) {
+      double a = L.eg_start[e][j] + s * L.eg_step[e][j];
+      double b = L.eg_start[e][j] + (s + 1) * L.eg_step[e][j];
+      double d = (b - a) * (b - a);
+      t += d * 1.0;
+      if (rb->rev[j]) r += d; else p += d;
+    }
+    L.u.seg[e][s][0] = sqrt(t);
+    L.u.seg[e][s][1] = sqrt(r);
+    L.u.seg[e][s][2] = sqrt(p);
+  }
+  __syncthreads();
+  if (threadIdx.x < E * 3) {
+    int e = threadIdx.x / 3, k = threadIdx.x - e * 3;
+    double acc = 0.0;
+    for (int s = 0; s < np; ++s) acc += L.u.seg[e][s][k];
+    L.eg_cost[e][k] = L.eg_base[e][k] + acc;
+  }
+  __syncthreads();
+}
+
+// isEdgeValid for the edges with eg_need[e] set: eg_first[e] = first colliding configuration index, or
+// n_pts + 1 if the whole edge is free.  Configurations of all needed edges are flattened into 32-wide tiles.
+__device__ void edge_validity(const Ctx& C, PlanLds& L, int E) {
+  const int np1 = L.S.n_pts + 1;
+  if (threadIdx.x < E) L.eg_first[threadIdx.x] = np1;
+  __syncthreads();
+  const int total = E * np1;
+  for (int base = 0; base < total; base += 32) {
+    // map tile slot -> (edge, point); skip edges not needed (their slots stay idle)
+    int nc = min(32, total - base);
+    if (threadIdx.x < nc * NJ) {
+      int c = threadIdx.x / NJ, j = threadIdx.x - c * NJ;
+      int f = base + c, e = f / np1, i = f - e * np1;
+      L.u.tile.tq[c][j] = L.eg_start[e][j] + i * L.eg_step[e][j];
+    }
+    // skip whole tile if no needed edge intersects it
+    int any = 0;
+    for (int c = 0; c < nc; ++c) any |= L.eg_need[(base + c) / np1];
+    if (!any) continue;
+    __syncthreads();
+    collide_tile<32>(C.rb, C.sc, C.mc, nc, L.u.tile.tq, L.S.self, L.S.map, L.u.tile.T);
+    if (threadIdx.x < nc) {
+      int f = base + threadIdx.x, e = f / np1, i = f - e * np1;
+      if (L.eg_need[e] && L.u.tile.T.coll[threadIdx.x]) atomicMin(&L.eg_first[e], i);
+    }
+    __syncthreads();
+  }
+  __syncthreads();
+}
+
+// Reference-semantics accounting of one isEdgeValid call (stops at the first collision).
+__device__ __forceinline__ void count_edge(PlanLds& L, int first) {
+  int np1 = L.S.n_pts + 1;
+  if (first >= np1) { L.S.checked += np1; L.S.valid += np1; }
+  else { L.S.checked += first + 1; L.S.valid += first; }
+}
+
+// stepTowardsRandSample (birrt_star.cpp:5712-5868), single lane.
+__device__ bool step_towards(const RobotDev* rb, const double* nn, double* x, double f) {
+  double ed[NJ], srev = 0.0, spr = 0.0;
+  for (int j = 0; j < NJ; ++j) {
+    ed[j] = x[j] - nn[j];
+    double d = ed[j] * ed[j];
+    if (rb->rev[j]) srev += d; else spr += d;
+  }
+  double lrev = sqrt(srev), lpr = sqrt(spr);
+  bool rev_done = lrev < 0.001, pr_done = lpr < 0.001;
+  double ext[NJ];
+  srev = 0.0; spr = 0.0;
+  for (int j = 0; j < NJ; ++j) {
+    ext[j] = 0.0;
+    if (!rb->rev[j]) {
+      if (!pr_done) { ed[j] = ed[j] / lpr; double c = f * ed[j]; ext[j] = nn[j] + c; spr += c * c; }
+    } else {
+      if (!rev_done) { ed[j] = ed[j] / lrev; double c = f * ed[j]; ext[j] = nn[j] + c; srev += c * c; }
+    }
+  }
+  double elp = spr == 0.0 ? 1000.0 : sqrt(spr);
+  double elr = srev == 0.0 ? 1000.0 : sqrt(srev);
+  bool reached = true;
+  if (elr < lrev) { for (int j = 0; j < NJ; ++j) if (rb->rev[j]) x[j] = ext[j]; reached = false; }
+  if (elp < lpr) { for (int j = 0; j < NJ; ++j) if (!rb->rev[j]) x[j] = ext[j]; reached = false; }
+  return reached;
+}
+
+// Stepping loop shared by choose_parent / connectGraphs: from `cur` towards `target` with
+// unconstraint_extend_step_factor, collecting via nodes (ids nn_t, nn_t+1, ...) until the target is
+// reached; the last edge becomes `sel` (id nn_t at that point).  No collision checks (reference behaviour).
+__device__ void via_chain(const Ctx& C, PlanLds& L, const double* target) {
+  for (;;) {
+    if (threadIdx.x == 0) {
+      for (int j = 0; j < NJ; ++j) L.ox[j] = target[j];
+      L.reached = step_towards(C.rb, L.cur.q, L.ox, L.S.step) ? 1 : 0;
+      for (int j = 0; j < NJ; ++j) { L.eg_start[0][j] = L.cur.q[j]; L.eg_target[0][j] = L.ox[j]; }
+      for (int k = 0; k < 3; ++k) L.eg_base[0][k] = L.cur.c[k];
+    }
+    __syncthreads();
+    edge_costs(C, L, 1);
+    if (threadIdx.x == 0) {
+      NodeRef g;
+      for (int j = 0; j < NJ; ++j) g.q[j] = L.eg_end[0][j];
+      for (int k = 0; k < 3; ++k) g.c[k] = L.eg_cost[0][k];
+      g.parent = L.cur.id;
+      if (!L.reached) {
+        g.id = L.nn_t++;
+        if (L.n_via >= L.S.via_cap) { L.S.status = -7; L.S.phase = 2; L.reached = 1; }
+        else {
+          ViaNode& v = C.Q.via[L.n_via++];
+          for (int j = 0; j < NJ; ++j) { v.q[j] = g.q[j]; v.e_start[j] = L.cur.q[j]; v.e_target[j] = L.ox[j]; }
+          for (int k = 0; k < 3; ++k) v.c[k] = g.c[k];
+          v.id = g.id;
+          v.parent = g.parent;
+        }
+        L.cur = g;
+      } else {
+        g.id = L.nn_t;
+        L.sel = g;
+        for (int j = 0; j < NJ; ++j) { L.sel_start[j] = L.cur.q[j]; L.sel_target[j] = L.ox[j]; }
+      }
+    }
+    __syncthreads();
+    if (L.reached) break;
+  }
+}
+
+__device__ void insert_via(const Ctx& C, PlanLds& L, int t) {
+  if (threadIdx.x == 0) {
+    for (int v = 0; v < L.n_via && L.S.status == 0; ++v) {
+      const ViaNode& w = C.Q.via[v];
+      NodeRef x;
+      for (int j = 0; j < NJ; ++j) x.q[j] = w.q[j];
+      for (int k = 0; k < 3; ++k) x.c[k] = w.c[k];
+      x.id = w.id;
+      x.parent = w.parent;
+      insert_node(C, L, t, w.e_start, w.e_target, x);
+    }
+    L.n_via = 0;
+  }
+  __syncthreads();
+}
+
+// --------------------------------------------------------------------------------------- sampling
+// getRandomConf (control_laws.cpp:1120-1188): draws in chain order until the EE z >= 0.  One lane per
+// inner attempt; the first valid attempt (lowest index) wins.  Used for outer attempt `outer`.
+__device__ void rand_conf_lane(const Ctx& C, const QState& S, uint32_t outer, uint32_t inner, double* q) {
+  const RobotDev* rb = C.rb;
+  bool env0 = S.env_x[0] == 0.0 && S.env_x[1] == 0.0 && S.env_y[0] == 0.0 && S.env_y[1] == 0.0;
+  for (int j = 0; j < NJ; ++j) {
+    double lo = rb->q_min[j], hi = rb->q_max[j];
+    if (!env0 && j == 0) { lo = S.env_x[0]; hi = S.env_x[1]; }
+    if (!env0 && j == 1) { lo = S.env_y[0]; hi = S.env_y[1]; }
+    double u = u01(S.seed, S.query, (uint32_t)S.iter, outer, inner, j);
+    q[j] = u * (hi - lo) + lo;
+  }
+}
+
+// sampleJointConfig_JntArray (birrt_star.cpp:3832-3878) -> L.xr; wave 0 tries 64 attempts at once.
+__device__ void sample_uniform(const Ctx& C, PlanLds& L) {
+  if (wave_id() == 0) {
+    for (uint32_t base = 0;; base += 64) {
+      if (base >= (1u << 24)) {  // no valid sample in 16M attempts: give up loudly
+        if (lane_id() == 0) { L.S.status = -1; L.S.phase = 2; }
+        break;
+      }
+      double q[NJ];
+      rand_conf_lane(C, L.S, 0, base + lane_id(), q);
+      bool ok = 0.0 <= ee_z(C.rb, q);
+      unsigned long long m = __ballot(ok);
+      if (m) {
+        int w = __ffsll((long long)m) - 1;
+        if (lane_id() == w) for (int j = 0; j < NJ; ++j) L.xr[j] = q[j];
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// sampleJointConfigfromEllipse_JntArray (birrt_star.cpp:3607-3829); lane = outer attempt b, inner
+// getRandomConf attempts run serially per lane; the lowest valid b wins.
+__device__ void sample_ellipse(const Ctx& C, PlanLds& L) {
+  const RobotDev* rb = C.rb;
+  const QState& S = L.S;
+  if (wave_id() == 0) {
+    bool env0 = S.env_x[0] == 0.0 && S.env_x[1] == 0.0 && S.env_y[0] == 0.0 && S.env_y[1] == 0.0;
+    for (uint32_t base = 0;; base += 64) {
+      if (base >= (1u << 20)) {
+        if (lane_id() == 0) { L.S.status = -1; L.S.phase = 2; }
+        break;
+      }
+      uint32_t b = base + lane_id();
+      double q[NJ];
+      for (uint32_t inner = 0; inner < (1u << 16); ++inner) {
+        rand_conf_lane(C, S, 1 + b, inner, q);
+        if (0.0 <= ee_z(rb, q)) break;
+      }
+      double br[6], bp[2], sr = 0.0, sp = 0.0;
+      int ir = 0, ip = 0;
+      for (int j = 0; j < NJ; ++j) { if (rb->rev[j]) br[ir++] = q[j]; else bp[ip++] = q[j]; }
+      for (int i = 0; i < 6; ++i) sr += br[i] * br[i];
+      for (int i = 0; i < 2; ++i) sp += bp[i] * bp[i];
+      double nr = sqrt(sr), npn = sqrt(sp);
+      double ps = u01(S.seed, S.query, (uint32_t)S.iter, 1 + b, 0, 8);
+      for (int i = 0; i < 6; ++i) br[i] = ps * (br[i] / nr);
+      for (int i = 0; i < 2; ++i) bp[i] = ps * (bp[i] / npn);
+      double srev = sqrt(S.cbest[1] * S.cbest[1] - S.h0[1] * S.h0[1]) / 2.0;
+      double spr = sqrt(S.cbest[2] * S.cbest[2] - S.h0[2] * S.h0[2]) / 2.0;
+      double lr[6], lp[2];
+      for (int i = 0; i < 6; ++i) lr[i] = i == 0 ? S.cbest[1] / 2.0 : srev;
+      for (int i = 0; i < 2; ++i) lp[i] = i == 0 ? S.cbest[2] / 2.0 : spr;
+      double r[NJ];
+      ir = 0; ip = 0;
+      double rr[6], rp[2];
+      for (int i = 0; i < 6; ++i) {
+        double s = 0.0;
+        for (int k = 0; k < 6; ++k) s += (S.Crev[i * 6 + k] * lr[k]) * br[k];
+        rr[i] = s + S.ctr_rev[i];
+      }
+      for (int i = 0; i < 2; ++i) {
+        double s = 0.0;
+        for (int k = 0; k < 2; ++k) s += (S.Cpr[i * 2 + k] * lp[k]) * bp[k];
+        rp[i] = s + S.ctr_pr[i];
+      }
+      for (int j = 0; j < NJ; ++j) r[j] = rb->rev[j] ? rr[ir++] : rp[ip++];
+      bool above = 0.0 <= ee_z(rb, r);
+      bool inside = (r[0] < S.env_x[1] && r[0] > S.env_x[0] && r[1] < S.env_y[1] && r[1] > S.env_y[0]) || env0;
+      unsigned long long m = __ballot(above && inside);
+      if (m) {
+        int w = __ffsll((long long)m) - 1;
+        if (lane_id() == w) for (int j = 0; j < NJ; ++j) L.xr[j] = r[j];
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// --------------------------------------------------------------------------------------- tree updates
+// recursiveNodeCostUpdate (birrt_star.cpp:5495-5606): subtree walk over child lists, single lane.
+__device__ void cost_update(const Ctx& C, PlanLds& L, int t, int v, const double* red) {
+  QState& S = L.S;
+  const TreeDev& T = C.Q.tr[t];
+  const int cap = S.cap;
+  int* stack = C.Q.stack;
+  int sp = 0;
+  stack[sp++] = v;
+  const bool connected = (t == 0) == (S.conn_start != 0);
+  int visits = 0;
+  while (sp > 0) {
+    if (++visits > S.n[t]) { S.status = -7; S.phase = 2; return; }  // a loop in the tree: fail loudly
+    int id = stack[--sp];
+    double nc[3];
+    for (int k = 0; k < 3; ++k) { nc[k] = T.cost[(size_t)k * cap + id] + red[k]; T.cost[(size_t)k * cap + id] = nc[k]; }
+    if (S.have_sol) {
+      if (id == S.nB.id && connected) {
+        for (int k = 0; k < 3; ++k) { S.cbest[k] = S.cbest[k] + red[k]; S.nB.c[k] = nc[k]; }
+        S.last_iter = S.iter;
+      }
+      if (id == S.nA.id && !connected) {
+        for (int k = 0; k < 3; ++k) { S.cbest[k] = S.cbest[k] + red[k]; S.nA.c[k] = nc[k]; }
+        S.last_iter = S.iter;
+      }
+    }
+    for (int c = T.first_child[id]; c >= 0; c = T.next_sib[c]) {
+      if (sp >= cap) { S.status = -7; S.phase = 2; return; }
+      stack[sp++] = c;
+    }
+  }
+}
+
+// choose_node_parent_interpolation, unconstrained (birrt_star.cpp:4594-4738, 4916-4935).
+// Uses L.lo_* (near list prefix) and L.xn / L.nn; may update L.xn, L.en_*; returns via L.ext_bp.
+__device__ void choose_parent(const Ctx& C, PlanLds& L, int t) {
+  if (threadIdx.x == 0) {
+    L.ext_bp = 0;
+    L.found = -1;
+    L.cnt = 0;
+    if (L.nk > 0) {
+      L.xn.parent = L.nn.id;
+      // candidate prefix: stop at the first near node whose cost is not below x_new's
+      int m = min(L.n_lo, L.S.max_near);
+      int E = 0;
+      for (int i = 0; i < m; ++i) {
+        if (!(L.lo_c[i] < L.xn.c[0])) break;
+        E++;
+      }
+      L.cnt = E;
+    }
+  }
+  __syncthreads();
+  const int E = L.cnt;
+  if (E > 0) {
+    if (threadIdx.x < E) {
+      int e = threadIdx.x;
+      NodeRef nd;
+      load_node(C, t, L.lo_i[e], &nd);
+      for (int j = 0; j < NJ; ++j) { L.eg_start[e][j] = nd.q[j]; L.eg_target[e][j] = L.xn.q[j]; }
+      for (int k = 0; k < 3; ++k) L.eg_base[e][k] = nd.c[k];
+      L.eg_near[e] = nd.id;
+    }
+    __syncthreads();
+    edge_costs(C, L, E);
+    if (threadIdx.x < E) L.eg_need[threadIdx.x] = L.eg_cost[threadIdx.x][0] <= L.xn.c[0];
+    for (int e = E + threadIdx.x; e < MAXE; e += BLOCK) L.eg_need[e] = 0;
+    __syncthreads();
+    edge_validity(C, L, E);
+    if (threadIdx.x == 0) {
+      for (int e = 0; e < E; ++e) {
+        if (!L.eg_need[e]) continue;
+        count_edge(L, L.eg_first[e]);
+        if (L.eg_first[e] > L.S.n_pts) { L.found = e; break; }
+      }
+      if (L.found >= 0) {
+        L.ext_bp = 1;
+        L.n_via = 0;
+        L.nn_t = L.S.n[t];
+        load_node(C, t, L.eg_near[L.found], &L.cur);
+      }
+    }
+    __syncthreads();
+    if (L.found >= 0) {
+      via_chain(C, L, L.xn.q);
+      if (threadIdx.x == 0) {
+        // x_new <- last stepped edge (birrt_star.cpp:4692-4711)
+        L.xn.id = L.sel.id;
+        L.xn.parent = L.sel.parent;
+        for (int j = 0; j < NJ; ++j) L.xn.q[j] = L.sel.q[j];
+        for (int k = 0; k < 3; ++k) L.xn.c[k] = L.sel.c[k];
+        for (int j = 0; j < NJ; ++j) { L.en_start[j] = L.sel_start[j]; L.en_target[j] = L.sel_target[j]; }
+      }
+      __syncthreads();
+      insert_via(C, L, t);
+    }
+  }
+  __syncthreads();
+}
+
+// rewireTreeInterpolation, unconstrained (birrt_star.cpp:5056-5230).  Validity of every candidate edge
+// x_new -> near is independent of the tree state, so all are checked at once; commits stay sequential.
+__device__ void rewire(const Ctx& C, PlanLds& L, int t) {
+  const int cap = L.S.cap;
+  const TreeDev& T = C.Q.tr[t];
+  if (threadIdx.x == 0) {
+    int n = L.nk;
+    int lower = n >= L.S.max_near ? n - L.S.max_near : 0;
+    int cnt = 0;
+    // L.hi_* holds positions n-n_hi .. n-1 in ascending order
+    for (int k = n - 1; k >= lower; --k) {
+      int pos = k - (n - L.n_hi);
+      if (L.xn.c[0] < T.cost[L.hi_i[pos]]) cnt++;
+    }
+    L.cnt = cnt;
+  }
+  __syncthreads();
+  const int cnt = L.cnt;
+  if (cnt == 0) return;
+  // candidates k = n-1 .. n-cnt  ->  edge slot e = n-1-k
+  if (threadIdx.x < cnt) {
+    int e = threadIdx.x;
+    int pos = L.n_hi - 1 - e;
+    int v = L.hi_i[pos];
+    NodeRef nd;
+    load_node(C, t, v, &nd);
+    for (int j = 0; j < NJ; ++j) { L.eg_start[e][j] = L.xn.q[j]; L.eg_target[e][j] = nd.q[j]; }
+    for (int k = 0; k < 3; ++k) L.eg_base[e][k] = L.xn.c[k];
+    L.eg_near[e] = v;
+  }
+  __syncthreads();
+  edge_costs(C, L, cnt);
+  if (threadIdx.x < cnt) {
+    int e = threadIdx.x, v = L.eg_near[e];
+    // costs only decrease during the loop, so a candidate failing against the current cost never passes
+    L.eg_need[e] = (v != L.xn.parent) && (T.parent[v] != 0) && (L.eg_cost[e][0] < T.cost[v]);
+  }
+  for (int e = cnt + threadIdx.x; e < MAXE; e += BLOCK) L.eg_need[e] = 0;
+  __syncthreads();
+  edge_validity(C, L, cnt);
+  if (threadIdx.x == 0) {
+    QState& S = L.S;
+    for (int e = 0; e < cnt && S.status == 0; ++e) {
+      int v = L.eg_near[e];
+      if (!(v != L.xn.parent && T.parent[v] != 0)) continue;
+      double cv[3];
+      for (int k = 0; k < 3; ++k) cv[k] = T.cost[(size_t)k * cap + v];
+      if (!(L.eg_cost[e][0] < cv[0])) continue;
+      count_edge(L, L.eg_first[e]);
+      if (L.eg_first[e] <= S.n_pts) continue;
+      double red[3];
+      for (int k = 0; k < 3; ++k) red[k] = L.eg_cost[e][k] - cv[k];
+      // unlink from the old parent (the reference erases the outgoing edge, birrt_star.cpp:5124-5169)
+      int p = T.parent[v];
+      int pv = T.prev_sib[v], nx = T.next_sib[v];
+      if (pv >= 0) T.next_sib[pv] = nx; else T.first_child[p] = nx;
+      if (nx >= 0) T.prev_sib[nx] = pv;
+      S.edges[t]--;
+      T.parent[v] = L.xn.id;
+      if (S.have_sol) {
+        bool connected = (t == 0) == (S.conn_start != 0);
+        if (v == S.nB.id && connected) S.nB.parent = L.xn.id;
+        else if (v == S.nA.id && !connected) S.nA.parent = L.xn.id;
+      }
+      for (int j = 0; j < NJ; ++j) {
+        T.q[(size_t)j * cap + v] = L.eg_end[e][j];
+        T.e_start[(size_t)j * cap + v] = L.eg_start[e][j];
+        T.e_target[(size_t)j * cap + v] = L.eg_target[e][j];
+      }
+      int f = T.first_child[L.xn.id];
+      T.next_sib[v] = f;
+      T.prev_sib[v] = -1;
+      if (f >= 0) T.prev_sib[f] = v;
+      T.first_child[L.xn.id] = v;
+      cost_update(C, L, t, v, red);
+      S.edges[t]++;
+      S.rewires[t]++;
+    }
+  }
+  __syncthreads();
+}
+
+// connectGraphsInterpolation, unconstrained branch + commit (birrt_star.cpp:2608-3046, 3219-3288).
+// t = tree_B; L.xc = its nearest node to x_new; L.xn = x_new (node of the other tree).
+__device__ void connect_graphs(const Ctx& C, PlanLds& L, int t) {
+  if (threadIdx.x == 0) {
+    L.tree_expand = 0;
+    L.best_nv = 10000.0;
+    L.n_via = 0;
+    for (int k = 0; k < 3; ++k) L.csp[k] = L.S.cbest[k];
+    for (int j = 0; j < NJ; ++j) { L.eg_start[0][j] = L.xc.q[j]; L.eg_target[0][j] = L.xn.q[j]; }
+    for (int k = 0; k < 3; ++k) L.eg_base[0][k] = L.xc.c[k];
+    L.sel.id = -1;
+  }
+  __syncthreads();
+  edge_costs(C, L, 1);
+  if (threadIdx.x == 0) {
+    for (int k = 0; k < 3; ++k) L.sol[k] = L.eg_cost[0][k] + L.xn.c[k];
+    L.eg_need[0] = L.sol[0] < L.csp[0];
+  }
+  __syncthreads();
+  if (L.eg_need[0]) {
+    edge_validity(C, L, 1);
+    if (threadIdx.x == 0) {
+      int f = L.eg_first[0];
+      count_edge(L, f);
+      L.flag = 0;
+      if (f > L.S.n_pts) {  // valid: connect, stepping without collision checks
+        for (int k = 0; k < 3; ++k) L.csp[k] = L.sol[k];
+        L.flag = 1;
+      } else {
+        int lv = f == 0 ? 0 : f - 1;
+        if (lv != 0) {  // extend towards the last valid configuration
+          for (int j = 0; j < NJ; ++j) L.ext[j] = L.eg_start[0][j] + lv * L.eg_step[0][j];
+          L.flag = 2;
+        }
+      }
+      L.nn_t = L.S.n[t];
+      L.cur = L.xc;
+    }
+    __syncthreads();
+    if (L.flag == 1) {
+      via_chain(C, L, L.xn.q);
+      if (threadIdx.x == 0) L.tree_expand = 0;
+    } else if (L.flag == 2) {
+      via_chain(C, L, L.ext);
+      if (threadIdx.x == 0) { L.tree_expand = 1; L.best_nv = L.sol[0]; }
+    }
+    __syncthreads();
+  }
+  if (L.S.have_sol) {
+    near_set<20>(C, L, t, L.xn.q, L.xn.id);
+    if (threadIdx.x == 0) {
+      int m = min(L.n_lo, L.S.max_near);
+      L.cnt = m;
+    }
+    __syncthreads();
+    const int E = L.cnt;
+    if (E > 0) {
+      if (threadIdx.x < E) {
+        int e = threadIdx.x;
+        NodeRef nd;
+        load_node(C, t, L.lo_i[e], &nd);
+        for (int j = 0; j < NJ; ++j) { L.eg_start[e][j] = nd.q[j]; L.eg_target[e][j] = L.xn.q[j]; }
+        for (int k = 0; k < 3; ++k) L.eg_base[e][k] = nd.c[k];
+        L.eg_near[e] = nd.id;
+      }
+      __syncthreads();
+      edge_costs(C, L, E);
+      if (threadIdx.x < E) {
+        int e = threadIdx.x;
+        double s0 = L.eg_cost[e][0] + L.xn.c[0];
+        L.eg_need[e] = (L.lo_c[e] < L.xn.c[0]) && (s0 < L.csp[0]);
+      }
+      for (int e = E + threadIdx.x; e < MAXE; e += BLOCK) L.eg_need[e] = 0;
+      __syncthreads();
+      edge_validity(C, L, E);
+      // sequential replay of the near loop (birrt_star.cpp:2820-3030)
+      for (int e = 0; e < E; ++e) {
+        if (threadIdx.x == 0) {
+          L.flag = 0;
+          if (L.eg_need[e]) {
+            double sol0 = L.eg_cost[e][0] + L.xn.c[0];
+            double sol1 = L.eg_cost[e][1] + L.xn.c[1];
+            double sol2 = L.eg_cost[e][2] + L.xn.c[2];
+            int f = L.eg_first[e];
+            count_edge(L, f);
+            if (f > L.S.n_pts) {
+              L.csp[0] = sol0; L.csp[1] = sol1; L.csp[2] = sol2;
+              L.flag = 1;
+            } else if (L.csp[0] == L.S.cbest[0] && sol0 < L.best_nv) {
+              int lv = f == 0 ? 0 : f - 1;
+              if (lv != 0) {
+                for (int j = 0; j < NJ; ++j) L.ext[j] = L.eg_start[e][j] + lv * L.eg_step[e][j];
+                L.flag = 2;
+                L.sol[0] = sol0;
+              }
+            }
+            if (L.flag) {
+              L.n_via = 0;
+              L.nn_t = L.S.n[t];
+              load_node(C, t, L.eg_near[e], &L.cur);
+            }
+          }
+        }
+        __syncthreads();
+        if (L.flag == 1) {
+          via_chain(C, L, L.xn.q);
+          if (threadIdx.x == 0) L.tree_expand = 0;
+          __syncthreads();
+          break;
+        } else if (L.flag == 2) {
+          via_chain(C, L, L.ext);
+          if (threadIdx.x == 0) { L.tree_expand = 1; L.best_nv = L.sol[0]; }
+          __syncthreads();
+        }
+      }
+    }
+  }
+  insert_via(C, L, t);
+  if (threadIdx.x == 0) {
+    QState& S = L.S;
+    if (L.csp[0] < S.cbest[0]) {
+      if (!S.have_sol) {
+        S.first_iter = S.iter;
+        S.t_first = wall_clock64();
+      }
+      S.have_sol = 1;
+      insert_node(C, L, t, L.sel_start, L.sel_target, L.sel);
+      S.conn_start = (t == 0);
+      S.nB = L.sel;
+      S.nA = L.xn;
+      for (int k = 0; k < 3; ++k) S.cbest[k] = L.csp[k];
+      S.last_iter = S.iter;
+    } else if (L.tree_expand) {
+      insert_node(C, L, t, L.sel_start, L.sel_target, L.sel);
+    }
+  }
+  __syncthreads();
+}
+
+// One C-space iteration of run_planner (birrt_star.cpp:1163-1338).
+__device__ void iteration(const Ctx& C, PlanLds& L) {
+  const int A = L.S.A, B = 1 - A;
+  if (L.S.informed && L.S.have_sol) sample_ellipse(C, L); else sample_uniform(C, L);
+  int nid = nearest(C, L, A, L.xr);
+  if (threadIdx.x == 0) {
+    load_node(C, A, nid, &L.nn);
+    // expandTree single step (birrt_star.cpp:2224-2256)
+    for (int j = 0; j < NJ; ++j) L.ext[j] = L.xr[j];
+    step_towards(C.rb, L.nn.q, L.ext, L.S.step);
+    for (int j = 0; j < NJ; ++j) { L.eg_start[0][j] = L.nn.q[j]; L.eg_target[0][j] = L.ext[j]; }
+    for (int k = 0; k < 3; ++k) L.eg_base[0][k] = L.nn.c[k];
+    L.eg_need[0] = 1;
+  }
+  __syncthreads();
+  edge_costs(C, L, 1);
+  edge_validity(C, L, 1);
+  if (threadIdx.x == 0) {
+    int f = L.eg_first[0];
+    count_edge(L, f);
+    L.ext_nn = f > L.S.n_pts;
+    if (L.ext_nn) {
+      for (int j = 0; j < NJ; ++j) { L.xn.q[j] = L.eg_end[0][j]; L.en_start[j] = L.eg_start[0][j]; L.en_target[j] = L.eg_target[0][j]; }
+      for (int k = 0; k < 3; ++k) L.xn.c[k] = L.eg_cost[0][k];
+      L.xn.id = L.S.n[A];
+      L.xn.parent = L.nn.id;
+    } else {  // x_new = x_rand with cost 10000 (birrt_star.cpp:1213-1217, 2252-2255)
+      for (int j = 0; j < NJ; ++j) L.xn.q[j] = L.xr[j];
+      L.xn.c[0] = 10000.0; L.xn.c[1] = 0.0; L.xn.c[2] = 0.0;
+      L.xn.id = L.S.n[A];
+      L.xn.parent = L.nn.id;
+    }
+    L.ext_bp = 0;
+    L.nk = 0;
+  }
+  __syncthreads();
+  const bool opt = L.S.tree_opt && L.S.have_sol;
+  if (opt) {
+    near_set<20>(C, L, A, L.xn.q, L.xn.id);
+    choose_parent(C, L, A);
+  }
+  if (L.ext_nn || L.ext_bp) {
+    if (threadIdx.x == 0) insert_node(C, L, A, L.en_start, L.en_target, L.xn);
+    __syncthreads();
+    if (opt) rewire(C, L, A);
+    int cid = nearest(C, L, B, L.xn.q);
+    if (threadIdx.x == 0) load_node(C, B, cid, &L.xc);
+    __syncthreads();
+    connect_graphs(C, L, B);
+  }
+  if (threadIdx.x == 0) {
+    QState& S = L.S;
+    S.A = B;
+    S.iter++;
+    if (C.Q.rows && S.n_rows < C.Q.rows_cap) {
+      double* row = C.Q.rows + S.n_rows * 5;
+      row[0] = (double)S.iter;
+      row[1] = (double)(wall_clock64() - S.t0);
+      row[2] = S.cbest[0]; row[3] = S.cbest[1]; row[4] = S.cbest[2];
+      S.n_rows++;
+    }
+    if ((S.cbest[0] - S.h0[0]) < S.opt_thresh) S.phase = 2;  // birrt_star.cpp:1333-1338
+    if (S.iter >= S.max_iter) S.phase = 2;
+    if (S.deadline && wall_clock64() >= S.deadline) S.phase = 2;
+  }
+  __syncthreads();
+}
+
+// Advances every query (one workgroup each) by at most `iters` planner iterations.
+__global__ void __launch_bounds__(BLOCK) plan_kernel(const RobotDev* __restrict__ rb, SceneDev sc,
+                                                     const MapCfg* __restrict__ mc, QueryDev* qs, int iters) {
+  __shared__ PlanLds L;
+  Ctx C;
+  C.rb = rb;
+  C.sc = sc;
+  C.mc = mc;
+  C.Q = qs[blockIdx.x];
+  if (threadIdx.x == 0) {
+    L.S = *C.Q.st;
+    if (L.S.phase == 0 && L.S.t0 == 0) L.S.t0 = wall_clock64();
+    L.n_via = 0;
+  }
+  __syncthreads();
+  if (L.S.status == 0 && L.S.phase == 0) {
+    // pre-loop direct connection of the two roots (birrt_star.cpp:1072-1075)
+    if (threadIdx.x == 0) {
+      load_node(C, 1, 0, &L.xn);
+      load_node(C, 0, 0, &L.xc);
+    }
+    __syncthreads();
+    connect_graphs(C, L, 0);
+    if (threadIdx.x == 0) L.S.phase = L.S.have_sol ? 2 : 1;
+    __syncthreads();
+  }
+  for (int k = 0; k < iters; ++k) {
+    if (L.S.status != 0 || L.S.phase != 1) break;
+    iteration(C, L);
+  }
+  if (threadIdx.x == 0) {
+    if (L.S.phase == 2 && L.S.t_end == 0) L.S.t_end = wall_clock64();
+    *C.Q.st = L.S;
+  }
+}
+
+// computeFinalSolutionPathTrajectories (birrt_star.cpp:6173-6274): the node chains of both trees, root
+// first for the start tree and connection first for the goal tree.  out[0] = n_start, out[1] = n_goal.
+__global__ void path_kernel(QueryDev* qs, int* counts) {
+  QueryDev Q = qs[blockIdx.x];
+  if (threadIdx.x != 0) return;
+  const QState& S = *Q.st;
+  int cap = S.cap;
+  int* ps = Q.path_nodes;
+  int* pg = Q.path_nodes + cap;
+  int ns = 0, ng = 0;
+  if (S.have_sol) {
+    int s_id = S.conn_start ? S.nB.id : S.nA.id, s_par = S.conn_start ? S.nB.parent : S.nA.parent;
+    int g_id = S.conn_start ? S.nA.id : S.nB.id, g_par = S.conn_start ? S.nA.parent : S.nB.parent;
+    while (s_id != 0 && ns < cap) { ps[ns++] = s_id; s_id = s_par; s_par = Q.tr[0].parent[s_id]; }
+    while (g_id != 0 && ng < cap) { pg[ng++] = g_id; g_id = g_par; g_par = Q.tr[1].parent[g_id]; }
+    for (int i = 0; i < ns / 2; ++i) { int t = ps[i]; ps[i] = ps[ns - 1 - i]; ps[ns - 1 - i] = t; }
+  }
+  counts[blockIdx.x * 2] = ns;
+  counts[blockIdx.x * 2 + 1] = ng;
+}
+
+}  // namespace smp

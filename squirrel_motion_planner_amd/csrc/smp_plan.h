@@ -1,0 +1,71 @@
+// Device-resident BiRRT* planner state (one workgroup per query).  Shared by smp_kernels.hip and the host.
+#pragma once
+#include <stdint.h>
+
+#include "smp_types.h"
+
+namespace smp {
+
+constexpr int MAX_PTS = 32;    // num_traj_segments_interp upper bound (reference default 20)
+constexpr int MAX_NEAR = 32;   // max_near_nodes upper bound (reference default 20)
+constexpr int MAXE = 24;       // edges per validity / cost batch
+
+struct NodeRef {               // what the reference passes by value (Node, data_structs.h:29-45)
+  double q[NJ];
+  double c[3];                 // cost_reach total, revolute, prismatic
+  int id;
+  int parent;
+};
+
+struct TreeDev {               // SoA node arrays of one tree; capacity `cap`
+  double* q;                   // [NJ][cap]
+  double* cost;                // [3][cap]
+  int* parent;
+  int* first_child;
+  int* next_sib;
+  int* prev_sib;
+  double* e_start;             // [NJ][cap] in-edge: interpolation start (parent config at creation)
+  double* e_target;            // [NJ][cap] in-edge: interpolation target
+};
+
+struct QState {                // per query, persisted in global memory across launches
+  int status;                  // 0 ok / running, negative SMP_ERR_*
+  int phase;                   // 0: pre-loop connect pending, 1: planning loop, 2: finished
+  int A;                       // tree acting as tree_A next iteration (0 start, 1 goal)
+  int have_sol, conn_start;
+  int n[2], edges[2], rewires[2];
+  int cap, via_cap;
+  long long iter, max_iter;
+  long long checked, valid, first_iter, last_iter;
+  unsigned long long t0, t_first, t_end, deadline;  // device wall clock (0 deadline = none)
+  double cbest[3], h0[3];
+  NodeRef nB, nA;              // m_node_tree_B / m_node_tree_A
+  double qs[NJ], qg[NJ];
+  double Crev[36], Cpr[4], ctr_rev[6], ctr_pr[2];
+  double env_x[2], env_y[2];
+  double near_r, step, opt_thresh;
+  int n_pts, max_near, tree_opt, informed, self, map;
+  unsigned long long seed;
+  unsigned query;
+  long long n_rows;
+};
+
+struct ViaNode {               // via node pending insertion (selected_via_nodes / edges)
+  double q[NJ];
+  double c[3];
+  double e_start[NJ];
+  double e_target[NJ];
+  int id, parent;
+};
+
+struct QueryDev {
+  QState* st;
+  TreeDev tr[2];
+  ViaNode* via;                // [via_cap]
+  int* stack;                  // [cap] DFS stack of recursiveNodeCostUpdate
+  double* rows;                // [max_iter][5] cost evolution rows (may be null)
+  long long rows_cap;
+  int* path_nodes;             // [2][cap] path extraction scratch
+};
+
+}  // namespace smp

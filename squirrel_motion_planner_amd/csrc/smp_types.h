@@ -1,0 +1,50 @@
+// Plain-old-data layouts shared by the host builder and the HIP kernels.
+#pragma once
+#include <stdint.h>
+
+namespace smp {
+
+constexpr int MAX_CHAIN = 16;   // body chain steps (11 for robotino)
+constexpr int MAX_SEG = 16;     // end-effector chain segments (12)
+constexpr int MAX_SPH = 72;     // collision spheres (64)
+constexpr int MAX_CLINK = 32;   // collision links (27)
+constexpr int MAX_PAIRS = 256;  // self-collision link pairs (165 non-rigid of the 230 SRDF-enabled)
+constexpr int MAX_BODY = 8;     // moving bodies (6)
+constexpr int NJ = 8;           // planning joints
+
+// Robot model (kinematics + sphere collision model).  Collision links are re-indexed into compact
+// "clink" slots; spheres are sorted by clink so each link owns a contiguous range.
+struct RobotDev {
+  int n_chain, n_seg, n_sph, n_clink, n_pairs, n_body;
+  double root_z;
+  int ch_type[MAX_CHAIN], ch_joint[MAX_CHAIN], ch_body[MAX_CHAIN];  // type: 0 fixed 1 revolute 2 prismatic
+  double ch_axis[MAX_CHAIN * 3], ch_origin[MAX_CHAIN * 3], ch_R[MAX_CHAIN * 9], ch_p[MAX_CHAIN * 3];
+  int seg_type[MAX_SEG], seg_joint[MAX_SEG];
+  double seg_axis[MAX_SEG * 3], seg_origin[MAX_SEG * 3], seg_R[MAX_SEG * 9], seg_p[MAX_SEG * 3];
+  int sph_body[MAX_SPH], sph_clink[MAX_SPH];
+  double sph_cb[MAX_SPH * 3], sph_r[MAX_SPH];
+  int cl_sph0[MAX_CLINK], cl_nsph[MAX_CLINK], cl_body[MAX_CLINK], cl_link[MAX_CLINK];
+  double cl_cb[MAX_CLINK * 3], cl_r[MAX_CLINK];
+  int pair_a[MAX_PAIRS], pair_b[MAX_PAIRS];
+  double q_min[NJ], q_max[NJ];
+  int rev[NJ];
+};
+
+// Occupancy grid of one scene (device pointers).  Cell (i,j,k) is the box
+// [o + i*res, o + (i+1)*res] per axis; bits are x-major rows of 64-bit words (bit i&63 of word i>>6);
+// d2 is the squared centre-to-centre distance (voxel units, clamped to 65535) to the nearest occupied cell.
+struct SceneDev {
+  int nx, ny, nz, wx;
+  double ox, oy, oz, res;
+  const uint64_t* bits;
+  const uint16_t* d2;
+};
+
+// Per (scene, disabled-link set) sphere constants.
+struct MapCfg {
+  uint32_t T[MAX_SPH];      // d2 prefilter threshold: free if d2 > T (r + sqrt(3) voxels)
+  int32_t map_on[MAX_SPH];  // 0 if the sphere's link is excluded from the map check
+  int32_t has_map;          // scene present
+};
+
+}  // namespace smp

@@ -1,0 +1,282 @@
+"""Host-side mirror of the reference planner interface, over the C ABI.
+
+`BiRRTstarPlanner` keeps the member names, argument meaning and bool/error behaviour of
+birrt_star_motion_planning::BiRRTstarPlanner (birrt_star.h:27-110) as the squirrel_8dof_planner node uses it
+(squirrel_8dof_planner.cpp:1221-1248): initialize, setOctree, setDisabledLinkMapCollisions,
+reset_planner_and_config, setPlanningSceneInfo, init_planner, run_planner, getJointTrajectoryRef,
+isConfigValid.  Every call lands in libsmp_gpu.so (HIP kernels on the GPU); nothing here computes planning
+or collision results on the CPU.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib as L
+from ._lib import check, lib
+
+_pd = ctypes.POINTER(ctypes.c_double)
+
+
+def default_params(**kw):
+    p = L.Params()
+    lib().smp_params_default(ctypes.byref(p))
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+class Robot:
+    """Robot model (KDL chain + sphere collision model) from the committed model JSON."""
+
+    def __init__(self, model_json=L.MODEL_JSON):
+        with open(model_json, "rb") as f:
+            text = f.read()
+        h = ctypes.c_void_p()
+        check(lib().smp_robot_create_json(text, ctypes.byref(h)), "smp_robot_create_json")
+        self.h = h
+
+    @property
+    def link_names(self):
+        n = lib().smp_robot_num_links(self.h)
+        return [lib().smp_robot_link_name(self.h, i).decode() for i in range(n)]
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().smp_robot_destroy(self.h)
+            self.h = None
+
+
+class Scene:
+    """Occupancy scene: octomap leaf keys (or a .bt stream) -> padded bitset + squared-EDT prefilter."""
+
+    def __init__(self, h):
+        self.h = h
+
+    @classmethod
+    def from_keys(cls, keys, res, z_offset=-0.02, floor_center=None, floor_distance=3.0):
+        keys = np.ascontiguousarray(np.asarray(keys).reshape(-1, 3), np.uint16)
+        o = L.SceneOpts()
+        lib().smp_scene_opts_default(ctypes.byref(o))
+        o.resolution = res
+        o.z_offset = z_offset
+        if floor_center is not None:
+            o.insert_floor = 1
+            o.floor_center[0], o.floor_center[1] = floor_center
+            o.floor_distance = floor_distance
+        h = ctypes.c_void_p()
+        check(lib().smp_scene_from_keys(keys.ctypes.data_as(ctypes.c_void_p), len(keys), ctypes.byref(o),
+                                        ctypes.byref(h)), "smp_scene_from_keys")
+        return cls(h)
+
+    @classmethod
+    def from_bt(cls, data, z_offset=-0.02, floor_center=None, floor_distance=3.0):
+        buf = ctypes.create_string_buffer(bytes(data), len(data))
+        o = L.SceneOpts()
+        lib().smp_scene_opts_default(ctypes.byref(o))
+        o.z_offset = z_offset
+        if floor_center is not None:
+            o.insert_floor = 1
+            o.floor_center[0], o.floor_center[1] = floor_center
+            o.floor_distance = floor_distance
+        h = ctypes.c_void_p()
+        check(lib().smp_scene_from_bt(buf, len(data), ctypes.byref(o), ctypes.byref(h)), "smp_scene_from_bt")
+        return cls(h)
+
+    def info(self):
+        dims = (ctypes.c_int * 3)()
+        org = (ctypes.c_double * 3)()
+        res = ctypes.c_double()
+        nocc = ctypes.c_int64()
+        bmin = (ctypes.c_double * 3)()
+        bmax = (ctypes.c_double * 3)()
+        check(lib().smp_scene_info(self.h, dims, org, ctypes.byref(res), ctypes.byref(nocc), bmin, bmax))
+        return dict(dims=tuple(dims), origin=tuple(org), res=res.value, n_occupied=nocc.value,
+                    bbox_min=tuple(bmin), bbox_max=tuple(bmax))
+
+    def export(self):
+        i = self.info()
+        nx, ny, nz = i["dims"]
+        wx = (nx + 63) // 64
+        bits = np.zeros(wx * ny * nz, np.uint64)
+        d2 = np.zeros(nx * ny * nz, np.uint16)
+        check(lib().smp_scene_export(self.h, bits.ctypes.data_as(ctypes.c_void_p), d2.ctypes.data_as(ctypes.c_void_p)))
+        return bits, d2
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().smp_scene_destroy(self.h)
+            self.h = None
+
+
+class GpuPlanner:
+    """Thin owner of an smp_planner (one GPU, one robot, one scene at a time)."""
+
+    def __init__(self, robot=None, device=0, **params):
+        self.robot = robot or Robot()
+        self.params = default_params(**params)
+        h = ctypes.c_void_p()
+        check(lib().smp_planner_create(device, self.robot.h, ctypes.byref(self.params), ctypes.byref(h)),
+              "smp_planner_create")
+        self.h = h
+        self.scene = None
+
+    def set_scene(self, scene):
+        check(lib().smp_planner_set_scene(self.h, scene.h), "smp_planner_set_scene")
+        self.scene = scene
+
+    def set_disabled_map_links(self, names):
+        arr = (ctypes.c_char_p * max(len(names), 1))(*[n.encode() for n in names])
+        check(lib().smp_set_disabled_map_links(self.h, arr, len(names)))
+
+    def check_configs(self, q, check_self=True, check_map=True):
+        q = np.asarray(q, np.float64).reshape(-1, 8)
+        soa = np.ascontiguousarray(q.T)
+        out = np.zeros(len(q), np.uint8)
+        check(lib().smp_check_configs(self.h, soa.ctypes.data_as(_pd), len(q), int(check_self), int(check_map),
+                                      out.ctypes.data_as(ctypes.c_void_p)), "smp_check_configs")
+        return out
+
+    def last_kernel_ms(self):
+        a, b = ctypes.c_double(), ctypes.c_double()
+        n = ctypes.c_int64()
+        check(lib().smp_last_kernel_ms(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(n)))
+        return a.value, b.value, n.value
+
+    @staticmethod
+    def make_query(start, goal, env_x=(0, 0), env_y=(0, 0), check_self=True, check_map=True, iterations=None,
+                   seconds=None, seed=1, query_id=0):
+        q = L.Query()
+        for j in range(8):
+            q.start[j] = float(start[j])
+            q.goal[j] = float(goal[j])
+        q.env_x[0], q.env_x[1] = env_x
+        q.env_y[0], q.env_y[1] = env_y
+        q.check_self, q.check_map = int(check_self), int(check_map)
+        if seconds is not None:
+            q.budget_is_time, q.budget = 1, float(seconds)
+        else:
+            q.budget_is_time, q.budget = 0, float(1000 if iterations is None else iterations)
+        q.seed = seed
+        q.query_id = query_id
+        return q
+
+    def plan_batch(self, queries):
+        n = len(queries)
+        qa = (L.Query * n)(*queries)
+        ra = (L.Result * n)()
+        lib().smp_plan_batch(self.h, qa, n, ra)
+        out = []
+        for r in ra:
+            d = _result_dict(r)
+            lib().smp_result_free(ctypes.byref(r))
+            out.append(d)
+        return out
+
+    def plan(self, query):
+        return self.plan_batch([query])[0]
+
+    def tree(self, which):
+        n = lib().smp_get_tree(self.h, which, None, None, None)
+        if n < 0:
+            raise L.SmpError(L.SMP_ERR_ARG, "smp_get_tree")
+        par = np.zeros(n, np.int32)
+        conf = np.zeros((n, 8))
+        cost = np.zeros((n, 3))
+        lib().smp_get_tree(self.h, which, par.ctypes.data_as(ctypes.c_void_p), conf.ctypes.data_as(ctypes.c_void_p),
+                           cost.ctypes.data_as(ctypes.c_void_p))
+        return par, conf, cost
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().smp_planner_destroy(self.h)
+            self.h = None
+
+
+def _result_dict(r):
+    s = r.stats
+    d = {f: getattr(s, f) for f, _ in L.Stats._fields_}
+    d["cost_best"] = list(s.cost_best)
+    d["cost_theoretical"] = list(s.cost_theoretical)
+    d["status"] = r.status
+    n = r.n_waypoints
+    d["path"] = np.ctypeslib.as_array(r.waypoints, shape=(n, 8)).copy() if n else np.zeros((0, 8))
+    m = r.n_cost_rows
+    d["cost_rows"] = np.ctypeslib.as_array(r.cost_rows, shape=(m, 5)).copy() if m else np.zeros((0, 5))
+    return d
+
+
+class BiRRTstarPlanner:
+    """Drop-in mirror of birrt_star_motion_planning::BiRRTstarPlanner for the C-space (search_space = 1) path.
+
+    Call sequence of the node (squirrel_8dof_planner.cpp:1221-1248):
+        initialize(); setOctree(...); setDisabledLinkMapCollisions([...]);
+        reset_planner_and_config(); setPlanningSceneInfo(x, y, name);
+        init_planner(start, goal, 1, self, map) -> bool; run_planner(1, 1, T, False, 0.0, n) -> bool;
+        getJointTrajectoryRef()
+    Extra (not in the reference): seed / query_id for reproducible runs, `stats` of the last run.
+    """
+
+    def __init__(self, device=0, seed=1):
+        self.device = device
+        self.seed = seed
+        self.query_id = 0
+        self._gpu = None
+        self._env = [(0.0, 0.0), (0.0, 0.0)]
+        self._start = self._goal = None
+        self._flags = (True, True)
+        self._traj = []
+        self.stats = None
+
+    def initialize(self, planning_group="robotino_robot", **params):
+        if planning_group != "robotino_robot":
+            raise ValueError("only the robotino_robot group (robotino_plan.srdf:4-6) is modelled")
+        self._gpu = GpuPlanner(device=self.device, **params)
+
+    def setOctree(self, octree, resolution=None, floor_center=None, floor_distance=3.0):
+        """octree: .bt bytes or an (n, 3) array of occupied octomap keys (then `resolution` is required)."""
+        if isinstance(octree, (bytes, bytearray)):
+            sc = Scene.from_bt(octree, floor_center=floor_center, floor_distance=floor_distance)
+        else:
+            sc = Scene.from_keys(octree, resolution, floor_center=floor_center, floor_distance=floor_distance)
+        self._gpu.set_scene(sc)
+
+    def setDisabledLinkMapCollisions(self, links):
+        self._gpu.set_disabled_map_links(list(links))
+
+    def setPlanningSceneInfo(self, size_x, size_y, scene_name="scenario"):
+        self._env = [(float(size_x[0]), float(size_x[1])), (float(size_y[0]), float(size_y[1]))]
+
+    def reset_planner_and_config(self):
+        self._env = [(0.0, 0.0), (0.0, 0.0)]
+        self._start = self._goal = None
+        self._traj = []
+
+    def isConfigValid(self, config, check_self_collision=True, check_map_collision=True):
+        return bool(self._gpu.check_configs([config], check_self_collision, check_map_collision)[0])
+
+    def init_planner(self, start_conf, goal_conf, search_space=1, check_self_collision=True, check_map_collision=True):
+        if len(start_conf) != 8 or len(goal_conf) != 8 or search_space != 1:
+            return False  # birrt_star.cpp:338-342 (control-space search is out of scope)
+        v = self._gpu.check_configs([start_conf, goal_conf], check_self_collision, check_map_collision)
+        if not v[0] or not v[1]:
+            return False  # birrt_star.cpp:350-362
+        self._start, self._goal = list(start_conf), list(goal_conf)
+        self._flags = (check_self_collision, check_map_collision)
+        return True
+
+    def run_planner(self, search_space=1, flag_iter_or_time=1, max_iter_time=30.0, show_tree_vis=False,
+                    iter_sleep=0.0, planner_run_number=0):
+        if self._start is None or search_space != 1:
+            return False
+        kw = dict(seconds=max_iter_time) if flag_iter_or_time else dict(iterations=int(max_iter_time))
+        q = GpuPlanner.make_query(self._start, self._goal, self._env[0], self._env[1], self._flags[0],
+                                  self._flags[1], seed=self.seed, query_id=self.query_id, **kw)
+        r = self._gpu.plan(q)
+        self.stats = r
+        if r["status"] not in (L.SMP_OK, L.SMP_ERR_NO_SOLUTION):
+            raise L.SmpError(r["status"], "run_planner")
+        self._traj = [list(map(float, w)) for w in r["path"]]
+        return r["status"] == L.SMP_OK
+
+    def getJointTrajectoryRef(self):
+        return self._traj
