@@ -10,6 +10,7 @@
  *                              (birrt_star.cpp:1621-1624, collision_checker.hpp:76-88) for occupied leaf keys
  *   smp_scene_from_bt          the same from an octomap binary (.bt / binary octomap_msgs payload), with the
  *                              node's floor insertion (squirrel_8dof_planner.cpp:862-917)
+ *   smp_scene_from_grid        the same from a broadcast grid (multi-GPU: one RCCL broadcast per scene)
  *   smp_planner_create         BiRRTstarPlanner::initialize (birrt_star.cpp:11-326) on one GPU
  *   smp_planner_set_scene      BiRRTstarPlanner::setOctree (copies; caller keeps ownership)
  *   smp_set_disabled_map_links BiRRTstarPlanner::setDisabledLinkMapCollisions (birrt_star.cpp:6916-6919)
@@ -98,6 +99,10 @@ typedef struct smp_stats {
   int64_t nodes_start, nodes_goal, edges_start, edges_goal, rewires_start, rewires_goal;
   int32_t connected_tree_is_start;
   int32_t conn_node_b, conn_node_a;
+  int64_t nn_nodes_scanned;      /* nodes streamed by nearest-neighbour scans (64 B each) */
+  int64_t near_nodes_scanned;    /* nodes streamed by near-vertex scans (72 B each) */
+  double phase_seconds[16];      /* device time per planner phase (sample, nn, expand, near, choose-parent,
+                                    rewire, connect, collision tiles, #tiles, edge costs, via chains, #via) */
 } smp_stats;
 
 typedef struct smp_result {
@@ -120,6 +125,9 @@ const char* smp_robot_link_name(const smp_robot* r, int i);
 
 int smp_scene_from_keys(const uint16_t* keys_xyz, int64_t n, const smp_scene_opts* opts, smp_scene** out);
 int smp_scene_from_bt(const uint8_t* data, size_t size, const smp_scene_opts* opts, smp_scene** out);
+/* A scene from an exported grid (bitset + d2), e.g. after the RCCL broadcast of rank 0's scene. */
+int smp_scene_from_grid(const uint64_t* bits, const uint16_t* d2, const int dims[3], const double origin[3],
+                        double resolution, smp_scene** out);
 void smp_scene_destroy(smp_scene* s);
 /* Grid geometry of a scene: dims[3], origin[3], resolution; bitset/d2 copies for inspection (may be NULL). */
 int smp_scene_info(const smp_scene* s, int dims[3], double origin[3], double* resolution,

@@ -51,7 +51,8 @@ class Stats(ctypes.Structure):
                 ("cost_best", _d * 3), ("cost_theoretical", _d * 3), ("nodes_start", _i64), ("nodes_goal", _i64),
                 ("edges_start", _i64), ("edges_goal", _i64), ("rewires_start", _i64), ("rewires_goal", _i64),
                 ("connected_tree_is_start", ctypes.c_int32), ("conn_node_b", ctypes.c_int32),
-                ("conn_node_a", ctypes.c_int32)]
+                ("conn_node_a", ctypes.c_int32), ("nn_nodes_scanned", _i64), ("near_nodes_scanned", _i64),
+                ("phase_seconds", _d * 16)]
 
 
 class Result(ctypes.Structure):
@@ -70,6 +71,7 @@ EXPORTS = [
     ("smp_robot_link_name", ctypes.c_char_p, [_p, _i]),
     ("smp_scene_from_keys", _i, [_p, _i64, ctypes.POINTER(SceneOpts), ctypes.POINTER(_p)]),
     ("smp_scene_from_bt", _i, [_p, ctypes.c_size_t, ctypes.POINTER(SceneOpts), ctypes.POINTER(_p)]),
+    ("smp_scene_from_grid", _i, [_p, _p, ctypes.POINTER(_i), _pd, _d, ctypes.POINTER(_p)]),
     ("smp_scene_destroy", None, [_p]),
     ("smp_scene_info", _i, [_p, ctypes.POINTER(_i), _pd, _pd, ctypes.POINTER(_i64), _pd, _pd]),
     ("smp_scene_export", _i, [_p, _p, _p]),

@@ -225,6 +225,23 @@ int smp_scene_from_bt(const uint8_t* data, size_t size, const smp_scene_opts* o,
   return SMP_OK;
 }
 
+int smp_scene_from_grid(const uint64_t* bits, const uint16_t* d2, const int dims[3], const double origin[3],
+                        double res, smp_scene** out) {
+  if (!bits || !d2 || !dims || !origin || !out || !(res > 0) || dims[0] <= 0 || dims[1] <= 0 || dims[2] <= 0)
+    return SMP_ERR_ARG;
+  smp_scene* s = new smp_scene();
+  SceneHost& h = s->h;
+  h.nx = dims[0]; h.ny = dims[1]; h.nz = dims[2]; h.wx = (h.nx + 63) / 64;
+  h.ox = origin[0]; h.oy = origin[1]; h.oz = origin[2]; h.res = res;
+  size_t nw = (size_t)h.wx * h.ny * h.nz, nc = (size_t)h.nx * h.ny * h.nz;
+  h.bits.assign(bits, bits + nw);
+  h.d2.assign(d2, d2 + nc);
+  h.n_occupied = 0;
+  for (uint64_t w : h.bits) h.n_occupied += __builtin_popcountll(w);
+  *out = s;
+  return SMP_OK;
+}
+
 void smp_scene_destroy(smp_scene* s) { delete s; }
 
 int smp_scene_info(const smp_scene* s, int dims[3], double origin[3], double* resolution, int64_t* n_occupied,
@@ -595,6 +612,10 @@ extern "C" int smp_plan_batch(smp_planner* p, const smp_query* qs, int nq, smp_r
     st.rewires_start = s.rewires[0]; st.rewires_goal = s.rewires[1];
     st.connected_tree_is_start = s.conn_start;
     st.conn_node_b = s.nB.id; st.conn_node_a = s.nA.id;
+    st.nn_nodes_scanned = s.nn_nodes;
+    st.near_nodes_scanned = s.near_nodes;
+    for (int k = 0; k < 16; ++k)
+      st.phase_seconds[k] = (k == 8 || k == 11) ? (double)s.prof[k] : (double)s.prof[k] / p->wall_rate_hz;
     if (i == 0) { p->last_n[0] = s.n[0]; p->last_n[1] = s.n[1]; }
     // cost rows
     r.n_cost_rows = s.n_rows;

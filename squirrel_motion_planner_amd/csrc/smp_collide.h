@@ -115,8 +115,9 @@ struct TileLds {
 template <int CT>
 __device__ __forceinline__ void collide_tile(const RobotDev* __restrict__ rb, const SceneDev& sc,
                                              const MapCfg* __restrict__ mc, int nc, const double (*q_lds)[NJ],
-                                             int self, int map, TileLds<CT>& L) {
+                                             int self, int map, TileLds<CT>& L, unsigned long long* prof = nullptr) {
   const int tid = threadIdx.x;
+  unsigned long long t0 = (prof && tid == 0) ? wall_clock64() : 0;
   if (tid < nc) {
     double q[NJ];
     for (int j = 0; j < NJ; ++j) q[j] = q_lds[tid][j];
@@ -124,6 +125,7 @@ __device__ __forceinline__ void collide_tile(const RobotDev* __restrict__ rb, co
     L.coll[tid] = 0;
   }
   __syncthreads();
+  unsigned long long t1 = (prof && tid == 0) ? wall_clock64() : 0;
   const int nsph = rb->n_sph, ncl = rb->n_clink;
   for (int it = tid; it < nc * nsph; it += BLOCK) {
     int c = it / nsph, s = it - c * nsph;
@@ -141,6 +143,7 @@ __device__ __forceinline__ void collide_tile(const RobotDev* __restrict__ rb, co
     }
   }
   __syncthreads();
+  unsigned long long t2 = (prof && tid == 0) ? wall_clock64() : 0;
   if (self) {
     const int np = rb->n_pairs;
     for (int it = tid; it < nc * np; it += BLOCK) {
@@ -163,6 +166,10 @@ __device__ __forceinline__ void collide_tile(const RobotDev* __restrict__ rb, co
     }
   }
   __syncthreads();
+  if (prof && tid == 0) {
+    unsigned long long t3 = wall_clock64();
+    prof[0] += t1 - t0; prof[1] += t2 - t1; prof[2] += t3 - t2;
+  }
 }
 
 }  // namespace smp

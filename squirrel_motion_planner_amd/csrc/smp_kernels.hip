@@ -124,6 +124,12 @@ struct Ctx {
   QueryDev Q;
 };
 
+// Phase clocks (thread 0, s_memrealtime ticks): where an iteration spends its time.
+enum { P_SAMPLE, P_NN, P_EXPAND, P_NEAR, P_CHOOSE, P_REWIRE, P_CONNECT, P_TILES, P_NTILES, P_COSTS, P_VIA, P_NVIA,
+       P_TFK, P_TMAP, P_TSELF };
+#define PROF_BEGIN() unsigned long long _pt = threadIdx.x == 0 ? wall_clock64() : 0
+#define PROF_END(k) if (threadIdx.x == 0) { L.S.prof[k] += wall_clock64() - _pt; }
+
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
 
@@ -184,6 +190,7 @@ __device__ int block_argmin(PlanLds& L, double d, int i) {
 __device__ int nearest(const Ctx& C, PlanLds& L, int t, const double* q) {
   const TreeDev& T = C.Q.tr[t];
   const int n = L.S.n[t], cap = L.S.cap;
+  if (threadIdx.x == 0) L.S.nn_nodes += n;
   double qq[NJ];
   for (int j = 0; j < NJ; ++j) qq[j] = q[j];
   double best = 10000.0;
@@ -213,6 +220,7 @@ __device__ void near_set(const Ctx& C, PlanLds& L, int t, const double* q, int e
   const TreeDev& T = C.Q.tr[t];
   const int n = L.S.n[t], cap = L.S.cap;
   const double r = L.S.near_r;
+  if (threadIdx.x == 0) L.S.near_nodes += n;
   double qq[NJ];
   for (int j = 0; j < NJ; ++j) qq[j] = q[j];
   double lc[K], hc[K];
@@ -308,6 +316,7 @@ __device__ void near_set(const Ctx& C, PlanLds& L, int t, const double* q, int e
 // 4162-4242) for E <= MAXE edges eg_start -> eg_target, base costs eg_base.  Segment norms in parallel,
 // ordered sums per edge.  Fills eg_step, eg_end (the child configuration) and eg_cost.
 __device__ void edge_costs(const Ctx& C, PlanLds& L, int E) {
+  PROF_BEGIN();
   const int np = L.S.n_pts;
   const RobotDev* rb = C.rb;
   if (threadIdx.x < E * NJ) {
@@ -339,6 +348,7 @@ __device__ void edge_costs(const Ctx& C, PlanLds& L, int E) {
     L.eg_cost[e][k] = L.eg_base[e][k] + acc;
   }
   __syncthreads();
+  PROF_END(P_COSTS);
 }
 
 // isEdgeValid for the edges with eg_need[e] set: eg_first[e] = first colliding configuration index, or
@@ -361,7 +371,10 @@ __device__ void edge_validity(const Ctx& C, PlanLds& L, int E) {
     for (int c = 0; c < nc; ++c) any |= L.eg_need[(base + c) / np1];
     if (!any) continue;
     __syncthreads();
-    collide_tile<32>(C.rb, C.sc, C.mc, nc, L.u.tile.tq, L.S.self, L.S.map, L.u.tile.T);
+    PROF_BEGIN();
+    collide_tile<32>(C.rb, C.sc, C.mc, nc, L.u.tile.tq, L.S.self, L.S.map, L.u.tile.T, &L.S.prof[P_TFK]);
+    PROF_END(P_TILES);
+    if (threadIdx.x == 0) L.S.prof[P_NTILES]++;
     if (threadIdx.x < nc) {
       int f = base + threadIdx.x, e = f / np1, i = f - e * np1;
       if (L.eg_need[e] && L.u.tile.T.coll[threadIdx.x]) atomicMin(&L.eg_first[e], i);
@@ -410,7 +423,9 @@ __device__ bool step_towards(const RobotDev* rb, const double* nn, double* x, do
 // unconstraint_extend_step_factor, collecting via nodes (ids nn_t, nn_t+1, ...) until the target is
 // reached; the last edge becomes `sel` (id nn_t at that point).  No collision checks (reference behaviour).
 __device__ void via_chain(const Ctx& C, PlanLds& L, const double* target) {
+  PROF_BEGIN();
   for (;;) {
+    if (threadIdx.x == 0) L.S.prof[P_NVIA]++;
     if (threadIdx.x == 0) {
       for (int j = 0; j < NJ; ++j) L.ox[j] = target[j];
       L.reached = step_towards(C.rb, L.cur.q, L.ox, L.S.step) ? 1 : 0;
@@ -444,6 +459,7 @@ __device__ void via_chain(const Ctx& C, PlanLds& L, const double* target) {
     __syncthreads();
     if (L.reached) break;
   }
+  PROF_END(P_VIA);
 }
 
 __device__ void insert_via(const Ctx& C, PlanLds& L, int t) {
@@ -882,8 +898,12 @@ __device__ void connect_graphs(const Ctx& C, PlanLds& L, int t) {
 // One C-space iteration of run_planner (birrt_star.cpp:1163-1338).
 __device__ void iteration(const Ctx& C, PlanLds& L) {
   const int A = L.S.A, B = 1 - A;
+  unsigned long long _t0 = threadIdx.x == 0 ? wall_clock64() : 0, _t1;
+#define PHASE(k) if (threadIdx.x == 0) { _t1 = wall_clock64(); L.S.prof[k] += _t1 - _t0; _t0 = _t1; }
   if (L.S.informed && L.S.have_sol) sample_ellipse(C, L); else sample_uniform(C, L);
+  PHASE(P_SAMPLE);
   int nid = nearest(C, L, A, L.xr);
+  PHASE(P_NN);
   if (threadIdx.x == 0) {
     load_node(C, A, nid, &L.nn);
     // expandTree single step (birrt_star.cpp:2224-2256)
@@ -915,20 +935,27 @@ __device__ void iteration(const Ctx& C, PlanLds& L) {
     L.nk = 0;
   }
   __syncthreads();
+  PHASE(P_EXPAND);
   const bool opt = L.S.tree_opt && L.S.have_sol;
   if (opt) {
     near_set<20>(C, L, A, L.xn.q, L.xn.id);
+    PHASE(P_NEAR);
     choose_parent(C, L, A);
+    PHASE(P_CHOOSE);
   }
   if (L.ext_nn || L.ext_bp) {
     if (threadIdx.x == 0) insert_node(C, L, A, L.en_start, L.en_target, L.xn);
     __syncthreads();
     if (opt) rewire(C, L, A);
+    PHASE(P_REWIRE);
     int cid = nearest(C, L, B, L.xn.q);
     if (threadIdx.x == 0) load_node(C, B, cid, &L.xc);
     __syncthreads();
+    PHASE(P_NN);
     connect_graphs(C, L, B);
+    PHASE(P_CONNECT);
   }
+#undef PHASE
   if (threadIdx.x == 0) {
     QState& S = L.S;
     S.A = B;

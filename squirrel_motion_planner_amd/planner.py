@@ -82,6 +82,17 @@ class Scene:
         check(lib().smp_scene_from_bt(buf, len(data), ctypes.byref(o), ctypes.byref(h)), "smp_scene_from_bt")
         return cls(h)
 
+    @classmethod
+    def from_grid(cls, bits, d2, dims, origin, res):
+        bits = np.ascontiguousarray(bits, np.uint64)
+        d2 = np.ascontiguousarray(d2, np.uint16)
+        dd = (ctypes.c_int * 3)(*dims)
+        oo = (ctypes.c_double * 3)(*origin)
+        h = ctypes.c_void_p()
+        check(lib().smp_scene_from_grid(bits.ctypes.data_as(ctypes.c_void_p), d2.ctypes.data_as(ctypes.c_void_p), dd,
+                                        oo, res, ctypes.byref(h)), "smp_scene_from_grid")
+        return cls(h)
+
     def info(self):
         dims = (ctypes.c_int * 3)()
         org = (ctypes.c_double * 3)()
@@ -197,6 +208,9 @@ def _result_dict(r):
     d = {f: getattr(s, f) for f, _ in L.Stats._fields_}
     d["cost_best"] = list(s.cost_best)
     d["cost_theoretical"] = list(s.cost_theoretical)
+    names = ["sample", "nearest", "expand", "near", "choose_parent", "rewire", "connect", "collide_tiles",
+             "n_tiles", "edge_costs", "via_chains", "n_via_steps", "tile_fk", "tile_map", "tile_self"]
+    d["phases"] = {n: s.phase_seconds[i] for i, n in enumerate(names)}
     d["status"] = r.status
     n = r.n_waypoints
     d["path"] = np.ctypeslib.as_array(r.waypoints, shape=(n, 8)).copy() if n else np.zeros((0, 8))

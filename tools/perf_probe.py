@@ -1,0 +1,36 @@
+"""Timing probe of the planner kernel at growing iteration budgets (C2) and of the batch check kernel."""
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from squirrel_motion_planner_amd import scenes  # noqa: E402
+from squirrel_motion_planner_amd.planner import GpuPlanner, Scene  # noqa: E402
+
+sc = scenes.box_room()
+gp = GpuPlanner(path_optimality_threshold=-math.inf)
+gp.set_scene(Scene.from_keys(sc.keys, sc.res))
+for iters in [int(v) for v in (sys.argv[1:] or ["2000", "10000", "50000"])]:
+    t = time.perf_counter()
+    r = gp.plan(GpuPlanner.make_query(sc.start, sc.goal, sc.env_x, sc.env_y, iterations=iters, seed=1))
+    dt = time.perf_counter() - t
+    _, pms, nl = gp.last_kernel_ms()
+    print("iters %7d wall %.2fs kernel %.2fs launches %d  us/iter %.1f  checked %d (%.0f/s)  nodes %d/%d "
+          "nn %d near %d first_iter %d t_first %.3f cost %.3f" %
+          (iters, dt, pms / 1e3, nl, pms * 1e3 / iters, r["configs_checked"], r["configs_checked"] / (pms / 1e3),
+           r["nodes_start"], r["nodes_goal"], r["nn_nodes_scanned"], r["near_nodes_scanned"],
+           r["first_solution_iter"], r["time_first_solution"], r["cost_best"][0]), flush=True)
+    print("   phases:", {k: round(v, 3) for k, v in r["phases"].items()}, flush=True)
+rng = np.random.default_rng(0)
+n = 2_000_000
+q = np.column_stack([rng.uniform(-6, 5, n), rng.uniform(-6, 5, n)] + [rng.uniform(-2, 2, n) for _ in range(6)])
+gp.check_configs(q[:1000])
+t = time.perf_counter()
+v = gp.check_configs(q)
+dt = time.perf_counter() - t
+ms, _, _ = gp.last_kernel_ms()
+print("check_configs: %d configs, kernel %.2f ms -> %.3g configs/s (wall %.2f s), valid %.3f" %
+      (n, ms, n / (ms / 1e3), dt, v.mean()))
