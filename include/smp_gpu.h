@@ -101,8 +101,9 @@ typedef struct smp_stats {
   int32_t conn_node_b, conn_node_a;
   int64_t nn_nodes_scanned;      /* nodes streamed by nearest-neighbour scans (64 B each) */
   int64_t near_nodes_scanned;    /* nodes streamed by near-vertex scans (72 B each) */
-  double phase_seconds[16];      /* device time per planner phase (sample, nn, expand, near, choose-parent,
-                                    rewire, connect, collision tiles, #tiles, edge costs, via chains, #via) */
+  double phase_seconds[24];      /* device time per planner phase (sample, nn, expand, near, choose-parent,
+                                    rewire, connect, collision tiles, #tiles, edge costs, via chains, #via,
+                                    tile FK, tile tests); #tiles and #via are counts */
 } smp_stats;
 
 typedef struct smp_result {

@@ -225,8 +225,9 @@ class OracleScene:
         padded[:, :, :self.nx] = occ
         self.bits = np.packbits(padded.reshape(-1, 64), axis=1, bitorder="little").view("<u8").astype(np.uint64).ravel()
         if occ.any():
-            from scipy.ndimage import distance_transform_edt
-            d = distance_transform_edt(~occ)
+            # squared box-to-box gap to the nearest occupied cell = squared EDT of the 3x3x3-dilated occupancy
+            from scipy.ndimage import binary_dilation, distance_transform_edt
+            d = distance_transform_edt(~binary_dilation(occ, structure=np.ones((3, 3, 3), bool)))
             d2 = np.rint(d * d)
             self.d2 = np.minimum(d2, 65535).astype(np.uint16).ravel()
         else:

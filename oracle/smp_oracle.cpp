@@ -144,9 +144,10 @@ static inline bool occ(const Scene& s, int i, int j, int k) {
   return (s.bits[((size_t)k * s.ny + j) * s.wx + (i >> 6)] >> (i & 63)) & 1ull;
 }
 
-// Map test of one sphere against the occupied voxel boxes (DESIGN.md "Collision model").  The D2
-// prefilter rejects spheres whose centre cell is farther than r + sqrt(3) voxels from every occupied
-// voxel centre; otherwise every voxel box in reach is tested exactly.
+// Map test of one sphere against the occupied voxel boxes (DESIGN.md "Collision model").  d2 holds, per
+// cell, the squared box-to-box gap (voxel units) to the nearest occupied cell -- a lower bound of the
+// distance from any point of the cell to any occupied box -- so a sphere whose centre cell has
+// d2 > floor(((r + 1e-6) / res)^2) is free; otherwise every voxel box in reach is tested exactly.
 static inline bool sphere_hits_map(const Scene& s, const double* c, double r, uint32_t T) {
   double fx = std::floor((c[0] - s.ox) / s.res), fy = std::floor((c[1] - s.oy) / s.res), fz = std::floor((c[2] - s.oz) / s.res);
   if (!(fx >= 0 && fx < s.nx && fy >= 0 && fy < s.ny && fz >= 0 && fz < s.nz)) return false;
@@ -176,8 +177,8 @@ static inline bool sphere_hits_map(const Scene& s, const double* c, double r, ui
 }
 
 static inline uint32_t sphere_threshold(double r, double res) {
-  double a = r / res + 1.7320508075688772 + 1e-3;
-  return (uint32_t)std::ceil(a * a);
+  double a = (r + 1e-6) / res;
+  return (uint32_t)std::floor(a * a);
 }
 
 // Tree FK of every link (CC:519-539): movable links use joint->pose(q) only, the rest their stored

@@ -94,7 +94,7 @@ struct smp_planner {
   RobotDev* d_rb = nullptr;
   MapCfg mc_host;
   MapCfg* d_mc = nullptr;
-  DBuf<uint64_t> d_bits;
+  DBuf<uint64_t> d_bricks;
   DBuf<uint16_t> d_d2;
   SceneDev sc{};
   bool have_scene = false;
@@ -238,6 +238,7 @@ int smp_scene_from_grid(const uint64_t* bits, const uint16_t* d2, const int dims
   h.d2.assign(d2, d2 + nc);
   h.n_occupied = 0;
   for (uint64_t w : h.bits) h.n_occupied += __builtin_popcountll(w);
+  build_bricks(&h);
   *out = s;
   return SMP_OK;
 }
@@ -301,7 +302,7 @@ void smp_planner_destroy(smp_planner* p) {
   (void)hipStreamSynchronize(p->stream);
   for (auto& q : p->qb) q.release();
   p->d_qdev.release(); p->d_counts.release(); p->d_cq.release(); p->d_valid.release();
-  p->d_bits.release(); p->d_d2.release();
+  p->d_bricks.release(); p->d_d2.release();
   if (p->d_rb) (void)hipFree(p->d_rb);
   if (p->d_mc) (void)hipFree(p->d_mc);
   if (p->ev0) (void)hipEventDestroy(p->ev0);
@@ -313,13 +314,14 @@ void smp_planner_destroy(smp_planner* p) {
 int smp_planner_set_scene(smp_planner* p, const smp_scene* s) {
   if (!p || !s) return SMP_ERR_ARG;
   HIPCHK(hipSetDevice(p->device));
-  HIPCHK(p->d_bits.reserve(s->h.bits.size()));
+  HIPCHK(p->d_bricks.reserve(s->h.bricks.size()));
   HIPCHK(p->d_d2.reserve(s->h.d2.size()));
-  HIPCHK(hipMemcpyAsync(p->d_bits.p, s->h.bits.data(), s->h.bits.size() * sizeof(uint64_t), hipMemcpyHostToDevice, p->stream));
+  HIPCHK(hipMemcpyAsync(p->d_bricks.p, s->h.bricks.data(), s->h.bricks.size() * sizeof(uint64_t), hipMemcpyHostToDevice, p->stream));
   HIPCHK(hipMemcpyAsync(p->d_d2.p, s->h.d2.data(), s->h.d2.size() * sizeof(uint16_t), hipMemcpyHostToDevice, p->stream));
-  p->sc.nx = s->h.nx; p->sc.ny = s->h.ny; p->sc.nz = s->h.nz; p->sc.wx = s->h.wx;
+  p->sc.nx = s->h.nx; p->sc.ny = s->h.ny; p->sc.nz = s->h.nz;
+  p->sc.bnx = s->h.bnx; p->sc.bny = s->h.bny;
   p->sc.ox = s->h.ox; p->sc.oy = s->h.oy; p->sc.oz = s->h.oz; p->sc.res = s->h.res;
-  p->sc.bits = p->d_bits.p;
+  p->sc.bricks = p->d_bricks.p;
   p->sc.d2 = p->d_d2.p;
   p->have_scene = true;
   p->scene_res = s->h.res;
@@ -341,10 +343,10 @@ int smp_check_configs(smp_planner* p, const double* q_soa, int64_t n, int check_
   HIPCHK(p->d_cq.reserve((size_t)n * NJ));
   HIPCHK(p->d_valid.reserve((size_t)n));
   HIPCHK(hipMemcpyAsync(p->d_cq.p, q_soa, (size_t)n * NJ * sizeof(double), hipMemcpyHostToDevice, p->stream));
-  long long tiles = (n + 15) / 16;
+  long long tiles = (n + 31) / 32;
   int grid = (int)std::min<long long>(tiles, 256 * 8);
   HIPCHK(hipEventRecord(p->ev0, p->stream));
-  hipLaunchKernelGGL(check_kernel, dim3(grid), dim3(256), 0, p->stream, p->d_rb, p->sc, p->d_mc, p->d_cq.p, (long long)n,
+  hipLaunchKernelGGL(check_kernel, dim3(grid), dim3(BLOCK), 0, p->stream, p->d_rb, p->sc, p->d_mc, p->d_cq.p, (long long)n,
                      check_self, check_map && p->have_scene, p->d_valid.p);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(p->ev1, p->stream));
@@ -557,7 +559,7 @@ extern "C" int smp_plan_batch(smp_planner* p, const smp_query* qs, int nq, smp_r
     if (tmax > 0 && std::chrono::duration<double>(std::chrono::steady_clock::now() - t_begin).count() > tmax * 4 + 60)
       return SMP_ERR_HIP;
     HIPCHK(hipEventRecord(p->ev0, p->stream));
-    hipLaunchKernelGGL(plan_kernel, dim3(nq), dim3(256), 0, p->stream, p->d_rb, p->sc, p->d_mc, p->d_qdev.p, chunk);
+    hipLaunchKernelGGL(plan_kernel, dim3(nq), dim3(BLOCK), 0, p->stream, p->d_rb, p->sc, p->d_mc, p->d_qdev.p, chunk);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(p->ev1, p->stream));
     launches++;
@@ -614,8 +616,8 @@ extern "C" int smp_plan_batch(smp_planner* p, const smp_query* qs, int nq, smp_r
     st.conn_node_b = s.nB.id; st.conn_node_a = s.nA.id;
     st.nn_nodes_scanned = s.nn_nodes;
     st.near_nodes_scanned = s.near_nodes;
-    for (int k = 0; k < 16; ++k)
-      st.phase_seconds[k] = (k == 8 || k == 11) ? (double)s.prof[k] : (double)s.prof[k] / p->wall_rate_hz;
+    for (int k = 0; k < 24; ++k)
+      st.phase_seconds[k] = (k == 8 || k == 11 || k >= 16) ? (double)s.prof[k] : (double)s.prof[k] / p->wall_rate_hz;
     if (i == 0) { p->last_n[0] = s.n[0]; p->last_n[1] = s.n[1]; }
     // cost rows
     r.n_cost_rows = s.n_rows;

@@ -111,9 +111,11 @@ void robot_from_json(const std::string& text, RobotHost* out) {
 // ------------------------------------------------------------------------------------------ scene
 int grid_pad_cells(double res) { return (int)std::ceil(0.30 / res) + 2; }
 
+// d2 is a lower bound of (distance from any point of the cell to any occupied box / res)^2, so a sphere of
+// radius r whose centre cell has d2 > T cannot touch an occupied box; the 1e-6 m margin absorbs rounding.
 uint32_t sphere_threshold(double r, double res) {
-  double a = r / res + 1.7320508075688772 + 1e-3;
-  return (uint32_t)std::ceil(a * a);
+  double a = (r + 1e-6) / res;
+  return (uint32_t)std::floor(a * a);
 }
 
 // 1-D squared distance transform of f (Felzenszwalb & Huttenlocher 2012), in place.
@@ -166,6 +168,49 @@ void edt_squared(const std::vector<uint8_t>& occ, int nx, int ny, int nz, std::v
   for (size_t i = 0; i < n; ++i) (*d2)[i] = f[i] >= 65535.0 ? 65535 : (uint16_t)f[i];
 }
 
+void box_gap_squared(const std::vector<uint8_t>& occ, int nx, int ny, int nz, std::vector<uint16_t>* d2) {
+  // 3x3x3 dilation (separable max over +-1 per axis), then the EDT: the squared distance from cell u to the
+  // dilated set is min over occupied o of sum_axis max(|u - o| - 1, 0)^2, the box-to-box gap.
+  std::vector<uint8_t> a(occ), b(occ.size());
+  const size_t sx = 1, sy = (size_t)nx, sz = (size_t)nx * ny;
+  const int n[3] = {nx, ny, nz};
+  const size_t st[3] = {sx, sy, sz};
+  for (int ax = 0; ax < 3; ++ax) {
+    for (int k = 0; k < nz; ++k)
+      for (int j = 0; j < ny; ++j)
+        for (int i = 0; i < nx; ++i) {
+          size_t c = (size_t)k * sz + (size_t)j * sy + i;
+          int pos = ax == 0 ? i : (ax == 1 ? j : k);
+          uint8_t v = a[c];
+          if (pos > 0) v |= a[c - st[ax]];
+          if (pos + 1 < n[ax]) v |= a[c + st[ax]];
+          b[c] = v;
+        }
+    a.swap(b);
+  }
+  edt_squared(a, nx, ny, nz, d2);
+}
+
+void build_bricks(SceneHost* h) {
+  h->bnx = (h->nx + 3) / 4;
+  h->bny = (h->ny + 3) / 4;
+  h->bnz = (h->nz + 3) / 4;
+  h->bricks.assign((size_t)h->bnx * h->bny * h->bnz, 0);
+  for (int k = 0; k < h->nz; ++k)
+    for (int j = 0; j < h->ny; ++j) {
+      const uint64_t* row = h->bits.data() + ((size_t)k * h->ny + j) * h->wx;
+      for (int w = 0; w < h->wx; ++w) {
+        uint64_t m = row[w];
+        while (m) {
+          int i = w * 64 + __builtin_ctzll(m);
+          m &= m - 1;
+          size_t b = ((size_t)(k >> 2) * h->bny + (j >> 2)) * h->bnx + (i >> 2);
+          h->bricks[b] |= 1ull << (((k & 3) << 4) | ((j & 3) << 2) | (i & 3));
+        }
+      }
+    }
+}
+
 void scene_from_keys(const uint16_t* keys, int64_t n, double res, double z_offset, SceneHost* out) {
   out->res = res;
   out->n_occupied = 0;
@@ -177,6 +222,7 @@ void scene_from_keys(const uint16_t* keys, int64_t n, double res, double z_offse
     out->bits.assign(1, 0);
     out->d2.assign(1, 65535);
     for (int d = 0; d < 3; ++d) out->bbox_min[d] = out->bbox_max[d] = 0.0;
+    build_bricks(out);
     return;
   }
   int kmin[3] = {1 << 30, 1 << 30, 1 << 30}, kmax[3] = {-1, -1, -1};
@@ -212,7 +258,8 @@ void scene_from_keys(const uint16_t* keys, int64_t n, double res, double z_offse
       out->bits[((size_t)z * out->ny + y) * out->wx + (x >> 6)] |= 1ull << (x & 63);
     }
   }
-  edt_squared(occ, out->nx, out->ny, out->nz, &out->d2);
+  box_gap_squared(occ, out->nx, out->ny, out->nz, &out->d2);
+  build_bricks(out);
 }
 
 void floor_keys(double cx, double cy, double res, double distance, std::vector<uint16_t>* keys) {

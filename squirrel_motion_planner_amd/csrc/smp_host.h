@@ -17,8 +17,10 @@ struct RobotHost {
 struct SceneHost {
   int nx = 1, ny = 1, nz = 1, wx = 1;
   double ox = 0, oy = 0, oz = 0, res = 0.05;
-  std::vector<uint64_t> bits;
-  std::vector<uint16_t> d2;
+  std::vector<uint64_t> bits;     // x-major rows of 64-bit words
+  std::vector<uint16_t> d2;       // squared box-to-box gap (voxels) to the nearest occupied cell, <= 65535
+  int bnx = 1, bny = 1, bnz = 1;  // 4x4x4 bricks
+  std::vector<uint64_t> bricks;   // bit (z&3)*16 + (y&3)*4 + (x&3) of brick (z>>2, y>>2, x>>2)
   int64_t n_occupied = 0;
   double bbox_min[3] = {0, 0, 0}, bbox_max[3] = {0, 0, 0};  // metric bbox of the occupied keys (octree frame)
 };
@@ -37,6 +39,10 @@ void octomap_bt_keys(const uint8_t* data, size_t size, double* res, std::vector<
 void floor_keys(double cx, double cy, double res, double distance, std::vector<uint16_t>* keys);
 // Exact squared Euclidean distance transform (voxel units) of a dense occupancy mask (x fastest).
 void edt_squared(const std::vector<uint8_t>& occ, int nx, int ny, int nz, std::vector<uint16_t>* d2);
+// Squared box-to-box gap field (voxel units): EDT of the 3x3x3-dilated occupancy.
+void box_gap_squared(const std::vector<uint8_t>& occ, int nx, int ny, int nz, std::vector<uint16_t>* d2);
+// 4x4x4 occupancy bricks from the bitset.
+void build_bricks(SceneHost* h);
 uint32_t sphere_threshold(double r, double res);
 
 }  // namespace smp

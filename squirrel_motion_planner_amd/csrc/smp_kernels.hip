@@ -21,13 +21,28 @@ namespace smp {
 
 // ============================================================================================ batch check
 // valid[i] = !isInCollision(q_i) for n configurations given as SoA q[j*n + i].
-constexpr int CHECK_CT = 16;
+constexpr int CHECK_CT = 32;
+
+// Robot model and map configuration staged in LDS by every kernel that runs collision tiles.
+__shared__ RobotDev g_rb;
+__shared__ MapCfg g_mc;
+
+// Copies the robot model and the map configuration into LDS (read by every collision stage).
+__device__ __forceinline__ void stage_model(const RobotDev* rb, const MapCfg* mc, RobotDev* rbl, MapCfg* mcl) {
+  static_assert(sizeof(RobotDev) % 8 == 0 && sizeof(MapCfg) % 4 == 0, "staging granularity");
+  for (int i = threadIdx.x; i < (int)(sizeof(RobotDev) / 8); i += BLOCK)
+    reinterpret_cast<uint64_t*>(rbl)[i] = reinterpret_cast<const uint64_t*>(rb)[i];
+  for (int i = threadIdx.x; i < (int)(sizeof(MapCfg) / 4); i += BLOCK)
+    reinterpret_cast<uint32_t*>(mcl)[i] = reinterpret_cast<const uint32_t*>(mc)[i];
+  __syncthreads();
+}
 
 __global__ void __launch_bounds__(BLOCK) check_kernel(const RobotDev* __restrict__ rb, SceneDev sc,
                                                       const MapCfg* __restrict__ mc, const double* __restrict__ q,
                                                       long long n, int self, int map, uint8_t* __restrict__ valid) {
   __shared__ TileLds<CHECK_CT> L;
   __shared__ double ql[CHECK_CT][NJ];
+  stage_model(rb, mc, &g_rb, &g_mc);
   const long long ntiles = (n + CHECK_CT - 1) / CHECK_CT;
   for (long long t = blockIdx.x; t < ntiles; t += gridDim.x) {
     long long base = t * CHECK_CT;
@@ -37,7 +52,7 @@ __global__ void __launch_bounds__(BLOCK) check_kernel(const RobotDev* __restrict
       ql[c][j] = q[(long long)j * n + base + c];
     }
     __syncthreads();
-    collide_tile<CHECK_CT>(rb, sc, mc, nc, ql, self, map, L);
+    collide_tile<CHECK_CT>(&g_rb, sc, &g_mc, nc, ql, self, map, L);
     if (threadIdx.x < nc) valid[base + threadIdx.x] = L.coll[threadIdx.x] ? 0 : 1;
     __syncthreads();
   }
@@ -93,7 +108,8 @@ struct PlanLds {
   // edge batch
   double eg_start[MAXE][NJ], eg_target[MAXE][NJ], eg_step[MAXE][NJ], eg_end[MAXE][NJ];
   double eg_base[MAXE][3], eg_cost[MAXE][3];
-  int eg_first[MAXE], eg_need[MAXE], eg_near[MAXE];
+  int eg_first[MAXE], eg_need[MAXE], eg_near[MAXE], eg_ptr[MAXE];
+  int tile_e[32], tile_i[32], tile_n;
   // near lists (ascending (cost,id) for the first max_near; last max_near in ascending order)
   int nk;
   int lo_i[MAX_NEAR], hi_i[MAX_NEAR];
@@ -117,18 +133,20 @@ struct PlanLds {
   long long wcount[BLOCK / 64];
 };
 
+// The planner's LDS objects live at namespace scope so that every device function addresses them as LDS
+// (ds_read/ds_write) rather than through generic pointers.
+__shared__ PlanLds g_L;
+
 struct Ctx {
-  const RobotDev* __restrict__ rb;
   SceneDev sc;
-  const MapCfg* __restrict__ mc;
   QueryDev Q;
 };
 
 // Phase clocks (thread 0, s_memrealtime ticks): where an iteration spends its time.
 enum { P_SAMPLE, P_NN, P_EXPAND, P_NEAR, P_CHOOSE, P_REWIRE, P_CONNECT, P_TILES, P_NTILES, P_COSTS, P_VIA, P_NVIA,
-       P_TFK, P_TMAP, P_TSELF };
+       P_TFK, P_TTEST };
 #define PROF_BEGIN() unsigned long long _pt = threadIdx.x == 0 ? wall_clock64() : 0
-#define PROF_END(k) if (threadIdx.x == 0) { L.S.prof[k] += wall_clock64() - _pt; }
+#define PROF_END(k) if (threadIdx.x == 0) { g_L.S.prof[k] += wall_clock64() - _pt; }
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
@@ -144,8 +162,8 @@ __device__ __forceinline__ void load_node(const Ctx& C, int t, int id, NodeRef* 
 }
 
 // insertNode (birrt_star.cpp:3298-3322), single lane.  Appends at index n[t] (== node id).
-__device__ void insert_node(const Ctx& C, PlanLds& L, int t, const double* e_start, const double* e_target, const NodeRef& x) {
-  QState& S = L.S;
+__device__ void insert_node(const Ctx& C, int t, const double* e_start, const double* e_target, const NodeRef& x) {
+  QState& S = g_L.S;
   int i = S.n[t];
   if (i >= S.cap || x.id != i) { S.status = -7; S.phase = 2; return; }
   const TreeDev& T = C.Q.tr[t];
@@ -170,27 +188,27 @@ __device__ void insert_node(const Ctx& C, PlanLds& L, int t, const double* e_sta
 
 // --------------------------------------------------------------------------------------- scans
 // Block argmin of (d, i): smallest d, then smallest i; d >= 10000 never wins (birrt_star.cpp:4090,4122).
-__device__ int block_argmin(PlanLds& L, double d, int i) {
+__device__ int block_argmin(double d, int i) {
   for (int off = 32; off > 0; off >>= 1) {
     double od = __shfl_xor(d, off);
     int oi = __shfl_xor(i, off);
     if (od < d || (od == d && oi < i)) { d = od; i = oi; }
   }
-  if (lane_id() == 0) { L.wd[wave_id()] = d; L.wi[wave_id()] = i; }
+  if (lane_id() == 0) { g_L.wd[wave_id()] = d; g_L.wi[wave_id()] = i; }
   __syncthreads();
-  double bd = L.wd[0];
-  int bi = L.wi[0];
+  double bd = g_L.wd[0];
+  int bi = g_L.wi[0];
   for (int w = 1; w < BLOCK / 64; ++w)
-    if (L.wd[w] < bd || (L.wd[w] == bd && L.wi[w] < bi)) { bd = L.wd[w]; bi = L.wi[w]; }
+    if (g_L.wd[w] < bd || (g_L.wd[w] == bd && g_L.wi[w] < bi)) { bd = g_L.wd[w]; bi = g_L.wi[w]; }
   __syncthreads();
   return bd < 10000.0 ? bi : 0;
 }
 
 // find_nearest_neighbour_interpolation: first strict minimum of the Euclidean joint distance (DH:128-156).
-__device__ int nearest(const Ctx& C, PlanLds& L, int t, const double* q) {
+__device__ int nearest(const Ctx& C, int t, const double* q) {
   const TreeDev& T = C.Q.tr[t];
-  const int n = L.S.n[t], cap = L.S.cap;
-  if (threadIdx.x == 0) L.S.nn_nodes += n;
+  const int n = g_L.S.n[t], cap = g_L.S.cap;
+  if (threadIdx.x == 0) g_L.S.nn_nodes += n;
   double qq[NJ];
   for (int j = 0; j < NJ; ++j) qq[j] = q[j];
   double best = 10000.0;
@@ -205,7 +223,7 @@ __device__ int nearest(const Ctx& C, PlanLds& L, int t, const double* q) {
     double dist = sqrt(s);
     if (dist < best) { best = dist; bid = i; }
   }
-  return block_argmin(L, best, bid);
+  return block_argmin(best, bid);
 }
 
 // (cost,id) lexicographic order of the near list (std::sort order made total).
@@ -216,11 +234,11 @@ __device__ __forceinline__ bool ci_less(double ca, int ia, double cb, int ib) {
 // find_near_vertices_interpolation (birrt_star.cpp:4272-4324): count k, the first MAX_NEAR and the last
 // MAX_NEAR entries of the (cost,id)-sorted near list.  Per-thread register lists + 20-round block merge.
 template <int K>
-__device__ void near_set(const Ctx& C, PlanLds& L, int t, const double* q, int excl) {
+__device__ void near_set(const Ctx& C, int t, const double* q, int excl) {
   const TreeDev& T = C.Q.tr[t];
-  const int n = L.S.n[t], cap = L.S.cap;
-  const double r = L.S.near_r;
-  if (threadIdx.x == 0) L.S.near_nodes += n;
+  const int n = g_L.S.n[t], cap = g_L.S.cap;
+  const double r = g_L.S.near_r;
+  if (threadIdx.x == 0) g_L.S.near_nodes += n;
   double qq[NJ];
   for (int j = 0; j < NJ; ++j) qq[j] = q[j];
   double lc[K], hc[K];
@@ -271,10 +289,10 @@ __device__ void near_set(const Ctx& C, PlanLds& L, int t, const double* q, int e
   }
   // total count
   for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
-  if (lane_id() == 0) L.wcount[wave_id()] = cnt;
+  if (lane_id() == 0) g_L.wcount[wave_id()] = cnt;
   __syncthreads();
   long long total = 0;
-  for (int w = 0; w < BLOCK / 64; ++w) total += L.wcount[w];
+  for (int w = 0; w < BLOCK / 64; ++w) total += g_L.wcount[w];
   const int take = (int)min((long long)K, total);
   // merge: `take` rounds of block-wide min (lo) and max (hi) over list heads
   for (int rnd = 0; rnd < take; ++rnd) {
@@ -286,15 +304,15 @@ __device__ void near_set(const Ctx& C, PlanLds& L, int t, const double* q, int e
       if (ci_less(odl, oil, dl, il)) { dl = odl; il = oil; }
       if (ci_less(dh, ih, odh, oih)) { dh = odh; ih = oih; }
     }
-    if (lane_id() == 0) { L.u.red.rd[wave_id()] = dl; L.u.red.ri[wave_id()] = il; L.u.red.rc2[wave_id()] = dh; L.u.red.ri2[wave_id()] = ih; }
+    if (lane_id() == 0) { g_L.u.red.rd[wave_id()] = dl; g_L.u.red.ri[wave_id()] = il; g_L.u.red.rc2[wave_id()] = dh; g_L.u.red.ri2[wave_id()] = ih; }
     __syncthreads();
-    dl = L.u.red.rd[0]; il = L.u.red.ri[0]; dh = L.u.red.rc2[0]; ih = L.u.red.ri2[0];
+    dl = g_L.u.red.rd[0]; il = g_L.u.red.ri[0]; dh = g_L.u.red.rc2[0]; ih = g_L.u.red.ri2[0];
     for (int w = 1; w < BLOCK / 64; ++w) {
-      if (ci_less(L.u.red.rd[w], L.u.red.ri[w], dl, il)) { dl = L.u.red.rd[w]; il = L.u.red.ri[w]; }
-      if (ci_less(dh, ih, L.u.red.rc2[w], L.u.red.ri2[w])) { dh = L.u.red.rc2[w]; ih = L.u.red.ri2[w]; }
+      if (ci_less(g_L.u.red.rd[w], g_L.u.red.ri[w], dl, il)) { dl = g_L.u.red.rd[w]; il = g_L.u.red.ri[w]; }
+      if (ci_less(dh, ih, g_L.u.red.rc2[w], g_L.u.red.ri2[w])) { dh = g_L.u.red.rc2[w]; ih = g_L.u.red.ri2[w]; }
     }
     __syncthreads();
-    if (threadIdx.x == 0) { L.lo_c[rnd] = dl; L.lo_i[rnd] = il; L.hi_c[take - 1 - rnd] = dh; L.hi_i[take - 1 - rnd] = ih; }
+    if (threadIdx.x == 0) { g_L.lo_c[rnd] = dl; g_L.lo_i[rnd] = il; g_L.hi_c[take - 1 - rnd] = dh; g_L.hi_i[take - 1 - rnd] = ih; }
     // pop the winners' heads (ids are unique: exactly one thread owns each)
     if (li[0] == il) {
 #pragma unroll
@@ -307,7 +325,7 @@ __device__ void near_set(const Ctx& C, PlanLds& L, int t, const double* q, int e
       hc[K - 1] = -__builtin_inf(); hi[K - 1] = -1;
     }
   }
-  if (threadIdx.x == 0) { L.nk = (int)total; L.n_lo = take; L.n_hi = take; }
+  if (threadIdx.x == 0) { g_L.nk = (int)total; g_L.n_lo = take; g_L.n_hi = take; }
   __syncthreads();
 }
 
@@ -315,80 +333,101 @@ __device__ void near_set(const Ctx& C, PlanLds& L, int t, const double* q, int e
 // connectNodesInterpolation + compute_edge_cost_interpolation (birrt_star.cpp:4380-4440, 4443-4526,
 // 4162-4242) for E <= MAXE edges eg_start -> eg_target, base costs eg_base.  Segment norms in parallel,
 // ordered sums per edge.  Fills eg_step, eg_end (the child configuration) and eg_cost.
-__device__ void edge_costs(const Ctx& C, PlanLds& L, int E) {
+__device__ void edge_costs(const Ctx& C, int E) {
   PROF_BEGIN();
-  const int np = L.S.n_pts;
-  const RobotDev* rb = C.rb;
+  const int np = g_L.S.n_pts;
+  const RobotDev* rb = (&g_rb);
   if (threadIdx.x < E * NJ) {
     int e = threadIdx.x / NJ, j = threadIdx.x - e * NJ;
-    double st = (L.eg_target[e][j] - L.eg_start[e][j]) / double(np);
-    L.eg_step[e][j] = st;
-    L.eg_end[e][j] = L.eg_start[e][j] + np * st;
+    double st = (g_L.eg_target[e][j] - g_L.eg_start[e][j]) / double(np);
+    g_L.eg_step[e][j] = st;
+    g_L.eg_end[e][j] = g_L.eg_start[e][j] + np * st;
   }
   __syncthreads();
   for (int it = threadIdx.x; it < E * np; it += BLOCK) {
     int e = it / np, s = it - e * np;
     double t = 0.0, r = 0.0, p = 0.0;
     for (int j = 0; j < NJ; ++j) {
-      double a = L.eg_start[e][j] + s * L.eg_step[e][j];
-      double b = L.eg_start[e][j] + (s + 1) * L.eg_step[e][j];
+      double a = g_L.eg_start[e][j] + s * g_L.eg_step[e][j];
+      double b = g_L.eg_start[e][j] + (s + 1) * g_L.eg_step[e][j];
       double d = (b - a) * (b - a);
       t += d * 1.0;
       if (rb->rev[j]) r += d; else p += d;
     }
-    L.u.seg[e][s][0] = sqrt(t);
-    L.u.seg[e][s][1] = sqrt(r);
-    L.u.seg[e][s][2] = sqrt(p);
+    g_L.u.seg[e][s][0] = sqrt(t);
+    g_L.u.seg[e][s][1] = sqrt(r);
+    g_L.u.seg[e][s][2] = sqrt(p);
   }
   __syncthreads();
   if (threadIdx.x < E * 3) {
     int e = threadIdx.x / 3, k = threadIdx.x - e * 3;
     double acc = 0.0;
-    for (int s = 0; s < np; ++s) acc += L.u.seg[e][s][k];
-    L.eg_cost[e][k] = L.eg_base[e][k] + acc;
+    for (int s = 0; s < np; ++s) acc += g_L.u.seg[e][s][k];
+    g_L.eg_cost[e][k] = g_L.eg_base[e][k] + acc;
   }
   __syncthreads();
   PROF_END(P_COSTS);
 }
 
-// isEdgeValid for the edges with eg_need[e] set: eg_first[e] = first colliding configuration index, or
-// n_pts + 1 if the whole edge is free.  Configurations of all needed edges are flattened into 32-wide tiles.
-__device__ void edge_validity(const Ctx& C, PlanLds& L, int E) {
-  const int np1 = L.S.n_pts + 1;
-  if (threadIdx.x < E) L.eg_first[threadIdx.x] = np1;
+// isEdgeValid for the edges with eg_need[e] set: eg_first[e] = index of the first colliding configuration,
+// or n_pts + 1 if the edge is free.  Each 32-configuration tile takes the next unchecked points of the
+// unresolved needed edges in edge order, so an edge leaves the schedule at its first collision and every
+// point before eg_first[e] has been checked.  With stop_first_valid the scan ends as soon as the first needed
+// edge not in collision is fully checked (choose-parent and the connect near loop consume the edges in
+// order and stop there); eg_first of the edges after it is then undefined.
+__device__ void edge_validity(const Ctx& C, int E, bool stop_first_valid) {
+  const int np1 = g_L.S.n_pts + 1;
+  if (threadIdx.x < E) { g_L.eg_first[threadIdx.x] = np1; g_L.eg_ptr[threadIdx.x] = 0; }
   __syncthreads();
-  const int total = E * np1;
-  for (int base = 0; base < total; base += 32) {
-    // map tile slot -> (edge, point); skip edges not needed (their slots stay idle)
-    int nc = min(32, total - base);
+  for (;;) {
+    if (threadIdx.x == 0) {
+      int nc = 0;
+      for (int e = 0; e < E && nc < 32; ++e) {
+        if (!g_L.eg_need[e] || g_L.eg_first[e] < np1 || g_L.eg_ptr[e] >= np1) continue;
+        int take = min(np1 - g_L.eg_ptr[e], 32 - nc);
+        for (int i = 0; i < take; ++i) { g_L.tile_e[nc + i] = e; g_L.tile_i[nc + i] = g_L.eg_ptr[e] + i; }
+        g_L.eg_ptr[e] += take;
+        nc += take;
+      }
+      g_L.tile_n = nc;
+    }
+    __syncthreads();
+    const int nc = g_L.tile_n;
+    if (nc == 0) break;
     if (threadIdx.x < nc * NJ) {
       int c = threadIdx.x / NJ, j = threadIdx.x - c * NJ;
-      int f = base + c, e = f / np1, i = f - e * np1;
-      L.u.tile.tq[c][j] = L.eg_start[e][j] + i * L.eg_step[e][j];
+      int e = g_L.tile_e[c];
+      g_L.u.tile.tq[c][j] = g_L.eg_start[e][j] + g_L.tile_i[c] * g_L.eg_step[e][j];
     }
-    // skip whole tile if no needed edge intersects it
-    int any = 0;
-    for (int c = 0; c < nc; ++c) any |= L.eg_need[(base + c) / np1];
-    if (!any) continue;
     __syncthreads();
     PROF_BEGIN();
-    collide_tile<32>(C.rb, C.sc, C.mc, nc, L.u.tile.tq, L.S.self, L.S.map, L.u.tile.T, &L.S.prof[P_TFK]);
+    const TileOrder order{g_L.tile_e, g_L.tile_i, g_L.eg_first};
+    collide_tile<32>((&g_rb), C.sc, (&g_mc), nc, g_L.u.tile.tq, g_L.S.self, g_L.S.map, g_L.u.tile.T, &order,
+                     &g_L.S.prof[P_TFK]);
     PROF_END(P_TILES);
-    if (threadIdx.x == 0) L.S.prof[P_NTILES]++;
-    if (threadIdx.x < nc) {
-      int f = base + threadIdx.x, e = f / np1, i = f - e * np1;
-      if (L.eg_need[e] && L.u.tile.T.coll[threadIdx.x]) atomicMin(&L.eg_first[e], i);
+    if (threadIdx.x == 0) g_L.S.prof[P_NTILES]++;
+    if (stop_first_valid) {
+      if (threadIdx.x == 0) {
+        int stop = 0;
+        for (int e = 0; e < E; ++e) {
+          if (!g_L.eg_need[e] || g_L.eg_first[e] < np1) continue;  // not needed / resolved in collision
+          stop = g_L.eg_ptr[e] >= np1;                           // first candidate still free: resolved?
+          break;
+        }
+        g_L.tile_n = stop;
+      }
+      __syncthreads();
+      if (g_L.tile_n) break;
     }
-    __syncthreads();
   }
   __syncthreads();
 }
 
 // Reference-semantics accounting of one isEdgeValid call (stops at the first collision).
-__device__ __forceinline__ void count_edge(PlanLds& L, int first) {
-  int np1 = L.S.n_pts + 1;
-  if (first >= np1) { L.S.checked += np1; L.S.valid += np1; }
-  else { L.S.checked += first + 1; L.S.valid += first; }
+__device__ __forceinline__ void count_edge(int first) {
+  int np1 = g_L.S.n_pts + 1;
+  if (first >= np1) { g_L.S.checked += np1; g_L.S.valid += np1; }
+  else { g_L.S.checked += first + 1; g_L.S.valid += first; }
 }
 
 // stepTowardsRandSample (birrt_star.cpp:5712-5868), single lane.
@@ -422,58 +461,58 @@ __device__ bool step_towards(const RobotDev* rb, const double* nn, double* x, do
 // Stepping loop shared by choose_parent / connectGraphs: from `cur` towards `target` with
 // unconstraint_extend_step_factor, collecting via nodes (ids nn_t, nn_t+1, ...) until the target is
 // reached; the last edge becomes `sel` (id nn_t at that point).  No collision checks (reference behaviour).
-__device__ void via_chain(const Ctx& C, PlanLds& L, const double* target) {
+__device__ void via_chain(const Ctx& C, const double* target) {
   PROF_BEGIN();
   for (;;) {
-    if (threadIdx.x == 0) L.S.prof[P_NVIA]++;
+    if (threadIdx.x == 0) g_L.S.prof[P_NVIA]++;
     if (threadIdx.x == 0) {
-      for (int j = 0; j < NJ; ++j) L.ox[j] = target[j];
-      L.reached = step_towards(C.rb, L.cur.q, L.ox, L.S.step) ? 1 : 0;
-      for (int j = 0; j < NJ; ++j) { L.eg_start[0][j] = L.cur.q[j]; L.eg_target[0][j] = L.ox[j]; }
-      for (int k = 0; k < 3; ++k) L.eg_base[0][k] = L.cur.c[k];
+      for (int j = 0; j < NJ; ++j) g_L.ox[j] = target[j];
+      g_L.reached = step_towards((&g_rb), g_L.cur.q, g_L.ox, g_L.S.step) ? 1 : 0;
+      for (int j = 0; j < NJ; ++j) { g_L.eg_start[0][j] = g_L.cur.q[j]; g_L.eg_target[0][j] = g_L.ox[j]; }
+      for (int k = 0; k < 3; ++k) g_L.eg_base[0][k] = g_L.cur.c[k];
     }
     __syncthreads();
-    edge_costs(C, L, 1);
+    edge_costs(C, 1);
     if (threadIdx.x == 0) {
       NodeRef g;
-      for (int j = 0; j < NJ; ++j) g.q[j] = L.eg_end[0][j];
-      for (int k = 0; k < 3; ++k) g.c[k] = L.eg_cost[0][k];
-      g.parent = L.cur.id;
-      if (!L.reached) {
-        g.id = L.nn_t++;
-        if (L.n_via >= L.S.via_cap) { L.S.status = -7; L.S.phase = 2; L.reached = 1; }
+      for (int j = 0; j < NJ; ++j) g.q[j] = g_L.eg_end[0][j];
+      for (int k = 0; k < 3; ++k) g.c[k] = g_L.eg_cost[0][k];
+      g.parent = g_L.cur.id;
+      if (!g_L.reached) {
+        g.id = g_L.nn_t++;
+        if (g_L.n_via >= g_L.S.via_cap) { g_L.S.status = -7; g_L.S.phase = 2; g_L.reached = 1; }
         else {
-          ViaNode& v = C.Q.via[L.n_via++];
-          for (int j = 0; j < NJ; ++j) { v.q[j] = g.q[j]; v.e_start[j] = L.cur.q[j]; v.e_target[j] = L.ox[j]; }
+          ViaNode& v = C.Q.via[g_L.n_via++];
+          for (int j = 0; j < NJ; ++j) { v.q[j] = g.q[j]; v.e_start[j] = g_L.cur.q[j]; v.e_target[j] = g_L.ox[j]; }
           for (int k = 0; k < 3; ++k) v.c[k] = g.c[k];
           v.id = g.id;
           v.parent = g.parent;
         }
-        L.cur = g;
+        g_L.cur = g;
       } else {
-        g.id = L.nn_t;
-        L.sel = g;
-        for (int j = 0; j < NJ; ++j) { L.sel_start[j] = L.cur.q[j]; L.sel_target[j] = L.ox[j]; }
+        g.id = g_L.nn_t;
+        g_L.sel = g;
+        for (int j = 0; j < NJ; ++j) { g_L.sel_start[j] = g_L.cur.q[j]; g_L.sel_target[j] = g_L.ox[j]; }
       }
     }
     __syncthreads();
-    if (L.reached) break;
+    if (g_L.reached) break;
   }
   PROF_END(P_VIA);
 }
 
-__device__ void insert_via(const Ctx& C, PlanLds& L, int t) {
+__device__ void insert_via(const Ctx& C, int t) {
   if (threadIdx.x == 0) {
-    for (int v = 0; v < L.n_via && L.S.status == 0; ++v) {
+    for (int v = 0; v < g_L.n_via && g_L.S.status == 0; ++v) {
       const ViaNode& w = C.Q.via[v];
       NodeRef x;
       for (int j = 0; j < NJ; ++j) x.q[j] = w.q[j];
       for (int k = 0; k < 3; ++k) x.c[k] = w.c[k];
       x.id = w.id;
       x.parent = w.parent;
-      insert_node(C, L, t, w.e_start, w.e_target, x);
+      insert_node(C, t, w.e_start, w.e_target, x);
     }
-    L.n_via = 0;
+    g_L.n_via = 0;
   }
   __syncthreads();
 }
@@ -482,7 +521,7 @@ __device__ void insert_via(const Ctx& C, PlanLds& L, int t) {
 // getRandomConf (control_laws.cpp:1120-1188): draws in chain order until the EE z >= 0.  One lane per
 // inner attempt; the first valid attempt (lowest index) wins.  Used for outer attempt `outer`.
 __device__ void rand_conf_lane(const Ctx& C, const QState& S, uint32_t outer, uint32_t inner, double* q) {
-  const RobotDev* rb = C.rb;
+  const RobotDev* rb = (&g_rb);
   bool env0 = S.env_x[0] == 0.0 && S.env_x[1] == 0.0 && S.env_y[0] == 0.0 && S.env_y[1] == 0.0;
   for (int j = 0; j < NJ; ++j) {
     double lo = rb->q_min[j], hi = rb->q_max[j];
@@ -493,21 +532,21 @@ __device__ void rand_conf_lane(const Ctx& C, const QState& S, uint32_t outer, ui
   }
 }
 
-// sampleJointConfig_JntArray (birrt_star.cpp:3832-3878) -> L.xr; wave 0 tries 64 attempts at once.
-__device__ void sample_uniform(const Ctx& C, PlanLds& L) {
+// sampleJointConfig_JntArray (birrt_star.cpp:3832-3878) -> g_L.xr; wave 0 tries 64 attempts at once.
+__device__ void sample_uniform(const Ctx& C) {
   if (wave_id() == 0) {
     for (uint32_t base = 0;; base += 64) {
       if (base >= (1u << 24)) {  // no valid sample in 16M attempts: give up loudly
-        if (lane_id() == 0) { L.S.status = -1; L.S.phase = 2; }
+        if (lane_id() == 0) { g_L.S.status = -1; g_L.S.phase = 2; }
         break;
       }
       double q[NJ];
-      rand_conf_lane(C, L.S, 0, base + lane_id(), q);
-      bool ok = 0.0 <= ee_z(C.rb, q);
+      rand_conf_lane(C, g_L.S, 0, base + lane_id(), q);
+      bool ok = 0.0 <= ee_z((&g_rb), q);
       unsigned long long m = __ballot(ok);
       if (m) {
         int w = __ffsll((long long)m) - 1;
-        if (lane_id() == w) for (int j = 0; j < NJ; ++j) L.xr[j] = q[j];
+        if (lane_id() == w) for (int j = 0; j < NJ; ++j) g_L.xr[j] = q[j];
         break;
       }
     }
@@ -517,14 +556,14 @@ __device__ void sample_uniform(const Ctx& C, PlanLds& L) {
 
 // sampleJointConfigfromEllipse_JntArray (birrt_star.cpp:3607-3829); lane = outer attempt b, inner
 // getRandomConf attempts run serially per lane; the lowest valid b wins.
-__device__ void sample_ellipse(const Ctx& C, PlanLds& L) {
-  const RobotDev* rb = C.rb;
-  const QState& S = L.S;
+__device__ void sample_ellipse(const Ctx& C) {
+  const RobotDev* rb = (&g_rb);
+  const QState& S = g_L.S;
   if (wave_id() == 0) {
     bool env0 = S.env_x[0] == 0.0 && S.env_x[1] == 0.0 && S.env_y[0] == 0.0 && S.env_y[1] == 0.0;
     for (uint32_t base = 0;; base += 64) {
       if (base >= (1u << 20)) {
-        if (lane_id() == 0) { L.S.status = -1; L.S.phase = 2; }
+        if (lane_id() == 0) { g_L.S.status = -1; g_L.S.phase = 2; }
         break;
       }
       uint32_t b = base + lane_id();
@@ -566,7 +605,7 @@ __device__ void sample_ellipse(const Ctx& C, PlanLds& L) {
       unsigned long long m = __ballot(above && inside);
       if (m) {
         int w = __ffsll((long long)m) - 1;
-        if (lane_id() == w) for (int j = 0; j < NJ; ++j) L.xr[j] = r[j];
+        if (lane_id() == w) for (int j = 0; j < NJ; ++j) g_L.xr[j] = r[j];
         break;
       }
     }
@@ -576,8 +615,8 @@ __device__ void sample_ellipse(const Ctx& C, PlanLds& L) {
 
 // --------------------------------------------------------------------------------------- tree updates
 // recursiveNodeCostUpdate (birrt_star.cpp:5495-5606): subtree walk over child lists, single lane.
-__device__ void cost_update(const Ctx& C, PlanLds& L, int t, int v, const double* red) {
-  QState& S = L.S;
+__device__ void cost_update(const Ctx& C, int t, int v, const double* red) {
+  QState& S = g_L.S;
   const TreeDev& T = C.Q.tr[t];
   const int cap = S.cap;
   int* stack = C.Q.stack;
@@ -608,67 +647,67 @@ __device__ void cost_update(const Ctx& C, PlanLds& L, int t, int v, const double
 }
 
 // choose_node_parent_interpolation, unconstrained (birrt_star.cpp:4594-4738, 4916-4935).
-// Uses L.lo_* (near list prefix) and L.xn / L.nn; may update L.xn, L.en_*; returns via L.ext_bp.
-__device__ void choose_parent(const Ctx& C, PlanLds& L, int t) {
+// Uses g_L.lo_* (near list prefix) and g_L.xn / g_L.nn; may update g_L.xn, g_L.en_*; returns via g_L.ext_bp.
+__device__ void choose_parent(const Ctx& C, int t) {
   if (threadIdx.x == 0) {
-    L.ext_bp = 0;
-    L.found = -1;
-    L.cnt = 0;
-    if (L.nk > 0) {
-      L.xn.parent = L.nn.id;
+    g_L.ext_bp = 0;
+    g_L.found = -1;
+    g_L.cnt = 0;
+    if (g_L.nk > 0) {
+      g_L.xn.parent = g_L.nn.id;
       // candidate prefix: stop at the first near node whose cost is not below x_new's
-      int m = min(L.n_lo, L.S.max_near);
+      int m = min(g_L.n_lo, g_L.S.max_near);
       int E = 0;
       for (int i = 0; i < m; ++i) {
-        if (!(L.lo_c[i] < L.xn.c[0])) break;
+        if (!(g_L.lo_c[i] < g_L.xn.c[0])) break;
         E++;
       }
-      L.cnt = E;
+      g_L.cnt = E;
     }
   }
   __syncthreads();
-  const int E = L.cnt;
+  const int E = g_L.cnt;
   if (E > 0) {
     if (threadIdx.x < E) {
       int e = threadIdx.x;
       NodeRef nd;
-      load_node(C, t, L.lo_i[e], &nd);
-      for (int j = 0; j < NJ; ++j) { L.eg_start[e][j] = nd.q[j]; L.eg_target[e][j] = L.xn.q[j]; }
-      for (int k = 0; k < 3; ++k) L.eg_base[e][k] = nd.c[k];
-      L.eg_near[e] = nd.id;
+      load_node(C, t, g_L.lo_i[e], &nd);
+      for (int j = 0; j < NJ; ++j) { g_L.eg_start[e][j] = nd.q[j]; g_L.eg_target[e][j] = g_L.xn.q[j]; }
+      for (int k = 0; k < 3; ++k) g_L.eg_base[e][k] = nd.c[k];
+      g_L.eg_near[e] = nd.id;
     }
     __syncthreads();
-    edge_costs(C, L, E);
-    if (threadIdx.x < E) L.eg_need[threadIdx.x] = L.eg_cost[threadIdx.x][0] <= L.xn.c[0];
-    for (int e = E + threadIdx.x; e < MAXE; e += BLOCK) L.eg_need[e] = 0;
+    edge_costs(C, E);
+    if (threadIdx.x < E) g_L.eg_need[threadIdx.x] = g_L.eg_cost[threadIdx.x][0] <= g_L.xn.c[0];
+    for (int e = E + threadIdx.x; e < MAXE; e += BLOCK) g_L.eg_need[e] = 0;
     __syncthreads();
-    edge_validity(C, L, E);
+    edge_validity(C, E, true);
     if (threadIdx.x == 0) {
       for (int e = 0; e < E; ++e) {
-        if (!L.eg_need[e]) continue;
-        count_edge(L, L.eg_first[e]);
-        if (L.eg_first[e] > L.S.n_pts) { L.found = e; break; }
+        if (!g_L.eg_need[e]) continue;
+        count_edge(g_L.eg_first[e]);
+        if (g_L.eg_first[e] > g_L.S.n_pts) { g_L.found = e; break; }
       }
-      if (L.found >= 0) {
-        L.ext_bp = 1;
-        L.n_via = 0;
-        L.nn_t = L.S.n[t];
-        load_node(C, t, L.eg_near[L.found], &L.cur);
+      if (g_L.found >= 0) {
+        g_L.ext_bp = 1;
+        g_L.n_via = 0;
+        g_L.nn_t = g_L.S.n[t];
+        load_node(C, t, g_L.eg_near[g_L.found], &g_L.cur);
       }
     }
     __syncthreads();
-    if (L.found >= 0) {
-      via_chain(C, L, L.xn.q);
+    if (g_L.found >= 0) {
+      via_chain(C, g_L.xn.q);
       if (threadIdx.x == 0) {
         // x_new <- last stepped edge (birrt_star.cpp:4692-4711)
-        L.xn.id = L.sel.id;
-        L.xn.parent = L.sel.parent;
-        for (int j = 0; j < NJ; ++j) L.xn.q[j] = L.sel.q[j];
-        for (int k = 0; k < 3; ++k) L.xn.c[k] = L.sel.c[k];
-        for (int j = 0; j < NJ; ++j) { L.en_start[j] = L.sel_start[j]; L.en_target[j] = L.sel_target[j]; }
+        g_L.xn.id = g_L.sel.id;
+        g_L.xn.parent = g_L.sel.parent;
+        for (int j = 0; j < NJ; ++j) g_L.xn.q[j] = g_L.sel.q[j];
+        for (int k = 0; k < 3; ++k) g_L.xn.c[k] = g_L.sel.c[k];
+        for (int j = 0; j < NJ; ++j) { g_L.en_start[j] = g_L.sel_start[j]; g_L.en_target[j] = g_L.sel_target[j]; }
       }
       __syncthreads();
-      insert_via(C, L, t);
+      insert_via(C, t);
     }
   }
   __syncthreads();
@@ -676,79 +715,79 @@ __device__ void choose_parent(const Ctx& C, PlanLds& L, int t) {
 
 // rewireTreeInterpolation, unconstrained (birrt_star.cpp:5056-5230).  Validity of every candidate edge
 // x_new -> near is independent of the tree state, so all are checked at once; commits stay sequential.
-__device__ void rewire(const Ctx& C, PlanLds& L, int t) {
-  const int cap = L.S.cap;
+__device__ void rewire(const Ctx& C, int t) {
+  const int cap = g_L.S.cap;
   const TreeDev& T = C.Q.tr[t];
   if (threadIdx.x == 0) {
-    int n = L.nk;
-    int lower = n >= L.S.max_near ? n - L.S.max_near : 0;
+    int n = g_L.nk;
+    int lower = n >= g_L.S.max_near ? n - g_L.S.max_near : 0;
     int cnt = 0;
-    // L.hi_* holds positions n-n_hi .. n-1 in ascending order
+    // g_L.hi_* holds positions n-n_hi .. n-1 in ascending order
     for (int k = n - 1; k >= lower; --k) {
-      int pos = k - (n - L.n_hi);
-      if (L.xn.c[0] < T.cost[L.hi_i[pos]]) cnt++;
+      int pos = k - (n - g_L.n_hi);
+      if (g_L.xn.c[0] < T.cost[g_L.hi_i[pos]]) cnt++;
     }
-    L.cnt = cnt;
+    g_L.cnt = cnt;
   }
   __syncthreads();
-  const int cnt = L.cnt;
+  const int cnt = g_L.cnt;
   if (cnt == 0) return;
   // candidates k = n-1 .. n-cnt  ->  edge slot e = n-1-k
   if (threadIdx.x < cnt) {
     int e = threadIdx.x;
-    int pos = L.n_hi - 1 - e;
-    int v = L.hi_i[pos];
+    int pos = g_L.n_hi - 1 - e;
+    int v = g_L.hi_i[pos];
     NodeRef nd;
     load_node(C, t, v, &nd);
-    for (int j = 0; j < NJ; ++j) { L.eg_start[e][j] = L.xn.q[j]; L.eg_target[e][j] = nd.q[j]; }
-    for (int k = 0; k < 3; ++k) L.eg_base[e][k] = L.xn.c[k];
-    L.eg_near[e] = v;
+    for (int j = 0; j < NJ; ++j) { g_L.eg_start[e][j] = g_L.xn.q[j]; g_L.eg_target[e][j] = nd.q[j]; }
+    for (int k = 0; k < 3; ++k) g_L.eg_base[e][k] = g_L.xn.c[k];
+    g_L.eg_near[e] = v;
   }
   __syncthreads();
-  edge_costs(C, L, cnt);
+  edge_costs(C, cnt);
   if (threadIdx.x < cnt) {
-    int e = threadIdx.x, v = L.eg_near[e];
+    int e = threadIdx.x, v = g_L.eg_near[e];
     // costs only decrease during the loop, so a candidate failing against the current cost never passes
-    L.eg_need[e] = (v != L.xn.parent) && (T.parent[v] != 0) && (L.eg_cost[e][0] < T.cost[v]);
+    g_L.eg_need[e] = (v != g_L.xn.parent) && (T.parent[v] != 0) && (g_L.eg_cost[e][0] < T.cost[v]);
   }
-  for (int e = cnt + threadIdx.x; e < MAXE; e += BLOCK) L.eg_need[e] = 0;
+  for (int e = cnt + threadIdx.x; e < MAXE; e += BLOCK) g_L.eg_need[e] = 0;
   __syncthreads();
-  edge_validity(C, L, cnt);
+  edge_validity(C, cnt, false);
   if (threadIdx.x == 0) {
-    QState& S = L.S;
+    QState& S = g_L.S;
     for (int e = 0; e < cnt && S.status == 0; ++e) {
-      int v = L.eg_near[e];
-      if (!(v != L.xn.parent && T.parent[v] != 0)) continue;
+      int v = g_L.eg_near[e];
+      if (!(v != g_L.xn.parent && T.parent[v] != 0)) continue;
       double cv[3];
       for (int k = 0; k < 3; ++k) cv[k] = T.cost[(size_t)k * cap + v];
-      if (!(L.eg_cost[e][0] < cv[0])) continue;
-      count_edge(L, L.eg_first[e]);
-      if (L.eg_first[e] <= S.n_pts) continue;
+      if (!(g_L.eg_cost[e][0] < cv[0])) continue;
+      count_edge(g_L.eg_first[e]);
+      if (g_L.eg_first[e] <= S.n_pts) continue;
       double red[3];
-      for (int k = 0; k < 3; ++k) red[k] = L.eg_cost[e][k] - cv[k];
+      for (int k = 0; k < 3; ++k) red[k] = g_L.eg_cost[e][k] - cv[k];
       // unlink from the old parent (the reference erases the outgoing edge, birrt_star.cpp:5124-5169)
       int p = T.parent[v];
       int pv = T.prev_sib[v], nx = T.next_sib[v];
       if (pv >= 0) T.next_sib[pv] = nx; else T.first_child[p] = nx;
       if (nx >= 0) T.prev_sib[nx] = pv;
       S.edges[t]--;
-      T.parent[v] = L.xn.id;
+      T.parent[v] = g_L.xn.id;
       if (S.have_sol) {
         bool connected = (t == 0) == (S.conn_start != 0);
-        if (v == S.nB.id && connected) S.nB.parent = L.xn.id;
-        else if (v == S.nA.id && !connected) S.nA.parent = L.xn.id;
+        if (v == S.nB.id && connected) S.nB.parent = g_L.xn.id;
+        else if (v == S.nA.id && !connected) S.nA.parent = g_L.xn.id;
       }
       for (int j = 0; j < NJ; ++j) {
-        T.q[(size_t)j * cap + v] = L.eg_end[e][j];
-        T.e_start[(size_t)j * cap + v] = L.eg_start[e][j];
-        T.e_target[(size_t)j * cap + v] = L.eg_target[e][j];
+        T.q[(size_t)j * cap + v] = g_L.eg_end[e][j];
+        T.e_start[(size_t)j * cap + v] = g_L.eg_start[e][j];
+        T.e_target[(size_t)j * cap + v] = g_L.eg_target[e][j];
       }
-      int f = T.first_child[L.xn.id];
+      int f = T.first_child[g_L.xn.id];
       T.next_sib[v] = f;
       T.prev_sib[v] = -1;
       if (f >= 0) T.prev_sib[f] = v;
-      T.first_child[L.xn.id] = v;
-      cost_update(C, L, t, v, red);
+      T.first_child[g_L.xn.id] = v;
+      cost_update(C, t, v, red);
       S.edges[t]++;
       S.rewires[t]++;
     }
@@ -757,207 +796,207 @@ __device__ void rewire(const Ctx& C, PlanLds& L, int t) {
 }
 
 // connectGraphsInterpolation, unconstrained branch + commit (birrt_star.cpp:2608-3046, 3219-3288).
-// t = tree_B; L.xc = its nearest node to x_new; L.xn = x_new (node of the other tree).
-__device__ void connect_graphs(const Ctx& C, PlanLds& L, int t) {
+// t = tree_B; g_L.xc = its nearest node to x_new; g_L.xn = x_new (node of the other tree).
+__device__ void connect_graphs(const Ctx& C, int t) {
   if (threadIdx.x == 0) {
-    L.tree_expand = 0;
-    L.best_nv = 10000.0;
-    L.n_via = 0;
-    for (int k = 0; k < 3; ++k) L.csp[k] = L.S.cbest[k];
-    for (int j = 0; j < NJ; ++j) { L.eg_start[0][j] = L.xc.q[j]; L.eg_target[0][j] = L.xn.q[j]; }
-    for (int k = 0; k < 3; ++k) L.eg_base[0][k] = L.xc.c[k];
-    L.sel.id = -1;
+    g_L.tree_expand = 0;
+    g_L.best_nv = 10000.0;
+    g_L.n_via = 0;
+    for (int k = 0; k < 3; ++k) g_L.csp[k] = g_L.S.cbest[k];
+    for (int j = 0; j < NJ; ++j) { g_L.eg_start[0][j] = g_L.xc.q[j]; g_L.eg_target[0][j] = g_L.xn.q[j]; }
+    for (int k = 0; k < 3; ++k) g_L.eg_base[0][k] = g_L.xc.c[k];
+    g_L.sel.id = -1;
   }
   __syncthreads();
-  edge_costs(C, L, 1);
+  edge_costs(C, 1);
   if (threadIdx.x == 0) {
-    for (int k = 0; k < 3; ++k) L.sol[k] = L.eg_cost[0][k] + L.xn.c[k];
-    L.eg_need[0] = L.sol[0] < L.csp[0];
+    for (int k = 0; k < 3; ++k) g_L.sol[k] = g_L.eg_cost[0][k] + g_L.xn.c[k];
+    g_L.eg_need[0] = g_L.sol[0] < g_L.csp[0];
   }
   __syncthreads();
-  if (L.eg_need[0]) {
-    edge_validity(C, L, 1);
+  if (g_L.eg_need[0]) {
+    edge_validity(C, 1, false);
     if (threadIdx.x == 0) {
-      int f = L.eg_first[0];
-      count_edge(L, f);
-      L.flag = 0;
-      if (f > L.S.n_pts) {  // valid: connect, stepping without collision checks
-        for (int k = 0; k < 3; ++k) L.csp[k] = L.sol[k];
-        L.flag = 1;
+      int f = g_L.eg_first[0];
+      count_edge(f);
+      g_L.flag = 0;
+      if (f > g_L.S.n_pts) {  // valid: connect, stepping without collision checks
+        for (int k = 0; k < 3; ++k) g_L.csp[k] = g_L.sol[k];
+        g_L.flag = 1;
       } else {
         int lv = f == 0 ? 0 : f - 1;
         if (lv != 0) {  // extend towards the last valid configuration
-          for (int j = 0; j < NJ; ++j) L.ext[j] = L.eg_start[0][j] + lv * L.eg_step[0][j];
-          L.flag = 2;
+          for (int j = 0; j < NJ; ++j) g_L.ext[j] = g_L.eg_start[0][j] + lv * g_L.eg_step[0][j];
+          g_L.flag = 2;
         }
       }
-      L.nn_t = L.S.n[t];
-      L.cur = L.xc;
+      g_L.nn_t = g_L.S.n[t];
+      g_L.cur = g_L.xc;
     }
     __syncthreads();
-    if (L.flag == 1) {
-      via_chain(C, L, L.xn.q);
-      if (threadIdx.x == 0) L.tree_expand = 0;
-    } else if (L.flag == 2) {
-      via_chain(C, L, L.ext);
-      if (threadIdx.x == 0) { L.tree_expand = 1; L.best_nv = L.sol[0]; }
+    if (g_L.flag == 1) {
+      via_chain(C, g_L.xn.q);
+      if (threadIdx.x == 0) g_L.tree_expand = 0;
+    } else if (g_L.flag == 2) {
+      via_chain(C, g_L.ext);
+      if (threadIdx.x == 0) { g_L.tree_expand = 1; g_L.best_nv = g_L.sol[0]; }
     }
     __syncthreads();
   }
-  if (L.S.have_sol) {
-    near_set<20>(C, L, t, L.xn.q, L.xn.id);
+  if (g_L.S.have_sol) {
+    near_set<20>(C, t, g_L.xn.q, g_L.xn.id);
     if (threadIdx.x == 0) {
-      int m = min(L.n_lo, L.S.max_near);
-      L.cnt = m;
+      int m = min(g_L.n_lo, g_L.S.max_near);
+      g_L.cnt = m;
     }
     __syncthreads();
-    const int E = L.cnt;
+    const int E = g_L.cnt;
     if (E > 0) {
       if (threadIdx.x < E) {
         int e = threadIdx.x;
         NodeRef nd;
-        load_node(C, t, L.lo_i[e], &nd);
-        for (int j = 0; j < NJ; ++j) { L.eg_start[e][j] = nd.q[j]; L.eg_target[e][j] = L.xn.q[j]; }
-        for (int k = 0; k < 3; ++k) L.eg_base[e][k] = nd.c[k];
-        L.eg_near[e] = nd.id;
+        load_node(C, t, g_L.lo_i[e], &nd);
+        for (int j = 0; j < NJ; ++j) { g_L.eg_start[e][j] = nd.q[j]; g_L.eg_target[e][j] = g_L.xn.q[j]; }
+        for (int k = 0; k < 3; ++k) g_L.eg_base[e][k] = nd.c[k];
+        g_L.eg_near[e] = nd.id;
       }
       __syncthreads();
-      edge_costs(C, L, E);
+      edge_costs(C, E);
       if (threadIdx.x < E) {
         int e = threadIdx.x;
-        double s0 = L.eg_cost[e][0] + L.xn.c[0];
-        L.eg_need[e] = (L.lo_c[e] < L.xn.c[0]) && (s0 < L.csp[0]);
+        double s0 = g_L.eg_cost[e][0] + g_L.xn.c[0];
+        g_L.eg_need[e] = (g_L.lo_c[e] < g_L.xn.c[0]) && (s0 < g_L.csp[0]);
       }
-      for (int e = E + threadIdx.x; e < MAXE; e += BLOCK) L.eg_need[e] = 0;
+      for (int e = E + threadIdx.x; e < MAXE; e += BLOCK) g_L.eg_need[e] = 0;
       __syncthreads();
-      edge_validity(C, L, E);
+      edge_validity(C, E, true);
       // sequential replay of the near loop (birrt_star.cpp:2820-3030)
       for (int e = 0; e < E; ++e) {
         if (threadIdx.x == 0) {
-          L.flag = 0;
-          if (L.eg_need[e]) {
-            double sol0 = L.eg_cost[e][0] + L.xn.c[0];
-            double sol1 = L.eg_cost[e][1] + L.xn.c[1];
-            double sol2 = L.eg_cost[e][2] + L.xn.c[2];
-            int f = L.eg_first[e];
-            count_edge(L, f);
-            if (f > L.S.n_pts) {
-              L.csp[0] = sol0; L.csp[1] = sol1; L.csp[2] = sol2;
-              L.flag = 1;
-            } else if (L.csp[0] == L.S.cbest[0] && sol0 < L.best_nv) {
+          g_L.flag = 0;
+          if (g_L.eg_need[e]) {
+            double sol0 = g_L.eg_cost[e][0] + g_L.xn.c[0];
+            double sol1 = g_L.eg_cost[e][1] + g_L.xn.c[1];
+            double sol2 = g_L.eg_cost[e][2] + g_L.xn.c[2];
+            int f = g_L.eg_first[e];
+            count_edge(f);
+            if (f > g_L.S.n_pts) {
+              g_L.csp[0] = sol0; g_L.csp[1] = sol1; g_L.csp[2] = sol2;
+              g_L.flag = 1;
+            } else if (g_L.csp[0] == g_L.S.cbest[0] && sol0 < g_L.best_nv) {
               int lv = f == 0 ? 0 : f - 1;
               if (lv != 0) {
-                for (int j = 0; j < NJ; ++j) L.ext[j] = L.eg_start[e][j] + lv * L.eg_step[e][j];
-                L.flag = 2;
-                L.sol[0] = sol0;
+                for (int j = 0; j < NJ; ++j) g_L.ext[j] = g_L.eg_start[e][j] + lv * g_L.eg_step[e][j];
+                g_L.flag = 2;
+                g_L.sol[0] = sol0;
               }
             }
-            if (L.flag) {
-              L.n_via = 0;
-              L.nn_t = L.S.n[t];
-              load_node(C, t, L.eg_near[e], &L.cur);
+            if (g_L.flag) {
+              g_L.n_via = 0;
+              g_L.nn_t = g_L.S.n[t];
+              load_node(C, t, g_L.eg_near[e], &g_L.cur);
             }
           }
         }
         __syncthreads();
-        if (L.flag == 1) {
-          via_chain(C, L, L.xn.q);
-          if (threadIdx.x == 0) L.tree_expand = 0;
+        if (g_L.flag == 1) {
+          via_chain(C, g_L.xn.q);
+          if (threadIdx.x == 0) g_L.tree_expand = 0;
           __syncthreads();
           break;
-        } else if (L.flag == 2) {
-          via_chain(C, L, L.ext);
-          if (threadIdx.x == 0) { L.tree_expand = 1; L.best_nv = L.sol[0]; }
+        } else if (g_L.flag == 2) {
+          via_chain(C, g_L.ext);
+          if (threadIdx.x == 0) { g_L.tree_expand = 1; g_L.best_nv = g_L.sol[0]; }
           __syncthreads();
         }
       }
     }
   }
-  insert_via(C, L, t);
+  insert_via(C, t);
   if (threadIdx.x == 0) {
-    QState& S = L.S;
-    if (L.csp[0] < S.cbest[0]) {
+    QState& S = g_L.S;
+    if (g_L.csp[0] < S.cbest[0]) {
       if (!S.have_sol) {
         S.first_iter = S.iter;
         S.t_first = wall_clock64();
       }
       S.have_sol = 1;
-      insert_node(C, L, t, L.sel_start, L.sel_target, L.sel);
+      insert_node(C, t, g_L.sel_start, g_L.sel_target, g_L.sel);
       S.conn_start = (t == 0);
-      S.nB = L.sel;
-      S.nA = L.xn;
-      for (int k = 0; k < 3; ++k) S.cbest[k] = L.csp[k];
+      S.nB = g_L.sel;
+      S.nA = g_L.xn;
+      for (int k = 0; k < 3; ++k) S.cbest[k] = g_L.csp[k];
       S.last_iter = S.iter;
-    } else if (L.tree_expand) {
-      insert_node(C, L, t, L.sel_start, L.sel_target, L.sel);
+    } else if (g_L.tree_expand) {
+      insert_node(C, t, g_L.sel_start, g_L.sel_target, g_L.sel);
     }
   }
   __syncthreads();
 }
 
 // One C-space iteration of run_planner (birrt_star.cpp:1163-1338).
-__device__ void iteration(const Ctx& C, PlanLds& L) {
-  const int A = L.S.A, B = 1 - A;
+__device__ void iteration(const Ctx& C) {
+  const int A = g_L.S.A, B = 1 - A;
   unsigned long long _t0 = threadIdx.x == 0 ? wall_clock64() : 0, _t1;
-#define PHASE(k) if (threadIdx.x == 0) { _t1 = wall_clock64(); L.S.prof[k] += _t1 - _t0; _t0 = _t1; }
-  if (L.S.informed && L.S.have_sol) sample_ellipse(C, L); else sample_uniform(C, L);
+#define PHASE(k) if (threadIdx.x == 0) { _t1 = wall_clock64(); g_L.S.prof[k] += _t1 - _t0; _t0 = _t1; }
+  if (g_L.S.informed && g_L.S.have_sol) sample_ellipse(C); else sample_uniform(C);
   PHASE(P_SAMPLE);
-  int nid = nearest(C, L, A, L.xr);
+  int nid = nearest(C, A, g_L.xr);
   PHASE(P_NN);
   if (threadIdx.x == 0) {
-    load_node(C, A, nid, &L.nn);
+    load_node(C, A, nid, &g_L.nn);
     // expandTree single step (birrt_star.cpp:2224-2256)
-    for (int j = 0; j < NJ; ++j) L.ext[j] = L.xr[j];
-    step_towards(C.rb, L.nn.q, L.ext, L.S.step);
-    for (int j = 0; j < NJ; ++j) { L.eg_start[0][j] = L.nn.q[j]; L.eg_target[0][j] = L.ext[j]; }
-    for (int k = 0; k < 3; ++k) L.eg_base[0][k] = L.nn.c[k];
-    L.eg_need[0] = 1;
+    for (int j = 0; j < NJ; ++j) g_L.ext[j] = g_L.xr[j];
+    step_towards((&g_rb), g_L.nn.q, g_L.ext, g_L.S.step);
+    for (int j = 0; j < NJ; ++j) { g_L.eg_start[0][j] = g_L.nn.q[j]; g_L.eg_target[0][j] = g_L.ext[j]; }
+    for (int k = 0; k < 3; ++k) g_L.eg_base[0][k] = g_L.nn.c[k];
+    g_L.eg_need[0] = 1;
   }
   __syncthreads();
-  edge_costs(C, L, 1);
-  edge_validity(C, L, 1);
+  edge_costs(C, 1);
+  edge_validity(C, 1, false);
   if (threadIdx.x == 0) {
-    int f = L.eg_first[0];
-    count_edge(L, f);
-    L.ext_nn = f > L.S.n_pts;
-    if (L.ext_nn) {
-      for (int j = 0; j < NJ; ++j) { L.xn.q[j] = L.eg_end[0][j]; L.en_start[j] = L.eg_start[0][j]; L.en_target[j] = L.eg_target[0][j]; }
-      for (int k = 0; k < 3; ++k) L.xn.c[k] = L.eg_cost[0][k];
-      L.xn.id = L.S.n[A];
-      L.xn.parent = L.nn.id;
+    int f = g_L.eg_first[0];
+    count_edge(f);
+    g_L.ext_nn = f > g_L.S.n_pts;
+    if (g_L.ext_nn) {
+      for (int j = 0; j < NJ; ++j) { g_L.xn.q[j] = g_L.eg_end[0][j]; g_L.en_start[j] = g_L.eg_start[0][j]; g_L.en_target[j] = g_L.eg_target[0][j]; }
+      for (int k = 0; k < 3; ++k) g_L.xn.c[k] = g_L.eg_cost[0][k];
+      g_L.xn.id = g_L.S.n[A];
+      g_L.xn.parent = g_L.nn.id;
     } else {  // x_new = x_rand with cost 10000 (birrt_star.cpp:1213-1217, 2252-2255)
-      for (int j = 0; j < NJ; ++j) L.xn.q[j] = L.xr[j];
-      L.xn.c[0] = 10000.0; L.xn.c[1] = 0.0; L.xn.c[2] = 0.0;
-      L.xn.id = L.S.n[A];
-      L.xn.parent = L.nn.id;
+      for (int j = 0; j < NJ; ++j) g_L.xn.q[j] = g_L.xr[j];
+      g_L.xn.c[0] = 10000.0; g_L.xn.c[1] = 0.0; g_L.xn.c[2] = 0.0;
+      g_L.xn.id = g_L.S.n[A];
+      g_L.xn.parent = g_L.nn.id;
     }
-    L.ext_bp = 0;
-    L.nk = 0;
+    g_L.ext_bp = 0;
+    g_L.nk = 0;
   }
   __syncthreads();
   PHASE(P_EXPAND);
-  const bool opt = L.S.tree_opt && L.S.have_sol;
+  const bool opt = g_L.S.tree_opt && g_L.S.have_sol;
   if (opt) {
-    near_set<20>(C, L, A, L.xn.q, L.xn.id);
+    near_set<20>(C, A, g_L.xn.q, g_L.xn.id);
     PHASE(P_NEAR);
-    choose_parent(C, L, A);
+    choose_parent(C, A);
     PHASE(P_CHOOSE);
   }
-  if (L.ext_nn || L.ext_bp) {
-    if (threadIdx.x == 0) insert_node(C, L, A, L.en_start, L.en_target, L.xn);
+  if (g_L.ext_nn || g_L.ext_bp) {
+    if (threadIdx.x == 0) insert_node(C, A, g_L.en_start, g_L.en_target, g_L.xn);
     __syncthreads();
-    if (opt) rewire(C, L, A);
+    if (opt) rewire(C, A);
     PHASE(P_REWIRE);
-    int cid = nearest(C, L, B, L.xn.q);
-    if (threadIdx.x == 0) load_node(C, B, cid, &L.xc);
+    int cid = nearest(C, B, g_L.xn.q);
+    if (threadIdx.x == 0) load_node(C, B, cid, &g_L.xc);
     __syncthreads();
     PHASE(P_NN);
-    connect_graphs(C, L, B);
+    connect_graphs(C, B);
     PHASE(P_CONNECT);
   }
 #undef PHASE
   if (threadIdx.x == 0) {
-    QState& S = L.S;
+    QState& S = g_L.S;
     S.A = B;
     S.iter++;
     if (C.Q.rows && S.n_rows < C.Q.rows_cap) {
@@ -977,36 +1016,34 @@ __device__ void iteration(const Ctx& C, PlanLds& L) {
 // Advances every query (one workgroup each) by at most `iters` planner iterations.
 __global__ void __launch_bounds__(BLOCK) plan_kernel(const RobotDev* __restrict__ rb, SceneDev sc,
                                                      const MapCfg* __restrict__ mc, QueryDev* qs, int iters) {
-  __shared__ PlanLds L;
+  stage_model(rb, mc, &g_rb, &g_mc);
   Ctx C;
-  C.rb = rb;
   C.sc = sc;
-  C.mc = mc;
   C.Q = qs[blockIdx.x];
   if (threadIdx.x == 0) {
-    L.S = *C.Q.st;
-    if (L.S.phase == 0 && L.S.t0 == 0) L.S.t0 = wall_clock64();
-    L.n_via = 0;
+    g_L.S = *C.Q.st;
+    if (g_L.S.phase == 0 && g_L.S.t0 == 0) g_L.S.t0 = wall_clock64();
+    g_L.n_via = 0;
   }
   __syncthreads();
-  if (L.S.status == 0 && L.S.phase == 0) {
+  if (g_L.S.status == 0 && g_L.S.phase == 0) {
     // pre-loop direct connection of the two roots (birrt_star.cpp:1072-1075)
     if (threadIdx.x == 0) {
-      load_node(C, 1, 0, &L.xn);
-      load_node(C, 0, 0, &L.xc);
+      load_node(C, 1, 0, &g_L.xn);
+      load_node(C, 0, 0, &g_L.xc);
     }
     __syncthreads();
-    connect_graphs(C, L, 0);
-    if (threadIdx.x == 0) L.S.phase = L.S.have_sol ? 2 : 1;
+    connect_graphs(C, 0);
+    if (threadIdx.x == 0) g_L.S.phase = g_L.S.have_sol ? 2 : 1;
     __syncthreads();
   }
   for (int k = 0; k < iters; ++k) {
-    if (L.S.status != 0 || L.S.phase != 1) break;
-    iteration(C, L);
+    if (g_L.S.status != 0 || g_L.S.phase != 1) break;
+    iteration(C);
   }
   if (threadIdx.x == 0) {
-    if (L.S.phase == 2 && L.S.t_end == 0) L.S.t_end = wall_clock64();
-    *C.Q.st = L.S;
+    if (g_L.S.phase == 2 && g_L.S.t_end == 0) g_L.S.t_end = wall_clock64();
+    *C.Q.st = g_L.S;
   }
 }
 

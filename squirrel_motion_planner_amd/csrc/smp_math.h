@@ -78,10 +78,8 @@ SMP_HD void xform(const Frame& F, const double* c, double* o) {
   }
 }
 
-// KDL Rotation::Rot2(axis, angle)
-SMP_HD void rot2(const double* ax, double q, double* R) {
-  double st, ct;
-  psincos(q, &st, &ct);
+// KDL Rotation::Rot2(axis, angle) from sin/cos of the angle
+SMP_HD void rot2_sc(const double* ax, double st, double ct, double* R) {
   double vt = 1 - ct;
   double m_vt_0 = vt * ax[0], m_vt_1 = vt * ax[1], m_vt_2 = vt * ax[2];
   double m_st_0 = ax[0] * st, m_st_1 = ax[1] * st, m_st_2 = ax[2] * st;
@@ -89,6 +87,13 @@ SMP_HD void rot2(const double* ax, double q, double* R) {
   R[0] = ct + m_vt_0 * ax[0]; R[1] = -m_st_2 + m_vt_0_1; R[2] = m_st_1 + m_vt_0_2;
   R[3] = m_st_2 + m_vt_0_1;  R[4] = ct + m_vt_1 * ax[1]; R[5] = -m_st_0 + m_vt_1_2;
   R[6] = -m_st_1 + m_vt_0_2; R[7] = m_st_0 + m_vt_1_2;  R[8] = ct + m_vt_2 * ax[2];
+}
+
+// KDL Rotation::Rot2(axis, angle)
+SMP_HD void rot2(const double* ax, double q, double* R) {
+  double st, ct;
+  psincos(q, &st, &ct);
+  rot2_sc(ax, st, ct, R);
 }
 
 // Philox4x32-10 counter RNG.  Draw (seed, query, iteration, outer attempt, inner attempt, joint idx).

@@ -11,6 +11,7 @@ constexpr int MAX_CLINK = 32;   // collision links (27)
 constexpr int MAX_PAIRS = 256;  // self-collision link pairs (165 non-rigid of the 230 SRDF-enabled)
 constexpr int MAX_BODY = 8;     // moving bodies (6)
 constexpr int NJ = 8;           // planning joints
+constexpr int BLOCK = 512;      // threads per workgroup (8 wavefronts, 2 per SIMD)
 
 // Robot model (kinematics + sphere collision model).  Collision links are re-indexed into compact
 // "clink" slots; spheres are sorted by clink so each link owns a contiguous range.
@@ -30,19 +31,20 @@ struct RobotDev {
   int rev[NJ];
 };
 
-// Occupancy grid of one scene (device pointers).  Cell (i,j,k) is the box
-// [o + i*res, o + (i+1)*res] per axis; bits are x-major rows of 64-bit words (bit i&63 of word i>>6);
-// d2 is the squared centre-to-centre distance (voxel units, clamped to 65535) to the nearest occupied cell.
+// Occupancy grid of one scene (device pointers).  Cell (i,j,k) is the box [o + i*res, o + (i+1)*res] per
+// axis.  bricks: one 64-bit occupancy mask per 4x4x4 cells, bit (k&3)*16 + (j&3)*4 + (i&3) of brick
+// ((k>>2)*bny + (j>>2))*bnx + (i>>2).  d2: per cell the squared box-to-box gap (voxel units, clamped to
+// 65535) to the nearest occupied cell -- a lower bound of (distance to any occupied box / res)^2.
 struct SceneDev {
-  int nx, ny, nz, wx;
+  int nx, ny, nz, bnx, bny;
   double ox, oy, oz, res;
-  const uint64_t* bits;
+  const uint64_t* bricks;
   const uint16_t* d2;
 };
 
 // Per (scene, disabled-link set) sphere constants.
 struct MapCfg {
-  uint32_t T[MAX_SPH];      // d2 prefilter threshold: free if d2 > T (r + sqrt(3) voxels)
+  uint32_t T[MAX_SPH];      // d2 prefilter threshold: free if d2 > T = floor(((r + 1e-6) / res)^2)
   int32_t map_on[MAX_SPH];  // 0 if the sphere's link is excluded from the map check
   int32_t has_map;          // scene present
 };

@@ -209,7 +209,7 @@ def _result_dict(r):
     d["cost_best"] = list(s.cost_best)
     d["cost_theoretical"] = list(s.cost_theoretical)
     names = ["sample", "nearest", "expand", "near", "choose_parent", "rewire", "connect", "collide_tiles",
-             "n_tiles", "edge_costs", "via_chains", "n_via_steps", "tile_fk", "tile_map", "tile_self"]
+             "n_tiles", "edge_costs", "via_chains", "n_via_steps", "tile_fk", "tile_tests"]
     d["phases"] = {n: s.phase_seconds[i] for i, n in enumerate(names)}
     d["status"] = r.status
     n = r.n_waypoints

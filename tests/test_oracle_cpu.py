@@ -96,15 +96,40 @@ def test_room_fixture(room):
         assert np.array_equal(np.unique(keys, axis=0), np.unique(f["keys"].astype(np.int64), axis=0))
 
 
-def test_oracle_scene_edt_matches_bruteforce():
+def test_oracle_scene_box_gap_matches_bruteforce():
+    """d2 = squared box-to-box gap (voxels) to the nearest occupied cell: sum over axes of max(|du| - 1, 0)^2."""
     rng = np.random.default_rng(4)
     keys = 32768 + rng.integers(0, 12, (30, 3))
     g = O.OracleScene(keys, 0.05)
     occ = g.occ
     pts = np.argwhere(occ)
     idx = np.argwhere(np.ones_like(occ))
-    d2 = ((idx[:, None, :] - pts[None, :, :]) ** 2).sum(-1).min(1)
+    gap = np.maximum(np.abs(idx[:, None, :] - pts[None, :, :]) - 1, 0)
+    d2 = (gap ** 2).sum(-1).min(1)
     assert np.array_equal(g.d2, np.minimum(d2, 65535).astype(np.uint16))
+
+
+def test_box_gap_is_a_lower_bound_of_the_exact_map_test():
+    """Random spheres: whenever the prefilter says free (d2 > floor(((r + 1e-6)/res)^2)), no occupied box is
+    within r of the centre (brute force over every occupied box)."""
+    rng = np.random.default_rng(5)
+    keys = 32768 + rng.integers(0, 16, (60, 3))
+    g = O.OracleScene(keys, 0.05)
+    occ_idx = np.argwhere(g.occ)  # (k, j, i)
+    lo = np.stack([g.ox + occ_idx[:, 2] * g.res, g.oy + occ_idx[:, 1] * g.res, g.oz + occ_idx[:, 0] * g.res], 1)
+    hi = lo + g.res
+    d2 = g.d2.reshape(g.occ.shape)
+    n_free = 0
+    for _ in range(3000):
+        c = np.array([g.ox, g.oy, g.oz]) + rng.uniform(0, 1, 3) * np.array([g.nx, g.ny, g.nz]) * g.res
+        r = rng.uniform(0.001, 0.3)
+        ci = np.floor((c - np.array([g.ox, g.oy, g.oz])) / g.res).astype(int)
+        T = np.floor(((r + 1e-6) / g.res) ** 2)
+        if d2[ci[2], ci[1], ci[0]] > T:
+            n_free += 1
+            gap = np.maximum(np.maximum(lo - c, c - hi), 0.0)
+            assert (gap ** 2).sum(1).min() > r * r
+    assert n_free > 500
 
 
 @pytest.mark.parametrize("name", ["c1_direct", "c2_boxes_300", "c2_boxes_yaml", "c4_passage"])
