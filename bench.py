@@ -1,9 +1,9 @@
 #!/usr/bin/env python3
 """Benchmark of the BiRRT* hot path on MI355X (BASELINE.json metric).
 
-A step = one planning query of the C2 configuration (single query, 10 m x 10 m x 2 m octomap @ 5 cm with 20
-box obstacles, iteration budget --iterations; path_optimality_threshold = -inf so the whole budget runs,
-SURVEY.md 8d) through the C ABI.  value = collision-checked configurations per second over all ranks
+A step = one planning query of the C2 configuration (BASELINE.json configs[1]: single query, 10 m x 10 m x 2 m
+octomap @ 5 cm with 20 box obstacles, budget of 1e6 collision-checked samples; path_optimality_threshold = -inf
+so the whole budget runs) through the C ABI.  value = collision-checked configurations per second over all ranks
 (reference semantics: every isInCollision call up to the first collision of an edge).  With N GPUs each rank
 plans its own queries against the scene rank 0 broadcast over RCCL (weak scaling, no per-iteration
 collectives).  rank 0 prints one JSON line.
@@ -29,22 +29,26 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--iterations", type=int, default=int(os.environ.get("SMP_BENCH_ITERS", 1_000_000)))
-    ap.add_argument("--warmup-iterations", type=int, default=2000)
+    ap.add_argument("--samples", type=int, default=int(os.environ.get("SMP_BENCH_SAMPLES", 1_000_000)),
+                    help="budget of collision-checked configurations per query")
+    ap.add_argument("--warmup-samples", type=int, default=None,
+                    help="budget of each warmup query (default: --samples, so warmup launches match timed ones)")
     ap.add_argument("--queries-per-gpu", type=int, default=1)
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
 
 
-def cpu_baseline(sc, seconds, seed):
-    """The oracle (sequential C++ restatement, 1 thread) on the same query for a bounded time."""
+def cpu_baseline(sc, samples, seed):
+    """The oracle (sequential C++ restatement of the reference loop, 1 thread) on the same query and budget.
+
+    Same seed, scene and sample budget as GPU step 0, so the CPU run plans the identical trees; the bench
+    records whether its counters match the GPU's (a parity check of the measured run itself)."""
     from oracle import oracle as O
     rob = O.OracleRobot(os.path.join(ROOT, "squirrel_motion_planner_amd", "data", "robotino_model.json"))
     orc = O.Oracle(rob, O.OracleScene(sc.keys, sc.res))
-    r = orc.plan(sc.start, sc.goal, env_x=sc.env_x, env_y=sc.env_y, max_time=seconds, seed=seed,
+    r = orc.plan(sc.start, sc.goal, env_x=sc.env_x, env_y=sc.env_y, max_checked=samples, seed=seed,
                  opt_thresh=-math.inf)
     cpu = "unknown"
     try:
@@ -55,11 +59,12 @@ def cpu_baseline(sc, seconds, seed):
     except OSError:
         pass
     return {"value": r["checked"] / r["t_total"], "unit": "configs/s", "cores": 1, "kind": "port",
-            "sample": "C2 query (seed %d), oracle/smp_oracle.cpp single thread, time budget %.0f s: %d iterations, "
-                      "%d configs checked in %.2f s on %s" % (seed, seconds, r["iterations"], r["checked"],
+            "sample": "C2 query (seed %d), oracle/smp_oracle.cpp single thread, budget %d samples: %d iterations, "
+                      "%d configs checked in %.2f s on %s" % (seed, samples, r["iterations"], r["checked"],
                                                            r["t_total"], cpu),
-            "iterations": r["iterations"], "time_first_solution_s": r["t_first"],
-            "iters_per_s": r["iterations"] / r["t_total"]}
+            "valid_configs_per_s": r["valid"] / r["t_total"],
+            "iterations": r["iterations"], "checked": r["checked"], "time_first_solution_s": r["t_first"],
+            "iters_per_s": r["iterations"] / r["t_total"], "cost_best": r["cost"][0]}
 
 
 def main():
@@ -108,25 +113,28 @@ def main():
     gp = GpuPlanner(device=local, path_optimality_threshold=-math.inf)
     gp.set_scene(scene)
 
-    def queries(step, iters):
+    def queries(step, samples):
         out = []
         for k in range(a.queries_per_gpu):
             qid = rank * a.queries_per_gpu + k
-            out.append(GpuPlanner.make_query(sc.start, sc.goal, sc.env_x, sc.env_y, iterations=iters,
+            out.append(GpuPlanner.make_query(sc.start, sc.goal, sc.env_x, sc.env_y, samples=samples,
                                              seed=a.seed + 1000 * step, query_id=qid))
         return out
 
     for w in range(a.warmup):
-        gp.plan_batch(queries(-1 - w, a.warmup_iterations))
+        gp.plan_batch(queries(-1 - w, a.warmup_samples or a.samples))
 
     totals = dict(checked=0, valid=0, iters=0, nn=0, near=0, plan_ms=0.0, launches=0)
     first_t = []
+    step0 = None
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for step in range(a.steps):
-        rs = gp.plan_batch(queries(step, a.iterations))
+        rs = gp.plan_batch(queries(step, a.samples))
+        if step0 is None:
+            step0 = rs[0]
         for r in rs:
             if r["status"] not in (0, -4):
                 raise RuntimeError("plan failed with status %d" % r["status"])
@@ -161,12 +169,15 @@ def main():
 
     if rank == 0:
         alg_bytes_rank0 = 64.0 * totals["nn"] + 72.0 * totals["near"] + BYTES_PER_CONFIG * totals["checked"]
+        # per launch: algorithmic bytes of one launch / its average duration (HIP events on the planner stream)
         achieved = alg_bytes_rank0 / (plan_ms_rank0 * 1e-3) / 1e9 if plan_ms_rank0 > 0 else 0.0
         traffic = None
-        pmc = os.path.join(ROOT, "profiles", "pmc_plan_kernel.json")
-        if os.path.exists(pmc):
+        # HBM bytes per launch from the latest committed rocprofv3 FETCH_SIZE/WRITE_SIZE pass of this bench
+        import glob
+        pmcs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_plan_kernel.json")))
+        if pmcs:
             try:
-                traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+                traffic = json.load(open(pmcs[-1])).get("hbm_bytes_per_launch")
             except (OSError, ValueError):
                 traffic = None
         out = {
@@ -182,9 +193,9 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (seeded box scene + seeded Philox samples)",
-            "config": {"workload": "C2: single start->goal query, 10x10x2 m octomap @5 cm, 20 boxes, %d-iteration "
-                                   "budget, path_optimality_threshold=-inf" % a.iterations,
-                       "queries_per_gpu": a.queries_per_gpu, "iterations_per_query": a.iterations,
+            "config": {"workload": "C2: single start->goal query, 10x10x2 m octomap @5 cm, 20 boxes, budget %d "
+                                   "collision-checked samples, path_optimality_threshold=-inf" % a.samples,
+                       "queries_per_gpu": a.queries_per_gpu, "samples_per_query": a.samples,
                        "robot": "robotino 8-DoF, 64-sphere model", "parallelism": "one workgroup per query, "
                        "queries sharded over ranks, scene broadcast once"},
             "valid_configs_per_s": valid / elapsed,
@@ -193,11 +204,16 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "smp::plan_kernel", "kernel_ms_rank0": plan_ms_rank0,
+                         "avg_launch_ms": plan_ms_rank0 / max(totals["launches"], 1),
                          "launches_rank0": totals["launches"],
                          "algorithmic_bytes_rank0": alg_bytes_rank0},
         }
         if not a.no_cpu and world == 1:
-            out["cpu_baseline"] = cpu_baseline(sc, a.cpu_seconds, a.seed)
+            cb = cpu_baseline(sc, a.samples, a.seed)
+            cb["same_result_as_gpu_step0"] = bool(cb["checked"] == step0["configs_checked"] and
+                                                  cb["iterations"] == step0["iterations"] and
+                                                  cb["cost_best"] == step0["cost_best"][0])
+            out["cpu_baseline"] = cb
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)

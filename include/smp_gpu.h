@@ -50,6 +50,8 @@ enum {
   SMP_ERR_NO_DEVICE = -8      /* no usable GPU: the library never falls back to the CPU */
 };
 
+enum { SMP_BUDGET_ITERATIONS = 0, SMP_BUDGET_SECONDS = 1, SMP_BUDGET_SAMPLES = 2 };
+
 typedef struct smp_robot smp_robot;
 typedef struct smp_scene smp_scene;
 typedef struct smp_planner smp_planner;
@@ -80,8 +82,9 @@ typedef struct smp_query {
   double env_y[2];
   int check_self;
   int check_map;
-  int budget_is_time;      /* 0: max iterations (flag_iter_or_time = 0), 1: max seconds */
-  double budget;           /* iterations or seconds */
+  int budget_kind;         /* SMP_BUDGET_*: iterations (flag_iter_or_time = 0), seconds (= 1), or
+                              collision-checked configurations (checked before each iteration) */
+  double budget;
   uint64_t seed;
   uint32_t query_id;       /* RNG stream of this query */
 } smp_query;
@@ -138,6 +141,10 @@ int smp_scene_export(const smp_scene* s, uint64_t* bits, uint16_t* d2);
 int smp_planner_create(int device, const smp_robot* robot, const smp_params* params, smp_planner** out);
 void smp_planner_destroy(smp_planner* p);
 int smp_planner_set_scene(smp_planner* p, const smp_scene* s);
+/* Planner parameters for subsequent smp_plan calls (activate/deactivateTreeOptimization,
+ * activate/deactivateInformedSampling, birrt_star.h:57-63; setEdgeCostWeights keeps weights 1). */
+int smp_planner_set_params(smp_planner* p, const smp_params* params);
+int smp_planner_get_params(const smp_planner* p, smp_params* params);
 int smp_set_disabled_map_links(smp_planner* p, const char* const* link_names, int n);
 
 int smp_plan(smp_planner* p, const smp_query* q, smp_result* out);

@@ -46,7 +46,7 @@ class Params(ctypes.Structure):
     _fields_ = [("near_r", _d), ("step", _d), ("n_pts", _i), ("max_near", _i), ("opt_thresh", _d),
                 ("tree_opt", _i), ("informed", _i), ("env_x", _d * 2), ("env_y", _d * 2),
                 ("self_", _i), ("map", _i), ("seed", ctypes.c_uint64), ("query", ctypes.c_uint32),
-                ("max_iter", _i), ("max_time", _d)]
+                ("max_iter", _i), ("max_time", _d), ("max_checked", ctypes.c_longlong)]
 
 
 class Result(ctypes.Structure):
@@ -245,7 +245,7 @@ class OracleScene:
 # ------------------------------------------------------------------------------------------ planner
 DEFAULT_PARAMS = dict(near_r=4.0, step=0.5, n_pts=20, max_near=20, opt_thresh=1.0, tree_opt=1, informed=1,
                       env_x=(0.0, 0.0), env_y=(0.0, 0.0), self_=1, map=1, seed=1, query=0, max_iter=1000,
-                      max_time=0.0)
+                      max_time=0.0, max_checked=0)
 
 
 class Oracle:

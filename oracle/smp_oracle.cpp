@@ -351,6 +351,7 @@ struct Params {
   uint32_t query = 0;
   int max_iter = 1000;
   double max_time = 0;         // >0: time budget instead of iterations (flag_iter_or_time = 1)
+  long long max_checked = 0;   // >0: budget of collision-checked configurations instead of iterations
 };
 
 struct Stats {
@@ -886,7 +887,11 @@ struct Planner {
     bool no_planning = have_sol;
     while (!no_planning) {
       double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-      if (P.max_time > 0 ? !(el < P.max_time) : !(iter < P.max_iter)) break;
+      if (P.max_checked > 0) {
+        if (!(st.checked < P.max_checked)) break;
+      } else if (P.max_time > 0 ? !(el < P.max_time) : !(iter < P.max_iter)) {
+        break;
+      }
       Node xr;
       if (P.informed && have_sol) sample_ellipse(xr.q); else sample_uniform(xr.q);
       xr.node_id = (int)A->nodes.size();
@@ -994,6 +999,7 @@ struct orc_params {
   uint32_t query;
   int max_iter;
   double max_time;
+  long long max_checked;
 };
 
 struct orc_result {
@@ -1150,7 +1156,7 @@ int orc_plan(void* hp, const double* start, const double* goal, const orc_params
   pl.P.opt_thresh = p->opt_thresh; pl.P.tree_opt = p->tree_opt; pl.P.informed = p->informed;
   pl.P.env_x[0] = p->env_x[0]; pl.P.env_x[1] = p->env_x[1]; pl.P.env_y[0] = p->env_y[0]; pl.P.env_y[1] = p->env_y[1];
   pl.P.self = p->self; pl.P.map = p->map; pl.P.seed = p->seed; pl.P.query = p->query;
-  pl.P.max_iter = p->max_iter; pl.P.max_time = p->max_time;
+  pl.P.max_iter = p->max_iter; pl.P.max_time = p->max_time; pl.P.max_checked = p->max_checked;
   orc::Conf s, g;
   for (int j = 0; j < 8; ++j) { s[j] = start[j]; g[j] = goal[j]; }
   std::memset(res, 0, sizeof(*res));

@@ -21,6 +21,10 @@ SMP_ERR_PARSE = -6
 SMP_ERR_CAPACITY = -7
 SMP_ERR_NO_DEVICE = -8
 
+BUDGET_ITERATIONS = 0
+BUDGET_SECONDS = 1
+BUDGET_SAMPLES = 2
+
 _d = ctypes.c_double
 _i = ctypes.c_int
 _i64 = ctypes.c_int64
@@ -41,7 +45,7 @@ class Params(ctypes.Structure):
 
 class Query(ctypes.Structure):
     _fields_ = [("start", _d * 8), ("goal", _d * 8), ("env_x", _d * 2), ("env_y", _d * 2), ("check_self", _i),
-                ("check_map", _i), ("budget_is_time", _i), ("budget", _d), ("seed", ctypes.c_uint64),
+                ("check_map", _i), ("budget_kind", _i), ("budget", _d), ("seed", ctypes.c_uint64),
                 ("query_id", ctypes.c_uint32)]
 
 
@@ -78,6 +82,8 @@ EXPORTS = [
     ("smp_planner_create", _i, [_i, _p, ctypes.POINTER(Params), ctypes.POINTER(_p)]),
     ("smp_planner_destroy", None, [_p]),
     ("smp_planner_set_scene", _i, [_p, _p]),
+    ("smp_planner_set_params", _i, [_p, ctypes.POINTER(Params)]),
+    ("smp_planner_get_params", _i, [_p, ctypes.POINTER(Params)]),
     ("smp_set_disabled_map_links", _i, [_p, ctypes.POINTER(ctypes.c_char_p), _i]),
     ("smp_plan", _i, [_p, ctypes.POINTER(Query), ctypes.POINTER(Result)]),
     ("smp_plan_batch", _i, [_p, ctypes.POINTER(Query), _i, ctypes.POINTER(Result)]),

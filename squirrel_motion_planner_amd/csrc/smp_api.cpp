@@ -266,6 +266,23 @@ int smp_scene_export(const smp_scene* s, uint64_t* bits, uint16_t* d2) {
   return SMP_OK;
 }
 
+static bool params_ok(const smp_params& q) {
+  return q.max_near_nodes >= 1 && q.max_near_nodes <= 20 && q.num_traj_segments >= 1 && q.num_traj_segments <= MAX_PTS &&
+         q.near_threshold > 0 && q.step_factor > 0 && q.node_capacity >= 0;
+}
+
+int smp_planner_set_params(smp_planner* p, const smp_params* params) {
+  if (!p || !params || !params_ok(*params)) return SMP_ERR_ARG;
+  p->params = *params;
+  return SMP_OK;
+}
+
+int smp_planner_get_params(const smp_planner* p, smp_params* params) {
+  if (!p || !params) return SMP_ERR_ARG;
+  *params = p->params;
+  return SMP_OK;
+}
+
 int smp_planner_create(int device, const smp_robot* robot, const smp_params* params, smp_planner** out) {
   if (!robot || !out) return SMP_ERR_ARG;
   int ndev = 0;
@@ -275,8 +292,7 @@ int smp_planner_create(int device, const smp_robot* robot, const smp_params* par
   p->device = device;
   p->robot = robot->h;
   if (params) p->params = *params; else smp_params_default(&p->params);
-  if (p->params.max_near_nodes > 20 || p->params.max_near_nodes < 1 || p->params.num_traj_segments < 1 ||
-      p->params.num_traj_segments > MAX_PTS) {
+  if (!params_ok(p->params)) {
     delete p;
     return SMP_ERR_ARG;
   }
@@ -404,7 +420,8 @@ static void init_qstate(const smp_planner* p, const smp_query& q, int64_t cap, i
   S->n[0] = S->n[1] = 1;
   S->cap = (int)cap;
   S->via_cap = via_cap;
-  S->max_iter = q.budget_is_time ? (long long)1 << 62 : (long long)q.budget;
+  S->max_iter = q.budget_kind == SMP_BUDGET_ITERATIONS ? (long long)q.budget : (long long)1 << 62;
+  S->max_checked = q.budget_kind == SMP_BUDGET_SAMPLES ? std::max<long long>((long long)q.budget, 1) : 0;
   S->first_iter = -1;
   S->last_iter = -1;
   S->cbest[0] = S->cbest[1] = S->cbest[2] = 10000.0;
@@ -526,15 +543,20 @@ extern "C" int smp_plan_batch(smp_planner* p, const smp_query* qs, int nq, smp_r
   for (int i = 0; i < nq; ++i) {
     const smp_query& q = qs[i];
     int64_t cap = p->params.node_capacity;
-    long long iters = q.budget_is_time ? 0 : (long long)q.budget;
-    if (cap <= 0) cap = q.budget_is_time ? (int64_t)4 << 20 : std::min<int64_t>(1024 + 16 * iters, (int64_t)1 << 27);
-    rows_cap[i] = q.budget_is_time ? 1 << 20 : std::max<long long>(iters, 1);
+    const bool by_iter = q.budget_kind == SMP_BUDGET_ITERATIONS;
+    long long iters = by_iter ? (long long)q.budget : 0;
+    if (cap <= 0) {
+      if (by_iter) cap = std::min<int64_t>(1024 + 16 * iters, (int64_t)1 << 27);
+      else if (q.budget_kind == SMP_BUDGET_SAMPLES) cap = std::min<int64_t>(1024 + (int64_t)q.budget / 2, (int64_t)1 << 27);
+      else cap = (int64_t)4 << 20;
+    }
+    rows_cap[i] = by_iter ? std::max<long long>(iters, 1) : 1 << 20;
     int via_cap = 4096;
     HIPCHK(alloc_query(p->qb[i], (size_t)cap, via_cap, rows_cap[i]));
     qdev[i] = make_qdev(p->qb[i], (size_t)cap, rows_cap[i]);
     init_qstate(p, q, cap, via_cap, &S[i]);
     if (status[i] != SMP_OK) { S[i].status = status[i]; S[i].phase = 2; }
-    if (!q.budget_is_time && iters <= 0 && S[i].phase == 0) S[i].max_iter = 0;
+    if (by_iter && iters <= 0 && S[i].phase == 0) S[i].max_iter = 0;
     int st = upload_roots(p, p->qb[i], qdev[i], q, (size_t)cap);
     if (st) return st;
     HIPCHK(hipMemcpyAsync(qdev[i].st, &S[i], sizeof(QState), hipMemcpyHostToDevice, p->stream));
@@ -546,14 +568,15 @@ extern "C" int smp_plan_batch(smp_planner* p, const smp_query* qs, int nq, smp_r
 
   // launch loop: each launch advances every query by `chunk` iterations; time budgets use a device deadline
   double tmax = 0;
-  for (int i = 0; i < nq; ++i) if (qs[i].budget_is_time) tmax = std::max(tmax, qs[i].budget);
+  for (int i = 0; i < nq; ++i) if (qs[i].budget_kind == SMP_BUDGET_SECONDS) tmax = std::max(tmax, qs[i].budget);
   auto t_begin = std::chrono::steady_clock::now();
   int chunk = 256;
   float total_ms = 0;
   int64_t launches = 0;
   bool deadline_set = false;
   long long max_iters = 0;
-  for (int i = 0; i < nq; ++i) max_iters = std::max(max_iters, qs[i].budget_is_time ? 0LL : (long long)qs[i].budget);
+  for (int i = 0; i < nq; ++i)
+    if (qs[i].budget_kind != SMP_BUDGET_SECONDS) max_iters = std::max(max_iters, (long long)qs[i].budget);
   for (;;) {
     if (tmax == 0 && launches > max_iters / 256 + 64) return SMP_ERR_HIP;  // no progress: never spin forever
     if (tmax > 0 && std::chrono::duration<double>(std::chrono::steady_clock::now() - t_begin).count() > tmax * 4 + 60)
@@ -575,7 +598,7 @@ extern "C" int smp_plan_batch(smp_planner* p, const smp_query* qs, int nq, smp_r
     if (tmax > 0 && !deadline_set) {
       // convert the wall-clock budget into a device-clock deadline per timed query
       for (int i = 0; i < nq; ++i) {
-        if (!qs[i].budget_is_time || S[i].phase == 2) continue;
+        if (qs[i].budget_kind != SMP_BUDGET_SECONDS || S[i].phase == 2) continue;
         S[i].deadline = S[i].t0 + (unsigned long long)(qs[i].budget * p->wall_rate_hz);
         HIPCHK(hipMemcpyAsync(&qdev[i].st->deadline, &S[i].deadline, sizeof(unsigned long long), hipMemcpyHostToDevice, p->stream));
       }

@@ -1008,6 +1008,7 @@ __device__ void iteration(const Ctx& C) {
     }
     if ((S.cbest[0] - S.h0[0]) < S.opt_thresh) S.phase = 2;  // birrt_star.cpp:1333-1338
     if (S.iter >= S.max_iter) S.phase = 2;
+    if (S.max_checked && S.checked >= S.max_checked) S.phase = 2;
     if (S.deadline && wall_clock64() >= S.deadline) S.phase = 2;
   }
   __syncthreads();
@@ -1034,7 +1035,8 @@ __global__ void __launch_bounds__(BLOCK) plan_kernel(const RobotDev* __restrict_
     }
     __syncthreads();
     connect_graphs(C, 0);
-    if (threadIdx.x == 0) g_L.S.phase = g_L.S.have_sol ? 2 : 1;
+    if (threadIdx.x == 0)
+      g_L.S.phase = (g_L.S.have_sol || (g_L.S.max_checked && g_L.S.checked >= g_L.S.max_checked)) ? 2 : 1;
     __syncthreads();
   }
   for (int k = 0; k < iters; ++k) {

@@ -36,6 +36,7 @@ struct QState {                // per query, persisted in global memory across l
   int n[2], edges[2], rewires[2];
   int cap, via_cap;
   long long iter, max_iter;
+  long long max_checked;       // > 0: stop once this many configurations were collision-checked
   long long checked, valid, first_iter, last_iter;
   long long nn_nodes, near_nodes;  // nodes streamed by nearest / near scans (algorithmic bytes)
   unsigned long long prof[24];     // device-clock ticks per planner phase (SMP_PROF_* in smp_kernels.hip)

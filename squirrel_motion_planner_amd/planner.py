@@ -155,7 +155,9 @@ class GpuPlanner:
 
     @staticmethod
     def make_query(start, goal, env_x=(0, 0), env_y=(0, 0), check_self=True, check_map=True, iterations=None,
-                   seconds=None, seed=1, query_id=0):
+                   seconds=None, samples=None, seed=1, query_id=0):
+        """One query; the budget is `seconds`, else `samples` (collision-checked configurations), else
+        `iterations` (default 1000)."""
         q = L.Query()
         for j in range(8):
             q.start[j] = float(start[j])
@@ -164,9 +166,11 @@ class GpuPlanner:
         q.env_y[0], q.env_y[1] = env_y
         q.check_self, q.check_map = int(check_self), int(check_map)
         if seconds is not None:
-            q.budget_is_time, q.budget = 1, float(seconds)
+            q.budget_kind, q.budget = L.BUDGET_SECONDS, float(seconds)
+        elif samples is not None:
+            q.budget_kind, q.budget = L.BUDGET_SAMPLES, float(samples)
         else:
-            q.budget_is_time, q.budget = 0, float(1000 if iterations is None else iterations)
+            q.budget_kind, q.budget = L.BUDGET_ITERATIONS, float(1000 if iterations is None else iterations)
         q.seed = seed
         q.query_id = query_id
         return q

@@ -1,0 +1,67 @@
+// Replays squirrel_8dof_planner.cpp's planner call sequence (SP:16, 482, 872-915, 1221-1248) through the C++
+// drop-in shim include/smp_birrt_star.hpp, the way the ROS node would after swapping the include.
+//
+//   shim_plan <robot_model.json> <scene.bt> <iterations> <seed> <start x8> <goal x8> <env_x0 env_x1 env_y0 env_y1>
+//
+// Prints "status <0|1>" and the trajectory rows; exit 0 on success, 2 on usage error, 3 when no GPU is usable
+// (the shim throws: there is no CPU fallback).
+#include <cstdio>
+#include <cstdlib>
+#include <fstream>
+#include <iterator>
+#include <string>
+#include <vector>
+
+#include "smp_birrt_star.hpp"
+
+namespace {
+// Minimal stand-in for octomap::OcTree: the shim only needs getResolution() and writeBinaryConst().
+struct BtFileTree {
+  std::string bytes;
+  double res;
+  double getResolution() const { return res; }
+  std::ostream& writeBinaryConst(std::ostream& s) const { return s.write(bytes.data(), (std::streamsize)bytes.size()); }
+};
+}  // namespace
+
+int main(int argc, char** argv) {
+  if (argc != 1 + 4 + 16 + 4) {
+    std::fprintf(stderr, "usage: shim_plan model.json scene.bt iterations seed start[8] goal[8] env[4]\n");
+    return 2;
+  }
+  setenv("SMP_ROBOT_MODEL", argv[1], 1);
+  setenv("SMP_SEED", argv[4], 1);
+  std::ifstream f(argv[2], std::ios::binary);
+  BtFileTree tree{std::string(std::istreambuf_iterator<char>(f), std::istreambuf_iterator<char>()), 0.05};
+  std::vector<double> start(8), goal(8);
+  for (int j = 0; j < 8; ++j) { start[j] = std::atof(argv[5 + j]); goal[j] = std::atof(argv[13 + j]); }
+  std::vector<double> ex = {std::atof(argv[21]), std::atof(argv[22])}, ey = {std::atof(argv[23]), std::atof(argv[24])};
+  birrt_star_motion_planning::BiRRTstarPlanner planner;
+  try {
+    planner.initialize("robotino_robot");                        // SP:16
+  } catch (const std::exception& e) {
+    std::printf("error %s\n", e.what());
+    return 3;
+  }
+  planner.setOctree(&tree);                                       // SP:872-873 (floor already in the tree)
+  planner.setDisabledLinkMapCollisions(std::vector<std::string>());  // SP:482
+  planner.reset_planner_and_config();                             // SP:1224
+  planner.setPlanningSceneInfo(ex, ey, "scenario");               // SP:1232
+  if (!planner.init_planner(start, goal, 1, true, true)) {        // SP:1234
+    std::printf("status init_failed\n");
+    return 0;
+  }
+  bool ok = planner.run_planner(1, false, std::atof(argv[3]), false, 0.0, 0);  // SP:1238 (iteration budget)
+  std::printf("status %d\n", ok ? 0 : 1);
+  const std::vector<std::vector<double> >& traj = planner.getJointTrajectoryRef();  // SP:1241
+  std::printf("waypoints %zu checked %lld\n", traj.size(), (long long)planner.lastStats().configs_checked);
+  for (const auto& w : traj) {
+    for (int j = 0; j < 8; ++j) std::printf("%s%.17g", j ? " " : "", w[j]);
+    std::printf("\n");
+  }
+  // dimension mismatch: init_planner returns false (birrt_star.cpp:338-342)
+  std::vector<double> short_conf(start.begin(), start.begin() + 7);
+  std::printf("dim_mismatch_rejected %d\n", planner.init_planner(short_conf, goal, 1, true, true) ? 0 : 1);
+  std::printf("start_valid %d\n", planner.isConfigValid(start, true, true) ? 1 : 0);
+  return 0;
+}

@@ -181,6 +181,20 @@ def test_planner_parity(gp, orobot, name, seed, iters):
     assert_same_run(gp, r, o)
 
 
+@pytest.mark.parametrize("name,seed,samples", [("c2", 11, 30000), ("c4", 2, 20000), ("room3", 2, 20000)])
+def test_planner_parity_sample_budget(orobot, robot, name, seed, samples):
+    """The bench's budget: collision-checked configurations, path_optimality_threshold = -inf."""
+    gp2 = GpuPlanner(robot, path_optimality_threshold=-np.inf)
+    sc, gscene, osc = scene_pair(name)
+    gp2.set_scene(gscene)
+    r = gp2.plan(GpuPlanner.make_query(sc.start, sc.goal, sc.env_x, sc.env_y, samples=samples, seed=seed))
+    o = O.Oracle(orobot, osc).plan(sc.start, sc.goal, env_x=sc.env_x, env_y=sc.env_y, max_checked=samples,
+                                   seed=seed, opt_thresh=-np.inf)
+    if o["iterations"] > 0:  # (room3 connects directly before the loop, birrt_star.cpp:1072-1075)
+        assert o["checked"] >= samples
+    assert_same_run(gp2, r, o)
+
+
 def test_planner_parity_yaml_profile(orobot, robot):
     gp2 = GpuPlanner(robot, near_threshold=1.5, step_factor=0.6)
     sc, r, o = run_both(gp2, orobot, "c2", 5, 200, near_threshold=1.5, step_factor=0.6)

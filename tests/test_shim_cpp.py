@@ -1,0 +1,74 @@
+"""The C++ drop-in shim (include/smp_birrt_star.hpp) compiled with g++ and driven through the node's call
+sequence (tests/cpp/shim_plan.cpp).  CPU: it builds, links libsmp_gpu.so and fails loudly without a GPU.
+GPU: the trajectory it returns equals the oracle's for the same scene, seed and budget."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+from oracle import octomap_bt, oracle as O
+from squirrel_motion_planner_amd import scenes
+
+LIBDIR = os.path.join(ROOT, "squirrel_motion_planner_amd", "lib")
+MODEL = os.path.join(ROOT, "squirrel_motion_planner_amd", "data", "robotino_model.json")
+
+
+def build_shim(tmpdir):
+    exe = os.path.join(str(tmpdir), "shim_plan")
+    cmd = ["g++", "-std=c++11", "-O2", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+           os.path.join(ROOT, "tests", "cpp", "shim_plan.cpp"), "-L", LIBDIR, "-lsmp_gpu",
+           "-Wl,-rpath," + LIBDIR, "-o", exe]
+    subprocess.run(cmd, check=True, capture_output=True, text=True)
+    return exe
+
+
+def room3_case(tmpdir):
+    f = np.load(os.path.join(ROOT, "tests", "golden", "room3_keys.npz"))
+    keys = np.concatenate([f["keys"].astype(np.int64), scenes.floor_keys([0.0, 0.0], 0.05, 3.0)])
+    bt = os.path.join(str(tmpdir), "room3_floor.bt")
+    open(bt, "wb").write(octomap_bt.write_bt(keys, 0.05))
+    sc = scenes.Scene("room3", keys, 0.05, [0.3, -0.4, 0.0] + scenes.ARM_FOLDED,
+                      [1.4, 1.1, 1.2] + scenes.ARM_UNFOLDED, (0, 0), (0, 0))
+    sc.env_x, sc.env_y = sc.bounds()
+    return sc, bt
+
+
+def run_shim(exe, model, bt, sc, iters, seed):
+    args = [exe, model, bt, str(iters), str(seed)] + ["%.17g" % v for v in list(sc.start) + list(sc.goal)]
+    args += ["%.17g" % v for v in list(sc.env_x) + list(sc.env_y)]
+    return subprocess.run(args, capture_output=True, text=True, timeout=300)
+
+
+def test_shim_builds_and_fails_loudly_without_gpu(tmp_path):
+    exe = build_shim(tmp_path)
+    sc, bt = room3_case(tmp_path)
+    p = run_shim(exe, MODEL, bt, sc, 10, 1)
+    if p.returncode == 3:  # no GPU here: the shim throws, no CPU fallback
+        assert "no usable GPU" in p.stdout or "NO_DEVICE" in p.stdout.upper(), p.stdout
+    else:
+        assert p.returncode == 0, p.stderr
+
+
+@pytest.mark.gpu
+def test_shim_node_sequence_matches_oracle(tmp_path):
+    exe = build_shim(tmp_path)
+    sc, bt = room3_case(tmp_path)
+    iters, seed = 200, 5
+    p = run_shim(exe, MODEL, bt, sc, iters, seed)
+    assert p.returncode == 0, p.stdout + p.stderr
+    lines = p.stdout.splitlines()
+    assert lines[0] in ("status 0", "status 1")
+    n = int(lines[1].split()[1])
+    checked = int(lines[1].split()[3])
+    path = np.array([[float(v) for v in ln.split()] for ln in lines[2:2 + n]]).reshape(-1, 8)
+    assert lines[2 + n] == "dim_mismatch_rejected 1"
+    assert lines[3 + n] == "start_valid 1"
+    res, keys = octomap_bt.read_bt(open(bt, "rb").read())
+    o = O.Oracle(O.OracleRobot(MODEL), O.OracleScene(keys, res)).plan(
+        sc.start, sc.goal, env_x=sc.env_x, env_y=sc.env_y, max_iter=iters, seed=seed)
+    assert lines[0] == "status %d" % o["status"]
+    assert checked == o["checked"]
+    assert path.shape == o["path"].reshape(-1, 8).shape
+    assert np.array_equal(path, o["path"].reshape(-1, 8))

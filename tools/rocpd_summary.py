@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 SQLite output (ROCm 7.x `*_results.db`) into the files committed under profiles/.
+
+  python tools/rocpd_summary.py stats  <kernel-trace .db>  <out.txt>
+      per-kernel calls / total / average / share (the `--stats` kernel summary)
+  python tools/rocpd_summary.py pmc    <pmc .db> <kernel substring> <out.json>
+      per-dispatch FETCH_SIZE / WRITE_SIZE of one kernel -> HBM bytes per launch
+
+FETCH_SIZE and WRITE_SIZE are kilobytes (the counter description says so; x1024).  MI355X_MICROARCH.md
+(HBM section): on gfx950 FETCH_SIZE reports 1/2 of the bytes of wide coalesced reads, so the corrected
+fetch is 2 x FETCH_SIZE x 1024; WRITE_SIZE is taken as is.  Both are recorded.
+"""
+import json
+import sqlite3
+import sys
+
+
+def stats(db, out):
+    c = sqlite3.connect(db)
+    rows = c.execute("select name, total_calls, total_duration, average, percentage from top_kernels").fetchall()
+    lines = ["# rocprofv3 --kernel-trace --stats summary (%s)" % db,
+             "# %-90s %8s %16s %14s %8s" % ("kernel", "calls", "total_ns", "avg_ns", "pct")]
+    for name, calls, tot, avg, pct in rows:
+        lines.append("%-92s %8d %16.0f %14.0f %8.3f" % (name[:92], calls, tot, avg, pct))
+    open(out, "w").write("\n".join(lines) + "\n")
+    print("\n".join(lines))
+
+
+def pmc(db, kernel, out):
+    c = sqlite3.connect(db)
+    q = ("select dispatch_id, kernel_name, counter_name, value, duration from counters_collection "
+         "where kernel_name like ? order by dispatch_id")
+    per = {}
+    for did, name, cname, value, dur in c.execute(q, ("%" + kernel + "%",)):
+        d = per.setdefault(did, {"kernel": name, "duration_ns": dur})
+        d[cname] = d.get(cname, 0.0) + value
+    disp = list(per.values())
+    fetch_kb = sum(d.get("FETCH_SIZE", 0.0) for d in disp)
+    write_kb = sum(d.get("WRITE_SIZE", 0.0) for d in disp)
+    n = max(len(disp), 1)
+    res = {
+        "source": db, "kernel": kernel, "dispatches": len(disp),
+        "fetch_size_kb_total": fetch_kb, "write_size_kb_total": write_kb,
+        "fetch_bytes_corrected_total": 2.0 * fetch_kb * 1024.0,
+        "write_bytes_total": write_kb * 1024.0,
+        "hbm_bytes_per_launch": (2.0 * fetch_kb + write_kb) * 1024.0 / n,
+        "correction": "FETCH_SIZE (KB) x1024 x2 (gfx950 half-count, MI355X_MICROARCH.md HBM section); WRITE_SIZE x1024",
+        "per_dispatch": disp,
+    }
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps({k: v for k, v in res.items() if k != "per_dispatch"}, indent=1))
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "stats":
+        stats(sys.argv[2], sys.argv[3])
+    else:
+        pmc(sys.argv[2], sys.argv[3], sys.argv[4])
