@@ -56,7 +56,7 @@ class Stats(ctypes.Structure):
                 ("edges_start", _i64), ("edges_goal", _i64), ("rewires_start", _i64), ("rewires_goal", _i64),
                 ("connected_tree_is_start", ctypes.c_int32), ("conn_node_b", ctypes.c_int32),
                 ("conn_node_a", ctypes.c_int32), ("nn_nodes_scanned", _i64), ("near_nodes_scanned", _i64),
-                ("phase_seconds", _d * 24)]
+                ("phase_seconds", _d * 32)]
 
 
 class Result(ctypes.Structure):
@@ -100,6 +100,7 @@ PROBES = [
     ("smp_probe_u01", _i, [_i, ctypes.c_uint64, ctypes.c_uint32, _p, _i, _pd]),
     ("smp_probe_fk", _i, [_p, _pd, _i, _pd, _pd]),
     ("smp_probe_sqrt_div", _i, [_i, _pd, _pd, _i, _pd, _pd]),
+    ("smp_probe_check_latency", _i, [_p, _pd, _i64, _i, _i, _i, _i, _pd, ctypes.POINTER(ctypes.c_uint64), _pd]),
 ]
 
 _lib = None

@@ -19,8 +19,8 @@
 #include "smp_types.h"
 
 namespace smp {
-__global__ void check_kernel(const RobotDev* rb, SceneDev sc, const MapCfg* mc, const double* q, long long n, int self,
-                             int map, uint8_t* valid);
+void launch_check(int ct, int grid, hipStream_t st, const RobotDev* rb, SceneDev sc, const MapCfg* mc, const double* q,
+                  long long n, int self, int map, uint8_t* valid, unsigned long long* prof);
 __global__ void plan_kernel(const RobotDev* rb, SceneDev sc, const MapCfg* mc, QueryDev* qs, int iters);
 __global__ void path_kernel(QueryDev* qs, int* counts);
 __global__ void sincos_kernel(const double* x, int n, double* s, double* c);
@@ -336,7 +336,7 @@ int smp_planner_set_scene(smp_planner* p, const smp_scene* s) {
   HIPCHK(hipMemcpyAsync(p->d_d2.p, s->h.d2.data(), s->h.d2.size() * sizeof(uint16_t), hipMemcpyHostToDevice, p->stream));
   p->sc.nx = s->h.nx; p->sc.ny = s->h.ny; p->sc.nz = s->h.nz;
   p->sc.bnx = s->h.bnx; p->sc.bny = s->h.bny;
-  p->sc.ox = s->h.ox; p->sc.oy = s->h.oy; p->sc.oz = s->h.oz; p->sc.res = s->h.res;
+  p->sc.ox = s->h.ox; p->sc.oy = s->h.oy; p->sc.oz = s->h.oz; p->sc.res = s->h.res; p->sc.inv_res = 1.0 / s->h.res;
   p->sc.bricks = p->d_bricks.p;
   p->sc.d2 = p->d_d2.p;
   p->have_scene = true;
@@ -362,8 +362,8 @@ int smp_check_configs(smp_planner* p, const double* q_soa, int64_t n, int check_
   long long tiles = (n + 31) / 32;
   int grid = (int)std::min<long long>(tiles, 256 * 8);
   HIPCHK(hipEventRecord(p->ev0, p->stream));
-  hipLaunchKernelGGL(check_kernel, dim3(grid), dim3(BLOCK), 0, p->stream, p->d_rb, p->sc, p->d_mc, p->d_cq.p, (long long)n,
-                     check_self, check_map && p->have_scene, p->d_valid.p);
+  launch_check(32, grid, p->stream, p->d_rb, p->sc, p->d_mc, p->d_cq.p, (long long)n, check_self,
+               check_map && p->have_scene, p->d_valid.p, nullptr);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(p->ev1, p->stream));
   HIPCHK(hipMemcpyAsync(valid, p->d_valid.p, (size_t)n, hipMemcpyDeviceToHost, p->stream));
@@ -639,8 +639,8 @@ extern "C" int smp_plan_batch(smp_planner* p, const smp_query* qs, int nq, smp_r
     st.conn_node_b = s.nB.id; st.conn_node_a = s.nA.id;
     st.nn_nodes_scanned = s.nn_nodes;
     st.near_nodes_scanned = s.near_nodes;
-    for (int k = 0; k < 24; ++k)
-      st.phase_seconds[k] = (k == 8 || k == 11 || k >= 16) ? (double)s.prof[k] : (double)s.prof[k] / p->wall_rate_hz;
+    for (int k = 0; k < 32; ++k)
+      st.phase_seconds[k] = (k == 8 || k == 11 || k >= 20) ? (double)s.prof[k] : (double)s.prof[k] / p->wall_rate_hz;
     if (i == 0) { p->last_n[0] = s.n[0]; p->last_n[1] = s.n[1]; }
     // cost rows
     r.n_cost_rows = s.n_rows;
@@ -764,6 +764,34 @@ extern "C" int smp_probe_fk(smp_planner* p, const double* q, int n, double* fram
   HIPCHK(hipMemcpy(frames, df, (size_t)n * nb * 12 * sizeof(double), hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(eez, dz, (size_t)n * sizeof(double), hipMemcpyDeviceToHost));
   (void)hipFree(dq); (void)hipFree(df); (void)hipFree(dz);
+  return SMP_OK;
+}
+
+// Latency probe of the collision tile: check_kernel with `grid` workgroups (grid 1: one workgroup streams
+// every tile back to back); ticks[0..3] = block 0's device-clock ticks in tile stages A, B, C-centres, C;
+// ticks[4] / ticks[5] = block 0's shader cycles / device-clock ticks over the kernel (effective shader clock).
+extern "C" int smp_probe_check_latency(smp_planner* p, const double* q_soa, int64_t n, int check_self, int check_map,
+                                       int grid, int tile, double* ms, unsigned long long* ticks, double* clock_hz) {
+  if (!p || n <= 0 || !q_soa || grid <= 0) return SMP_ERR_ARG;
+  HIPCHK(hipSetDevice(p->device));
+  HIPCHK(p->d_cq.reserve((size_t)n * NJ));
+  HIPCHK(p->d_valid.reserve((size_t)n));
+  unsigned long long* dprof = nullptr;
+  HIPCHK(hipMalloc(&dprof, 8 * sizeof(unsigned long long)));
+  HIPCHK(hipMemset(dprof, 0, 8 * sizeof(unsigned long long)));
+  HIPCHK(hipMemcpy(p->d_cq.p, q_soa, (size_t)n * NJ * sizeof(double), hipMemcpyHostToDevice));
+  HIPCHK(hipEventRecord(p->ev0, p->stream));
+  launch_check(tile, grid, p->stream, p->d_rb, p->sc, p->d_mc, p->d_cq.p, (long long)n, check_self,
+               check_map && p->have_scene, p->d_valid.p, dprof);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(p->ev1, p->stream));
+  HIPCHK(hipStreamSynchronize(p->stream));
+  float f = 0;
+  HIPCHK(hipEventElapsedTime(&f, p->ev0, p->ev1));
+  *ms = f;
+  HIPCHK(hipMemcpy(ticks, dprof, 6 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  (void)hipFree(dprof);
+  *clock_hz = p->wall_rate_hz;
   return SMP_OK;
 }
 

@@ -93,20 +93,22 @@ __device__ __forceinline__ double ee_z(const RobotDev* __restrict__ rb, const do
 
 // Grid cell of a sphere centre, or -1 outside the grid (such a sphere is free: the grid is padded by more
 // than the largest radius around every occupied cell).
+// Multiplying by 1/res instead of dividing may put a centre within an ulp of a cell face into the neighbour
+// cell; that cell's closed box still contains the centre up to that ulp, far inside the 1e-6 m margin of T.
 __device__ __forceinline__ long long centre_cell(const SceneDev& s, const double* c) {
-  double fx = floor((c[0] - s.ox) / s.res), fy = floor((c[1] - s.oy) / s.res), fz = floor((c[2] - s.oz) / s.res);
+  double fx = floor((c[0] - s.ox) * s.inv_res), fy = floor((c[1] - s.oy) * s.inv_res), fz = floor((c[2] - s.oz) * s.inv_res);
   if (!(fx >= 0 && fx < s.nx && fy >= 0 && fy < s.ny && fz >= 0 && fz < s.nz)) return -1;
   return ((long long)(int)fz * s.ny + (int)fy) * s.nx + (int)fx;
 }
 
 // Cells that can hold a box within r of c (one cell of margin against rounding), clipped to the grid.
 __device__ __forceinline__ void sphere_reach(const SceneDev& s, const double* c, double r, int* lo, int* hi) {
-  lo[0] = max((int)floor((c[0] - r - s.ox) / s.res) - 1, 0);
-  lo[1] = max((int)floor((c[1] - r - s.oy) / s.res) - 1, 0);
-  lo[2] = max((int)floor((c[2] - r - s.oz) / s.res) - 1, 0);
-  hi[0] = min((int)floor((c[0] + r - s.ox) / s.res) + 1, s.nx - 1);
-  hi[1] = min((int)floor((c[1] + r - s.oy) / s.res) + 1, s.ny - 1);
-  hi[2] = min((int)floor((c[2] + r - s.oz) / s.res) + 1, s.nz - 1);
+  lo[0] = max((int)floor((c[0] - r - s.ox) * s.inv_res) - 1, 0);
+  lo[1] = max((int)floor((c[1] - r - s.oy) * s.inv_res) - 1, 0);
+  lo[2] = max((int)floor((c[2] - r - s.oz) * s.inv_res) - 1, 0);
+  hi[0] = min((int)floor((c[0] + r - s.ox) * s.inv_res) + 1, s.nx - 1);
+  hi[1] = min((int)floor((c[1] + r - s.oy) * s.inv_res) + 1, s.ny - 1);
+  hi[2] = min((int)floor((c[2] + r - s.oz) * s.inv_res) + 1, s.nz - 1);
 }
 
 // Exact sphere vs the box of cell (i,j,k), if that cell is occupied.
@@ -122,13 +124,6 @@ __device__ __forceinline__ bool cell_hit(const SceneDev& s, const double* c, dou
   return dx * dx + dy * dy + dz * dz <= r2;
 }
 
-// Self-collision sphere test of one (a, b) sphere pair (collision_checker.hpp:541-552 on the sphere model).
-__device__ __forceinline__ bool spheres_touch(const double* wa, const double* wb, double ra, double rb) {
-  double ex = wa[0] - wb[0], ey = wa[1] - wb[1], ez = wa[2] - wb[2];
-  double r2 = ra + rb;
-  return ex * ex + ey * ey + ez * ez <= r2 * r2;
-}
-
 // Makes this wave's earlier LDS writes visible to all of its lanes (LDS ops of one wave complete in order;
 // the fence keeps the compiler from caching or reordering across it).
 __device__ __forceinline__ void wave_sync() {
@@ -137,13 +132,12 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Local frame of body-chain step k (the same construction as body_frames_sc).
-__device__ __forceinline__ void chain_local(const RobotDev* __restrict__ rb, int k, const double* q, const double (*sc)[2],
+// Local frame of body-chain step k (the same construction as body_frames / body_frames_sc).
+__device__ __forceinline__ void chain_local(const RobotDev* __restrict__ rb, int k, const double* q, double st, double ct,
                                             Frame* L) {
   int ty = rb->ch_type[k];
   if (ty == 1) {
-    int j = rb->ch_joint[k];
-    rot2_sc(&rb->ch_axis[k * 3], sc[j][0], sc[j][1], L->R);
+    rot2_sc(&rb->ch_axis[k * 3], st, ct, L->R);
     L->p[0] = rb->ch_origin[k * 3]; L->p[1] = rb->ch_origin[k * 3 + 1]; L->p[2] = rb->ch_origin[k * 3 + 2];
   } else if (ty == 2) {
     frame_identity(L);
@@ -155,51 +149,57 @@ __device__ __forceinline__ void chain_local(const RobotDev* __restrict__ rb, int
   }
 }
 
-__device__ __forceinline__ double sel3(int i, double a, double b, double c) { return i == 0 ? a : (i == 1 ? b : c); }
+__device__ __forceinline__ uint32_t shfl_u32(uint32_t v, int src) { return (uint32_t)__shfl((int)v, src); }
 
-// Element e (R[0..8], p[9..11]) of the KDL product a * b, with fmul's evaluation order.  a is in LDS; b's
-// column is picked with selects (no dynamically indexed private array).
-__device__ __forceinline__ double fmul_elem(const double* a, const Frame& b, int e) {
-  const bool rot = e < 9;
-  const int r = rot ? e / 3 : e - 9, c = rot ? e - r * 3 : 0;
-  double b0 = rot ? sel3(c, b.R[0], b.R[1], b.R[2]) : b.p[0];
-  double b1 = rot ? sel3(c, b.R[3], b.R[4], b.R[5]) : b.p[1];
-  double b2 = rot ? sel3(c, b.R[6], b.R[7], b.R[8]) : b.p[2];
-  double m = a[r * 3 + 0] * b0 + a[r * 3 + 1] * b1 + a[r * 3 + 2] * b2;
-  return rot ? m : m + a[9 + r];
-}
-
-constexpr int NWAVE = BLOCK / 64;
-constexpr int FK_LANES = 12;                 // one lane per frame element
-constexpr int FK_GROUPS = 64 / FK_LANES;     // configurations per wave in the FK stage
-
-// LDS work area of one collision tile of CT configurations.
-template <int CT>
-struct TileLds {
-  double fr[CT][MAX_BODY][12];    // body frames (R row-major, p)
-  double tf[CT][2][12];           // FK chain product, ping-pong
-  double scs[CT][NJ][2];          // sin / cos of every joint
-  double wc[NWAVE][MAX_SPH][3];   // sphere world centres of the configuration a wave is testing
-  double lbw[NWAVE][MAX_CLINK][3];// link-bound world centres of that configuration
-  int coll[CT];                   // 1 = in collision
-};
-
-// Optional ordering of a tile's configurations: configuration c is point ord[c] of group grp[c] (an edge);
-// grp_first[g] is the lowest colliding point index of group g found so far.  A configuration whose index
-// exceeds it is skipped (it cannot change the group's first collision); a colliding one lowers it.
-struct TileOrder {
-  const int* grp;
-  const int* ord;
-  int* grp_first;
-};
-
-// Cooperative exact map test of sphere centre cc, radius r by one wavefront: lanes over the cells in reach.
+// Cooperative exact map test of sphere centre cc, radius r by one wavefront.  The brick words covering the
+// reach (<= 64) are loaded once, one per lane, and handed to the lanes testing their cells by shuffles; then
+// lanes sweep the cells in reach (exact box test, ballot early exit).  Larger reaches load per cell.
 __device__ __forceinline__ bool wave_sphere_map(const SceneDev& sc, const double* cc, double r, int lane) {
   int lo[3], hi[3];
   sphere_reach(sc, cc, r, lo, hi);
   const int ni = hi[0] - lo[0] + 1, nj = hi[1] - lo[1] + 1, nk = hi[2] - lo[2] + 1;
   const int nv = ni * nj * nk;
   const double r2 = r * r;
+  const int bi0 = lo[0] >> 2, bj0 = lo[1] >> 2, bk0 = lo[2] >> 2;
+  const int nbi = (hi[0] >> 2) - bi0 + 1, nbj = (hi[1] >> 2) - bj0 + 1, nbk = (hi[2] >> 2) - bk0 + 1;
+  const int nb = nbi * nbj * nbk;
+  if (nb <= 64) {
+    uint64_t w = 0;
+    if (lane < nb) {
+      int bi = lane % nbi, t = lane / nbi;
+      int bj = t % nbj, bk = t / nbj;
+      w = sc.bricks[((size_t)(bk0 + bk) * sc.bny + (bj0 + bj)) * sc.bnx + (bi0 + bi)];
+    }
+    const uint32_t wlo = (uint32_t)w, whi = (uint32_t)(w >> 32);
+    for (int v0 = 0; v0 < nv; v0 += 64) {
+      const int v = v0 + lane;
+      int i = 0, j = 0, k = 0, src = 0;
+      if (v < nv) {
+        int t = v / ni;
+        i = lo[0] + (v - t * ni);
+        j = lo[1] + t % nj;
+        k = lo[2] + t / nj;
+        src = ((k >> 2) - bk0) * nbj * nbi + ((j >> 2) - bj0) * nbi + ((i >> 2) - bi0);
+      }
+      const uint32_t a = shfl_u32(wlo, src), b = shfl_u32(whi, src);
+      bool hit = false;
+      if (v < nv) {
+        const int bit = ((k & 3) << 4) | ((j & 3) << 2) | (i & 3);
+        const uint32_t word = bit < 32 ? a : b;
+        if ((word >> (bit & 31)) & 1u) {
+          double xlo = sc.ox + (double)i * sc.res, xhi = sc.ox + (double)(i + 1) * sc.res;
+          double ylo = sc.oy + (double)j * sc.res, yhi = sc.oy + (double)(j + 1) * sc.res;
+          double zlo = sc.oz + (double)k * sc.res, zhi = sc.oz + (double)(k + 1) * sc.res;
+          double dx = cc[0] < xlo ? xlo - cc[0] : (cc[0] > xhi ? cc[0] - xhi : 0.0);
+          double dy = cc[1] < ylo ? ylo - cc[1] : (cc[1] > yhi ? cc[1] - yhi : 0.0);
+          double dz = cc[2] < zlo ? zlo - cc[2] : (cc[2] > zhi ? cc[2] - zhi : 0.0);
+          hit = dx * dx + dy * dy + dz * dz <= r2;
+        }
+      }
+      if (__ballot(hit)) return true;
+    }
+    return false;
+  }
   for (int v0 = 0; v0 < nv; v0 += 64) {
     int v = v0 + lane;
     bool hit = false;
@@ -213,43 +213,91 @@ __device__ __forceinline__ bool wave_sphere_map(const SceneDev& sc, const double
   return false;
 }
 
+constexpr int NWAVE = BLOCK / 64;
+
+// LDS work area of one collision tile of CT configurations (CT a multiple of the wave count).
+template <int CT>
+struct TileLds {
+  static constexpr int CPW = CT / NWAVE;  // configurations per wavefront in stage C
+  static constexpr int SW = (MAX_SPH + 31) / 32;
+  double fr[CT][MAX_BODY][12];              // body frames (R row-major, p)
+  double tf[CT][2][12];                     // stage B: chain product, ping-pong
+  union {
+    double lf[CT][MAX_CHAIN][12];           // stages A/B: local frame of every chain step
+    struct {
+      double wc[CT][MAX_SPH][3];            // stage C: sphere world centres
+    } c;
+  } u;
+  uint32_t cand[CT][SW];                    // spheres needing the exact map sweep
+  int coll[CT];                             // 1 = in collision
+};
+
+// Optional ordering of a tile's configurations: configuration c is point ord[c] of group grp[c] (an edge);
+// grp_first[g] is the lowest colliding point index of group g found so far.  A configuration whose index
+// exceeds it is skipped (it cannot change the group's first collision); a colliding one lowers it.
+struct TileOrder {
+  const int* grp;
+  const int* ord;
+  int* grp_first;
+};
+
 // Collision test of nc <= CT configurations already placed in q_lds[c][8] (LDS), all block threads.
 // On return coll[c] is 1 for colliding configurations (0 for free or skipped ones).
-//   A. sin/cos of every joint (one lane each);
-//   B. body frames: 12 lanes per configuration, one frame element each, chain steps in order;
-//   C. one wavefront per configuration: lanes over spheres (world centre + box-gap prefilter), the rare
-//      spheres near an occupied box swept cooperatively (lanes over cells in reach, ballot early exit);
-//      then lanes over link pairs (bound test) and, per overlapping pair, lanes over its sphere pairs.
-// Stage C has no block barrier: each wave moves on to its next configuration as soon as it is decided.
+//   A. local frame of every (configuration, chain step), sin/cos included, one lane each;
+//   B. body frames: one lane per configuration multiplies its chain in order (KDL Frame*Frame);
+//   C. wavefront w owns configurations w, w + 8, ...: lanes over (configuration, sphere) items with the d2
+//      loads of all of them issued together; the rare spheres near an occupied box are swept by the whole
+//      wave; then lanes over the flat list of sphere pairs of the enabled link pairs, the wave's
+//      configurations interleaved per pair.  No block barrier inside stage C.
+// gfx950 fp64 has ~40 cycles of dependent latency (tools/micro/fp64_latency.hip), so every stage is laid
+// out as many short independent chains per lane rather than one long chain.
 template <int CT>
 __device__ __forceinline__ void collide_tile(const RobotDev* __restrict__ rb, const SceneDev& sc,
                                              const MapCfg* __restrict__ mc, int nc, const double (*q_lds)[NJ],
                                              int self, int map, TileLds<CT>& L, const TileOrder* ord = nullptr,
                                              unsigned long long* prof = nullptr) {
+  static_assert(CT % NWAVE == 0, "tile size");
+  constexpr int CPW = TileLds<CT>::CPW, SW = TileLds<CT>::SW;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   unsigned long long t0 = (prof && tid == 0) ? wall_clock64() : 0;
-  for (int it = tid; it < nc * NJ; it += BLOCK) {
-    int c = it / NJ, j = it - c * NJ;
-    psincos(q_lds[c][j], &L.scs[c][j][0], &L.scs[c][j][1]);
+  const int nch = rb->n_chain;
+  // A
+  for (int it = tid; it < nc * nch; it += BLOCK) {
+    const int c = it / nch, k = it - c * nch;
+    double st = 0.0, ct = 1.0;
+    if (rb->ch_type[k] == 1) psincos(q_lds[c][rb->ch_joint[k]], &st, &ct);
+    Frame F;
+    chain_local(rb, k, q_lds[c], st, ct, &F);
+    double* o = L.u.lf[c][k];
+    for (int i = 0; i < 9; ++i) o[i] = F.R[i];
+    o[9] = F.p[0]; o[10] = F.p[1]; o[11] = F.p[2];
   }
+  for (int it = tid; it < CT * SW; it += BLOCK) (&L.cand[0][0])[it] = 0u;
   if (tid < nc) L.coll[tid] = 0;
   __syncthreads();
+  unsigned long long ta = (prof && tid == 0) ? wall_clock64() : 0;
+  // B: 12 lanes per configuration, one frame element each (fmul's evaluation order), steps in chain order
   {
-    const int e = lane % FK_LANES, g = lane / FK_LANES;
-    for (int c0 = 0; c0 < nc; c0 += NWAVE * FK_GROUPS) {
-      const int c = c0 + wave * FK_GROUPS + g;
-      const bool act = g < FK_GROUPS && c < nc;
+    constexpr int G = 64 / 12;  // configurations per wave per round
+    const int e = lane % 12, g = lane / 12;
+    for (int c0 = 0; c0 < nc; c0 += NWAVE * G) {
+      const int c = c0 + wave * G + g;
+      const bool act = g < G && c < nc;
+      const bool rot = e < 9;
+      const int r = rot ? e / 3 : e - 9, col = rot ? e - r * 3 : 0;
       if (act) L.tf[c][0][e] = (e == 0 || e == 4 || e == 8) ? 1.0 : (e == 11 ? rb->root_z : 0.0);
       wave_sync();
       int cur = 0;
-      for (int k = 0; k < rb->n_chain; ++k) {
+      for (int k = 0; k < nch; ++k) {
         if (act) {
-          Frame Lk;
-          chain_local(rb, k, q_lds[c], L.scs[c], &Lk);
-          double v = fmul_elem(L.tf[c][cur], Lk, e);
+          const double* A = L.tf[c][cur];
+          const double* l = L.u.lf[c][k];
+          const double b0 = rot ? l[col] : l[9], b1 = rot ? l[3 + col] : l[10], b2 = rot ? l[6 + col] : l[11];
+          const double m = A[r * 3 + 0] * b0 + A[r * 3 + 1] * b1 + A[r * 3 + 2] * b2;
+          const double v = rot ? m : m + A[9 + r];
           L.tf[c][cur ^ 1][e] = v;
-          int b = rb->ch_body[k];
-          if (b >= 0) L.fr[c][b][e] = v;
+          const int bd = rb->ch_body[k];
+          if (bd >= 0) L.fr[c][bd][e] = v;
         }
         wave_sync();
         cur ^= 1;
@@ -258,90 +306,100 @@ __device__ __forceinline__ void collide_tile(const RobotDev* __restrict__ rb, co
   }
   __syncthreads();
   unsigned long long t1 = (prof && tid == 0) ? wall_clock64() : 0;
-  const int nsph = rb->n_sph, ncl = rb->n_clink, npair = rb->n_pairs;
+  // C
+  const int nsph = rb->n_sph;
   const bool do_map = map && mc->has_map;
-  double (*wc)[3] = L.wc[wave];
-  double (*lbw)[3] = L.lbw[wave];
-  for (int c = wave; c < nc; c += NWAVE) {
-    if (ord && ord->ord[c] > __atomic_load_n(&ord->grp_first[ord->grp[c]], __ATOMIC_RELAXED)) continue;
-    const double* F = &L.fr[c][0][0];
-    bool hit = false;
-    for (int s0 = 0; s0 < nsph && !hit; s0 += 64) {
-      const int s = s0 + lane;
-      bool need = false;
-      if (s < nsph) {
-        const double* B = F + rb->sph_body[s] * 12;
+  // live configurations of this wave (skipped ones stay coll = 0)
+  uint32_t live = 0;
+  for (int k = 0; k < CPW; ++k) {
+    const int c = k * NWAVE + wave;
+    if (c < nc && !(ord && ord->ord[c] > __atomic_load_n(&ord->grp_first[ord->grp[c]], __ATOMIC_RELAXED)))
+      live |= 1u << k;
+  }
+  if (live) {
+    constexpr int MAXU = (CPW * MAX_SPH + 63) / 64;
+    long long cell[MAXU];
+#pragma unroll
+    for (int u = 0; u < MAXU; ++u) {
+      const int it = u * 64 + lane;
+      cell[u] = -1;
+      const int k = it / nsph, s = it - k * nsph;
+      if (k < CPW && ((live >> k) & 1u)) {
+        const int c = k * NWAVE + wave;
+        const double* B = L.fr[c][rb->sph_body[s]];
         const double* p = &rb->sph_cb[s * 3];
         double w[3];
         for (int r = 0; r < 3; ++r) {
           double m = B[r * 3 + 0] * p[0] + B[r * 3 + 1] * p[1] + B[r * 3 + 2] * p[2];
           w[r] = m + B[9 + r];
         }
-        wc[s][0] = w[0]; wc[s][1] = w[1]; wc[s][2] = w[2];
-        if (do_map && mc->map_on[s]) {
-          long long cell = centre_cell(sc, w);
-          need = cell >= 0 && (uint32_t)sc.d2[cell] <= mc->T[s];
-        }
-      }
-      wave_sync();
-      uint64_t m = __ballot(need);
-      while (m) {
-        const int sl = s0 + __builtin_ctzll(m);
-        m &= m - 1;
-        const double cc[3] = {wc[sl][0], wc[sl][1], wc[sl][2]};
-        if (wave_sphere_map(sc, cc, rb->sph_r[sl], lane)) { hit = true; break; }
+        L.u.c.wc[c][s][0] = w[0]; L.u.c.wc[c][s][1] = w[1]; L.u.c.wc[c][s][2] = w[2];
+        if (do_map && mc->map_on[s]) cell[u] = centre_cell(sc, w);
       }
     }
-    if (!hit && self) {
-      for (int l = lane; l < ncl; l += 64) {
-        const double* B = F + rb->cl_body[l] * 12;
-        const double* p = &rb->cl_cb[l * 3];
-        for (int r = 0; r < 3; ++r) {
-          double m = B[r * 3 + 0] * p[0] + B[r * 3 + 1] * p[1] + B[r * 3 + 2] * p[2];
-          lbw[l][r] = m + B[9 + r];
-        }
-      }
-      wave_sync();
-      for (int p0 = 0; p0 < npair && !hit; p0 += 64) {
-        const int pp = p0 + lane;
-        bool over = false;
-        if (pp < npair) {
-          int a = rb->pair_a[pp], b = rb->pair_b[pp];
-          double dx = lbw[a][0] - lbw[b][0], dy = lbw[a][1] - lbw[b][1], dz = lbw[a][2] - lbw[b][2];
-          double rr = rb->cl_r[a] + rb->cl_r[b];
-          over = !(dx * dx + dy * dy + dz * dz > rr * rr);
-        }
-        uint64_t m = __ballot(over);
-        while (m) {
-          const int pq = p0 + __builtin_ctzll(m);
-          m &= m - 1;
-          const int a = rb->pair_a[pq], b = rb->pair_b[pq];
-          const int sa0 = rb->cl_sph0[a], sb0 = rb->cl_sph0[b], nb = rb->cl_nsph[b];
-          const int K = rb->cl_nsph[a] * nb;
-          bool h = false;
-          for (int l0 = 0; l0 < K && !h; l0 += 64) {
-            const int l = l0 + lane;
-            bool t = false;
-            if (l < K) {
-              const int sa = sa0 + l / nb, sb = sb0 + l % nb;
-              t = spheres_touch(wc[sa], wc[sb], rb->sph_r[sa], rb->sph_r[sb]);
-            }
-            h = __ballot(t) != 0;
-          }
-          if (h) { hit = true; break; }
-        }
-      }
-    }
-    if (hit && lane == 0) {
-      L.coll[c] = 1;
-      if (ord) atomicMin(&ord->grp_first[ord->grp[c]], ord->ord[c]);
+    uint32_t dv[MAXU];
+#pragma unroll
+    for (int u = 0; u < MAXU; ++u) dv[u] = cell[u] >= 0 ? (uint32_t)sc.d2[cell[u]] : 0xffffffffu;
+#pragma unroll
+    for (int u = 0; u < MAXU; ++u) {
+      const int it = u * 64 + lane;
+      const int k = it / nsph, s = it - k * nsph;
+      if (cell[u] >= 0 && dv[u] <= mc->T[s]) atomicOr(&L.cand[k * NWAVE + wave][s >> 5], 1u << (s & 31));
     }
     wave_sync();
+    if (prof && tid == 0) prof[2] += wall_clock64() - t1;
+    // map sweeps
+    uint32_t hitm = 0;
+    for (int k = 0; k < CPW; ++k) {
+      if (!((live >> k) & 1u)) continue;
+      const int c = k * NWAVE + wave;
+      bool hit = false;
+      for (int wd = 0; wd < SW && !hit; ++wd) {
+        uint32_t m = L.cand[c][wd];
+        while (m) {
+          const int s = wd * 32 + __builtin_ctz(m);
+          m &= m - 1;
+          const double cc[3] = {L.u.c.wc[c][s][0], L.u.c.wc[c][s][1], L.u.c.wc[c][s][2]};
+          if (wave_sphere_map(sc, cc, rb->sph_r[s], lane)) { hit = true; break; }
+        }
+      }
+      if (hit) hitm |= 1u << k;
+    }
+    if (self) {
+      // every sphere pair of the enabled link pairs, the CPW configurations of this wave interleaved
+      const uint32_t todo = live & ~hitm;
+      if (todo) {
+        const int nsp = rb->n_spairs;
+        uint32_t sh = 0;
+        for (int p = lane; p < nsp; p += 64) {
+          const uint32_t ab = rb->sp_ab[p];
+          const int a = ab & 0xff, b = ab >> 8;
+          const double rr2 = rb->sp_rr2[p];
+#pragma unroll
+          for (int k = 0; k < CPW; ++k) {
+            const double* wa = L.u.c.wc[k * NWAVE + wave][a];
+            const double* wb = L.u.c.wc[k * NWAVE + wave][b];
+            const double ex = wa[0] - wb[0], ey = wa[1] - wb[1], ez = wa[2] - wb[2];
+            if (ex * ex + ey * ey + ez * ez <= rr2) sh |= 1u << k;
+          }
+        }
+        for (int k = 0; k < CPW; ++k)
+          if (((todo >> k) & 1u) && __ballot((sh >> k) & 1u)) hitm |= 1u << k;
+      }
+    }
+    if (lane == 0) {
+      for (int k = 0; k < CPW; ++k) {
+        if (!((hitm >> k) & 1u)) continue;
+        const int c = k * NWAVE + wave;
+        L.coll[c] = 1;
+        if (ord) atomicMin(&ord->grp_first[ord->grp[c]], ord->ord[c]);
+      }
+    }
   }
   __syncthreads();
   if (prof && tid == 0) {
     unsigned long long t2 = wall_clock64();
-    prof[0] += t1 - t0; prof[1] += t2 - t1;
+    prof[0] += ta - t0; prof[1] += t1 - ta; prof[3] += t2 - t1;
   }
 }
 

@@ -101,6 +101,20 @@ void robot_from_json(const std::string& text, RobotHost* out) {
     d.pair_b[p] = out->clink_of_link[P[p][1].i()];
     if (d.pair_a[p] < 0 || d.pair_b[p] < 0) throw std::runtime_error("model: pair on a link without geometry");
   }
+  // sphere pairs in (link pair, sphere of a, sphere of b) order; (ra + rb)^2 rounded as the device would
+  d.n_spairs = 0;
+  for (int p = 0; p < d.n_pairs; ++p) {
+    int a = d.pair_a[p], b = d.pair_b[p];
+    for (int sa = d.cl_sph0[a]; sa < d.cl_sph0[a] + d.cl_nsph[a]; ++sa)
+      for (int sb = d.cl_sph0[b]; sb < d.cl_sph0[b] + d.cl_nsph[b]; ++sb) {
+        if (d.n_spairs >= MAX_SPAIRS) throw std::runtime_error("model: too many sphere pairs");
+        if (sa > 255 || sb > 255) throw std::runtime_error("model: sphere index out of range");
+        volatile double rs = d.sph_r[sa] + d.sph_r[sb];
+        d.sp_ab[d.n_spairs] = (uint16_t)(sa | (sb << 8));
+        d.sp_rr2[d.n_spairs] = rs * rs;
+        d.n_spairs++;
+      }
+  }
   for (int j = 0; j < NJ; ++j) {
     d.q_min[j] = m["q_min"][j].d();
     d.q_max[j] = m["q_max"][j].d();

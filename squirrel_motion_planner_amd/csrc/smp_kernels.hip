@@ -37,24 +37,40 @@ __device__ __forceinline__ void stage_model(const RobotDev* rb, const MapCfg* mc
   __syncthreads();
 }
 
-__global__ void __launch_bounds__(BLOCK) check_kernel(const RobotDev* __restrict__ rb, SceneDev sc,
-                                                      const MapCfg* __restrict__ mc, const double* __restrict__ q,
-                                                      long long n, int self, int map, uint8_t* __restrict__ valid) {
-  __shared__ TileLds<CHECK_CT> L;
-  __shared__ double ql[CHECK_CT][NJ];
+template <int CT>
+__global__ void __launch_bounds__(BLOCK) check_kernel_t(const RobotDev* __restrict__ rb, SceneDev sc,
+                                                        const MapCfg* __restrict__ mc, const double* __restrict__ q,
+                                                        long long n, int self, int map, uint8_t* __restrict__ valid,
+                                                        unsigned long long* prof) {
+  __shared__ TileLds<CT> L;
+  __shared__ double ql[CT][NJ];
+  unsigned long long* pr = blockIdx.x == 0 ? prof : nullptr;  // stage clocks of block 0 (latency probe)
+  unsigned long long c0 = 0, w0 = 0;
+  if (pr && threadIdx.x == 0) { c0 = __builtin_amdgcn_s_memtime(); w0 = wall_clock64(); }
   stage_model(rb, mc, &g_rb, &g_mc);
-  const long long ntiles = (n + CHECK_CT - 1) / CHECK_CT;
+  const long long ntiles = (n + CT - 1) / CT;
   for (long long t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    long long base = t * CHECK_CT;
-    int nc = (int)min((long long)CHECK_CT, n - base);
-    if (threadIdx.x < nc * NJ) {
-      int c = threadIdx.x / NJ, j = threadIdx.x - c * NJ;
+    long long base = t * CT;
+    int nc = (int)min((long long)CT, n - base);
+    for (int it = threadIdx.x; it < nc * NJ; it += BLOCK) {
+      int c = it / NJ, j = it - c * NJ;
       ql[c][j] = q[(long long)j * n + base + c];
     }
     __syncthreads();
-    collide_tile<CHECK_CT>(&g_rb, sc, &g_mc, nc, ql, self, map, L);
+    collide_tile<CT>(&g_rb, sc, &g_mc, nc, ql, self, map, L, nullptr, pr);
     if (threadIdx.x < nc) valid[base + threadIdx.x] = L.coll[threadIdx.x] ? 0 : 1;
     __syncthreads();
+  }
+  if (pr && threadIdx.x == 0) { pr[4] = __builtin_amdgcn_s_memtime() - c0; pr[5] = wall_clock64() - w0; }
+}
+
+// Batched isConfigValid (birrt_star.cpp:6897-6908): grid-stride over tiles of CT configurations.
+void launch_check(int ct, int grid, hipStream_t st, const RobotDev* rb, SceneDev sc, const MapCfg* mc, const double* q,
+                  long long n, int self, int map, uint8_t* valid, unsigned long long* prof) {
+  switch (ct) {
+    case 8: hipLaunchKernelGGL(check_kernel_t<8>, dim3(grid), dim3(BLOCK), 0, st, rb, sc, mc, q, n, self, map, valid, prof); break;
+    case 16: hipLaunchKernelGGL(check_kernel_t<16>, dim3(grid), dim3(BLOCK), 0, st, rb, sc, mc, q, n, self, map, valid, prof); break;
+    default: hipLaunchKernelGGL(check_kernel_t<CHECK_CT>, dim3(grid), dim3(BLOCK), 0, st, rb, sc, mc, q, n, self, map, valid, prof); break;
   }
 }
 
@@ -98,18 +114,18 @@ struct PlanLds {
       double tq[32][NJ];
     } tile;
     double seg[MAXE][MAX_PTS][3];
-    struct {
-      double rd[BLOCK / 64];
-      int ri[BLOCK / 64];
-      double rc2[BLOCK / 64];
-      int ri2[BLOCK / 64];
-    } red;
+    struct {  // near_set: per-wave sorted low / high ends of the near list
+      unsigned long long wlk[BLOCK / 64][MAX_NEAR], whk[BLOCK / 64][MAX_NEAR];
+      int wli[BLOCK / 64][MAX_NEAR], whi[BLOCK / 64][MAX_NEAR];
+      int wn[BLOCK / 64], wtot[BLOCK / 64];
+    } nr;
   } u;
   // edge batch
   double eg_start[MAXE][NJ], eg_target[MAXE][NJ], eg_step[MAXE][NJ], eg_end[MAXE][NJ];
   double eg_base[MAXE][3], eg_cost[MAXE][3];
   int eg_first[MAXE], eg_need[MAXE], eg_near[MAXE], eg_ptr[MAXE];
   int tile_e[32], tile_i[32], tile_n;
+  int count_slot;  // profiling: phase the checked configurations are attributed to
   // near lists (ascending (cost,id) for the first max_near; last max_near in ascending order)
   int nk;
   int lo_i[MAX_NEAR], hi_i[MAX_NEAR];
@@ -144,7 +160,7 @@ struct Ctx {
 
 // Phase clocks (thread 0, s_memrealtime ticks): where an iteration spends its time.
 enum { P_SAMPLE, P_NN, P_EXPAND, P_NEAR, P_CHOOSE, P_REWIRE, P_CONNECT, P_TILES, P_NTILES, P_COSTS, P_VIA, P_NVIA,
-       P_TFK, P_TTEST };
+       P_TFK, P_TCHAIN, P_TCENTRE, P_TTEST, P_XEXPAND, P_XCHOOSE, P_XREWIRE, P_XCONNECT };
 #define PROF_BEGIN() unsigned long long _pt = threadIdx.x == 0 ? wall_clock64() : 0
 #define PROF_END(k) if (threadIdx.x == 0) { g_L.S.prof[k] += wall_clock64() - _pt; }
 
@@ -226,106 +242,128 @@ __device__ int nearest(const Ctx& C, int t, const double* q) {
   return block_argmin(best, bid);
 }
 
-// (cost,id) lexicographic order of the near list (std::sort order made total).
-__device__ __forceinline__ bool ci_less(double ca, int ia, double cb, int ib) {
-  return ca < cb || (ca == cb && ia < ib);
+// (cost,id) lexicographic order of the near list (std::sort order made total).  Costs are
+// non-negative doubles, whose bit patterns order like the values, so keys compare as integers (fp64 compares
+// carry ~40 cycles of dependent latency on gfx950).
+__device__ __forceinline__ bool ki_less(unsigned long long ka, int ia, unsigned long long kb, int ib) {
+  return ka < kb || (ka == kb && ia < ib);
 }
 
-// find_near_vertices_interpolation (birrt_star.cpp:4272-4324): count k, the first MAX_NEAR and the last
-// MAX_NEAR entries of the (cost,id)-sorted near list.  Per-thread register lists + 20-round block merge.
+// find_near_vertices_interpolation (birrt_star.cpp:4272-4324): count k, the first K and the last K entries of
+// the (cost,id)-sorted near list.
+//   1. scan: each wave keeps the K smallest and the K largest (key, id) of its nodes as sorted lists spread
+//      over lanes (lane k holds entry k); a 64-node batch only inserts the candidates that beat the current
+//      K-th entry, each insertion one compare + ballot + popcount + shfl_up;
+//   2. wave 0 merges the NW sorted wave lists of the low end, wave 1 those of the high end, in LDS.
 template <int K>
 __device__ void near_set(const Ctx& C, int t, const double* q, int excl) {
+  static_assert(K <= 64, "lane-distributed lists");
+  constexpr int NW = BLOCK / 64;
   const TreeDev& T = C.Q.tr[t];
   const int n = g_L.S.n[t], cap = g_L.S.cap;
   const double r = g_L.S.near_r;
+  const int lane = lane_id(), wave = wave_id();
   if (threadIdx.x == 0) g_L.S.near_nodes += n;
   double qq[NJ];
   for (int j = 0; j < NJ; ++j) qq[j] = q[j];
-  double lc[K], hc[K];
-  int li[K], hi[K];
+  const unsigned long long KMAX = ~0ull;
+  // lane k < K: entry k of the wave's low list (ascending) and of its high list (descending)
+  unsigned long long lk = KMAX, hk = 0;
+  int li = 0x7fffffff, hi = -1;
+  int wc = 0;
+  for (int base = wave * 64; base < n; base += BLOCK) {
+    const int i = base + lane;
+    bool near = false;
+    unsigned long long key = 0;
+    if (i < n) {
+      double s = 0.0;
 #pragma unroll
-  for (int k = 0; k < K; ++k) { lc[k] = __builtin_inf(); li[k] = 0x7fffffff; hc[k] = -__builtin_inf(); hi[k] = -1; }
-  long long cnt = 0;
-  for (int i = threadIdx.x; i < n; i += BLOCK) {
-    double s = 0.0;
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      double d = qq[j] - T.q[(size_t)j * cap + i];
-      s += d * d;
+      for (int j = 0; j < NJ; ++j) {
+        double d = qq[j] - T.q[(size_t)j * cap + i];
+        s += d * d;
+      }
+      near = sqrt(s) < r && i != excl;
+      if (near) key = (unsigned long long)__double_as_longlong(T.cost[i]);
     }
-    double dist = sqrt(s);
-    if (dist < r && i != excl) {
-      cnt++;
-      double c = T.cost[i];
-      if (ci_less(c, i, lc[K - 1], li[K - 1])) {
-        double cc = c;
-        int ii = i;
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-          bool sw = ci_less(cc, ii, lc[k], li[k]);
-          double tc = lc[k];
-          int ti = li[k];
-          lc[k] = sw ? cc : lc[k];
-          li[k] = sw ? ii : li[k];
-          cc = sw ? tc : cc;
-          ii = sw ? ti : ii;
+    const unsigned long long m_near = __ballot(near);
+    wc += __popcll(m_near);
+    // low list: candidates below the current K-th entry
+    {
+      const unsigned long long tk = __shfl(lk, K - 1);
+      const int ti = __shfl(li, K - 1);
+      unsigned long long m = __ballot(near && ki_less(key, i, tk, ti));
+      while (m) {
+        const int src = __builtin_ctzll(m);
+        m &= m - 1;
+        const unsigned long long kk = __shfl(key, src);
+        const int ii = src + base;
+        const int pos = __popcll(__ballot(lane < K && ki_less(lk, li, kk, ii)));
+        const unsigned long long uk = __shfl_up(lk, 1);
+        const int ui = __shfl_up(li, 1);
+        if (lane < K && lane >= pos) {
+          if (lane == pos) { lk = kk; li = ii; } else { lk = uk; li = ui; }
         }
       }
-      if (ci_less(hc[K - 1], hi[K - 1], c, i)) {
-        double cc = c;
-        int ii = i;
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-          bool sw = ci_less(hc[k], hi[k], cc, ii);
-          double tc = hc[k];
-          int ti = hi[k];
-          hc[k] = sw ? cc : hc[k];
-          hi[k] = sw ? ii : hi[k];
-          cc = sw ? tc : cc;
-          ii = sw ? ti : ii;
+    }
+    // high list (descending): candidates above the current K-th entry
+    {
+      const unsigned long long tk = __shfl(hk, K - 1);
+      const int ti = __shfl(hi, K - 1);
+      unsigned long long m = __ballot(near && ki_less(tk, ti, key, i));
+      while (m) {
+        const int src = __builtin_ctzll(m);
+        m &= m - 1;
+        const unsigned long long kk = __shfl(key, src);
+        const int ii = src + base;
+        const int pos = __popcll(__ballot(lane < K && ki_less(kk, ii, hk, hi)));
+        const unsigned long long uk = __shfl_up(hk, 1);
+        const int ui = __shfl_up(hi, 1);
+        if (lane < K && lane >= pos) {
+          if (lane == pos) { hk = kk; hi = ii; } else { hk = uk; hi = ui; }
         }
       }
     }
   }
-  // total count
-  for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
-  if (lane_id() == 0) g_L.wcount[wave_id()] = cnt;
+  const int take_w = min(K, wc);
+  if (lane < take_w) {
+    g_L.u.nr.wlk[wave][lane] = lk; g_L.u.nr.wli[wave][lane] = li;
+    g_L.u.nr.whk[wave][lane] = hk; g_L.u.nr.whi[wave][lane] = hi;
+  }
+  if (lane == 0) { g_L.u.nr.wn[wave] = take_w; g_L.u.nr.wtot[wave] = wc; }
   __syncthreads();
-  long long total = 0;
-  for (int w = 0; w < BLOCK / 64; ++w) total += g_L.wcount[w];
-  const int take = (int)min((long long)K, total);
-  // merge: `take` rounds of block-wide min (lo) and max (hi) over list heads
-  for (int rnd = 0; rnd < take; ++rnd) {
-    double dl = lc[0], dh = hc[0];
-    int il = li[0], ih = hi[0];
-    for (int off = 32; off > 0; off >>= 1) {
-      double odl = __shfl_xor(dl, off), odh = __shfl_xor(dh, off);
-      int oil = __shfl_xor(il, off), oih = __shfl_xor(ih, off);
-      if (ci_less(odl, oil, dl, il)) { dl = odl; il = oil; }
-      if (ci_less(dh, ih, odh, oih)) { dh = odh; ih = oih; }
+  // merge: wave 0 the low ends, wave 1 the high ends; lane w < NW owns wave w's sorted list
+  if (wave < 2) {
+    const bool low = wave == 0;
+    int head = 0;
+    const int len = lane < NW ? g_L.u.nr.wn[lane] : 0;
+    int tot = 0;
+    for (int w = 0; w < NW; ++w) tot += g_L.u.nr.wtot[w];
+    const int take = min(K, tot);
+    for (int rnd = 0; rnd < take; ++rnd) {
+      unsigned long long kv;
+      int iv;
+      if (head < len) {
+        kv = low ? g_L.u.nr.wlk[lane][head] : g_L.u.nr.whk[lane][head];
+        iv = low ? g_L.u.nr.wli[lane][head] : g_L.u.nr.whi[lane][head];
+      } else {
+        kv = low ? KMAX : 0;
+        iv = low ? 0x7fffffff : -1;
+      }
+      unsigned long long bk = kv;
+      int bi = iv;
+      for (int off = 4; off > 0; off >>= 1) {
+        unsigned long long ok = __shfl_xor(bk, off);
+        int oi = __shfl_xor(bi, off);
+        if (low ? ki_less(ok, oi, bk, bi) : ki_less(bk, bi, ok, oi)) { bk = ok; bi = oi; }
+      }
+      if (iv == bi && head < len) head++;
+      if (lane == 0) {
+        if (low) { g_L.lo_c[rnd] = __longlong_as_double((long long)bk); g_L.lo_i[rnd] = bi; }
+        else { g_L.hi_c[take - 1 - rnd] = __longlong_as_double((long long)bk); g_L.hi_i[take - 1 - rnd] = bi; }
+      }
     }
-    if (lane_id() == 0) { g_L.u.red.rd[wave_id()] = dl; g_L.u.red.ri[wave_id()] = il; g_L.u.red.rc2[wave_id()] = dh; g_L.u.red.ri2[wave_id()] = ih; }
-    __syncthreads();
-    dl = g_L.u.red.rd[0]; il = g_L.u.red.ri[0]; dh = g_L.u.red.rc2[0]; ih = g_L.u.red.ri2[0];
-    for (int w = 1; w < BLOCK / 64; ++w) {
-      if (ci_less(g_L.u.red.rd[w], g_L.u.red.ri[w], dl, il)) { dl = g_L.u.red.rd[w]; il = g_L.u.red.ri[w]; }
-      if (ci_less(dh, ih, g_L.u.red.rc2[w], g_L.u.red.ri2[w])) { dh = g_L.u.red.rc2[w]; ih = g_L.u.red.ri2[w]; }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) { g_L.lo_c[rnd] = dl; g_L.lo_i[rnd] = il; g_L.hi_c[take - 1 - rnd] = dh; g_L.hi_i[take - 1 - rnd] = ih; }
-    // pop the winners' heads (ids are unique: exactly one thread owns each)
-    if (li[0] == il) {
-#pragma unroll
-      for (int k = 0; k < K - 1; ++k) { lc[k] = lc[k + 1]; li[k] = li[k + 1]; }
-      lc[K - 1] = __builtin_inf(); li[K - 1] = 0x7fffffff;
-    }
-    if (hi[0] == ih) {
-#pragma unroll
-      for (int k = 0; k < K - 1; ++k) { hc[k] = hc[k + 1]; hi[k] = hi[k + 1]; }
-      hc[K - 1] = -__builtin_inf(); hi[K - 1] = -1;
-    }
+    if (threadIdx.x == 0) { g_L.nk = tot; g_L.n_lo = take; g_L.n_hi = take; }
   }
-  if (threadIdx.x == 0) { g_L.nk = (int)total; g_L.n_lo = take; g_L.n_hi = take; }
   __syncthreads();
 }
 
@@ -375,21 +413,34 @@ __device__ void edge_costs(const Ctx& C, int E) {
 // point before eg_first[e] has been checked.  With stop_first_valid the scan ends as soon as the first needed
 // edge not in collision is fully checked (choose-parent and the connect near loop consume the edges in
 // order and stop there); eg_first of the edges after it is then undefined.
-__device__ void edge_validity(const Ctx& C, int E, bool stop_first_valid) {
+__device__ void edge_validity(const Ctx& C, int E, bool stop_first_valid, int pslot) {
   const int np1 = g_L.S.n_pts + 1;
+  if (threadIdx.x == 0) g_L.count_slot = pslot + 4;
   if (threadIdx.x < E) { g_L.eg_first[threadIdx.x] = np1; g_L.eg_ptr[threadIdx.x] = 0; }
   __syncthreads();
   for (;;) {
-    if (threadIdx.x == 0) {
-      int nc = 0;
-      for (int e = 0; e < E && nc < 32; ++e) {
-        if (!g_L.eg_need[e] || g_L.eg_first[e] < np1 || g_L.eg_ptr[e] >= np1) continue;
-        int take = min(np1 - g_L.eg_ptr[e], 32 - nc);
-        for (int i = 0; i < take; ++i) { g_L.tile_e[nc + i] = e; g_L.tile_i[nc + i] = g_L.eg_ptr[e] + i; }
-        g_L.eg_ptr[e] += take;
-        nc += take;
+    // wave 0 (lane e = edge e): stop check, then the next tile's slots by a prefix sum of remaining points
+    if (threadIdx.x < 64) {
+      const int e = threadIdx.x;
+      const bool live = e < E && g_L.eg_need[e] && g_L.eg_first[e] >= np1;  // needed, no collision found
+      const int ptr = e < E ? g_L.eg_ptr[e] : np1;
+      bool stop = false;
+      if (stop_first_valid) {
+        const unsigned long long m = __ballot(live);
+        if (m) stop = __shfl(ptr, __builtin_ctzll(m)) >= np1;  // first live candidate fully checked: free
       }
-      g_L.tile_n = nc;
+      const int rem = (live && ptr < np1) ? np1 - ptr : 0;
+      int inc = rem;
+      for (int off = 1; off < 32; off <<= 1) {
+        int v = __shfl_up(inc, off);
+        if (e >= off) inc += v;
+      }
+      const int start = inc - rem;
+      const int take = stop ? 0 : max(0, min(rem, 32 - start));
+      for (int i = 0; i < take; ++i) { g_L.tile_e[start + i] = e; g_L.tile_i[start + i] = ptr + i; }
+      if (e < E) g_L.eg_ptr[e] = ptr + take;
+      const int total = __shfl(inc, 31);
+      if (e == 0) g_L.tile_n = stop ? 0 : min(32, total);
     }
     __syncthreads();
     const int nc = g_L.tile_n;
@@ -405,19 +456,10 @@ __device__ void edge_validity(const Ctx& C, int E, bool stop_first_valid) {
     collide_tile<32>((&g_rb), C.sc, (&g_mc), nc, g_L.u.tile.tq, g_L.S.self, g_L.S.map, g_L.u.tile.T, &order,
                      &g_L.S.prof[P_TFK]);
     PROF_END(P_TILES);
-    if (threadIdx.x == 0) g_L.S.prof[P_NTILES]++;
-    if (stop_first_valid) {
-      if (threadIdx.x == 0) {
-        int stop = 0;
-        for (int e = 0; e < E; ++e) {
-          if (!g_L.eg_need[e] || g_L.eg_first[e] < np1) continue;  // not needed / resolved in collision
-          stop = g_L.eg_ptr[e] >= np1;                           // first candidate still free: resolved?
-          break;
-        }
-        g_L.tile_n = stop;
-      }
-      __syncthreads();
-      if (g_L.tile_n) break;
+    if (threadIdx.x == 0) {
+      g_L.S.prof[pslot] += wall_clock64() - _pt;
+      g_L.S.prof[P_NTILES]++;
+      g_L.S.prof[pslot + 8] += nc;
     }
   }
   __syncthreads();
@@ -426,6 +468,7 @@ __device__ void edge_validity(const Ctx& C, int E, bool stop_first_valid) {
 // Reference-semantics accounting of one isEdgeValid call (stops at the first collision).
 __device__ __forceinline__ void count_edge(int first) {
   int np1 = g_L.S.n_pts + 1;
+  g_L.S.prof[g_L.count_slot] += first >= np1 ? np1 : first + 1;
   if (first >= np1) { g_L.S.checked += np1; g_L.S.valid += np1; }
   else { g_L.S.checked += first + 1; g_L.S.valid += first; }
 }
@@ -681,7 +724,7 @@ __device__ void choose_parent(const Ctx& C, int t) {
     if (threadIdx.x < E) g_L.eg_need[threadIdx.x] = g_L.eg_cost[threadIdx.x][0] <= g_L.xn.c[0];
     for (int e = E + threadIdx.x; e < MAXE; e += BLOCK) g_L.eg_need[e] = 0;
     __syncthreads();
-    edge_validity(C, E, true);
+    edge_validity(C, E, true, P_XCHOOSE);
     if (threadIdx.x == 0) {
       for (int e = 0; e < E; ++e) {
         if (!g_L.eg_need[e]) continue;
@@ -752,7 +795,7 @@ __device__ void rewire(const Ctx& C, int t) {
   }
   for (int e = cnt + threadIdx.x; e < MAXE; e += BLOCK) g_L.eg_need[e] = 0;
   __syncthreads();
-  edge_validity(C, cnt, false);
+  edge_validity(C, cnt, false, P_XREWIRE);
   if (threadIdx.x == 0) {
     QState& S = g_L.S;
     for (int e = 0; e < cnt && S.status == 0; ++e) {
@@ -815,7 +858,7 @@ __device__ void connect_graphs(const Ctx& C, int t) {
   }
   __syncthreads();
   if (g_L.eg_need[0]) {
-    edge_validity(C, 1, false);
+    edge_validity(C, 1, false, P_XCONNECT);
     if (threadIdx.x == 0) {
       int f = g_L.eg_first[0];
       count_edge(f);
@@ -869,7 +912,7 @@ __device__ void connect_graphs(const Ctx& C, int t) {
       }
       for (int e = E + threadIdx.x; e < MAXE; e += BLOCK) g_L.eg_need[e] = 0;
       __syncthreads();
-      edge_validity(C, E, true);
+      edge_validity(C, E, true, P_XCONNECT);
       // sequential replay of the near loop (birrt_star.cpp:2820-3030)
       for (int e = 0; e < E; ++e) {
         if (threadIdx.x == 0) {
@@ -954,7 +997,7 @@ __device__ void iteration(const Ctx& C) {
   }
   __syncthreads();
   edge_costs(C, 1);
-  edge_validity(C, 1, false);
+  edge_validity(C, 1, false, P_XEXPAND);
   if (threadIdx.x == 0) {
     int f = g_L.eg_first[0];
     count_edge(f);

@@ -39,7 +39,7 @@ struct QState {                // per query, persisted in global memory across l
   long long max_checked;       // > 0: stop once this many configurations were collision-checked
   long long checked, valid, first_iter, last_iter;
   long long nn_nodes, near_nodes;  // nodes streamed by nearest / near scans (algorithmic bytes)
-  unsigned long long prof[24];     // device-clock ticks per planner phase (SMP_PROF_* in smp_kernels.hip)
+  unsigned long long prof[32];     // device-clock ticks per planner phase (SMP_PROF_* in smp_kernels.hip)
   unsigned long long t0, t_first, t_end, deadline;  // device wall clock (0 deadline = none)
   double cbest[3], h0[3];
   NodeRef nB, nA;              // m_node_tree_B / m_node_tree_A

@@ -10,6 +10,7 @@ constexpr int MAX_SPH = 72;     // collision spheres (64)
 constexpr int MAX_CLINK = 32;   // collision links (27)
 constexpr int MAX_PAIRS = 256;  // self-collision link pairs (165 non-rigid of the 230 SRDF-enabled)
 constexpr int MAX_BODY = 8;     // moving bodies (6)
+constexpr int MAX_SPAIRS = 768; // sphere pairs of the enabled link pairs (584)
 constexpr int NJ = 8;           // planning joints
 constexpr int BLOCK = 512;      // threads per workgroup (8 wavefronts, 2 per SIMD)
 
@@ -27,6 +28,10 @@ struct RobotDev {
   int cl_sph0[MAX_CLINK], cl_nsph[MAX_CLINK], cl_body[MAX_CLINK], cl_link[MAX_CLINK];
   double cl_cb[MAX_CLINK * 3], cl_r[MAX_CLINK];
   int pair_a[MAX_PAIRS], pair_b[MAX_PAIRS];
+  // flat self-collision list: every sphere pair of every enabled link pair, (a | b << 8) and (ra + rb)^2
+  int n_spairs;
+  uint16_t sp_ab[MAX_SPAIRS];
+  double sp_rr2[MAX_SPAIRS];
   double q_min[NJ], q_max[NJ];
   int rev[NJ];
 };
@@ -37,7 +42,7 @@ struct RobotDev {
 // 65535) to the nearest occupied cell -- a lower bound of (distance to any occupied box / res)^2.
 struct SceneDev {
   int nx, ny, nz, bnx, bny;
-  double ox, oy, oz, res;
+  double ox, oy, oz, res, inv_res;
   const uint64_t* bricks;
   const uint16_t* d2;
 };

@@ -1,0 +1,45 @@
+"""Collision-tile latency probe: one workgroup streams tiles of C2 configurations back to back (grid 1), and
+the full-chip batch rate (grid = all tiles).  Configurations: points of the edges a C2 planner run checks
+(tree nodes -> parents, interpolated), plus uniformly random ones."""
+import ctypes
+import math
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from squirrel_motion_planner_amd import _lib as L, scenes  # noqa: E402
+from squirrel_motion_planner_amd.planner import GpuPlanner, Scene  # noqa: E402
+
+sc = scenes.box_room()
+gp = GpuPlanner(path_optimality_threshold=-math.inf)
+gp.set_scene(Scene.from_keys(sc.keys, sc.res))
+r = gp.plan(GpuPlanner.make_query(sc.start, sc.goal, sc.env_x, sc.env_y, iterations=1500, seed=1))
+qs = []
+for w in (0, 1):
+    par, conf, _ = gp.tree(w)
+    for i in range(1, len(par)):
+        p = par[i]
+        for s in range(21):
+            qs.append(conf[p] + s * (conf[i] - conf[p]) / 20.0)
+Q = np.array(qs)
+rng = np.random.default_rng(0)
+R = np.column_stack([rng.uniform(-5, 5, len(Q)), rng.uniform(-5, 5, len(Q))] +
+                    [rng.uniform(-2, 2, len(Q)) for _ in range(6)])
+lib = L.lib()
+for name, X in (("tree-edges", Q), ("random", R)):
+    soa = np.ascontiguousarray(X.T)
+    n = len(X)
+    for tile, grid in ((32, 1), (16, 1), (8, 1), (32, 2048)):
+        ms = ctypes.c_double()
+        hz = ctypes.c_double()
+        ticks = (ctypes.c_uint64 * 6)()
+        L.check(lib.smp_probe_check_latency(gp.h, soa.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), n, 1, 1, grid, tile,
+                                            ctypes.byref(ms), ticks, ctypes.byref(hz)))
+        tiles = (n + tile - 1) // tile
+        per_tile_us = [t / hz.value * 1e6 / (tiles if grid == 1 else max(1, tiles // grid)) for t in ticks]
+        print("%-10s tile %2d n %7d grid %5d: %.2f ms  %.3g configs/s  per tile %.2f us  stages(us) A %.2f B %.2f C0 %.2f C %.2f"
+              % (name, tile, n, grid, ms.value, n / (ms.value * 1e-3), ms.value * 1e3 / tiles * (grid if grid > 1 else 1) /
+                 (1 if grid == 1 else min(grid, tiles)), *per_tile_us[:4]), flush=True)
+        print("   shader clock %.3f GHz" % (ticks[4] / (ticks[5] / hz.value) / 1e9 if ticks[5] else 0), flush=True)
