@@ -69,7 +69,6 @@ def cpu_baseline(sc, samples, seed):
 
 def main():
     a = parse()
-    import numpy as np
     import torch
     import torch.distributed as dist
 
@@ -80,35 +79,13 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    from squirrel_motion_planner_amd import scenes
+    from squirrel_motion_planner_amd import distributed as D, scenes
     from squirrel_motion_planner_amd.planner import GpuPlanner, Scene
 
     sc = scenes.box_room()
-    # scene: rank 0 builds the grid (octomap keys -> bitset + squared EDT) and broadcasts it once (RCCL/xGMI)
-    if rank == 0:
-        s0 = Scene.from_keys(sc.keys, sc.res)
-        info = s0.info()
-        bits, d2 = s0.export()
-    if world > 1:
-        meta = torch.zeros(7, dtype=torch.float64, device="cuda")
-        if rank == 0:
-            meta[:] = torch.tensor(list(info["dims"]) + list(info["origin"]) + [info["res"]], dtype=torch.float64)
-        dist.broadcast(meta, 0)
-        dims = [int(v) for v in meta[:3].tolist()]
-        origin = meta[3:6].tolist()
-        res = float(meta[6])
-        nw = ((dims[0] + 63) // 64) * dims[1] * dims[2]
-        nc = dims[0] * dims[1] * dims[2]
-        tb = torch.zeros(nw, dtype=torch.int64, device="cuda")
-        td = torch.zeros(nc, dtype=torch.int16, device="cuda")
-        if rank == 0:
-            tb.copy_(torch.from_numpy(bits.view(np.int64)))
-            td.copy_(torch.from_numpy(d2.view(np.int16)))
-        dist.broadcast(tb, 0)
-        dist.broadcast(td, 0)
-        scene = Scene.from_grid(tb.cpu().numpy().view(np.uint64), td.cpu().numpy().view(np.uint16), dims, origin, res)
-    else:
-        scene = s0
+    # scene: rank 0 builds the grid (octomap keys -> bitset + box-gap field) and broadcasts it once (RCCL/xGMI)
+    s0 = Scene.from_keys(sc.keys, sc.res) if rank == 0 else None
+    scene = D.broadcast_scene(s0, device="cuda") if world > 1 else s0
 
     gp = GpuPlanner(device=local, path_optimality_threshold=-math.inf)
     gp.set_scene(scene)
@@ -156,12 +133,9 @@ def main():
     local_vec = [elapsed, totals["checked"], totals["valid"], totals["iters"], totals["nn"], totals["near"],
                  totals["plan_ms"], totals["launches"]]
     if world > 1:
-        tt = torch.tensor(local_vec, dtype=torch.float64, device="cuda")
-        tmax = tt.clone()
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        dist.all_reduce(tt, op=dist.ReduceOp.SUM)
-        elapsed = float(tmax[0])
-        checked, valid, iters, nn, near, plan_ms, launches = [float(v) for v in tt[1:].tolist()]
+        tsum, tmax = D.reduce_counters(local_vec, device="cuda")
+        elapsed = tmax[0]
+        checked, valid, iters, nn, near, plan_ms, launches = tsum[1:]
         plan_ms_rank0 = totals["plan_ms"]
     else:
         checked, valid, iters, nn, near, plan_ms, launches = local_vec[1:]

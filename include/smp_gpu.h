@@ -73,6 +73,8 @@ typedef struct smp_params {
   int tree_optimization;   /* m_tree_optimization_active (default 1) */
   int informed_sampling;   /* m_informed_sampling_active (default 1) */
   int64_t node_capacity;   /* per-tree node capacity on the device (0: derived from the budget) */
+  int helpers;             /* helper workgroups per query that share its collision tiles across CUs
+                              (0: automatic, up to 63; -1: none, the query runs on its own workgroup) */
 } smp_params;
 
 typedef struct smp_query {

@@ -40,7 +40,7 @@ class SceneOpts(ctypes.Structure):
 class Params(ctypes.Structure):
     _fields_ = [("near_threshold", _d), ("step_factor", _d), ("num_traj_segments", _i), ("max_near_nodes", _i),
                 ("path_optimality_threshold", _d), ("tree_optimization", _i), ("informed_sampling", _i),
-                ("node_capacity", _i64)]
+                ("node_capacity", _i64), ("helpers", _i)]
 
 
 class Query(ctypes.Structure):

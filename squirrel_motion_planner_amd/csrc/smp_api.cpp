@@ -1,5 +1,6 @@
 // C ABI implementation (include/smp_gpu.h): device memory, launches, result assembly.
 // No CPU fallback: without a usable GPU every compute entry point returns SMP_ERR_NO_DEVICE.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -22,6 +23,7 @@ namespace smp {
 void launch_check(int ct, int grid, hipStream_t st, const RobotDev* rb, SceneDev sc, const MapCfg* mc, const double* q,
                   long long n, int self, int map, uint8_t* valid, unsigned long long* prof);
 __global__ void plan_kernel(const RobotDev* rb, SceneDev sc, const MapCfg* mc, QueryDev* qs, int iters);
+__global__ void helper_kernel(const RobotDev* rb, SceneDev sc, const MapCfg* mc, QueryDev* qs, int nq);
 __global__ void path_kernel(QueryDev* qs, int* counts);
 __global__ void sincos_kernel(const double* x, int n, double* s, double* c);
 __global__ void u01_kernel(unsigned long long seed, unsigned query, const uint32_t* ctr, int n, double* out);
@@ -75,11 +77,12 @@ struct QueryBuffers {
   DBuf<double> q, cost, e_start, e_target, rows;
   DBuf<int> parent, first_child, next_sib, prev_sib, stack, path_nodes;
   DBuf<ViaNode> via;
+  DBuf<JobBoard> jb;
   size_t cap = 0;
   void release() {
     st.release(); q.release(); cost.release(); e_start.release(); e_target.release(); rows.release();
     parent.release(); first_child.release(); next_sib.release(); prev_sib.release(); stack.release();
-    path_nodes.release(); via.release();
+    path_nodes.release(); via.release(); jb.release();
     cap = 0;
   }
 };
@@ -89,6 +92,8 @@ struct QueryBuffers {
 struct smp_planner {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t hstream = nullptr;   // helper_kernel (collision-job helpers), concurrent with plan_kernel
+  hipEvent_t ev_board = nullptr;
   RobotHost robot;
   smp_params params;
   RobotDev* d_rb = nullptr;
@@ -109,6 +114,7 @@ struct smp_planner {
   double last_check_ms = 0, last_plan_ms = 0;
   int64_t last_plan_launches = 0;
   double wall_rate_hz = 1e8;
+  int num_cus = 256;
   // last plan (query 0) bookkeeping for smp_get_tree
   int last_n[2] = {0, 0};
 };
@@ -138,6 +144,7 @@ void smp_params_default(smp_params* p) {
   p->tree_optimization = 1;
   p->informed_sampling = 1;
   p->node_capacity = 0;
+  p->helpers = 0;
 }
 
 void smp_scene_opts_default(smp_scene_opts* o) {
@@ -297,6 +304,10 @@ int smp_planner_create(int device, const smp_robot* robot, const smp_params* par
     return SMP_ERR_ARG;
   }
   HIPCHK(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
+  int prio_lo = 0, prio_hi = 0;
+  HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+  HIPCHK(hipStreamCreateWithPriority(&p->hstream, hipStreamNonBlocking, prio_hi));
+  HIPCHK(hipEventCreateWithFlags(&p->ev_board, hipEventDisableTiming));
   HIPCHK(hipMalloc(&p->d_rb, sizeof(RobotDev)));
   HIPCHK(hipMalloc(&p->d_mc, sizeof(MapCfg)));
   HIPCHK(hipMemcpy(p->d_rb, &p->robot.dev, sizeof(RobotDev), hipMemcpyHostToDevice));
@@ -305,6 +316,9 @@ int smp_planner_create(int device, const smp_robot* robot, const smp_params* par
   int khz = 0;
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) == hipSuccess && khz > 0)
     p->wall_rate_hz = khz * 1000.0;
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+    p->num_cus = cus;
   std::memset(&p->sc, 0, sizeof(p->sc));
   int st = update_mapcfg(p);
   if (st) { delete p; return st; }
@@ -324,6 +338,8 @@ void smp_planner_destroy(smp_planner* p) {
   if (p->ev0) (void)hipEventDestroy(p->ev0);
   if (p->ev1) (void)hipEventDestroy(p->ev1);
   if (p->stream) (void)hipStreamDestroy(p->stream);
+  if (p->hstream) (void)hipStreamDestroy(p->hstream);
+  if (p->ev_board) (void)hipEventDestroy(p->ev_board);
   delete p;
 }
 
@@ -471,6 +487,7 @@ static hipError_t alloc_query(QueryBuffers& b, size_t cap, int via_cap, long lon
   if ((e = b.path_nodes.reserve(cap * 2))) return e;
   if ((e = b.via.reserve(via_cap))) return e;
   if ((e = b.rows.reserve(std::max<long long>(rows, 1) * 5))) return e;
+  if ((e = b.jb.reserve(1))) return e;
   b.cap = cap;
   return hipSuccess;
 }
@@ -494,6 +511,8 @@ static QueryDev make_qdev(QueryBuffers& b, size_t cap, long long rows) {
   d.rows = b.rows.p;
   d.rows_cap = rows;
   d.path_nodes = b.path_nodes.p;
+  d.jb = nullptr;
+  d.trace = nullptr;
   return d;
 }
 
@@ -561,6 +580,20 @@ extern "C" int smp_plan_batch(smp_planner* p, const smp_query* qs, int nq, smp_r
     if (st) return st;
     HIPCHK(hipMemcpyAsync(qdev[i].st, &S[i], sizeof(QState), hipMemcpyHostToDevice, p->stream));
   }
+  // helper workgroups per query (DESIGN.md "Helpers"): one workgroup per CU, leaders first
+  int nh = p->params.helpers;
+  if (nh == 0) nh = std::min(63, std::max(0, p->num_cus / nq - 1));
+  if (nh < 0) nh = 0;
+  for (int i = 0; i < nq; ++i) qdev[i].jb = nh > 0 ? p->qb[i].jb.p : nullptr;
+  static int* trace_host = nullptr;
+  const bool debug = std::getenv("SMP_DEBUG") != nullptr;
+  if (debug && !trace_host) HIPCHK(hipHostMalloc(&trace_host, 256 * sizeof(int), hipHostMallocMapped));
+  if (debug) {
+    int* trace_dev = nullptr;
+    std::memset(trace_host, 0, 256 * sizeof(int));
+    HIPCHK(hipHostGetDevicePointer((void**)&trace_dev, trace_host, 0));
+    qdev[0].trace = trace_dev;
+  }
   HIPCHK(p->d_qdev.reserve(nq));
   HIPCHK(p->d_counts.reserve(2 * nq));
   HIPCHK(hipMemcpyAsync(p->d_qdev.p, qdev.data(), nq * sizeof(QueryDev), hipMemcpyHostToDevice, p->stream));
@@ -581,17 +614,63 @@ extern "C" int smp_plan_batch(smp_planner* p, const smp_query* qs, int nq, smp_r
     if (tmax == 0 && launches > max_iters / 256 + 64) return SMP_ERR_HIP;  // no progress: never spin forever
     if (tmax > 0 && std::chrono::duration<double>(std::chrono::steady_clock::now() - t_begin).count() > tmax * 4 + 60)
       return SMP_ERR_HIP;
+    if (nh > 0) {
+      // fresh boards, then the helpers on their own (high-priority, separate hardware queue) stream; they wait
+      // for the reset and leave when the leader signals stop
+      for (int i = 0; i < nq; ++i) HIPCHK(hipMemsetAsync(qdev[i].jb, 0, sizeof(JobBoard), p->stream));
+      HIPCHK(hipEventRecord(p->ev_board, p->stream));
+      HIPCHK(hipStreamWaitEvent(p->hstream, p->ev_board, 0));
+      hipLaunchKernelGGL(helper_kernel, dim3(nq * nh), dim3(BLOCK), 0, p->hstream, p->d_rb, p->sc, p->d_mc,
+                         p->d_qdev.p, nq);
+      HIPCHK(hipGetLastError());
+    }
     HIPCHK(hipEventRecord(p->ev0, p->stream));
     hipLaunchKernelGGL(plan_kernel, dim3(nq), dim3(BLOCK), 0, p->stream, p->d_rb, p->sc, p->d_mc, p->d_qdev.p, chunk);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(p->ev1, p->stream));
     launches++;
+    if (debug) {  // bounded wait: print the leader's progress markers if the launch does not finish
+      auto tw = std::chrono::steady_clock::now();
+      hipError_t qe;
+      while ((qe = hipStreamQuery(p->stream)) == hipErrorNotReady || qe != hipSuccess) {
+        if (qe != hipErrorNotReady || std::chrono::duration<double>(std::chrono::steady_clock::now() - tw).count() > 10.0) {
+          if (qe != hipErrorNotReady) std::fprintf(stderr, "[smp] launch %lld failed: %s\n", (long long)launches, hipGetErrorString(qe));
+          std::fprintf(stderr, "[smp] launch %lld did not finish in 10 s; trace:", (long long)launches);
+          for (int i = 0; i < 8; ++i) std::fprintf(stderr, " %d", trace_host[i]);
+          for (int h = 0; h < std::min(nh, 63); ++h)
+            std::fprintf(stderr, " | h%d %d %d %d", h, trace_host[8 + 3 * h], trace_host[9 + 3 * h], trace_host[10 + 3 * h]);
+          std::fprintf(stderr, "\n");
+          std::_Exit(3);
+        }
+      }
+    }
     for (int i = 0; i < nq; ++i)
       HIPCHK(hipMemcpyAsync(&S[i], qdev[i].st, sizeof(QState), hipMemcpyDeviceToHost, p->stream));
     HIPCHK(hipStreamSynchronize(p->stream));
+    if (nh > 0) HIPCHK(hipStreamSynchronize(p->hstream));
     float ms = 0;
     HIPCHK(hipEventElapsedTime(&ms, p->ev0, p->ev1));
     total_ms += ms;
+    if (debug) {
+      std::fprintf(stderr, "[smp] scene view: leader d2 %08x%08x nx %d bricks %08x |", trace_host[97], trace_host[96],
+                   trace_host[98], trace_host[99]);
+      for (int h = 0; h < std::min(nh, 30); ++h)
+        std::fprintf(stderr, " h%d d2 %08x%08x nx %d bricks %08x", h, trace_host[101 + 4 * h], trace_host[100 + 4 * h],
+                     trace_host[102 + 4 * h], trace_host[103 + 4 * h]);
+      for (int h = 0; h < std::min(nh, 16); ++h)
+        if (trace_host[200 + 2 * h]) std::fprintf(stderr, " CORRUPT h%d d2lo %08x", h, trace_host[201 + 2 * h]);
+      std::fprintf(stderr, "\n");
+    }
+    if (std::getenv("SMP_DEBUG")) {
+      JobBoard jbh;
+      if (nh > 0) HIPCHK(hipMemcpy(&jbh, qdev[0].jb, sizeof(JobBoard), hipMemcpyDeviceToHost));
+      std::fprintf(stderr, "[smp] launch %lld grid %d chunk %d: %.3f ms phase %d status %d iter %lld checked %lld"
+                   " board seq %d stop %d done %d claim %llx ntiles %d diag pub %d join %d casfail %d giveup %d "
+                   "leaderdone %d tiles %d\n", (long long)launches, nq * (1 + nh), chunk, ms,
+                   S[0].phase, S[0].status, S[0].iter, S[0].checked, nh ? jbh.seq : -1, nh ? jbh.stop : -1,
+                   nh ? jbh.done : -1, nh ? jbh.claim : 0ull, nh ? jbh.ntiles : -1, jbh.pad0[0], jbh.pad0[1],
+                   jbh.pad0[2], jbh.pad0[3], jbh.pad0[4], jbh.pad0[5]);
+    }
     bool all_done = true;
     for (int i = 0; i < nq; ++i) all_done &= (S[i].phase == 2 || S[i].status != 0);
     if (all_done) break;

@@ -235,10 +235,17 @@ struct TileLds {
 // Optional ordering of a tile's configurations: configuration c is point ord[c] of group grp[c] (an edge);
 // grp_first[g] is the lowest colliding point index of group g found so far.  A configuration whose index
 // exceeds it is skipped (it cannot change the group's first collision); a colliding one lowers it.
+// grp_first may live in LDS (one workgroup) or in HBM shared by several workgroups (agent = true: reads are
+// agent-scope loads, so a stale L1 line of an earlier job can never cause a skip).
 struct TileOrder {
   const int* grp;
   const int* ord;
   int* grp_first;
+  bool agent;
+  __device__ __forceinline__ int first(int g) const {
+    return agent ? __hip_atomic_load(&grp_first[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                 : __atomic_load_n(&grp_first[g], __ATOMIC_RELAXED);
+  }
 };
 
 // Collision test of nc <= CT configurations already placed in q_lds[c][8] (LDS), all block threads.
@@ -313,7 +320,7 @@ __device__ __forceinline__ void collide_tile(const RobotDev* __restrict__ rb, co
   uint32_t live = 0;
   for (int k = 0; k < CPW; ++k) {
     const int c = k * NWAVE + wave;
-    if (c < nc && !(ord && ord->ord[c] > __atomic_load_n(&ord->grp_first[ord->grp[c]], __ATOMIC_RELAXED)))
+    if (c < nc && !(ord && ord->ord[c] > ord->first(ord->grp[c])))
       live |= 1u << k;
   }
   if (live) {

@@ -106,13 +106,26 @@ __global__ void sqrt_div_kernel(const double* a, const double* b, int n, double*
 }
 
 // ============================================================================================ planner
+// LDS of job mode (leader and helper kernel): the published job + one job tile.
+struct JobLds {
+  TileLds<HELPER_CT> T;
+  double tq[HELPER_CT][NJ];
+  double start[MAXE][NJ], step[MAXE][NJ];
+  int slot_e[JOB_SLOTS], slot_i[JOB_SLOTS];
+  int E, np1, nslots, ntiles, self, map, seq, tile, go, hidx;
+};
+#ifndef SMP_PLAN_CT
+#define SMP_PLAN_CT 32
+#endif
+constexpr int PLAN_CT = SMP_PLAN_CT;  // configurations per collision tile of the planner
 struct PlanLds {
   QState S;
   union {
     struct {
-      TileLds<32> T;
-      double tq[32][NJ];
+      TileLds<PLAN_CT> T;
+      double tq[PLAN_CT][NJ];
     } tile;
+    JobLds job;  // job mode: the leader's LDS copy of its published job + one job tile
     double seg[MAXE][MAX_PTS][3];
     struct {  // near_set: per-wave sorted low / high ends of the near list
       unsigned long long wlk[BLOCK / 64][MAX_NEAR], whk[BLOCK / 64][MAX_NEAR];
@@ -124,8 +137,9 @@ struct PlanLds {
   double eg_start[MAXE][NJ], eg_target[MAXE][NJ], eg_step[MAXE][NJ], eg_end[MAXE][NJ];
   double eg_base[MAXE][3], eg_cost[MAXE][3];
   int eg_first[MAXE], eg_need[MAXE], eg_near[MAXE], eg_ptr[MAXE];
-  int tile_e[32], tile_i[32], tile_n;
+  int tile_e[PLAN_CT], tile_i[PLAN_CT], tile_n;
   int count_slot;  // profiling: phase the checked configurations are attributed to
+  int job_seq;     // last job published by this leader (this launch)
   // near lists (ascending (cost,id) for the first max_near; last max_near in ascending order)
   int nk;
   int lo_i[MAX_NEAR], hi_i[MAX_NEAR];
@@ -165,6 +179,10 @@ enum { P_SAMPLE, P_NN, P_EXPAND, P_NEAR, P_CHOOSE, P_REWIRE, P_CONNECT, P_TILES,
 #define PROF_END(k) if (threadIdx.x == 0) { g_L.S.prof[k] += wall_clock64() - _pt; }
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+// Block-uniform control value read from LDS, made provably wave-uniform (a scalar register): every loop
+// or branch that contains a __syncthreads() must be steered by such a value, or the compiler may lower it
+// as a divergent region and desynchronise the waves' barrier counts.
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
 
 // --------------------------------------------------------------------------------------- node access
@@ -413,9 +431,218 @@ __device__ void edge_costs(const Ctx& C, int E) {
 // point before eg_first[e] has been checked.  With stop_first_valid the scan ends as soon as the first needed
 // edge not in collision is fully checked (choose-parent and the connect near loop consume the edges in
 // order and stop there); eg_first of the edges after it is then undefined.
+// --------------------------------------------------------------------------------------- jobs (helpers)
+#define TRACE(C, slot, v) \
+  if ((C).Q.trace) __hip_atomic_store(&(C).Q.trace[slot], (int)(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+__device__ __forceinline__ void st_agent(int* p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ void st_agent(unsigned long long* p, unsigned long long v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int ld_agent(const int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ unsigned long long ld_agent(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Waits until this wave's vector-memory operations (stores, atomics) are performed.
+__device__ __forceinline__ void drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// One attempt to claim the next tile of job `seq`: the tile, -1 when none is left (or the board moved on to
+// another job), -2 when another workgroup won the race (retry).  One lane, straight-line code: loops inside
+// single-lane regions of a barrier loop can be restructured by the compiler into divergent barriers.
+// Claim word: job seq (bits 32-63) | slots of that job (16-31) | next tile (0-15).  The slot count travels
+// with the tag, so a claim is never validated against scalars of another job's payload.
+__device__ __forceinline__ unsigned long long claim_word(int seq, int nslots) {
+  return ((unsigned long long)(unsigned)seq << 32) | ((unsigned long long)(nslots & 0xffff) << 16);
+}
+__device__ __forceinline__ int job_claim_once(JobBoard* jb, int seq, int* nslots) {
+  unsigned long long v = ld_agent(&jb->claim);
+  const int ns = (int)((v >> 16) & 0xffff), next = (int)(v & 0xffff);
+  if ((int)(v >> 32) != seq || next >= (ns + HELPER_CT - 1) / HELPER_CT) return -1;
+  unsigned long long expect = v;
+  if (__hip_atomic_compare_exchange_strong(&jb->claim, &expect, v + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT)) {
+    *nslots = ns;
+    return next;
+  }
+  return -2;
+}
+
+// Takes tiles of the job held in g_L.u.job until none is left: configuration = start + i * step of its
+// (edge, point) slot (the leader's arithmetic), collision tile, first collisions by agent-scope atomicMin
+// into the board, then one `done` per tile after the results are performed.  All threads.
+__device__ __forceinline__ void job_work(const Ctx& C, JobBoard* jb, JobLds& J) {
+  for (;;) {
+    if (threadIdx.x == 0) J.tile = job_claim_once(jb, J.seq, &J.nslots);
+    __syncthreads();
+    const int t = uni(J.tile);
+    if (threadIdx.x == 0 && J.hidx >= 0) TRACE(C, 10 + 3 * (J.hidx & 63), t);
+    if (t == -1) break;
+    if (t < 0) continue;
+    const int base = t * HELPER_CT, nc = min(HELPER_CT, uni(J.nslots) - base);
+    if (threadIdx.x < nc * NJ) {
+      int c = threadIdx.x / NJ, j = threadIdx.x - c * NJ;
+      int e = J.slot_e[base + c];
+      J.tq[c][j] = J.start[e][j] + J.slot_i[base + c] * J.step[e][j];
+    }
+    __syncthreads();
+    collide_tile<HELPER_CT>((&g_rb), C.sc, (&g_mc), nc, J.tq, J.self, J.map, J.T);
+    if (threadIdx.x < nc && J.T.coll[threadIdx.x])
+      atomicMin(&jb->first[J.slot_e[base + threadIdx.x]], J.slot_i[base + threadIdx.x]);
+    drain();
+    __syncthreads();
+    if (threadIdx.x == 0) { atomicAdd(&jb->done, 1); atomicAdd(&jb->pad0[5], 1); }
+  }
+  __syncthreads();
+}
+
+// Leader: publishes the needed edges as one job (every point of every needed edge), works on it with the
+// helpers, waits for all its tiles and reads the first collision of each edge into eg_first.
+__device__ __forceinline__ void edge_validity_job(const Ctx& C, int E, int pslot) {
+  JobBoard* jb = C.Q.jb;
+  auto& J = g_L.u.job;
+  const int np1 = g_L.S.n_pts + 1;
+  if (threadIdx.x < 64) {
+    const int e = threadIdx.x;
+    const int cnt = (e < E && g_L.eg_need[e]) ? np1 : 0;
+    int inc = cnt;
+    for (int off = 1; off < 32; off <<= 1) {
+      int v = __shfl_up(inc, off);
+      if (e >= off) inc += v;
+    }
+    const int start = inc - cnt;
+    for (int i = 0; i < cnt; ++i) { J.slot_e[start + i] = e; J.slot_i[start + i] = i; }
+    const int total = __shfl(inc, 31);
+    if (e == 0) {
+      J.nslots = total;
+      J.ntiles = (total + HELPER_CT - 1) / HELPER_CT;
+      J.E = E; J.np1 = np1; J.self = g_L.S.self; J.map = g_L.S.map;
+      J.seq = ++g_L.job_seq;
+    }
+  }
+  if (threadIdx.x < E) g_L.eg_first[threadIdx.x] = np1;
+  __syncthreads();
+  if (threadIdx.x == 0) { TRACE(C, 0, 1); TRACE(C, 1, J.seq); TRACE(C, 2, J.nslots); TRACE(C, 3, J.ntiles); TRACE(C, 4, E); }
+  if (threadIdx.x == 0) J.hidx = -1;
+  if (uni(J.nslots) == 0) return;
+  for (int it = threadIdx.x; it < E * NJ; it += BLOCK) {
+    const int e = it / NJ, j = it - e * NJ;
+    J.start[e][j] = g_L.eg_start[e][j];
+    J.step[e][j] = g_L.eg_step[e][j];
+    st_agent(&jb->start[e][j], (unsigned long long)__double_as_longlong(g_L.eg_start[e][j]));
+    st_agent(&jb->step[e][j], (unsigned long long)__double_as_longlong(g_L.eg_step[e][j]));
+  }
+  for (int it = threadIdx.x; it < J.nslots; it += BLOCK) {
+    st_agent(&jb->slot_e[it], J.slot_e[it]);
+    st_agent(&jb->slot_i[it], J.slot_i[it]);
+  }
+  if (threadIdx.x < E) st_agent(&jb->first[threadIdx.x], np1);
+  if (threadIdx.x == 0) {
+    st_agent(&jb->E, E); st_agent(&jb->np1, np1); st_agent(&jb->nslots, J.nslots); st_agent(&jb->ntiles, J.ntiles);
+    st_agent(&jb->self, J.self); st_agent(&jb->map, J.map);
+    st_agent(&jb->done, 0);
+    st_agent(&jb->claim, claim_word(J.seq, J.nslots));
+  }
+  drain();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    drain();
+    st_agent(&jb->seq, J.seq);
+  }
+  PROF_BEGIN();
+  if (threadIdx.x == 0) atomicAdd(&jb->pad0[0], 1);  // diagnostics: jobs published
+  if (threadIdx.x == 0) TRACE(C, 0, 2);
+  job_work(C, jb, J);
+  if (threadIdx.x == 0) TRACE(C, 0, 3);
+  if (threadIdx.x == 0) atomicAdd(&jb->pad0[4], 1);  // diagnostics: leader finished its claims
+  // wait for the tiles other workgroups claimed (block-level loop; thread 0 polls)
+  const unsigned long long t_wait = wall_clock64();
+  for (;;) {
+    if (threadIdx.x == 0) {
+      const int d = ld_agent(&jb->done);
+      int st = d >= J.ntiles ? 1 : 0;
+      if (!st && wall_clock64() - t_wait > 200000000ull) {  // 2 s: a job never takes that long -- fail, never hang
+        g_L.S.status = -5;
+        g_L.S.phase = 2;
+        g_L.S.prof[28] = (unsigned long long)d;
+        g_L.S.prof[29] = (unsigned long long)J.ntiles;
+        g_L.S.prof[30] = ld_agent(&jb->claim);
+        g_L.S.prof[31] = (unsigned long long)J.seq;
+        st = 1;
+      }
+      J.go = st;
+    }
+    __syncthreads();
+    if (uni(J.go)) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  if (threadIdx.x == 0) TRACE(C, 0, 4);
+  if (threadIdx.x < E) g_L.eg_first[threadIdx.x] = ld_agent(&jb->first[threadIdx.x]);
+  PROF_END(P_TILES);
+  if (threadIdx.x == 0) {
+    g_L.S.prof[pslot] += wall_clock64() - _pt;
+    g_L.S.prof[P_NTILES] += J.ntiles;
+    g_L.S.prof[pslot + 8] += J.nslots;
+  }
+  __syncthreads();
+}
+
+// Helper workgroup: waits for jobs of its query and works on them until the leader signals stop (or after
+// two idle seconds, should the leader never start).  Never holds a claimed tile while waiting.
+__device__ __forceinline__ void helper_main(const Ctx& C, int hidx, JobLds& J) {
+  JobBoard* jb = C.Q.jb;
+  int last = 0;
+  J.hidx = hidx;
+  if (threadIdx.x == 0) TRACE(C, 8 + 3 * (hidx & 63), 1);
+  unsigned long long t_last = wall_clock64();
+  for (;;) {
+    // block-level poll (thread 0 reads the board): 0 = nothing yet, > 0 = new job, -1 = leave
+    if (threadIdx.x == 0) {
+      int go = 0;
+      const int s = ld_agent(&jb->seq);
+      if (s != last) go = s;
+      else if (ld_agent(&jb->stop) || wall_clock64() - t_last > 200000000ull) go = -1;  // 2 s idle
+      J.go = go;
+    }
+    __syncthreads();
+    const int go = uni(J.go);
+    if (go < 0) break;
+    if (go == 0) {
+      __builtin_amdgcn_s_sleep(2);
+      continue;
+    }
+    if (threadIdx.x == 0) TRACE(C, 9 + 3 * (hidx & 63), go);
+    last = go;
+    const int E = min(ld_agent(&jb->E), MAXE), nslots = min(ld_agent(&jb->nslots), JOB_SLOTS);
+    for (int it = threadIdx.x; it < E * NJ; it += BLOCK) {
+      const int e = it / NJ, j = it - e * NJ;
+      J.start[e][j] = __longlong_as_double((long long)ld_agent(&jb->start[e][j]));
+      J.step[e][j] = __longlong_as_double((long long)ld_agent(&jb->step[e][j]));
+    }
+    for (int it = threadIdx.x; it < nslots; it += BLOCK) {
+      J.slot_e[it] = min(max(ld_agent(&jb->slot_e[it]), 0), MAXE - 1);
+      J.slot_i[it] = ld_agent(&jb->slot_i[it]);
+    }
+    if (threadIdx.x == 0) {
+      J.nslots = nslots;
+      J.np1 = ld_agent(&jb->np1);
+      J.self = ld_agent(&jb->self);
+      J.map = ld_agent(&jb->map);
+      J.seq = go;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(&jb->pad0[1], 1);  // diagnostics: jobs joined by helpers
+    job_work(C, jb, J);
+    t_last = wall_clock64();
+  }
+  if (threadIdx.x == 0) TRACE(C, 8 + 3 * (hidx & 63), 2);
+}
+
 __device__ void edge_validity(const Ctx& C, int E, bool stop_first_valid, int pslot) {
   const int np1 = g_L.S.n_pts + 1;
   if (threadIdx.x == 0) g_L.count_slot = pslot + 4;
+  if (C.Q.jb) {
+    edge_validity_job(C, E, pslot);
+    return;
+  }
   if (threadIdx.x < E) { g_L.eg_first[threadIdx.x] = np1; g_L.eg_ptr[threadIdx.x] = 0; }
   __syncthreads();
   for (;;) {
@@ -436,14 +663,14 @@ __device__ void edge_validity(const Ctx& C, int E, bool stop_first_valid, int ps
         if (e >= off) inc += v;
       }
       const int start = inc - rem;
-      const int take = stop ? 0 : max(0, min(rem, 32 - start));
+      const int take = stop ? 0 : max(0, min(rem, PLAN_CT - start));
       for (int i = 0; i < take; ++i) { g_L.tile_e[start + i] = e; g_L.tile_i[start + i] = ptr + i; }
       if (e < E) g_L.eg_ptr[e] = ptr + take;
       const int total = __shfl(inc, 31);
-      if (e == 0) g_L.tile_n = stop ? 0 : min(32, total);
+      if (e == 0) g_L.tile_n = stop ? 0 : min(PLAN_CT, total);
     }
     __syncthreads();
-    const int nc = g_L.tile_n;
+    const int nc = uni(g_L.tile_n);
     if (nc == 0) break;
     if (threadIdx.x < nc * NJ) {
       int c = threadIdx.x / NJ, j = threadIdx.x - c * NJ;
@@ -452,8 +679,8 @@ __device__ void edge_validity(const Ctx& C, int E, bool stop_first_valid, int ps
     }
     __syncthreads();
     PROF_BEGIN();
-    const TileOrder order{g_L.tile_e, g_L.tile_i, g_L.eg_first};
-    collide_tile<32>((&g_rb), C.sc, (&g_mc), nc, g_L.u.tile.tq, g_L.S.self, g_L.S.map, g_L.u.tile.T, &order,
+    const TileOrder order{g_L.tile_e, g_L.tile_i, g_L.eg_first, false};
+    collide_tile<PLAN_CT>((&g_rb), C.sc, (&g_mc), nc, g_L.u.tile.tq, g_L.S.self, g_L.S.map, g_L.u.tile.T, &order,
                      &g_L.S.prof[P_TFK]);
     PROF_END(P_TILES);
     if (threadIdx.x == 0) {
@@ -539,7 +766,7 @@ __device__ void via_chain(const Ctx& C, const double* target) {
       }
     }
     __syncthreads();
-    if (g_L.reached) break;
+    if (uni(g_L.reached)) break;
   }
   PROF_END(P_VIA);
 }
@@ -709,7 +936,7 @@ __device__ void choose_parent(const Ctx& C, int t) {
     }
   }
   __syncthreads();
-  const int E = g_L.cnt;
+  const int E = uni(g_L.cnt);
   if (E > 0) {
     if (threadIdx.x < E) {
       int e = threadIdx.x;
@@ -739,7 +966,7 @@ __device__ void choose_parent(const Ctx& C, int t) {
       }
     }
     __syncthreads();
-    if (g_L.found >= 0) {
+    if (uni(g_L.found) >= 0) {
       via_chain(C, g_L.xn.q);
       if (threadIdx.x == 0) {
         // x_new <- last stepped edge (birrt_star.cpp:4692-4711)
@@ -773,7 +1000,7 @@ __device__ void rewire(const Ctx& C, int t) {
     g_L.cnt = cnt;
   }
   __syncthreads();
-  const int cnt = g_L.cnt;
+  const int cnt = uni(g_L.cnt);
   if (cnt == 0) return;
   // candidates k = n-1 .. n-cnt  ->  edge slot e = n-1-k
   if (threadIdx.x < cnt) {
@@ -857,7 +1084,7 @@ __device__ void connect_graphs(const Ctx& C, int t) {
     g_L.eg_need[0] = g_L.sol[0] < g_L.csp[0];
   }
   __syncthreads();
-  if (g_L.eg_need[0]) {
+  if (uni(g_L.eg_need[0])) {
     edge_validity(C, 1, false, P_XCONNECT);
     if (threadIdx.x == 0) {
       int f = g_L.eg_first[0];
@@ -877,23 +1104,24 @@ __device__ void connect_graphs(const Ctx& C, int t) {
       g_L.cur = g_L.xc;
     }
     __syncthreads();
-    if (g_L.flag == 1) {
+    const int flag = uni(g_L.flag);
+    if (flag == 1) {
       via_chain(C, g_L.xn.q);
       if (threadIdx.x == 0) g_L.tree_expand = 0;
-    } else if (g_L.flag == 2) {
+    } else if (flag == 2) {
       via_chain(C, g_L.ext);
       if (threadIdx.x == 0) { g_L.tree_expand = 1; g_L.best_nv = g_L.sol[0]; }
     }
     __syncthreads();
   }
-  if (g_L.S.have_sol) {
+  if (uni(g_L.S.have_sol)) {
     near_set<20>(C, t, g_L.xn.q, g_L.xn.id);
     if (threadIdx.x == 0) {
       int m = min(g_L.n_lo, g_L.S.max_near);
       g_L.cnt = m;
     }
     __syncthreads();
-    const int E = g_L.cnt;
+    const int E = uni(g_L.cnt);
     if (E > 0) {
       if (threadIdx.x < E) {
         int e = threadIdx.x;
@@ -942,12 +1170,13 @@ __device__ void connect_graphs(const Ctx& C, int t) {
           }
         }
         __syncthreads();
-        if (g_L.flag == 1) {
+        const int flag_e = uni(g_L.flag);
+        if (flag_e == 1) {
           via_chain(C, g_L.xn.q);
           if (threadIdx.x == 0) g_L.tree_expand = 0;
           __syncthreads();
           break;
-        } else if (g_L.flag == 2) {
+        } else if (flag_e == 2) {
           via_chain(C, g_L.ext);
           if (threadIdx.x == 0) { g_L.tree_expand = 1; g_L.best_nv = g_L.sol[0]; }
           __syncthreads();
@@ -979,10 +1208,10 @@ __device__ void connect_graphs(const Ctx& C, int t) {
 
 // One C-space iteration of run_planner (birrt_star.cpp:1163-1338).
 __device__ void iteration(const Ctx& C) {
-  const int A = g_L.S.A, B = 1 - A;
+  const int A = uni(g_L.S.A), B = 1 - A;
   unsigned long long _t0 = threadIdx.x == 0 ? wall_clock64() : 0, _t1;
 #define PHASE(k) if (threadIdx.x == 0) { _t1 = wall_clock64(); g_L.S.prof[k] += _t1 - _t0; _t0 = _t1; }
-  if (g_L.S.informed && g_L.S.have_sol) sample_ellipse(C); else sample_uniform(C);
+  if (uni(g_L.S.informed && g_L.S.have_sol)) sample_ellipse(C); else sample_uniform(C);
   PHASE(P_SAMPLE);
   int nid = nearest(C, A, g_L.xr);
   PHASE(P_NN);
@@ -1018,14 +1247,14 @@ __device__ void iteration(const Ctx& C) {
   }
   __syncthreads();
   PHASE(P_EXPAND);
-  const bool opt = g_L.S.tree_opt && g_L.S.have_sol;
+  const bool opt = uni(g_L.S.tree_opt && g_L.S.have_sol);
   if (opt) {
     near_set<20>(C, A, g_L.xn.q, g_L.xn.id);
     PHASE(P_NEAR);
     choose_parent(C, A);
     PHASE(P_CHOOSE);
   }
-  if (g_L.ext_nn || g_L.ext_bp) {
+  if (uni(g_L.ext_nn || g_L.ext_bp)) {
     if (threadIdx.x == 0) insert_node(C, A, g_L.en_start, g_L.en_target, g_L.xn);
     __syncthreads();
     if (opt) rewire(C, A);
@@ -1058,6 +1287,8 @@ __device__ void iteration(const Ctx& C) {
 }
 
 // Advances every query (one workgroup each) by at most `iters` planner iterations.
+// One block per query: the planner loop.  Its collision jobs are shared with helper_kernel's blocks when the
+// query has a job board (DESIGN.md "Helpers").
 __global__ void __launch_bounds__(BLOCK) plan_kernel(const RobotDev* __restrict__ rb, SceneDev sc,
                                                      const MapCfg* __restrict__ mc, QueryDev* qs, int iters) {
   stage_model(rb, mc, &g_rb, &g_mc);
@@ -1065,12 +1296,18 @@ __global__ void __launch_bounds__(BLOCK) plan_kernel(const RobotDev* __restrict_
   C.sc = sc;
   C.Q = qs[blockIdx.x];
   if (threadIdx.x == 0) {
+    TRACE(C, 96, (int)(reinterpret_cast<unsigned long long>(C.sc.d2) & 0xffffffffu));
+    TRACE(C, 97, (int)(reinterpret_cast<unsigned long long>(C.sc.d2) >> 32));
+    TRACE(C, 98, C.sc.nx);
+    TRACE(C, 99, (int)(reinterpret_cast<unsigned long long>(C.sc.bricks) & 0xffffffffu));
+    g_L.count_slot = 0;
+    g_L.job_seq = 0;
     g_L.S = *C.Q.st;
     if (g_L.S.phase == 0 && g_L.S.t0 == 0) g_L.S.t0 = wall_clock64();
     g_L.n_via = 0;
   }
   __syncthreads();
-  if (g_L.S.status == 0 && g_L.S.phase == 0) {
+  if (uni(g_L.S.status == 0 && g_L.S.phase == 0)) {
     // pre-loop direct connection of the two roots (birrt_star.cpp:1072-1075)
     if (threadIdx.x == 0) {
       load_node(C, 1, 0, &g_L.xn);
@@ -1083,17 +1320,31 @@ __global__ void __launch_bounds__(BLOCK) plan_kernel(const RobotDev* __restrict_
     __syncthreads();
   }
   for (int k = 0; k < iters; ++k) {
-    if (g_L.S.status != 0 || g_L.S.phase != 1) break;
+    if (uni(g_L.S.status != 0 || g_L.S.phase != 1)) break;
     iteration(C);
   }
   if (threadIdx.x == 0) {
     if (g_L.S.phase == 2 && g_L.S.t_end == 0) g_L.S.t_end = wall_clock64();
     *C.Q.st = g_L.S;
+    if (C.Q.jb) st_agent(&C.Q.jb->stop, 1);
   }
 }
 
 // computeFinalSolutionPathTrajectories (birrt_star.cpp:6173-6274): the node chains of both trees, root
 // first for the start tree and connection first for the goal tree.  out[0] = n_start, out[1] = n_goal.
+// Helper blocks (gridDim = nq * helpers): block b serves query b % nq -- waits for its leader's collision jobs
+// and takes tiles of them until the leader signals stop.  A separate kernel on its own stream, so its
+// resources stay small and a leader never depends on it being resident.
+__global__ void __launch_bounds__(BLOCK) helper_kernel(const RobotDev* __restrict__ rb, SceneDev sc,
+                                                       const MapCfg* __restrict__ mc, QueryDev* qs, int nq) {
+  __shared__ JobLds J;
+  stage_model(rb, mc, &g_rb, &g_mc);
+  Ctx C;
+  C.sc = sc;
+  C.Q = qs[blockIdx.x % nq];
+  if (C.Q.jb) helper_main(C, (int)blockIdx.x / nq, J);
+}
+
 __global__ void path_kernel(QueryDev* qs, int* counts) {
   QueryDev Q = qs[blockIdx.x];
   if (threadIdx.x != 0) return;

@@ -61,8 +61,32 @@ struct ViaNode {               // via node pending insertion (selected_via_nodes
   int id, parent;
 };
 
+// Collision-check job of one query, shared by its leader workgroup and its helper workgroups through HBM
+// (DESIGN.md "Helpers").  Control words sit on their own 128-byte lines.  Hand-off (MI355X_MICROARCH.md,
+// valid forms): payload and flags are agent-scope (sc1) stores drained with s_waitcnt vmcnt(0) behind a
+// workgroup barrier before the flag store; readers poll with sc1 loads and read the payload with sc1 loads.
+constexpr int HELPER_CT = 32;                   // configurations per job tile
+constexpr int JOB_SLOTS = MAXE * (MAX_PTS + 1); // (edge, point) slots of one job
+struct JobBoard {
+  int seq;                     // job number; the leader increments it to publish a job
+  int stop;                    // 1 once the leader left the launch: helpers exit
+  int pad0[30];
+  unsigned long long claim;    // (seq << 32) | next tile; claimed by compare-and-swap
+  int pad1[30];
+  int done;                    // tiles of the current job finished
+  int pad2[31];
+  int first[MAXE];             // first colliding point per edge (atomicMin); np1 = free
+  int pad3[32 - MAXE % 32];
+  int E, np1, nslots, ntiles, self, map;
+  int pad4[26];
+  unsigned long long start[MAXE][NJ], step[MAXE][NJ];  // fp64 bit patterns
+  int slot_e[JOB_SLOTS], slot_i[JOB_SLOTS];
+};
+
 struct QueryDev {
   QState* st;
+  JobBoard* jb;                // null: no helpers
+  int* trace;                  // debug only (SMP_DEBUG): host-mapped progress markers of the leader
   TreeDev tr[2];
   ViaNode* via;                // [via_cap]
   int* stack;                  // [cap] DFS stack of recursiveNodeCostUpdate

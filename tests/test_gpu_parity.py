@@ -195,6 +195,14 @@ def test_planner_parity_sample_budget(orobot, robot, name, seed, samples):
     assert_same_run(gp2, r, o)
 
 
+@pytest.mark.parametrize("helpers", [-1, 1, 7])
+def test_planner_parity_helper_counts(orobot, robot, helpers):
+    """The query alone on its workgroup (-1) and with helper workgroups sharing its collision tiles."""
+    gp2 = GpuPlanner(robot, helpers=helpers)
+    sc, r, o = run_both(gp2, orobot, "c2", 8, 400)
+    assert_same_run(gp2, r, o)
+
+
 def test_planner_parity_yaml_profile(orobot, robot):
     gp2 = GpuPlanner(robot, near_threshold=1.5, step_factor=0.6)
     sc, r, o = run_both(gp2, orobot, "c2", 5, 200, near_threshold=1.5, step_factor=0.6)

@@ -11,7 +11,7 @@ from squirrel_motion_planner_amd import scenes  # noqa: E402
 from squirrel_motion_planner_amd.planner import GpuPlanner, Scene  # noqa: E402
 
 sc = scenes.box_room()
-gp = GpuPlanner(path_optimality_threshold=-math.inf)
+gp = GpuPlanner(path_optimality_threshold=-math.inf, helpers=int(os.environ.get("SMP_HELPERS", "0")))
 gp.set_scene(Scene.from_keys(sc.keys, sc.res))
 for iters in [int(v) for v in (sys.argv[1:] or ["2000", "10000", "50000"])]:
     t = time.perf_counter()
