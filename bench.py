@@ -35,6 +35,9 @@ def parse():
                     help="budget of each warmup query (default: --samples, so warmup launches match timed ones)")
     ap.add_argument("--queries-per-gpu", type=int, default=1)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--helpers", type=int, default=0,
+                    help="helper workgroups per query (0 automatic, -1 none: e.g. for counter passes, which "
+                         "serialise dispatches)")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
@@ -87,7 +90,7 @@ def main():
     s0 = Scene.from_keys(sc.keys, sc.res) if rank == 0 else None
     scene = D.broadcast_scene(s0, device="cuda") if world > 1 else s0
 
-    gp = GpuPlanner(device=local, path_optimality_threshold=-math.inf)
+    gp = GpuPlanner(device=local, path_optimality_threshold=-math.inf, helpers=a.helpers)
     gp.set_scene(scene)
 
     def queries(step, samples):
@@ -170,8 +173,9 @@ def main():
             "config": {"workload": "C2: single start->goal query, 10x10x2 m octomap @5 cm, 20 boxes, budget %d "
                                    "collision-checked samples, path_optimality_threshold=-inf" % a.samples,
                        "queries_per_gpu": a.queries_per_gpu, "samples_per_query": a.samples,
-                       "robot": "robotino 8-DoF, 64-sphere model", "parallelism": "one workgroup per query, "
-                       "queries sharded over ranks, scene broadcast once"},
+                       "robot": "robotino 8-DoF, 64-sphere model", "helpers_per_query": a.helpers,
+                       "parallelism": "one leader workgroup per query + helper workgroups sharing its collision "
+                       "tiles; queries sharded over ranks, scene broadcast once"},
             "valid_configs_per_s": valid / elapsed,
             "iterations_per_s": iters / elapsed,
             "time_to_first_feasible_path_s": (sum(first_t) / len(first_t)) if first_t else None,

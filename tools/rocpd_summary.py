@@ -3,8 +3,9 @@
 
   python tools/rocpd_summary.py stats  <kernel-trace .db>  <out.txt>
       per-kernel calls / total / average / share (the `--stats` kernel summary)
-  python tools/rocpd_summary.py pmc    <pmc .db> <kernel substring> <out.json>
-      per-dispatch FETCH_SIZE / WRITE_SIZE of one kernel -> HBM bytes per launch
+  python tools/rocpd_summary.py pmc    <kernel substring> <out.json> <pmc .db> [<pmc .db> ...]
+      FETCH_SIZE / WRITE_SIZE of one kernel, one counter per pass (the two do not fit one pass on gfx950,
+      MI355X_MICROARCH.md "rocprofv3 PMC slots") -> HBM bytes per launch
 
 FETCH_SIZE and WRITE_SIZE are kilobytes (the counter description says so; x1024).  MI355X_MICROARCH.md
 (HBM section): on gfx950 FETCH_SIZE reports 1/2 of the bytes of wide coalesced reads, so the corrected
@@ -26,26 +27,31 @@ def stats(db, out):
     print("\n".join(lines))
 
 
-def pmc(db, kernel, out):
-    c = sqlite3.connect(db)
+def pmc(kernel, out, dbs):
     q = ("select dispatch_id, kernel_name, counter_name, value, duration from counters_collection "
          "where kernel_name like ? order by dispatch_id")
-    per = {}
-    for did, name, cname, value, dur in c.execute(q, ("%" + kernel + "%",)):
-        d = per.setdefault(did, {"kernel": name, "duration_ns": dur})
-        d[cname] = d.get(cname, 0.0) + value
-    disp = list(per.values())
-    fetch_kb = sum(d.get("FETCH_SIZE", 0.0) for d in disp)
-    write_kb = sum(d.get("WRITE_SIZE", 0.0) for d in disp)
-    n = max(len(disp), 1)
+    totals, launches, per = {}, {}, []
+    for db in dbs:
+        c = sqlite3.connect(db)
+        seen = set()
+        for did, name, cname, value, dur in c.execute(q, ("%" + kernel + "%",)):
+            totals[cname] = totals.get(cname, 0.0) + value
+            seen.add(did)
+            per.append({"db": db, "dispatch": did, "counter": cname, "value": value, "duration_ns": dur})
+        for cname in {p["counter"] for p in per if p["db"] == db}:
+            launches[cname] = len(seen)
+    fetch_kb = totals.get("FETCH_SIZE", 0.0)
+    write_kb = totals.get("WRITE_SIZE", 0.0)
+    nf = max(launches.get("FETCH_SIZE", 1), 1)
+    nw = max(launches.get("WRITE_SIZE", 1), 1)
     res = {
-        "source": db, "kernel": kernel, "dispatches": len(disp),
+        "sources": dbs, "kernel": kernel, "launches": launches,
         "fetch_size_kb_total": fetch_kb, "write_size_kb_total": write_kb,
-        "fetch_bytes_corrected_total": 2.0 * fetch_kb * 1024.0,
-        "write_bytes_total": write_kb * 1024.0,
-        "hbm_bytes_per_launch": (2.0 * fetch_kb + write_kb) * 1024.0 / n,
+        "fetch_bytes_per_launch": 2.0 * fetch_kb * 1024.0 / nf,
+        "write_bytes_per_launch": write_kb * 1024.0 / nw,
+        "hbm_bytes_per_launch": 2.0 * fetch_kb * 1024.0 / nf + write_kb * 1024.0 / nw,
         "correction": "FETCH_SIZE (KB) x1024 x2 (gfx950 half-count, MI355X_MICROARCH.md HBM section); WRITE_SIZE x1024",
-        "per_dispatch": disp,
+        "per_dispatch": per,
     }
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps({k: v for k, v in res.items() if k != "per_dispatch"}, indent=1))
@@ -55,4 +61,4 @@ if __name__ == "__main__":
     if sys.argv[1] == "stats":
         stats(sys.argv[2], sys.argv[3])
     else:
-        pmc(sys.argv[2], sys.argv[3], sys.argv[4])
+        pmc(sys.argv[2], sys.argv[3], sys.argv[4:])
