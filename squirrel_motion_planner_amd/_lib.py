@@ -8,7 +8,7 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libsmp_gpu.so")
+LIB_PATH = os.environ.get("SMP_LIB") or os.path.join(HERE, "lib", "libsmp_gpu.so")  # SMP_LIB: experiment builds
 MODEL_JSON = os.path.join(HERE, "data", "robotino_model.json")
 
 SMP_OK = 0
@@ -100,6 +100,8 @@ PROBES = [
     ("smp_probe_u01", _i, [_i, ctypes.c_uint64, ctypes.c_uint32, _p, _i, _pd]),
     ("smp_probe_fk", _i, [_p, _pd, _i, _pd, _pd]),
     ("smp_probe_sqrt_div", _i, [_i, _pd, _pd, _i, _pd, _pd]),
+    ("smp_probe_near", _i, [_i, _pd, _pd, _i, _pd, _p, _i, ctypes.c_double, _i, _p, _p, _p, _p,
+                            ctypes.POINTER(ctypes.c_uint64), _pd]),
     ("smp_probe_check_latency", _i, [_p, _pd, _i64, _i, _i, _i, _i, _pd, ctypes.POINTER(ctypes.c_uint64), _pd]),
 ]
 

@@ -29,6 +29,9 @@ __global__ void sincos_kernel(const double* x, int n, double* s, double* c);
 __global__ void u01_kernel(unsigned long long seed, unsigned query, const uint32_t* ctr, int n, double* out);
 __global__ void fk_kernel(const RobotDev* rb, const double* q, int n, double* frames, double* eez);
 __global__ void sqrt_div_kernel(const double* a, const double* b, int n, double* sq, double* dv);
+__global__ void near_probe_kernel(const double* tq, const double* tcost, int cap, int n, const double* queries,
+                                  const int* excl, int m, double r, int reps, int* nn, int* nk, int* lo, int* hi,
+                                  unsigned long long* ticks);
 }  // namespace smp
 
 using namespace smp;
@@ -886,5 +889,47 @@ extern "C" int smp_probe_sqrt_div(int device, const double* a, const double* b, 
   HIPCHK(hipMemcpy(sq, ds, n * sizeof(double), hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(dv, dd, n * sizeof(double), hipMemcpyDeviceToHost));
   (void)hipFree(da); (void)hipFree(db); (void)hipFree(ds); (void)hipFree(dd);
+  return SMP_OK;
+}
+
+// Tree-scan probe (near_probe_kernel): nearest and near_set<20> of m queries against one tree of n nodes
+// (q_soa [NJ][n], cost [n]); lo / hi: m x 20 ids (-1 padded); ticks[2]: device-clock ticks of all nearest /
+// near_set calls (clock_hz ticks per second); ticks[2..13]: the workgroup's profiling slots 20..31 (SMP_NEAR_PROF
+// builds: near_set step clocks and path counts).
+extern "C" int smp_probe_near(int device, const double* q_soa, const double* cost, int n, const double* queries,
+                              const int* excl, int m, double r, int reps, int* nn, int* nk, int* lo, int* hi,
+                              unsigned long long* ticks, double* clock_hz) {
+  if (n <= 0 || m <= 0 || reps <= 0 || !q_soa || !cost || !queries || !excl) return SMP_ERR_ARG;
+  if (hipSetDevice(device) != hipSuccess) return SMP_ERR_NO_DEVICE;
+  double *dq, *dc, *dqq;
+  int *dx, *dnn, *dnk, *dlo, *dhi;
+  unsigned long long* dt;
+  HIPCHK(hipMalloc(&dq, (size_t)n * NJ * sizeof(double)));
+  HIPCHK(hipMalloc(&dc, (size_t)n * sizeof(double)));
+  HIPCHK(hipMalloc(&dqq, (size_t)m * NJ * sizeof(double)));
+  HIPCHK(hipMalloc(&dx, (size_t)m * sizeof(int)));
+  HIPCHK(hipMalloc(&dnn, (size_t)m * sizeof(int)));
+  HIPCHK(hipMalloc(&dnk, (size_t)m * sizeof(int)));
+  HIPCHK(hipMalloc(&dlo, (size_t)m * 20 * sizeof(int)));
+  HIPCHK(hipMalloc(&dhi, (size_t)m * 20 * sizeof(int)));
+  HIPCHK(hipMalloc(&dt, 14 * sizeof(unsigned long long)));
+  HIPCHK(hipMemcpy(dq, q_soa, (size_t)n * NJ * sizeof(double), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dc, cost, (size_t)n * sizeof(double), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dqq, queries, (size_t)m * NJ * sizeof(double), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dx, excl, (size_t)m * sizeof(int), hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(near_probe_kernel, dim3(1), dim3(BLOCK), 0, 0, dq, dc, n, n, dqq, dx, m, r, reps, dnn, dnk, dlo,
+                     dhi, dt);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(nn, dnn, (size_t)m * sizeof(int), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(nk, dnk, (size_t)m * sizeof(int), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(lo, dlo, (size_t)m * 20 * sizeof(int), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(hi, dhi, (size_t)m * 20 * sizeof(int), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(ticks, dt, 14 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  (void)hipFree(dq); (void)hipFree(dc); (void)hipFree(dqq); (void)hipFree(dx); (void)hipFree(dnn);
+  (void)hipFree(dnk); (void)hipFree(dlo); (void)hipFree(dhi); (void)hipFree(dt);
+  int dev_clock_khz = 0;
+  HIPCHK(hipDeviceGetAttribute(&dev_clock_khz, hipDeviceAttributeWallClockRate, device));
+  *clock_hz = dev_clock_khz * 1000.0;
   return SMP_OK;
 }

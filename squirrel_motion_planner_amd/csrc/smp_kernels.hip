@@ -114,6 +114,9 @@ struct JobLds {
   int slot_e[JOB_SLOTS], slot_i[JOB_SLOTS];
   int E, np1, nslots, ntiles, self, map, seq, tile, go, hidx;
 };
+constexpr int NEAR_BINS = 256;   // near_set register path: cost histogram bins
+constexpr int NEAR_BUF = 128;    // near_set register path: candidate buffer entries per end
+constexpr int NEAR_NBK = 16;     // near_set register path: 64-node batches per wave held in registers
 #ifndef SMP_PLAN_CT
 #define SMP_PLAN_CT 32
 #endif
@@ -130,8 +133,16 @@ struct PlanLds {
     struct {  // near_set: per-wave sorted low / high ends of the near list
       unsigned long long wlk[BLOCK / 64][MAX_NEAR], whk[BLOCK / 64][MAX_NEAR];
       int wli[BLOCK / 64][MAX_NEAR], whi[BLOCK / 64][MAX_NEAR];
-      int wn[BLOCK / 64], wtot[BLOCK / 64];
+      int wtot[BLOCK / 64];
     } nr;
+    struct {  // near_set, register path: cost histogram and the two candidate buffers
+      unsigned hist[NEAR_BINS];
+      unsigned long long ck[2][NEAR_BUF];
+      int ci[2][NEAR_BUF];
+      unsigned long long wmin[BLOCK / 64], wmax[BLOCK / 64];
+      int wtot[BLOCK / 64];
+      int cnt[2], blo, bhi, fast;
+    } nh;
   } u;
   // edge batch
   double eg_start[MAXE][NJ], eg_target[MAXE][NJ], eg_step[MAXE][NJ], eg_end[MAXE][NJ];
@@ -142,6 +153,7 @@ struct PlanLds {
   int job_seq;     // last job published by this leader (this launch)
   // near lists (ascending (cost,id) for the first max_near; last max_near in ascending order)
   int nk;
+  unsigned long long near_blo, near_bhi;  // near_set: block-wide bounds on the K-th smallest / largest key
   int lo_i[MAX_NEAR], hi_i[MAX_NEAR];
   double lo_c[MAX_NEAR], hi_c[MAX_NEAR];
   int n_lo, n_hi;
@@ -184,6 +196,16 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 // as a divergent region and desynchronise the waves' barrier counts.
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
+// A block-uniform pointer made scalar (SGPR pair) and typed as global memory, so that streaming loads issue as
+// global_load with a scalar base instead of re-reading the pointer through the (scratch-resident) Ctx and
+// going through flat addressing.
+typedef const double __attribute__((address_space(1)))* gcdptr;
+__device__ __forceinline__ gcdptr uni_gptr(const double* p) {
+  const unsigned long long v = reinterpret_cast<unsigned long long>(p);
+  const unsigned lo = __builtin_amdgcn_readfirstlane((int)(unsigned)v);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((int)(unsigned)(v >> 32));
+  return (gcdptr)(((unsigned long long)hi << 32) | lo);
+}
 
 // --------------------------------------------------------------------------------------- node access
 __device__ __forceinline__ void load_node(const Ctx& C, int t, int id, NodeRef* o) {
@@ -239,23 +261,41 @@ __device__ int block_argmin(double d, int i) {
 }
 
 // find_nearest_neighbour_interpolation: first strict minimum of the Euclidean joint distance (DH:128-156).
+// sqrt is monotone, so a node can only beat the running minimum if its squared distance is below the minimum's
+// squared distance; the (correctly rounded) sqrt is taken only then and compared exactly as the reference does.
 __device__ int nearest(const Ctx& C, int t, const double* q) {
-  const TreeDev& T = C.Q.tr[t];
-  const int n = g_L.S.n[t], cap = g_L.S.cap;
+  const gcdptr tq = uni_gptr(C.Q.tr[t].q);
+  const int n = uni(g_L.S.n[t]), cap = uni(g_L.S.cap);
   if (threadIdx.x == 0) g_L.S.nn_nodes += n;
   double qq[NJ];
   for (int j = 0; j < NJ; ++j) qq[j] = q[j];
-  double best = 10000.0;
+  double best = 10000.0, best_s = 1e300;
   int bid = 0x7fffffff;
-  for (int i = threadIdx.x; i < n; i += BLOCK) {
-    double s = 0.0;
+  for (int i0 = threadIdx.x; i0 < n; i0 += 2 * BLOCK) {
+    const int i1 = i0 + BLOCK;
+    const bool v1 = i1 < n;
+    double a[NJ], b[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-      double d = qq[j] - T.q[(size_t)j * cap + i];
-      s += d * d;
+      a[j] = (tq + (size_t)j * cap)[(unsigned)i0];
+      b[j] = v1 ? (tq + (size_t)j * cap)[(unsigned)i1] : 0.0;
     }
-    double dist = sqrt(s);
-    if (dist < best) { best = dist; bid = i; }
+    double sa = 0.0, sb = 0.0;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      double d = qq[j] - a[j];
+      sa += d * d;
+      double e = qq[j] - b[j];
+      sb += e * e;
+    }
+    if (sa < best_s) {
+      double dist = sqrt(sa);
+      if (dist < best) { best = dist; bid = i0; best_s = sa; }
+    }
+    if (v1 && sb < best_s) {
+      double dist = sqrt(sb);
+      if (dist < best) { best = dist; bid = i1; best_s = sb; }
+    }
   }
   return block_argmin(best, bid);
 }
@@ -266,122 +306,442 @@ __device__ int nearest(const Ctx& C, int t, const double* q) {
 __device__ __forceinline__ bool ki_less(unsigned long long ka, int ia, unsigned long long kb, int ib) {
   return ka < kb || (ka == kb && ia < ib);
 }
+// Wave-uniform lane read (v_readlane: scalar result, no LDS round trip).
+__device__ __forceinline__ unsigned long long readlane_u64(unsigned long long v, int l) {
+  const unsigned lo = __builtin_amdgcn_readlane((int)(unsigned)v, l);
+  const unsigned hi = __builtin_amdgcn_readlane((int)(unsigned)(v >> 32), l);
+  return ((unsigned long long)hi << 32) | lo;
+}
+// Lane i receives lane i-1's value (DPP wave_shr:1, a GFX9 whole-wave shift); lane 0 keeps its own.
+__device__ __forceinline__ int wave_shr1(int v) { return __builtin_amdgcn_update_dpp(v, v, 0x138, 0xF, 0xF, false); }
+__device__ __forceinline__ unsigned long long wave_shr1_u64(unsigned long long v) {
+  const unsigned lo = wave_shr1((int)(unsigned)v), hi = wave_shr1((int)(unsigned)(v >> 32));
+  return ((unsigned long long)hi << 32) | lo;
+}
 
-// find_near_vertices_interpolation (birrt_star.cpp:4272-4324): count k, the first K and the last K entries of
-// the (cost,id)-sorted near list.
-//   1. scan: each wave keeps the K smallest and the K largest (key, id) of its nodes as sorted lists spread
-//      over lanes (lane k holds entry k); a 64-node batch only inserts the candidates that beat the current
-//      K-th entry, each insertion one compare + ballot + popcount + shfl_up;
-//   2. wave 0 merges the NW sorted wave lists of the low end, wave 1 those of the high end, in LDS.
+// One 64-node batch into a wave's two lane-distributed sorted lists (lane k holds entry k).  Only candidates
+// beating the wave's K-th entry and the block-wide bound are inserted; an insertion is a readlane, a compare +
+// ballot + popcount and a DPP shift of the list (~30 dependent instructions, so the bound matters).  Once the
+// wave holds K entries its K-th key tightens the block bound (LDS atomic): any wave's K entries are K near nodes,
+// so a node whose key lies beyond another wave's K-th key cannot be among the block's K smallest (largest).
 template <int K>
-__device__ void near_set(const Ctx& C, int t, const double* q, int excl) {
+__device__ __forceinline__ void near_batch(bool near, unsigned long long key, int base, int lane,
+                                           unsigned long long& lk, int& li, unsigned long long& hk, int& hi) {
+  const int i = base + lane;
+  const unsigned long long blo = g_L.near_blo, bhi = g_L.near_bhi;
+  {
+    const unsigned long long tk = readlane_u64(lk, K - 1);
+    const int ti = __builtin_amdgcn_readlane(li, K - 1);
+    unsigned long long m = __ballot(near && key <= blo && ki_less(key, i, tk, ti));
+    if (m) {
+      do {
+        const int src = __builtin_ctzll(m);
+        m &= m - 1;
+        const unsigned long long kk = readlane_u64(key, src);
+        const int ii = src + base;
+        const unsigned long long uk = wave_shr1_u64(lk);
+        const int ui = wave_shr1(li);
+        const int pos = __popcll(__ballot(ki_less(lk, li, kk, ii)));
+        if (lane >= pos) {
+          if (lane == pos) { lk = kk; li = ii; } else { lk = uk; li = ui; }
+        }
+      } while (m);
+      const unsigned long long nk = readlane_u64(lk, K - 1);
+      if (lane == 0 && nk < blo && __builtin_amdgcn_readlane(li, K - 1) != 0x7fffffff) atomicMin(&g_L.near_blo, nk);
+    }
+  }
+  {
+    const unsigned long long tk = readlane_u64(hk, K - 1);
+    const int ti = __builtin_amdgcn_readlane(hi, K - 1);
+    unsigned long long m = __ballot(near && key >= bhi && ki_less(tk, ti, key, i));
+    if (m) {
+      do {
+        const int src = __builtin_ctzll(m);
+        m &= m - 1;
+        const unsigned long long kk = readlane_u64(key, src);
+        const int ii = src + base;
+        const unsigned long long uk = wave_shr1_u64(hk);
+        const int ui = wave_shr1(hi);
+        const int pos = __popcll(__ballot(ki_less(kk, ii, hk, hi)));
+        if (lane >= pos) {
+          if (lane == pos) { hk = kk; hi = ii; } else { hk = uk; hi = ui; }
+        }
+      } while (m);
+      const unsigned long long nk = readlane_u64(hk, K - 1);
+      if (lane == 0 && nk > bhi && __builtin_amdgcn_readlane(hi, K - 1) != -1) atomicMax(&g_L.near_bhi, nk);
+    }
+  }
+}
+
+// Radius test sqrt(s) < r of the reference, decided on s against r^2 (1 -+ 1e-12); the (correctly rounded)
+// sqrt is only taken inside that band, where the two could disagree.
+__device__ __forceinline__ bool near_radius(bool valid, double s, double r, double r2lo, double r2hi, bool& amb) {
+  amb = valid && s >= r2lo && s <= r2hi;
+  return valid && s < r2lo;
+}
+
+// near_set, streaming path (trees above NEAR_NBK * BLOCK nodes, or cost distributions the histogram cannot
+// split, e.g. many equal costs):
+//   1. scan: four 64-node batches in flight per wave (q and cost loaded together); each wave keeps the K
+//      smallest and K largest (key, id) of its nodes (near_batch);
+//   2. rank merge: every wave entry finds its rank among all NW*K entries by binary searches in the other
+//      waves' sorted lists (advanced in lock-step) and is written to its place if the rank is below K.
+template <int K>
+__device__ __noinline__ void near_set_stream(const Ctx& C, int t, const double* q, int excl) {
   static_assert(K <= 64, "lane-distributed lists");
-  constexpr int NW = BLOCK / 64;
-  const TreeDev& T = C.Q.tr[t];
-  const int n = g_L.S.n[t], cap = g_L.S.cap;
+  constexpr int NW = BLOCK / 64, NB = 4;
+  const gcdptr tq = uni_gptr(C.Q.tr[t].q), tc = uni_gptr(C.Q.tr[t].cost);
+  const int n = uni(g_L.S.n[t]), cap = uni(g_L.S.cap);
   const double r = g_L.S.near_r;
+  const double r2 = r * r, r2lo = r2 * (1.0 - 1e-12), r2hi = r2 * (1.0 + 1e-12);
   const int lane = lane_id(), wave = wave_id();
   if (threadIdx.x == 0) g_L.S.near_nodes += n;
   double qq[NJ];
   for (int j = 0; j < NJ; ++j) qq[j] = q[j];
   const unsigned long long KMAX = ~0ull;
-  // lane k < K: entry k of the wave's low list (ascending) and of its high list (descending)
   unsigned long long lk = KMAX, hk = 0;
   int li = 0x7fffffff, hi = -1;
   int wc = 0;
-  for (int base = wave * 64; base < n; base += BLOCK) {
-    const int i = base + lane;
-    bool near = false;
-    unsigned long long key = 0;
-    if (i < n) {
-      double s = 0.0;
+  for (int base = wave * 64; base < n; base += NB * BLOCK) {
+    double x[NB][NJ];
+    unsigned long long key[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const int i = base + b * BLOCK + lane;
+      const bool v = i < n;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) x[b][j] = v ? (tq + (size_t)j * cap)[(unsigned)i] : 0.0;
+      key[b] = v ? (unsigned long long)__double_as_longlong(tc[(unsigned)i]) : 0ull;
+    }
+    bool nr[NB], amb[NB];
+    bool any_amb = false;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const int i = base + b * BLOCK + lane;
+      double sb = 0.0;
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
-        double d = qq[j] - T.q[(size_t)j * cap + i];
-        s += d * d;
+        double d = qq[j] - x[b][j];
+        sb += d * d;
       }
-      near = sqrt(s) < r && i != excl;
-      if (near) key = (unsigned long long)__double_as_longlong(T.cost[i]);
+      nr[b] = near_radius(i < n && i != excl, sb, r, r2lo, r2hi, amb[b]);
+      x[b][0] = sb;
+      any_amb |= amb[b];
     }
-    const unsigned long long m_near = __ballot(near);
-    wc += __popcll(m_near);
-    // low list: candidates below the current K-th entry
-    {
-      const unsigned long long tk = __shfl(lk, K - 1);
-      const int ti = __shfl(li, K - 1);
-      unsigned long long m = __ballot(near && ki_less(key, i, tk, ti));
-      while (m) {
-        const int src = __builtin_ctzll(m);
-        m &= m - 1;
-        const unsigned long long kk = __shfl(key, src);
-        const int ii = src + base;
-        const int pos = __popcll(__ballot(lane < K && ki_less(lk, li, kk, ii)));
-        const unsigned long long uk = __shfl_up(lk, 1);
-        const int ui = __shfl_up(li, 1);
-        if (lane < K && lane >= pos) {
-          if (lane == pos) { lk = kk; li = ii; } else { lk = uk; li = ui; }
-        }
-      }
+    if (__ballot(any_amb)) {
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+        if (amb[b]) nr[b] = sqrt(x[b][0]) < r;
     }
-    // high list (descending): candidates above the current K-th entry
-    {
-      const unsigned long long tk = __shfl(hk, K - 1);
-      const int ti = __shfl(hi, K - 1);
-      unsigned long long m = __ballot(near && ki_less(tk, ti, key, i));
-      while (m) {
-        const int src = __builtin_ctzll(m);
-        m &= m - 1;
-        const unsigned long long kk = __shfl(key, src);
-        const int ii = src + base;
-        const int pos = __popcll(__ballot(lane < K && ki_less(kk, ii, hk, hi)));
-        const unsigned long long uk = __shfl_up(hk, 1);
-        const int ui = __shfl_up(hi, 1);
-        if (lane < K && lane >= pos) {
-          if (lane == pos) { hk = kk; hi = ii; } else { hk = uk; hi = ui; }
-        }
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const int bb = base + b * BLOCK;
+      if (bb < n) {
+        wc += __popcll(__ballot(nr[b]));
+        near_batch<K>(nr[b], key[b], bb, lane, lk, li, hk, hi);
       }
     }
   }
-  const int take_w = min(K, wc);
-  if (lane < take_w) {
+  if (lane < K) {
     g_L.u.nr.wlk[wave][lane] = lk; g_L.u.nr.wli[wave][lane] = li;
     g_L.u.nr.whk[wave][lane] = hk; g_L.u.nr.whi[wave][lane] = hi;
   }
-  if (lane == 0) { g_L.u.nr.wn[wave] = take_w; g_L.u.nr.wtot[wave] = wc; }
+  if (lane == 0) g_L.u.nr.wtot[wave] = wc;
   __syncthreads();
-  // merge: wave 0 the low ends, wave 1 the high ends; lane w < NW owns wave w's sorted list
-  if (wave < 2) {
-    const bool low = wave == 0;
-    int head = 0;
-    const int len = lane < NW ? g_L.u.nr.wn[lane] : 0;
-    int tot = 0;
-    for (int w = 0; w < NW; ++w) tot += g_L.u.nr.wtot[w];
-    const int take = min(K, tot);
-    for (int rnd = 0; rnd < take; ++rnd) {
-      unsigned long long kv;
-      int iv;
-      if (head < len) {
-        kv = low ? g_L.u.nr.wlk[lane][head] : g_L.u.nr.whk[lane][head];
-        iv = low ? g_L.u.nr.wli[lane][head] : g_L.u.nr.whi[lane][head];
-      } else {
-        kv = low ? KMAX : 0;
-        iv = low ? 0x7fffffff : -1;
+  int tot = 0;
+  for (int w = 0; w < NW; ++w) tot += g_L.u.nr.wtot[w];
+  const int take = min(K, tot);
+  // threads [0, NW*K): low entries; [256, 256 + NW*K): high entries
+  static_assert(NW * K <= 256, "rank merge thread map");
+  const int hsel = threadIdx.x >= 256;
+  const int e = threadIdx.x - hsel * 256;
+  if (e < NW * K) {
+    const int w = e / K, k = e - w * K;
+    const unsigned long long ck = hsel ? g_L.u.nr.whk[w][k] : g_L.u.nr.wlk[w][k];
+    const int ci = hsel ? g_L.u.nr.whi[w][k] : g_L.u.nr.wli[w][k];
+    if (ci != (hsel ? -1 : 0x7fffffff)) {
+      // per list o: number of entries ahead of (ck, ci) in that list's order (ascending low, descending high)
+      int lo[NW];
+#pragma unroll
+      for (int o = 0; o < NW; ++o) lo[o] = 0;
+      constexpr int P = K >= 32 ? 32 : K >= 16 ? 16 : K >= 8 ? 8 : K >= 4 ? 4 : K >= 2 ? 2 : 1;
+#pragma unroll
+      for (int step = P; step > 0; step >>= 1) {
+        // lock-step binary search over the NW lists: entries [0, lo[o]) of list o are ahead
+#pragma unroll
+        for (int o = 0; o < NW; ++o) {
+          const int m = lo[o] + step - 1;
+          if (m < K) {
+            const unsigned long long ok = hsel ? g_L.u.nr.whk[o][m] : g_L.u.nr.wlk[o][m];
+            const int oi = hsel ? g_L.u.nr.whi[o][m] : g_L.u.nr.wli[o][m];
+            const bool ahead = hsel ? ki_less(ck, ci, ok, oi) : ki_less(ok, oi, ck, ci);
+            if (ahead) lo[o] += step;
+          }
+        }
       }
-      unsigned long long bk = kv;
-      int bi = iv;
-      for (int off = 4; off > 0; off >>= 1) {
-        unsigned long long ok = __shfl_xor(bk, off);
-        int oi = __shfl_xor(bi, off);
-        if (low ? ki_less(ok, oi, bk, bi) : ki_less(bk, bi, ok, oi)) { bk = ok; bi = oi; }
-      }
-      if (iv == bi && head < len) head++;
-      if (lane == 0) {
-        if (low) { g_L.lo_c[rnd] = __longlong_as_double((long long)bk); g_L.lo_i[rnd] = bi; }
-        else { g_L.hi_c[take - 1 - rnd] = __longlong_as_double((long long)bk); g_L.hi_i[take - 1 - rnd] = bi; }
+      int rank = k;
+#pragma unroll
+      for (int o = 0; o < NW; ++o)
+        if (o != w) rank += lo[o];
+      if (rank < take) {
+        if (!hsel) { g_L.lo_c[rank] = __longlong_as_double((long long)ck); g_L.lo_i[rank] = ci; }
+        else { g_L.hi_c[take - 1 - rank] = __longlong_as_double((long long)ck); g_L.hi_i[take - 1 - rank] = ci; }
       }
     }
-    if (threadIdx.x == 0) { g_L.nk = tot; g_L.n_lo = take; g_L.n_hi = take; }
   }
+  if (threadIdx.x == 0) { g_L.nk = tot; g_L.n_lo = take; g_L.n_hi = take; g_L.near_blo = KMAX; g_L.near_bhi = 0; }
+  __syncthreads();
+}
+
+// find_near_vertices_interpolation (birrt_star.cpp:4272-4324): count k, the first K and the last K entries of
+// the (cost,id)-sorted near list.  The tree is taken in chunks of NEAR_NBK * BLOCK nodes; the radius test leaves
+// every thread with up to NEAR_NBK (key, near) pairs of the chunk in registers; then
+//   1. block min / max of the chunk's near keys, and a NEAR_BINS-bin LDS histogram of cost over [min, max] (the
+//      bin map (c - cmin) * scale is monotone in c, so bins order like costs);
+//   2. wave 0 scans the histogram: b_lo = first bin where the cumulative count reaches K, b_hi = last bin whose
+//      suffix count reaches K;
+//   3. the chunk's near nodes in bins <= b_lo (>= b_hi) and the running low (high) list of the previous chunks
+//      are gathered in an LDS buffer (one atomic per wave and list) and every entry is ranked by counting the
+//      entries ahead of it (2-4 lanes per entry): the entries of rank < K are the new running list.
+// A buffer that would exceed NEAR_BUF entries (ties, clustered costs) sends the call to near_set_stream.
+#ifdef SMP_NEAR_PROF  // clocks of the barrier-separated steps into prof[20..24]; path counts in prof[26], prof[27]
+#define NEAR_CLOCK(k)                                                                    \
+  if (threadIdx.x == 0) {                                                                \
+    const unsigned long long _t = wall_clock64();                                        \
+    if (k > 0) g_L.S.prof[19 + k] += _t - _tn;                                           \
+    _tn = _t;                                                                            \
+  }
+#define NEAR_COUNT(k) if (threadIdx.x == 0) g_L.S.prof[k]++
+#else
+#define NEAR_CLOCK(k)
+#define NEAR_COUNT(k)
+#endif
+__device__ __forceinline__ int near_bin(unsigned long long key, double cmin, double scale) {
+  return (int)((__longlong_as_double((long long)key) - cmin) * scale);
+}
+
+template <int K>
+__device__ void near_set(const Ctx& C, int t, const double* q, int excl) {
+#ifdef SMP_NEAR_PROF
+  unsigned long long _tn = 0;
+#endif
+  static_assert(K <= 64 && NEAR_BUF == 128 && NEAR_BINS == 4 * 64, "register path layout");
+  constexpr int NW = BLOCK / 64, CH = NEAR_NBK * BLOCK;
+  const int n = uni(g_L.S.n[t]);
+  const gcdptr tq = uni_gptr(C.Q.tr[t].q), tc = uni_gptr(C.Q.tr[t].cost);
+  const int cap = uni(g_L.S.cap);
+  const double r = g_L.S.near_r;
+  const double r2 = r * r, r2lo = r2 * (1.0 - 1e-12), r2hi = r2 * (1.0 + 1e-12);
+  const int lane = lane_id(), wave = wave_id();
+  double qq[NJ];
+  for (int j = 0; j < NJ; ++j) qq[j] = q[j];
+  int tot_all = 0;  // near nodes of the chunks before this one (block-uniform)
+  if (threadIdx.x == 0) { g_L.n_lo = 0; g_L.n_hi = 0; }
+  for (int c0 = 0; c0 < n; c0 += CH) {
+    NEAR_CLOCK(0);
+    unsigned long long key[NEAR_NBK];
+    unsigned nmask = 0;
+    unsigned long long kmin = ~0ull, kmax = 0;
+    int wc = 0;
+#pragma unroll
+    for (int g = 0; g < NEAR_NBK; g += 4) {
+      key[g] = key[g + 1] = key[g + 2] = key[g + 3] = 0;
+      if (c0 + g * BLOCK + wave * 64 < n) {
+        double x[4][NJ];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const int i = c0 + (g + b) * BLOCK + wave * 64 + lane;
+          const bool v = i < n;
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) x[b][j] = v ? (tq + (size_t)j * cap)[(unsigned)i] : 0.0;
+          key[g + b] = v ? (unsigned long long)__double_as_longlong(tc[(unsigned)i]) : 0ull;
+        }
+        bool nr[4], amb[4];
+        bool any_amb = false;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const int i = c0 + (g + b) * BLOCK + wave * 64 + lane;
+          double sb = 0.0;
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) {
+            double d = qq[j] - x[b][j];
+            sb += d * d;
+          }
+          nr[b] = near_radius(i < n && i != excl, sb, r, r2lo, r2hi, amb[b]);
+          x[b][0] = sb;
+          any_amb |= amb[b];
+        }
+        if (__ballot(any_amb)) {
+#pragma unroll
+          for (int b = 0; b < 4; ++b)
+            if (amb[b]) nr[b] = sqrt(x[b][0]) < r;
+        }
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          if (nr[b]) {
+            nmask |= 1u << (g + b);
+            kmin = min(kmin, key[g + b]);
+            kmax = max(kmax, key[g + b]);
+          }
+          wc += __popcll(__ballot(nr[b]));
+        }
+      }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      kmin = min(kmin, (unsigned long long)__shfl_xor(kmin, off));
+      kmax = max(kmax, (unsigned long long)__shfl_xor(kmax, off));
+    }
+    if (lane == 0) { g_L.u.nh.wmin[wave] = kmin; g_L.u.nh.wmax[wave] = kmax; g_L.u.nh.wtot[wave] = wc; }
+    if (threadIdx.x < NEAR_BINS) g_L.u.nh.hist[threadIdx.x] = 0;
+    __syncthreads();
+    NEAR_CLOCK(1);
+    int tot = 0;
+    kmin = ~0ull; kmax = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      tot += g_L.u.nh.wtot[w];
+      kmin = min(kmin, g_L.u.nh.wmin[w]);
+      kmax = max(kmax, g_L.u.nh.wmax[w]);
+    }
+    tot = uni(tot);
+    if (tot == 0) continue;  // nothing near in this chunk: lists unchanged
+    const int take_c = min(K, tot);
+    const int prev_lo = g_L.n_lo, prev_hi = g_L.n_hi;
+    const double cmin = __longlong_as_double((long long)kmin), cmax = __longlong_as_double((long long)kmax);
+    const double scale = cmax > cmin ? (NEAR_BINS * (1.0 - 1e-9)) / (cmax - cmin) : 0.0;
+    unsigned bins[NEAR_NBK / 4] = {};  // 8-bit bin of every near key
+#pragma unroll
+    for (int b = 0; b < NEAR_NBK; ++b)
+      if (nmask >> b & 1) {
+        const int bin = near_bin(key[b], cmin, scale);
+        bins[b >> 2] |= (unsigned)bin << (8 * (b & 3));
+        atomicAdd(&g_L.u.nh.hist[bin], 1u);
+      }
+    __syncthreads();
+    NEAR_CLOCK(2);
+    if (wave == 0) {
+      // lane l owns bins 4l .. 4l+3: inclusive cumulative counts
+      const unsigned h0 = g_L.u.nh.hist[4 * lane], h1 = g_L.u.nh.hist[4 * lane + 1];
+      const unsigned h2 = g_L.u.nh.hist[4 * lane + 2], h3 = g_L.u.nh.hist[4 * lane + 3];
+      int inc = h0 + h1 + h2 + h3;
+      for (int off = 1; off < 64; off <<= 1) {
+        const int o = __shfl_up(inc, off);
+        if (lane >= off) inc += o;
+      }
+      const int c3 = inc, c2 = c3 - (int)h3, c1 = c2 - (int)h2, c0b = c1 - (int)h1;  // inclusive
+      const int e0 = c0b - (int)h0;                                                   // exclusive of bin 4l
+      // b_lo: first bin with inclusive count >= take_c
+      const int flo = c0b >= take_c ? 0 : c1 >= take_c ? 1 : c2 >= take_c ? 2 : c3 >= take_c ? 3 : 4;
+      const int Llo = __builtin_ctzll(__ballot(flo < 4));
+      const int blo = 4 * Llo + __shfl(flo, Llo);
+      const int cnt_lo = __shfl(flo == 0 ? c0b : flo == 1 ? c1 : flo == 2 ? c2 : c3, Llo);
+      // b_hi: last bin whose exclusive count is <= tot - take_c (suffix count >= take_c)
+      const int lim = tot - take_c;
+      const int fhi = c2 <= lim ? 3 : c1 <= lim ? 2 : c0b <= lim ? 1 : e0 <= lim ? 0 : -1;
+      const int Lhi = 63 - __builtin_clzll(__ballot(fhi >= 0));
+      const int fh = __shfl(fhi, Lhi);
+      const int bhi = 4 * Lhi + fh;
+      const int cnt_hi = tot - __shfl(fhi == 3 ? c2 : fhi == 2 ? c1 : fhi == 1 ? c0b : e0, Lhi);
+      if (lane == 0) {
+        g_L.u.nh.blo = blo;
+        g_L.u.nh.bhi = bhi;
+        g_L.u.nh.fast = cnt_lo + prev_lo <= NEAR_BUF && cnt_hi + prev_hi <= NEAR_BUF;
+        g_L.u.nh.cnt[0] = prev_lo;  // the running lists take the first buffer slots
+        g_L.u.nh.cnt[1] = prev_hi;
+      }
+    }
+    if (threadIdx.x < prev_lo) {
+      g_L.u.nh.ck[0][threadIdx.x] = (unsigned long long)__double_as_longlong(g_L.lo_c[threadIdx.x]);
+      g_L.u.nh.ci[0][threadIdx.x] = g_L.lo_i[threadIdx.x];
+    }
+    if (threadIdx.x >= 64 && threadIdx.x < 64 + prev_hi) {
+      g_L.u.nh.ck[1][threadIdx.x - 64] = (unsigned long long)__double_as_longlong(g_L.hi_c[threadIdx.x - 64]);
+      g_L.u.nh.ci[1][threadIdx.x - 64] = g_L.hi_i[threadIdx.x - 64];
+    }
+    __syncthreads();
+    NEAR_CLOCK(3);
+    if (!uni(g_L.u.nh.fast)) {
+      NEAR_COUNT(26);
+      __syncthreads();
+      near_set_stream<K>(C, t, q, excl);
+      return;
+    }
+    const int blo = g_L.u.nh.blo, bhi = g_L.u.nh.bhi;
+    // gather: count the wave's entries per list, one atomic per list, then write
+    int nw_lo = 0, nw_hi = 0;
+#pragma unroll
+    for (int g = 0; g < NEAR_NBK; ++g) {
+      if (c0 + g * BLOCK + wave * 64 < n) {
+        const bool nr = nmask >> g & 1;
+        const int bin = bins[g >> 2] >> (8 * (g & 3)) & 255;
+        nw_lo += __popcll(__ballot(nr && bin <= blo));
+        nw_hi += __popcll(__ballot(nr && bin >= bhi));
+      }
+    }
+    int base_lo = 0, base_hi = 0;
+    if (lane == 0 && nw_lo) base_lo = atomicAdd(&g_L.u.nh.cnt[0], nw_lo);
+    if (lane == 1 && nw_hi) base_hi = atomicAdd(&g_L.u.nh.cnt[1], nw_hi);
+    base_lo = __shfl(base_lo, 0);
+    base_hi = __shfl(base_hi, 1);
+    const unsigned long long below = (1ull << lane) - 1;
+#pragma unroll
+    for (int g = 0; g < NEAR_NBK; ++g) {
+      if (c0 + g * BLOCK + wave * 64 < n) {
+        const bool nr = nmask >> g & 1;
+        const int bin = bins[g >> 2] >> (8 * (g & 3)) & 255;
+        const int i = c0 + g * BLOCK + wave * 64 + lane;
+        const bool pl = nr && bin <= blo, ph = nr && bin >= bhi;
+        const unsigned long long ml = __ballot(pl), mh = __ballot(ph);
+        if (pl) {
+          const int slot = base_lo + __popcll(ml & below);
+          g_L.u.nh.ck[0][slot] = key[g];
+          g_L.u.nh.ci[0][slot] = i;
+        }
+        if (ph) {
+          const int slot = base_hi + __popcll(mh & below);
+          g_L.u.nh.ck[1][slot] = key[g];
+          g_L.u.nh.ci[1][slot] = i;
+        }
+        base_lo += __popcll(ml);
+        base_hi += __popcll(mh);
+      }
+    }
+    __syncthreads();
+    NEAR_CLOCK(4);
+    const int take = min(K, tot_all + tot);
+    {
+      // rank: threads [0, 256) the low buffer, [256, 512) the high buffer; L lanes per entry
+      const int e = threadIdx.x >= 256;
+      const int idx = threadIdx.x & 255;
+      const int m = g_L.u.nh.cnt[e];
+      const int L = m <= 64 ? 4 : 2;
+      const int c = L == 4 ? idx >> 2 : idx >> 1, sl = idx & (L - 1);
+      int rank = 0;
+      unsigned long long ck = 0;
+      int ci = 0;
+      if (c < m) {
+        ck = g_L.u.nh.ck[e][c];
+        ci = g_L.u.nh.ci[e][c];
+        for (int j = sl; j < m; j += L) {
+          const unsigned long long ok = g_L.u.nh.ck[e][j];
+          const int oi = g_L.u.nh.ci[e][j];
+          rank += e == 0 ? ki_less(ok, oi, ck, ci) : ki_less(ck, ci, ok, oi);
+        }
+      }
+      rank += __shfl_xor(rank, 1);
+      if (L == 4) rank += __shfl_xor(rank, 2);
+      if (c < m && sl == 0 && rank < take) {
+        if (e == 0) { g_L.lo_c[rank] = __longlong_as_double((long long)ck); g_L.lo_i[rank] = ci; }
+        else { g_L.hi_c[take - 1 - rank] = __longlong_as_double((long long)ck); g_L.hi_i[take - 1 - rank] = ci; }
+      }
+    }
+    tot_all += tot;
+    if (threadIdx.x == 0) { g_L.n_lo = take; g_L.n_hi = take; }
+    __syncthreads();
+    NEAR_CLOCK(5);
+    NEAR_COUNT(27);
+  }
+  if (threadIdx.x == 0) { g_L.nk = tot_all; g_L.S.near_nodes += n; }
   __syncthreads();
 }
 
@@ -469,14 +829,15 @@ __device__ __forceinline__ int job_claim_once(JobBoard* jb, int seq, int* nslots
 // Takes tiles of the job held in g_L.u.job until none is left: configuration = start + i * step of its
 // (edge, point) slot (the leader's arithmetic), collision tile, first collisions by agent-scope atomicMin
 // into the board, then one `done` per tile after the results are performed.  All threads.
-__device__ __forceinline__ void job_work(const Ctx& C, JobBoard* jb, JobLds& J) {
-  for (;;) {
+__device__ __forceinline__ void job_work(const Ctx& C, JobBoard* jb, JobLds& J, int max_tiles = 1 << 30) {
+  for (int taken = 0; taken < max_tiles;) {
     if (threadIdx.x == 0) J.tile = job_claim_once(jb, J.seq, &J.nslots);
     __syncthreads();
     const int t = uni(J.tile);
     if (threadIdx.x == 0 && J.hidx >= 0) TRACE(C, 10 + 3 * (J.hidx & 63), t);
     if (t == -1) break;
     if (t < 0) continue;
+    ++taken;
     const int base = t * HELPER_CT, nc = min(HELPER_CT, uni(J.nslots) - base);
     if (threadIdx.x < nc * NJ) {
       int c = threadIdx.x / NJ, j = threadIdx.x - c * NJ;
@@ -521,6 +882,7 @@ __device__ __forceinline__ void edge_validity_job(const Ctx& C, int E, int pslot
   if (threadIdx.x < E) g_L.eg_first[threadIdx.x] = np1;
   __syncthreads();
   if (threadIdx.x == 0) { TRACE(C, 0, 1); TRACE(C, 1, J.seq); TRACE(C, 2, J.nslots); TRACE(C, 3, J.ntiles); TRACE(C, 4, E); }
+  const unsigned long long tj0 = threadIdx.x == 0 ? wall_clock64() : 0;
   if (threadIdx.x == 0) J.hidx = -1;
   if (uni(J.nslots) == 0) return;
   for (int it = threadIdx.x; it < E * NJ; it += BLOCK) {
@@ -548,18 +910,26 @@ __device__ __forceinline__ void edge_validity_job(const Ctx& C, int E, int pslot
     st_agent(&jb->seq, J.seq);
   }
   PROF_BEGIN();
+  if (threadIdx.x == 0) { g_L.S.prof[P_TFK] += _pt - tj0; g_L.S.prof[P_TTEST]++; }  // job publication
   if (threadIdx.x == 0) atomicAdd(&jb->pad0[0], 1);  // diagnostics: jobs published
   if (threadIdx.x == 0) TRACE(C, 0, 2);
-  job_work(C, jb, J);
+  job_work(C, jb, J, 1);  // the leader takes one tile; helpers take the rest in parallel
   if (threadIdx.x == 0) TRACE(C, 0, 3);
   if (threadIdx.x == 0) atomicAdd(&jb->pad0[4], 1);  // diagnostics: leader finished its claims
-  // wait for the tiles other workgroups claimed (block-level loop; thread 0 polls)
+  const unsigned long long tj1 = threadIdx.x == 0 ? wall_clock64() : 0;
+  if (threadIdx.x == 0) g_L.S.prof[P_TCHAIN] += tj1 - _pt;  // the leader's own tiles
+  // wait for the other tiles (block-level loop; thread 0 polls).  Should the job stop progressing for 20 us
+  // (no helper resident, or all busy), the leader takes the next unclaimed tile itself.
   const unsigned long long t_wait = wall_clock64();
+  unsigned long long t_prog = t_wait;
+  int last_d = -1;
   for (;;) {
     if (threadIdx.x == 0) {
       const int d = ld_agent(&jb->done);
-      int st = d >= J.ntiles ? 1 : 0;
-      if (!st && wall_clock64() - t_wait > 200000000ull) {  // 2 s: a job never takes that long -- fail, never hang
+      const unsigned long long now = wall_clock64();
+      if (d != last_d) { last_d = d; t_prog = now; }
+      int st = d >= J.ntiles ? 1 : (now - t_prog > 2000ull ? 2 : 0);
+      if (st != 1 && now - t_wait > 200000000ull) {  // 2 s: a job never takes that long -- fail, never hang
         g_L.S.status = -5;
         g_L.S.phase = 2;
         g_L.S.prof[28] = (unsigned long long)d;
@@ -571,10 +941,17 @@ __device__ __forceinline__ void edge_validity_job(const Ctx& C, int E, int pslot
       J.go = st;
     }
     __syncthreads();
-    if (uni(J.go)) break;
+    const int go = uni(J.go);
+    if (go == 1) break;
+    if (go == 2) {
+      job_work(C, jb, J, 1);
+      if (threadIdx.x == 0) t_prog = wall_clock64();
+      continue;
+    }
     __builtin_amdgcn_s_sleep(1);
   }
   if (threadIdx.x == 0) TRACE(C, 0, 4);
+  if (threadIdx.x == 0) g_L.S.prof[P_TCENTRE] += wall_clock64() - tj1;  // waiting for helpers' tiles
   if (threadIdx.x < E) g_L.eg_first[threadIdx.x] = ld_agent(&jb->first[threadIdx.x]);
   PROF_END(P_TILES);
   if (threadIdx.x == 0) {
@@ -1305,6 +1682,8 @@ __global__ void __launch_bounds__(BLOCK) plan_kernel(const RobotDev* __restrict_
     g_L.S = *C.Q.st;
     if (g_L.S.phase == 0 && g_L.S.t0 == 0) g_L.S.t0 = wall_clock64();
     g_L.n_via = 0;
+    g_L.near_blo = ~0ull;
+    g_L.near_bhi = 0;
   }
   __syncthreads();
   if (uni(g_L.S.status == 0 && g_L.S.phase == 0)) {
@@ -1362,6 +1741,52 @@ __global__ void path_kernel(QueryDev* qs, int* counts) {
   }
   counts[blockIdx.x * 2] = ns;
   counts[blockIdx.x * 2 + 1] = ng;
+}
+
+
+// Probe of the tree scans alone (tests and tools/near_probe.py): one workgroup runs nearest() and
+// near_set<20>() for m query configurations against one tree (SoA q [NJ][cap], total cost [cap]), `reps` times
+// each; out: nearest id, near count, the first / last 20 near ids; ticks[0] / ticks[1] = device-clock ticks of
+// all nearest / near_set calls.
+__global__ void __launch_bounds__(BLOCK) near_probe_kernel(const double* tq, const double* tcost, int cap, int n,
+                                                           const double* queries, const int* excl, int m, double r,
+                                                           int reps, int* nn, int* nk, int* lo, int* hi,
+                                                           unsigned long long* ticks) {
+  Ctx C;
+  C.Q.tr[0].q = const_cast<double*>(tq);
+  C.Q.tr[0].cost = const_cast<double*>(tcost);
+  if (threadIdx.x == 0) {
+    g_L.S.n[0] = n;
+    g_L.S.cap = cap;
+    g_L.S.near_r = r;
+    g_L.near_blo = ~0ull;
+    g_L.near_bhi = 0;
+    for (int k = 0; k < 32; ++k) g_L.S.prof[k] = 0;
+  }
+  unsigned long long t_nn = 0, t_near = 0;
+  for (int k = 0; k < m; ++k) {
+    if (threadIdx.x < NJ) g_L.xr[threadIdx.x] = queries[(size_t)k * NJ + threadIdx.x];
+    __syncthreads();
+    int id = 0;
+    unsigned long long t0 = wall_clock64();
+    for (int rep = 0; rep < reps; ++rep) id = nearest(C, 0, g_L.xr);
+    unsigned long long t1 = wall_clock64();
+    for (int rep = 0; rep < reps; ++rep) near_set<20>(C, 0, g_L.xr, excl[k]);
+    unsigned long long t2 = wall_clock64();
+    t_nn += t1 - t0;
+    t_near += t2 - t1;
+    if (threadIdx.x == 0) { nn[k] = id; nk[k] = g_L.nk; }
+    if (threadIdx.x < 20) {
+      lo[k * 20 + threadIdx.x] = threadIdx.x < g_L.n_lo ? g_L.lo_i[threadIdx.x] : -1;
+      hi[k * 20 + threadIdx.x] = threadIdx.x < g_L.n_hi ? g_L.hi_i[threadIdx.x] : -1;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    ticks[0] = t_nn;
+    ticks[1] = t_near;
+    for (int k = 0; k < 12; ++k) ticks[2 + k] = g_L.S.prof[20 + k];
+  }
 }
 
 }  // namespace smp

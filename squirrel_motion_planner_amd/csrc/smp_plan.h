@@ -65,7 +65,10 @@ struct ViaNode {               // via node pending insertion (selected_via_nodes
 // (DESIGN.md "Helpers").  Control words sit on their own 128-byte lines.  Hand-off (MI355X_MICROARCH.md,
 // valid forms): payload and flags are agent-scope (sc1) stores drained with s_waitcnt vmcnt(0) behind a
 // workgroup barrier before the flag store; readers poll with sc1 loads and read the payload with sc1 loads.
-constexpr int HELPER_CT = 32;                   // configurations per job tile
+#ifndef SMP_HELPER_CT
+#define SMP_HELPER_CT 32
+#endif
+constexpr int HELPER_CT = SMP_HELPER_CT;          // configurations per job tile
 constexpr int JOB_SLOTS = MAXE * (MAX_PTS + 1); // (edge, point) slots of one job
 struct JobBoard {
   int seq;                     // job number; the leader increments it to publish a job

@@ -213,8 +213,8 @@ def _result_dict(r):
     d["cost_best"] = list(s.cost_best)
     d["cost_theoretical"] = list(s.cost_theoretical)
     names = ["sample", "nearest", "expand", "near", "choose_parent", "rewire", "connect", "collide_tiles",
-             "n_tiles", "edge_costs", "via_chains", "n_via_steps", "tile_local_frames", "tile_chain",
-             "tile_centres_w0", "tile_tests", "tiles_in_expand", "tiles_in_choose", "tiles_in_rewire",
+             "n_tiles", "edge_costs", "via_chains", "n_via_steps", "tile_local_frames|job_publish", "tile_chain|job_own_tiles",
+             "tile_centres_w0|job_wait", "tile_tests|n_jobs", "tiles_in_expand", "tiles_in_choose", "tiles_in_rewire",
              "tiles_in_connect", "checked_expand", "checked_choose", "checked_rewire", "checked_connect",
              "slots_expand", "slots_choose", "slots_rewire", "slots_connect"]
     d["phases"] = {n: s.phase_seconds[i] for i, n in enumerate(names)}

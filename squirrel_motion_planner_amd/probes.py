@@ -1,0 +1,37 @@
+"""Kernel-level probes of libsmp_gpu.so (tests and tools/): not part of the planner API.
+
+tree_scan: the planner's two tree scans run alone in one workgroup (near_probe_kernel, smp_kernels.hip):
+find_nearest_neighbour_interpolation and find_near_vertices_interpolation (birrt_star.cpp:4076-4133,
+4272-4324) of m query configurations against one tree.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib as L
+
+
+def tree_scan(q, cost, queries, excl, r, reps=1, device=0):
+    """q (n, 8) node configurations, cost (n,) total costs, queries (m, 8), excl (m,) node id left out of the near
+    set (-1: none).  Returns nearest ids, near counts, the first / last 20 near ids (ascending (cost, id); -1
+    padded) and the device seconds of all nearest / near_set calls."""
+    q = np.ascontiguousarray(np.asarray(q, np.float64).T)
+    cost = np.ascontiguousarray(cost, np.float64)
+    queries = np.ascontiguousarray(queries, np.float64)
+    excl = np.ascontiguousarray(excl, np.int32)
+    n, m = q.shape[1], queries.shape[0]
+    nn = np.zeros(m, np.int32)
+    nk = np.zeros(m, np.int32)
+    lo = np.zeros((m, 20), np.int32)
+    hi = np.zeros((m, 20), np.int32)
+    ticks = (ctypes.c_uint64 * 14)()
+    hz = ctypes.c_double()
+    pd = ctypes.POINTER(ctypes.c_double)
+    L.check(L.lib().smp_probe_near(device, q.ctypes.data_as(pd), cost.ctypes.data_as(pd), n, queries.ctypes.data_as(pd),
+                                   excl.ctypes.data_as(ctypes.c_void_p), m, float(r), reps,
+                                   nn.ctypes.data_as(ctypes.c_void_p), nk.ctypes.data_as(ctypes.c_void_p),
+                                   lo.ctypes.data_as(ctypes.c_void_p), hi.ctypes.data_as(ctypes.c_void_p), ticks,
+                                   ctypes.byref(hz)), "smp_probe_near")
+    return {"nearest": nn, "k": nk, "lo": lo, "hi": hi,
+            "t_nearest": ticks[0] / hz.value, "t_near": ticks[1] / hz.value,
+            "prof": [ticks[2 + k] for k in range(12)], "clock_hz": hz.value}

@@ -24,6 +24,14 @@ for iters in [int(v) for v in (sys.argv[1:] or ["2000", "10000", "50000"])]:
            r["nodes_start"], r["nodes_goal"], r["nn_nodes_scanned"], r["near_nodes_scanned"],
            r["first_solution_iter"], r["time_first_solution"], r["cost_best"][0]), flush=True)
     print("   phases:", {k: round(v, 3) for k, v in r["phases"].items()}, flush=True)
+    raw = r["phase_raw"]
+    nj = max(raw[15] * 1e8, 1)
+    print("   jobs %d: publish %.1f us, own %.1f us, wait %.1f us per job" % (
+        raw[15] * 1e8, raw[12] * 1e6 / nj, raw[13] * 1e6 / nj, raw[14] * 1e6 / nj), flush=True)
+    if raw[31] > 0:  # SMP_NEAR_PROF build: wave-0 clocks of near_set
+        nc = raw[31] * 1e8
+        print("   near_set (%d calls, wave 0): scan %.1f us (insert %.1f us), merge %.1f us per call" % (
+            nc, raw[28] * 1e6 / nc, raw[29] * 1e6 / nc, raw[30] * 1e6 / nc), flush=True)
 rng = np.random.default_rng(0)
 n = 2_000_000
 q = np.column_stack([rng.uniform(-6, 5, n), rng.uniform(-6, 5, n)] + [rng.uniform(-2, 2, n) for _ in range(6)])
