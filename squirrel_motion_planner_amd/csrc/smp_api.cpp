@@ -515,6 +515,7 @@ static QueryDev make_qdev(QueryBuffers& b, size_t cap, long long rows) {
   d.rows_cap = rows;
   d.path_nodes = b.path_nodes.p;
   d.jb = nullptr;
+  d.nworkers = 1;
   d.trace = nullptr;
   return d;
 }
@@ -587,7 +588,10 @@ extern "C" int smp_plan_batch(smp_planner* p, const smp_query* qs, int nq, smp_r
   int nh = p->params.helpers;
   if (nh == 0) nh = std::min(63, std::max(0, p->num_cus / nq - 1));
   if (nh < 0) nh = 0;
-  for (int i = 0; i < nq; ++i) qdev[i].jb = nh > 0 ? p->qb[i].jb.p : nullptr;
+  for (int i = 0; i < nq; ++i) {
+    qdev[i].jb = nh > 0 ? p->qb[i].jb.p : nullptr;
+    qdev[i].nworkers = 1 + nh;
+  }
   static int* trace_host = nullptr;
   const bool debug = std::getenv("SMP_DEBUG") != nullptr;
   if (debug && !trace_host) HIPCHK(hipHostMalloc(&trace_host, 256 * sizeof(int), hipHostMallocMapped));
@@ -668,11 +672,10 @@ extern "C" int smp_plan_batch(smp_planner* p, const smp_query* qs, int nq, smp_r
       JobBoard jbh;
       if (nh > 0) HIPCHK(hipMemcpy(&jbh, qdev[0].jb, sizeof(JobBoard), hipMemcpyDeviceToHost));
       std::fprintf(stderr, "[smp] launch %lld grid %d chunk %d: %.3f ms phase %d status %d iter %lld checked %lld"
-                   " board seq %d stop %d done %d claim %llx ntiles %d diag pub %d join %d casfail %d giveup %d "
-                   "leaderdone %d tiles %d\n", (long long)launches, nq * (1 + nh), chunk, ms,
-                   S[0].phase, S[0].status, S[0].iter, S[0].checked, nh ? jbh.seq : -1, nh ? jbh.stop : -1,
-                   nh ? jbh.done : -1, nh ? jbh.claim : 0ull, nh ? jbh.ntiles : -1, jbh.pad0[0], jbh.pad0[1],
-                   jbh.pad0[2], jbh.pad0[3], jbh.pad0[4], jbh.pad0[5]);
+                   " board seq %d stop %d done %d ntiles %d flag0 %u jobs published %d joined %d\n", (long long)launches,
+                   nq * (1 + nh), chunk, ms, S[0].phase, S[0].status, S[0].iter, S[0].checked, nh ? jbh.seq : -1,
+                   nh ? jbh.stop : -1, nh ? jbh.done : -1, nh ? jbh.ntiles : -1, nh ? jbh.tflag[0] : 0u, jbh.pad0[0],
+                   jbh.pad0[1]);
     }
     bool all_done = true;
     for (int i = 0; i < nq; ++i) all_done &= (S[i].phase == 2 || S[i].status != 0);

@@ -67,28 +67,47 @@ __device__ __forceinline__ void body_frames(const RobotDev* __restrict__ rb, con
 }
 
 // End-effector z of the 12-segment KDL chain (kdl_kuka_model.cpp:278-305): p_out = I; p_out *= J(q)*f_tip.
+// Only z is wanted, so only row 2 of p_out's rotation and p_out.z are carried: each of those entries of
+// P * L is the same three-term sum as in the full frame product (smp_math.h fmul), so the value is the one the
+// full product gives.  Fixed and prismatic segments skip the product with their identity joint rotation:
+// 1*a + 0*b + 0*c == a exactly up to the sign of a zero, which no later operation turns into a different
+// non-zero value and which `z >= 0` does not see.
 __device__ __forceinline__ double ee_z(const RobotDev* __restrict__ rb, const double* q) {
-  Frame P;
-  frame_identity(&P);
+  double r0 = 0.0, r1 = 0.0, r2 = 1.0, pz = 0.0;  // row 2 of P.R, P.p[2]
   for (int s = 0; s < rb->n_seg; ++s) {
-    Frame J;
-    frame_identity(&J);
-    int ty = rb->seg_type[s];
+    const int ty = rb->seg_type[s];
+    const double* FR = &rb->seg_R[s * 9];
+    const double* Fp = &rb->seg_p[s * 3];
+    double LR[9], Lp[3];
     if (ty == 1) {
-      rot2(&rb->seg_axis[s * 3], q[rb->seg_joint[s]], J.R);
-      J.p[0] = rb->seg_origin[s * 3]; J.p[1] = rb->seg_origin[s * 3 + 1]; J.p[2] = rb->seg_origin[s * 3 + 2];
-    } else if (ty == 2) {
-      double qq = q[rb->seg_joint[s]];
-      for (int d = 0; d < 3; ++d) J.p[d] = rb->seg_origin[s * 3 + d] + rb->seg_axis[s * 3 + d] * qq;
+      double JR[9];
+      rot2(&rb->seg_axis[s * 3], q[rb->seg_joint[s]], JR);
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+          LR[r * 3 + c] = JR[r * 3 + 0] * FR[0 * 3 + c] + JR[r * 3 + 1] * FR[1 * 3 + c] + JR[r * 3 + 2] * FR[2 * 3 + c];
+        Lp[r] = (JR[r * 3 + 0] * Fp[0] + JR[r * 3 + 1] * Fp[1] + JR[r * 3 + 2] * Fp[2]) + rb->seg_origin[s * 3 + r];
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 9; ++i) LR[i] = FR[i];
+      if (ty == 2) {
+        const double qq = q[rb->seg_joint[s]];
+#pragma unroll
+        for (int d = 0; d < 3; ++d) Lp[d] = Fp[d] + (rb->seg_origin[s * 3 + d] + rb->seg_axis[s * 3 + d] * qq);
+      } else {
+#pragma unroll
+        for (int d = 0; d < 3; ++d) Lp[d] = Fp[d];
+      }
     }
-    Frame F;
-    for (int i = 0; i < 9; ++i) F.R[i] = rb->seg_R[s * 9 + i];
-    for (int d = 0; d < 3; ++d) F.p[d] = rb->seg_p[s * 3 + d];
-    Frame L;
-    fmul(J, F, &L);
-    fmul(P, L, &P);
+    const double n0 = r0 * LR[0] + r1 * LR[3] + r2 * LR[6];
+    const double n1 = r0 * LR[1] + r1 * LR[4] + r2 * LR[7];
+    const double n2 = r0 * LR[2] + r1 * LR[5] + r2 * LR[8];
+    pz = (r0 * Lp[0] + r1 * Lp[1] + r2 * Lp[2]) + pz;
+    r0 = n0; r1 = n1; r2 = n2;
   }
-  return P.p[2];
+  return pz;
 }
 
 // Grid cell of a sphere centre, or -1 outside the grid (such a sphere is free: the grid is padded by more

@@ -59,6 +59,7 @@ void robot_from_json(const std::string& text, RobotHost* out) {
     copy3(e["ftip_R"], &d.seg_R[s * 9], 9);
     copy3(e["ftip_p"], &d.seg_p[s * 3]);
   }
+
   // collision links -> compact slots (order of link_bounds)
   const json::Value& lb = m["link_bounds"];
   d.n_clink = (int)lb.size();

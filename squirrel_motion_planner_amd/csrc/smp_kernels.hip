@@ -86,7 +86,7 @@ __global__ void u01_kernel(unsigned long long seed, unsigned query, const uint32
 }
 
 // body frames (n x n_body x 12) and end-effector z of n configurations (row-major q).
-__global__ void fk_kernel(const RobotDev* __restrict__ rb, const double* q, int n, double* frames, double* eez) {
+__global__ void __launch_bounds__(128) fk_kernel(const RobotDev* __restrict__ rb, const double* q, int n, double* frames, double* eez) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   double qq[NJ];
@@ -135,6 +135,11 @@ struct PlanLds {
       int wli[BLOCK / 64][MAX_NEAR], whi[BLOCK / 64][MAX_NEAR];
       int wtot[BLOCK / 64];
     } nr;
+    struct {  // sample_ellipse: first valid inner getRandomConf draw of 64 outer attempts
+      double q[64][NJ];
+      int ok[64];
+      int win;
+    } smp;
     struct {  // near_set, register path: cost histogram and the two candidate buffers
       unsigned hist[NEAR_BINS];
       unsigned long long ck[2][NEAR_BUF];
@@ -802,57 +807,67 @@ __device__ __forceinline__ int ld_agent(const int* p) { return __hip_atomic_load
 __device__ __forceinline__ unsigned long long ld_agent(const unsigned long long* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ __forceinline__ unsigned ld_agent(const unsigned* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 // Waits until this wave's vector-memory operations (stores, atomics) are performed.
 __device__ __forceinline__ void drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// One attempt to claim the next tile of job `seq`: the tile, -1 when none is left (or the board moved on to
-// another job), -2 when another workgroup won the race (retry).  One lane, straight-line code: loops inside
-// single-lane regions of a barrier loop can be restructured by the compiler into divergent barriers.
-// Claim word: job seq (bits 32-63) | slots of that job (16-31) | next tile (0-15).  The slot count travels
-// with the tag, so a claim is never validated against scalars of another job's payload.
-__device__ __forceinline__ unsigned long long claim_word(int seq, int nslots) {
-  return ((unsigned long long)(unsigned)seq << 32) | ((unsigned long long)(nslots & 0xffff) << 16);
-}
-__device__ __forceinline__ int job_claim_once(JobBoard* jb, int seq, int* nslots) {
-  unsigned long long v = ld_agent(&jb->claim);
-  const int ns = (int)((v >> 16) & 0xffff), next = (int)(v & 0xffff);
-  if ((int)(v >> 32) != seq || next >= (ns + HELPER_CT - 1) / HELPER_CT) return -1;
-  unsigned long long expect = v;
-  if (__hip_atomic_compare_exchange_strong(&jb->claim, &expect, v + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT)) {
-    *nslots = ns;
-    return next;
-  }
-  return -2;
+// Claims tile t of job `seq`.  Every tile has a flag holding the last job that claimed it (atomicMax), so the
+// claim succeeds iff no worker claimed t in this job.  Flags never decrease and a job is published only after
+// every tile of the previous one was claimed and finished, so a worker still holding an older job's number
+// can never claim a tile of a newer job.
+__device__ __forceinline__ bool claim_tile(JobBoard* jb, int t, int seq) {
+  return (int)__hip_atomic_fetch_max(&jb->tflag[t], (unsigned)seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < seq;
 }
 
-// Takes tiles of the job held in g_L.u.job until none is left: configuration = start + i * step of its
-// (edge, point) slot (the leader's arithmetic), collision tile, first collisions by agent-scope atomicMin
-// into the board, then one `done` per tile after the results are performed.  All threads.
-__device__ __forceinline__ void job_work(const Ctx& C, JobBoard* jb, JobLds& J, int max_tiles = 1 << 30) {
-  for (int taken = 0; taken < max_tiles;) {
-    if (threadIdx.x == 0) J.tile = job_claim_once(jb, J.seq, &J.nslots);
-    __syncthreads();
-    const int t = uni(J.tile);
-    if (threadIdx.x == 0 && J.hidx >= 0) TRACE(C, 10 + 3 * (J.hidx & 63), t);
-    if (t == -1) break;
-    if (t < 0) continue;
-    ++taken;
-    const int base = t * HELPER_CT, nc = min(HELPER_CT, uni(J.nslots) - base);
-    if (threadIdx.x < nc * NJ) {
-      int c = threadIdx.x / NJ, j = threadIdx.x - c * NJ;
-      int e = J.slot_e[base + c];
-      J.tq[c][j] = J.start[e][j] + J.slot_i[base + c] * J.step[e][j];
-    }
-    __syncthreads();
-    collide_tile<HELPER_CT>((&g_rb), C.sc, (&g_mc), nc, J.tq, J.self, J.map, J.T);
-    if (threadIdx.x < nc && J.T.coll[threadIdx.x])
-      atomicMin(&jb->first[J.slot_e[base + threadIdx.x]], J.slot_i[base + threadIdx.x]);
-    drain();
-    __syncthreads();
-    if (threadIdx.x == 0) { atomicAdd(&jb->done, 1); atomicAdd(&jb->pad0[5], 1); }
+// One job tile held in g_L.u.job / the helper's LDS: configuration = start + i * step of its (edge, point)
+// slot (the leader's arithmetic), collision tile, first collisions by agent-scope atomicMin into the board, then
+// `done` once the results are performed.  All threads.
+__device__ __forceinline__ void job_tile(const Ctx& C, JobBoard* jb, JobLds& J, int t) {
+  const int base = t * HELPER_CT, nc = min(HELPER_CT, uni(J.nslots) - base);
+  if (threadIdx.x < nc * NJ) {
+    int c = threadIdx.x / NJ, j = threadIdx.x - c * NJ;
+    int e = J.slot_e[base + c];
+    J.tq[c][j] = J.start[e][j] + J.slot_i[base + c] * J.step[e][j];
   }
   __syncthreads();
+  collide_tile<HELPER_CT>((&g_rb), C.sc, (&g_mc), nc, J.tq, J.self, J.map, J.T);
+  if (threadIdx.x < nc && J.T.coll[threadIdx.x])
+    atomicMin(&jb->first[J.slot_e[base + threadIdx.x]], J.slot_i[base + threadIdx.x]);
+  drain();
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(&jb->done, 1);
+}
+
+// Worker w's share of the job: tiles w, w + W, w + 2W, ... (W = leader + helpers), each claimed first (one
+// atomic, no contention between workers).  All threads; the claim result is broadcast through LDS.
+__device__ __forceinline__ void job_work(const Ctx& C, JobBoard* jb, JobLds& J, int w, int W) {
+  const int nt = uni(J.ntiles);
+  for (int t = w; t < nt; t += W) {
+    if (threadIdx.x == 0) J.tile = claim_tile(jb, t, J.seq) ? t : -1;
+    __syncthreads();
+    if (uni(J.tile) >= 0) job_tile(C, jb, J, t);
+  }
+  __syncthreads();
+}
+
+// Leader, when the job stops progressing (a helper not resident or late): wave 0 reads every tile flag,
+// thread 0 claims the first unclaimed tile, which the block then checks.  Returns 0 if none was left.
+__device__ __forceinline__ int job_steal_one(const Ctx& C, JobBoard* jb, JobLds& J) {
+  const int nt = uni(J.ntiles);
+  if (threadIdx.x < 64) {
+    int cand = 1 << 30;
+    for (int t = threadIdx.x; t < nt; t += 64)
+      if ((int)ld_agent(&jb->tflag[t]) < J.seq) { cand = t; break; }
+    for (int off = 32; off > 0; off >>= 1) cand = min(cand, __shfl_xor(cand, off));
+    if (threadIdx.x == 0) J.tile = cand < nt && claim_tile(jb, cand, J.seq) ? cand : (cand < nt ? -2 : -1);
+  }
+  __syncthreads();
+  const int t = uni(J.tile);
+  if (t >= 0) job_tile(C, jb, J, t);
+  __syncthreads();
+  return t != -1;
 }
 
 // Leader: publishes the needed edges as one job (every point of every needed edge), works on it with the
@@ -901,7 +916,6 @@ __device__ __forceinline__ void edge_validity_job(const Ctx& C, int E, int pslot
     st_agent(&jb->E, E); st_agent(&jb->np1, np1); st_agent(&jb->nslots, J.nslots); st_agent(&jb->ntiles, J.ntiles);
     st_agent(&jb->self, J.self); st_agent(&jb->map, J.map);
     st_agent(&jb->done, 0);
-    st_agent(&jb->claim, claim_word(J.seq, J.nslots));
   }
   drain();
   __syncthreads();
@@ -913,13 +927,13 @@ __device__ __forceinline__ void edge_validity_job(const Ctx& C, int E, int pslot
   if (threadIdx.x == 0) { g_L.S.prof[P_TFK] += _pt - tj0; g_L.S.prof[P_TTEST]++; }  // job publication
   if (threadIdx.x == 0) atomicAdd(&jb->pad0[0], 1);  // diagnostics: jobs published
   if (threadIdx.x == 0) TRACE(C, 0, 2);
-  job_work(C, jb, J, 1);  // the leader takes one tile; helpers take the rest in parallel
+  job_work(C, jb, J, 0, C.Q.nworkers);  // the leader is worker 0; helpers take their tiles in parallel
   if (threadIdx.x == 0) TRACE(C, 0, 3);
   if (threadIdx.x == 0) atomicAdd(&jb->pad0[4], 1);  // diagnostics: leader finished its claims
   const unsigned long long tj1 = threadIdx.x == 0 ? wall_clock64() : 0;
   if (threadIdx.x == 0) g_L.S.prof[P_TCHAIN] += tj1 - _pt;  // the leader's own tiles
-  // wait for the other tiles (block-level loop; thread 0 polls).  Should the job stop progressing for 20 us
-  // (no helper resident, or all busy), the leader takes the next unclaimed tile itself.
+  // wait for the other tiles (block-level loop; thread 0 polls).  Should the job stop progressing for 8 us
+  // (a helper not resident, or late), the leader takes unclaimed tiles itself.
   const unsigned long long t_wait = wall_clock64();
   unsigned long long t_prog = t_wait;
   int last_d = -1;
@@ -928,13 +942,13 @@ __device__ __forceinline__ void edge_validity_job(const Ctx& C, int E, int pslot
       const int d = ld_agent(&jb->done);
       const unsigned long long now = wall_clock64();
       if (d != last_d) { last_d = d; t_prog = now; }
-      int st = d >= J.ntiles ? 1 : (now - t_prog > 2000ull ? 2 : 0);
+      int st = d >= J.ntiles ? 1 : (now - t_prog > 800ull ? 2 : 0);
       if (st != 1 && now - t_wait > 200000000ull) {  // 2 s: a job never takes that long -- fail, never hang
         g_L.S.status = -5;
         g_L.S.phase = 2;
         g_L.S.prof[28] = (unsigned long long)d;
         g_L.S.prof[29] = (unsigned long long)J.ntiles;
-        g_L.S.prof[30] = ld_agent(&jb->claim);
+        g_L.S.prof[30] = (unsigned long long)ld_agent(&jb->tflag[0]);
         g_L.S.prof[31] = (unsigned long long)J.seq;
         st = 1;
       }
@@ -944,7 +958,7 @@ __device__ __forceinline__ void edge_validity_job(const Ctx& C, int E, int pslot
     const int go = uni(J.go);
     if (go == 1) break;
     if (go == 2) {
-      job_work(C, jb, J, 1);
+      job_steal_one(C, jb, J);
       if (threadIdx.x == 0) t_prog = wall_clock64();
       continue;
     }
@@ -1007,7 +1021,9 @@ __device__ __forceinline__ void helper_main(const Ctx& C, int hidx, JobLds& J) {
     }
     __syncthreads();
     if (threadIdx.x == 0) atomicAdd(&jb->pad0[1], 1);  // diagnostics: jobs joined by helpers
-    job_work(C, jb, J);
+    if (threadIdx.x == 0) J.ntiles = (nslots + HELPER_CT - 1) / HELPER_CT;
+    __syncthreads();
+    job_work(C, jb, J, 1 + hidx, C.Q.nworkers);
     t_last = wall_clock64();
   }
   if (threadIdx.x == 0) TRACE(C, 8 + 3 * (hidx & 63), 2);
@@ -1170,12 +1186,15 @@ __device__ void insert_via(const Ctx& C, int t) {
 __device__ void rand_conf_lane(const Ctx& C, const QState& S, uint32_t outer, uint32_t inner, double* q) {
   const RobotDev* rb = (&g_rb);
   bool env0 = S.env_x[0] == 0.0 && S.env_x[1] == 0.0 && S.env_y[0] == 0.0 && S.env_y[1] == 0.0;
+  double u[NJ];
+#pragma unroll
+  for (int p = 0; p < NJ / 2; ++p) u01_pair(S.seed, S.query, (uint32_t)S.iter, outer, inner, p, &u[2 * p], &u[2 * p + 1]);
+#pragma unroll
   for (int j = 0; j < NJ; ++j) {
     double lo = rb->q_min[j], hi = rb->q_max[j];
     if (!env0 && j == 0) { lo = S.env_x[0]; hi = S.env_x[1]; }
     if (!env0 && j == 1) { lo = S.env_y[0]; hi = S.env_y[1]; }
-    double u = u01(S.seed, S.query, (uint32_t)S.iter, outer, inner, j);
-    q[j] = u * (hi - lo) + lo;
+    q[j] = u[j] * (hi - lo) + lo;
   }
 }
 
@@ -1201,23 +1220,57 @@ __device__ void sample_uniform(const Ctx& C) {
   __syncthreads();
 }
 
-// sampleJointConfigfromEllipse_JntArray (birrt_star.cpp:3607-3829); lane = outer attempt b, inner
-// getRandomConf attempts run serially per lane; the lowest valid b wins.
+// sampleJointConfigfromEllipse_JntArray (birrt_star.cpp:3607-3829): outer attempt b draws getRandomConf inner
+// attempts 0, 1, ... until one has EE z >= 0, maps it into the informed ellipse, and the lowest outer attempt
+// whose mapped sample is above ground and inside the environment wins.  SE_OUT outer attempts per round:
+//   1. waves 0-3 (one per SIMD: the FK chain is fp64-latency bound, more waves would only queue behind each
+//      other): lane (b, i) evaluates inner attempt i < 8 of outer attempt b; the first valid i of each b goes to
+//      LDS;
+//   2. wave 0, lane b < SE_OUT: an outer attempt without a valid inner attempt in 0..7 continues serially from 8
+//      (p ~ 2^-8 each); ellipse map + EE z + environment test; the lowest valid b wins.
 __device__ void sample_ellipse(const Ctx& C) {
   const RobotDev* rb = (&g_rb);
   const QState& S = g_L.S;
-  if (wave_id() == 0) {
-    bool env0 = S.env_x[0] == 0.0 && S.env_x[1] == 0.0 && S.env_y[0] == 0.0 && S.env_y[1] == 0.0;
-    for (uint32_t base = 0;; base += 64) {
-      if (base >= (1u << 20)) {
-        if (lane_id() == 0) { g_L.S.status = -1; g_L.S.phase = 2; }
-        break;
-      }
-      uint32_t b = base + lane_id();
+  const bool env0 = S.env_x[0] == 0.0 && S.env_x[1] == 0.0 && S.env_y[0] == 0.0 && S.env_y[1] == 0.0;
+  const int lane = lane_id();
+  constexpr int SE_OUT = 32;
+#ifdef SMP_SAMPLE_PROF
+  unsigned long long _ts = wall_clock64();
+#endif
+  for (uint32_t base = 0;; base += SE_OUT) {
+    if (base >= (1u << 20)) {
+      if (threadIdx.x == 0) { g_L.S.status = -1; g_L.S.phase = 2; }
+      __syncthreads();
+      return;
+    }
+    if (threadIdx.x < SE_OUT * 8) {
+      const uint32_t b = base + (threadIdx.x >> 3), inner = threadIdx.x & 7;
       double q[NJ];
-      for (uint32_t inner = 0; inner < (1u << 16); ++inner) {
-        rand_conf_lane(C, S, 1 + b, inner, q);
-        if (0.0 <= ee_z(rb, q)) break;
+      rand_conf_lane(C, S, 1 + b, inner, q);
+      const bool ok = 0.0 <= ee_z(rb, q);
+      const unsigned long long m = __ballot(ok);
+      const unsigned grp = (unsigned)(m >> (lane & ~7)) & 0xffu;  // the 8 lanes of outer attempt b
+      const int first = grp ? __builtin_ctz(grp) : 8;
+      if ((int)inner == first)
+        for (int j = 0; j < NJ; ++j) g_L.u.smp.q[threadIdx.x >> 3][j] = q[j];
+      if (inner == 0) g_L.u.smp.ok[threadIdx.x >> 3] = grp != 0;
+    }
+    __syncthreads();
+#ifdef SMP_SAMPLE_PROF
+    if (threadIdx.x == 0) { const unsigned long long t = wall_clock64(); g_L.S.prof[28] += t - _ts; _ts = t; g_L.S.prof[30]++; }
+#endif
+    if (wave_id() == 0) {
+      const uint32_t b = base + lane;
+      double q[NJ];
+      if (lane >= SE_OUT) {
+        for (int j = 0; j < NJ; ++j) q[j] = 1.0;  // idle lanes: excluded from the ballot below
+      } else if (g_L.u.smp.ok[lane]) {
+        for (int j = 0; j < NJ; ++j) q[j] = g_L.u.smp.q[lane][j];
+      } else {
+        for (uint32_t inner = 8; inner < (1u << 16); ++inner) {
+          rand_conf_lane(C, S, 1 + b, inner, q);
+          if (0.0 <= ee_z(rb, q)) break;
+        }
       }
       double br[6], bp[2], sr = 0.0, sp = 0.0;
       int ir = 0, ip = 0;
@@ -1249,15 +1302,17 @@ __device__ void sample_ellipse(const Ctx& C) {
       for (int j = 0; j < NJ; ++j) r[j] = rb->rev[j] ? rr[ir++] : rp[ip++];
       bool above = 0.0 <= ee_z(rb, r);
       bool inside = (r[0] < S.env_x[1] && r[0] > S.env_x[0] && r[1] < S.env_y[1] && r[1] > S.env_y[0]) || env0;
-      unsigned long long m = __ballot(above && inside);
-      if (m) {
-        int w = __ffsll((long long)m) - 1;
-        if (lane_id() == w) for (int j = 0; j < NJ; ++j) g_L.xr[j] = r[j];
-        break;
-      }
+      unsigned long long m = __ballot(above && inside && lane < SE_OUT);
+      const int w = m ? __ffsll((long long)m) - 1 : -1;
+      if (lane == w) for (int j = 0; j < NJ; ++j) g_L.xr[j] = r[j];
+      if (lane == 0) g_L.u.smp.win = w;
     }
+    __syncthreads();
+#ifdef SMP_SAMPLE_PROF
+    if (threadIdx.x == 0) { const unsigned long long t = wall_clock64(); g_L.S.prof[29] += t - _ts; _ts = t; }
+#endif
+    if (uni(g_L.u.smp.win) >= 0) break;
   }
-  __syncthreads();
 }
 
 // --------------------------------------------------------------------------------------- tree updates

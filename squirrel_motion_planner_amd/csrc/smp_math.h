@@ -119,4 +119,13 @@ SMP_HD double u01(uint64_t seed, uint32_t query, uint32_t it, uint32_t outer, ui
   return (idx & 1) ? u53(c[2], c[3]) : u53(c[0], c[1]);
 }
 
+// The two draws idx = 2 * pair and 2 * pair + 1 of u01, which share one Philox block.
+SMP_HD void u01_pair(uint64_t seed, uint32_t query, uint32_t it, uint32_t outer, uint32_t inner, uint32_t pair,
+                     double* even, double* odd) {
+  uint32_t c[4] = {it, outer, inner, pair};
+  philox(c, (uint32_t)seed, (uint32_t)(seed >> 32) ^ query);
+  *even = u53(c[0], c[1]);
+  *odd = u53(c[2], c[3]);
+}
+
 }  // namespace smp

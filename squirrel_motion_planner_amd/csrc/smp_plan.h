@@ -66,22 +66,24 @@ struct ViaNode {               // via node pending insertion (selected_via_nodes
 // valid forms): payload and flags are agent-scope (sc1) stores drained with s_waitcnt vmcnt(0) behind a
 // workgroup barrier before the flag store; readers poll with sc1 loads and read the payload with sc1 loads.
 #ifndef SMP_HELPER_CT
-#define SMP_HELPER_CT 32
+#define SMP_HELPER_CT 8
 #endif
 constexpr int HELPER_CT = SMP_HELPER_CT;          // configurations per job tile
 constexpr int JOB_SLOTS = MAXE * (MAX_PTS + 1); // (edge, point) slots of one job
+constexpr int JOB_TILES = (JOB_SLOTS + HELPER_CT - 1) / HELPER_CT;
 struct JobBoard {
   int seq;                     // job number; the leader increments it to publish a job
   int stop;                    // 1 once the leader left the launch: helpers exit
   int pad0[30];
-  unsigned long long claim;    // (seq << 32) | next tile; claimed by compare-and-swap
-  int pad1[30];
+  int pad1[32];
   int done;                    // tiles of the current job finished
   int pad2[31];
   int first[MAXE];             // first colliding point per edge (atomicMin); np1 = free
   int pad3[32 - MAXE % 32];
   int E, np1, nslots, ntiles, self, map;
   int pad4[26];
+  unsigned tflag[JOB_TILES];   // per tile: the last job that claimed it (atomicMax; see claim_tile)
+  int pad5[32 - JOB_TILES % 32];
   unsigned long long start[MAXE][NJ], step[MAXE][NJ];  // fp64 bit patterns
   int slot_e[JOB_SLOTS], slot_i[JOB_SLOTS];
 };
@@ -90,6 +92,7 @@ struct QueryDev {
   QState* st;
   JobBoard* jb;                // null: no helpers
   int* trace;                  // debug only (SMP_DEBUG): host-mapped progress markers of the leader
+  int nworkers;                // leader + helper workgroups of this query (tile w, w + nworkers, ... is worker w's)
   TreeDev tr[2];
   ViaNode* via;                // [via_cap]
   int* stack;                  // [cap] DFS stack of recursiveNodeCostUpdate

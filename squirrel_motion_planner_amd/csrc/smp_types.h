@@ -36,6 +36,7 @@ struct RobotDev {
   int rev[NJ];
 };
 
+
 // Occupancy grid of one scene (device pointers).  Cell (i,j,k) is the box [o + i*res, o + (i+1)*res] per
 // axis.  bricks: one 64-bit occupancy mask per 4x4x4 cells, bit (k&3)*16 + (j&3)*4 + (i&3) of brick
 // ((k>>2)*bny + (j>>2))*bnx + (i>>2).  d2: per cell the squared box-to-box gap (voxel units, clamped to

@@ -28,6 +28,10 @@ for iters in [int(v) for v in (sys.argv[1:] or ["2000", "10000", "50000"])]:
     nj = max(raw[15] * 1e8, 1)
     print("   jobs %d: publish %.1f us, own %.1f us, wait %.1f us per job" % (
         raw[15] * 1e8, raw[12] * 1e6 / nj, raw[13] * 1e6 / nj, raw[14] * 1e6 / nj), flush=True)
+    if os.environ.get("SMP_SAMPLE_PROF"):  # SMP_SAMPLE_PROF build: ellipse sampler stage clocks (ticks, slots 28-30)
+        rounds = max(raw[30], 1)
+        print("   sample_ellipse: %d rounds, stage 1 %.2f us, stage 2 %.2f us per round" % (
+            rounds, raw[28] / 1e2 / rounds, raw[29] / 1e2 / rounds), flush=True)
     if raw[31] > 0:  # SMP_NEAR_PROF build: wave-0 clocks of near_set
         nc = raw[31] * 1e8
         print("   near_set (%d calls, wave 0): scan %.1f us (insert %.1f us), merge %.1f us per call" % (
