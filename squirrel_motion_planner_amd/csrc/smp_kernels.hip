@@ -112,7 +112,8 @@ struct JobLds {
   double tq[HELPER_CT][NJ];
   double start[MAXE][NJ], step[MAXE][NJ];
   int slot_e[JOB_SLOTS], slot_i[JOB_SLOTS];
-  int E, np1, nslots, ntiles, self, map, seq, tile, go, hidx;
+  int E, np1, nslots, ntiles, self, map, seq, tile, steal, hidx;
+  int go[2];  // poll-loop decisions, double-buffered by iteration parity (a slow wave may still read the last one)
 };
 constexpr int NEAR_BINS = 256;   // near_set register path: cost histogram bins
 constexpr int NEAR_BUF = 128;    // near_set register path: candidate buffer entries per end
@@ -153,6 +154,8 @@ struct PlanLds {
   double eg_start[MAXE][NJ], eg_target[MAXE][NJ], eg_step[MAXE][NJ], eg_end[MAXE][NJ];
   double eg_base[MAXE][3], eg_cost[MAXE][3];
   int eg_first[MAXE], eg_need[MAXE], eg_near[MAXE], eg_ptr[MAXE];
+  int rw_par[MAXE], rw_next;          // rewire: candidates' parents (refreshed after every commit), resume point
+  double rw_cost[MAXE][3];            // rewire: candidates' costs
   int tile_e[PLAN_CT], tile_i[PLAN_CT], tile_n;
   int count_slot;  // profiling: phase the checked configurations are attributed to
   int job_seq;     // last job published by this leader (this launch)
@@ -193,6 +196,13 @@ struct Ctx {
 enum { P_SAMPLE, P_NN, P_EXPAND, P_NEAR, P_CHOOSE, P_REWIRE, P_CONNECT, P_TILES, P_NTILES, P_COSTS, P_VIA, P_NVIA,
        P_TFK, P_TCHAIN, P_TCENTRE, P_TTEST, P_XEXPAND, P_XCHOOSE, P_XREWIRE, P_XCONNECT };
 #define PROF_BEGIN() unsigned long long _pt = threadIdx.x == 0 ? wall_clock64() : 0
+#ifdef SMP_DETAIL_PROF  // thread-0 clocks of serial sections into prof[28..31] (perf_probe.py SMP_DETAIL_PROF=1)
+#define DETAIL_BEGIN(v) const unsigned long long v = threadIdx.x == 0 ? wall_clock64() : 0
+#define DETAIL_END(v, k) if (threadIdx.x == 0) g_L.S.prof[k] += wall_clock64() - v
+#else
+#define DETAIL_BEGIN(v)
+#define DETAIL_END(v, k)
+#endif
 #define PROF_END(k) if (threadIdx.x == 0) { g_L.S.prof[k] += wall_clock64() - _pt; }
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
@@ -821,10 +831,16 @@ __device__ __forceinline__ bool claim_tile(JobBoard* jb, int t, int seq) {
   return (int)__hip_atomic_fetch_max(&jb->tflag[t], (unsigned)seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < seq;
 }
 
+// Marks tile t as claimed by job `seq` without waiting for the old value: for tiles no other worker can claim.
+__device__ __forceinline__ void mark_tile(JobBoard* jb, int t, int seq) {
+  __hip_atomic_fetch_max(&jb->tflag[t], (unsigned)seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // One job tile held in g_L.u.job / the helper's LDS: configuration = start + i * step of its (edge, point)
-// slot (the leader's arithmetic), collision tile, first collisions by agent-scope atomicMin into the board, then
-// `done` once the results are performed.  All threads.
-__device__ __forceinline__ void job_tile(const Ctx& C, JobBoard* jb, JobLds& J, int t) {
+// slot (the leader's arithmetic), collision tile, then -- only if thread 0's `mine` says the tile is this
+// workgroup's -- first collisions by agent-scope atomicMin into the board and `done` once they are performed.
+// The claim's round trip thus overlaps the tile's first stages.  All threads.
+__device__ __forceinline__ void job_tile(const Ctx& C, JobBoard* jb, JobLds& J, int t, bool mine) {
   const int base = t * HELPER_CT, nc = min(HELPER_CT, uni(J.nslots) - base);
   if (threadIdx.x < nc * NJ) {
     int c = threadIdx.x / NJ, j = threadIdx.x - c * NJ;
@@ -833,41 +849,54 @@ __device__ __forceinline__ void job_tile(const Ctx& C, JobBoard* jb, JobLds& J, 
   }
   __syncthreads();
   collide_tile<HELPER_CT>((&g_rb), C.sc, (&g_mc), nc, J.tq, J.self, J.map, J.T);
-  if (threadIdx.x < nc && J.T.coll[threadIdx.x])
-    atomicMin(&jb->first[J.slot_e[base + threadIdx.x]], J.slot_i[base + threadIdx.x]);
-  drain();
+  if (threadIdx.x == 0) J.tile = mine;
   __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(&jb->done, 1);
+  if (uni(J.tile)) {
+    if (threadIdx.x < nc && J.T.coll[threadIdx.x])
+      atomicMin(&jb->first[J.slot_e[base + threadIdx.x]], J.slot_i[base + threadIdx.x]);
+    drain();
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(&jb->done, 1);
+  }
 }
 
-// Worker w's share of the job: tiles w, w + W, w + 2W, ... (W = leader + helpers), each claimed first (one
-// atomic, no contention between workers).  All threads; the claim result is broadcast through LDS.
+// Worker w's share of the job: tiles w, w + W, w + 2W, ... (W = leader + helpers).  A helper claims each one
+// (one atomic, no contention between workers; only the stalled leader competes, see job_steal_one); the
+// leader's own tiles are never stolen, so it only marks them.  All threads.
 __device__ __forceinline__ void job_work(const Ctx& C, JobBoard* jb, JobLds& J, int w, int W) {
   const int nt = uni(J.ntiles);
   for (int t = w; t < nt; t += W) {
-    if (threadIdx.x == 0) J.tile = claim_tile(jb, t, J.seq) ? t : -1;
-    __syncthreads();
-    if (uni(J.tile) >= 0) job_tile(C, jb, J, t);
+    bool mine = true;
+    if (threadIdx.x == 0) {
+      if (w == 0) mark_tile(jb, t, J.seq);
+      else mine = claim_tile(jb, t, J.seq);
+    }
+    job_tile(C, jb, J, t, mine);
   }
   __syncthreads();
 }
 
-// Leader, when the job stops progressing (a helper not resident or late): wave 0 reads every tile flag,
-// thread 0 claims the first unclaimed tile, which the block then checks.  Returns 0 if none was left.
-__device__ __forceinline__ int job_steal_one(const Ctx& C, JobBoard* jb, JobLds& J) {
+// Leader, when the job stops progressing (a helper not resident or late): wave 0 reads the flags of the
+// helpers' tiles, thread 0 claims the first unclaimed one, which the block then checks.  Returns 0 if none
+// was left.
+__device__ __forceinline__ int job_steal_one(const Ctx& C, JobBoard* jb, JobLds& J, int W) {
   const int nt = uni(J.ntiles);
   if (threadIdx.x < 64) {
     int cand = 1 << 30;
     for (int t = threadIdx.x; t < nt; t += 64)
-      if ((int)ld_agent(&jb->tflag[t]) < J.seq) { cand = t; break; }
+      if (t % W != 0 && (int)ld_agent(&jb->tflag[t]) < J.seq) { cand = t; break; }
     for (int off = 32; off > 0; off >>= 1) cand = min(cand, __shfl_xor(cand, off));
-    if (threadIdx.x == 0) J.tile = cand < nt && claim_tile(jb, cand, J.seq) ? cand : (cand < nt ? -2 : -1);
+    if (threadIdx.x == 0) J.steal = cand < nt ? cand : -1;
   }
   __syncthreads();
-  const int t = uni(J.tile);
-  if (t >= 0) job_tile(C, jb, J, t);
+  const int t = uni(J.steal);
+  if (t >= 0) {
+    bool mine = false;
+    if (threadIdx.x == 0) mine = claim_tile(jb, t, J.seq);
+    job_tile(C, jb, J, t, mine);
+  }
   __syncthreads();
-  return t != -1;
+  return t >= 0;
 }
 
 // Leader: publishes the needed edges as one job (every point of every needed edge), works on it with the
@@ -937,7 +966,7 @@ __device__ __forceinline__ void edge_validity_job(const Ctx& C, int E, int pslot
   const unsigned long long t_wait = wall_clock64();
   unsigned long long t_prog = t_wait;
   int last_d = -1;
-  for (;;) {
+  for (int k = 0;; k ^= 1) {
     if (threadIdx.x == 0) {
       const int d = ld_agent(&jb->done);
       const unsigned long long now = wall_clock64();
@@ -952,13 +981,13 @@ __device__ __forceinline__ void edge_validity_job(const Ctx& C, int E, int pslot
         g_L.S.prof[31] = (unsigned long long)J.seq;
         st = 1;
       }
-      J.go = st;
+      J.go[k] = st;
     }
     __syncthreads();
-    const int go = uni(J.go);
+    const int go = uni(J.go[k]);
     if (go == 1) break;
     if (go == 2) {
-      job_steal_one(C, jb, J);
+      job_steal_one(C, jb, J, C.Q.nworkers);
       if (threadIdx.x == 0) t_prog = wall_clock64();
       continue;
     }
@@ -984,17 +1013,17 @@ __device__ __forceinline__ void helper_main(const Ctx& C, int hidx, JobLds& J) {
   J.hidx = hidx;
   if (threadIdx.x == 0) TRACE(C, 8 + 3 * (hidx & 63), 1);
   unsigned long long t_last = wall_clock64();
-  for (;;) {
+  for (int k = 0;; k ^= 1) {
     // block-level poll (thread 0 reads the board): 0 = nothing yet, > 0 = new job, -1 = leave
     if (threadIdx.x == 0) {
       int go = 0;
       const int s = ld_agent(&jb->seq);
       if (s != last) go = s;
       else if (ld_agent(&jb->stop) || wall_clock64() - t_last > 200000000ull) go = -1;  // 2 s idle
-      J.go = go;
+      J.go[k] = go;
     }
     __syncthreads();
-    const int go = uni(J.go);
+    const int go = uni(J.go[k]);
     if (go < 0) break;
     if (go == 0) {
       __builtin_amdgcn_s_sleep(2);
@@ -1164,19 +1193,54 @@ __device__ void via_chain(const Ctx& C, const double* target) {
   PROF_END(P_VIA);
 }
 
+// Inserts the pending via nodes (insertNode, birrt_star.cpp:3298-3322, once per node in order).  They form a
+// chain -- via k's parent is via k-1, the first one's an existing node p0 -- so the result of the sequential
+// inserts is known up front: node n0+k gets first child n0+k+1 (none for the last), and only p0's child list
+// changes among the existing nodes.  One thread per node; thread 0 also links the first node under p0.
 __device__ void insert_via(const Ctx& C, int t) {
-  if (threadIdx.x == 0) {
-    for (int v = 0; v < g_L.n_via && g_L.S.status == 0; ++v) {
-      const ViaNode& w = C.Q.via[v];
-      NodeRef x;
-      for (int j = 0; j < NJ; ++j) x.q[j] = w.q[j];
-      for (int k = 0; k < 3; ++k) x.c[k] = w.c[k];
-      x.id = w.id;
-      x.parent = w.parent;
-      insert_node(C, t, w.e_start, w.e_target, x);
+  DETAIL_BEGIN(_di);
+  const int nv = uni(g_L.n_via);
+  if (nv > 0) {
+    QState& S = g_L.S;
+    const TreeDev& T = C.Q.tr[t];
+    const int n0 = uni(S.n[t]), cap = uni(S.cap);
+    if (n0 + nv > cap) {
+      if (threadIdx.x == 0) { S.status = -7; S.phase = 2; }
+    } else {
+      for (int k = threadIdx.x; k < nv; k += BLOCK) {
+        const ViaNode& w = C.Q.via[k];
+        const int i = n0 + k;
+        if (w.id != i || (k > 0 && w.parent != i - 1)) S.status = -7;  // not the chain insert_node expects
+        for (int j = 0; j < NJ; ++j) {
+          T.q[(size_t)j * cap + i] = w.q[j];
+          T.e_start[(size_t)j * cap + i] = w.e_start[j];
+          T.e_target[(size_t)j * cap + i] = w.e_target[j];
+        }
+        for (int c = 0; c < 3; ++c) T.cost[(size_t)c * cap + i] = w.c[c];
+        T.parent[i] = w.parent;
+        T.first_child[i] = k + 1 < nv ? i + 1 : -1;
+        T.prev_sib[i] = -1;
+        if (k > 0) {
+          T.next_sib[i] = -1;
+        } else {
+          const int p = w.parent, f = T.first_child[p];
+          T.next_sib[i] = f;
+          if (f >= 0) T.prev_sib[f] = i;
+          T.first_child[p] = i;
+        }
+      }
+      if (threadIdx.x == 0) {
+        S.n[t] = n0 + nv;
+        S.edges[t] += nv;
+      }
     }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (g_L.S.status == -7) g_L.S.phase = 2;
     g_L.n_via = 0;
   }
+  DETAIL_END(_di, 31);
   __syncthreads();
 }
 
@@ -1455,45 +1519,66 @@ __device__ void rewire(const Ctx& C, int t) {
   for (int e = cnt + threadIdx.x; e < MAXE; e += BLOCK) g_L.eg_need[e] = 0;
   __syncthreads();
   edge_validity(C, cnt, false, P_XREWIRE);
-  if (threadIdx.x == 0) {
-    QState& S = g_L.S;
-    for (int e = 0; e < cnt && S.status == 0; ++e) {
-      int v = g_L.eg_near[e];
-      if (!(v != g_L.xn.parent && T.parent[v] != 0)) continue;
-      double cv[3];
-      for (int k = 0; k < 3; ++k) cv[k] = T.cost[(size_t)k * cap + v];
-      if (!(g_L.eg_cost[e][0] < cv[0])) continue;
-      count_edge(g_L.eg_first[e]);
-      if (g_L.eg_first[e] <= S.n_pts) continue;
-      double red[3];
-      for (int k = 0; k < 3; ++k) red[k] = g_L.eg_cost[e][k] - cv[k];
-      // unlink from the old parent (the reference erases the outgoing edge, birrt_star.cpp:5124-5169)
-      int p = T.parent[v];
-      int pv = T.prev_sib[v], nx = T.next_sib[v];
-      if (pv >= 0) T.next_sib[pv] = nx; else T.first_child[p] = nx;
-      if (nx >= 0) T.prev_sib[nx] = pv;
-      S.edges[t]--;
-      T.parent[v] = g_L.xn.id;
-      if (S.have_sol) {
-        bool connected = (t == 0) == (S.conn_start != 0);
-        if (v == S.nB.id && connected) S.nB.parent = g_L.xn.id;
-        else if (v == S.nA.id && !connected) S.nA.parent = g_L.xn.id;
-      }
-      for (int j = 0; j < NJ; ++j) {
-        T.q[(size_t)j * cap + v] = g_L.eg_end[e][j];
-        T.e_start[(size_t)j * cap + v] = g_L.eg_start[e][j];
-        T.e_target[(size_t)j * cap + v] = g_L.eg_target[e][j];
-      }
-      int f = T.first_child[g_L.xn.id];
-      T.next_sib[v] = f;
-      T.prev_sib[v] = -1;
-      if (f >= 0) T.prev_sib[f] = v;
-      T.first_child[g_L.xn.id] = v;
-      cost_update(C, t, v, red);
-      S.edges[t]++;
-      S.rewires[t]++;
+  DETAIL_BEGIN(_dr);
+  // Sequential commits (birrt_star.cpp:5096-5228).  The candidates' parents and costs are gathered into LDS by
+  // one thread each; thread 0 walks the candidates from the resume point and stops after a commit, which may
+  // change later candidates' costs (subtree update) -- the block then re-gathers and resumes.
+  for (int e0 = 0;;) {
+    if (threadIdx.x >= e0 && threadIdx.x < cnt) {
+      const int e = threadIdx.x, v = g_L.eg_near[e];
+      g_L.rw_par[e] = T.parent[v];
+      for (int k = 0; k < 3; ++k) g_L.rw_cost[e][k] = T.cost[(size_t)k * cap + v];
     }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      QState& S = g_L.S;
+      int next = cnt;
+      for (int e = e0; e < cnt && S.status == 0; ++e) {
+        const int v = g_L.eg_near[e];
+        if (!(v != g_L.xn.parent && g_L.rw_par[e] != 0)) continue;
+        if (!(g_L.eg_cost[e][0] < g_L.rw_cost[e][0])) continue;
+        count_edge(g_L.eg_first[e]);
+        if (g_L.eg_first[e] <= S.n_pts) continue;
+        double red[3];
+        for (int k = 0; k < 3; ++k) red[k] = g_L.eg_cost[e][k] - g_L.rw_cost[e][k];
+        // unlink from the old parent (the reference erases the outgoing edge, birrt_star.cpp:5124-5169)
+        const int p = g_L.rw_par[e];
+        const int pv = T.prev_sib[v], nx = T.next_sib[v];
+        if (pv >= 0) T.next_sib[pv] = nx; else T.first_child[p] = nx;
+        if (nx >= 0) T.prev_sib[nx] = pv;
+        S.edges[t]--;
+        T.parent[v] = g_L.xn.id;
+        if (S.have_sol) {
+          bool connected = (t == 0) == (S.conn_start != 0);
+          if (v == S.nB.id && connected) S.nB.parent = g_L.xn.id;
+          else if (v == S.nA.id && !connected) S.nA.parent = g_L.xn.id;
+        }
+        for (int j = 0; j < NJ; ++j) {
+          T.q[(size_t)j * cap + v] = g_L.eg_end[e][j];
+          T.e_start[(size_t)j * cap + v] = g_L.eg_start[e][j];
+          T.e_target[(size_t)j * cap + v] = g_L.eg_target[e][j];
+        }
+        int f = T.first_child[g_L.xn.id];
+        T.next_sib[v] = f;
+        T.prev_sib[v] = -1;
+        if (f >= 0) T.prev_sib[f] = v;
+        T.first_child[g_L.xn.id] = v;
+        DETAIL_BEGIN(_dc);
+        cost_update(C, t, v, red);
+        DETAIL_END(_dc, 29);
+        S.edges[t]++;
+        S.rewires[t]++;
+        next = e + 1;
+        break;
+      }
+      if (S.status != 0) next = cnt;
+      g_L.rw_next = next;
+    }
+    __syncthreads();
+    e0 = uni(g_L.rw_next);
+    if (e0 >= cnt) break;
   }
+  DETAIL_END(_dr, 28);
   __syncthreads();
 }
 
@@ -1573,47 +1658,69 @@ __device__ void connect_graphs(const Ctx& C, int t) {
       for (int e = E + threadIdx.x; e < MAXE; e += BLOCK) g_L.eg_need[e] = 0;
       __syncthreads();
       edge_validity(C, E, true, P_XCONNECT);
-      // sequential replay of the near loop (birrt_star.cpp:2820-3030)
-      for (int e = 0; e < E; ++e) {
-        if (threadIdx.x == 0) {
-          g_L.flag = 0;
-          if (g_L.eg_need[e]) {
-            double sol0 = g_L.eg_cost[e][0] + g_L.xn.c[0];
-            double sol1 = g_L.eg_cost[e][1] + g_L.xn.c[1];
-            double sol2 = g_L.eg_cost[e][2] + g_L.xn.c[2];
-            int f = g_L.eg_first[e];
-            count_edge(f);
-            if (f > g_L.S.n_pts) {
-              g_L.csp[0] = sol0; g_L.csp[1] = sol1; g_L.csp[2] = sol2;
-              g_L.flag = 1;
-            } else if (g_L.csp[0] == g_L.S.cbest[0] && sol0 < g_L.best_nv) {
-              int lv = f == 0 ? 0 : f - 1;
-              if (lv != 0) {
-                for (int j = 0; j < NJ; ++j) g_L.ext[j] = g_L.eg_start[e][j] + lv * g_L.eg_step[e][j];
+      DETAIL_BEGIN(_dn);
+      // replay of the near loop (birrt_star.cpp:2820-3030).  An edge acts (connects: 1, extends: 2) only on
+      // conditions of state that changes when an edge acts, so wave 0 evaluates every remaining edge against
+      // the current state and the first acting one is processed; the configurations of the needed edges up to
+      // it are counted as the sequential loop counts them.
+      for (int e0 = 0;;) {
+        if (threadIdx.x < 64) {
+          const int e = threadIdx.x;
+          const int np1 = g_L.S.n_pts + 1;
+          const bool act = e >= e0 && e < E && g_L.eg_need[e];
+          int fl = 0, f = 0;
+          if (act) {
+            f = g_L.eg_first[e];
+            const double sol0 = g_L.eg_cost[e][0] + g_L.xn.c[0];
+            if (f > g_L.S.n_pts) fl = 1;
+            else if (g_L.csp[0] == g_L.S.cbest[0] && sol0 < g_L.best_nv && f >= 2) fl = 2;  // lv = f - 1 != 0
+          }
+          const unsigned long long m = __ballot(fl != 0);
+          const int ev = m ? __builtin_ctzll(m) : 64;
+          int chk = 0, val = 0;
+          if (act && e <= ev) { chk = f >= np1 ? np1 : f + 1; val = f >= np1 ? np1 : f; }
+          for (int off = 32; off > 0; off >>= 1) { chk += __shfl_xor(chk, off); val += __shfl_xor(val, off); }
+          if (e == 0) {
+            g_L.S.prof[g_L.count_slot] += chk;
+            g_L.S.checked += chk;
+            g_L.S.valid += val;
+            g_L.flag = 0;
+            g_L.rw_next = ev;
+            if (ev < 64) {
+              const int fe = g_L.eg_first[ev];
+              const double sol0 = g_L.eg_cost[ev][0] + g_L.xn.c[0];
+              if (fe > g_L.S.n_pts) {
+                g_L.csp[0] = sol0;
+                g_L.csp[1] = g_L.eg_cost[ev][1] + g_L.xn.c[1];
+                g_L.csp[2] = g_L.eg_cost[ev][2] + g_L.xn.c[2];
+                g_L.flag = 1;
+              } else {
+                const int lv = fe - 1;
+                for (int j = 0; j < NJ; ++j) g_L.ext[j] = g_L.eg_start[ev][j] + lv * g_L.eg_step[ev][j];
                 g_L.flag = 2;
                 g_L.sol[0] = sol0;
               }
-            }
-            if (g_L.flag) {
               g_L.n_via = 0;
               g_L.nn_t = g_L.S.n[t];
-              load_node(C, t, g_L.eg_near[e], &g_L.cur);
+              load_node(C, t, g_L.eg_near[ev], &g_L.cur);
             }
           }
         }
         __syncthreads();
         const int flag_e = uni(g_L.flag);
+        if (flag_e == 0) break;
         if (flag_e == 1) {
           via_chain(C, g_L.xn.q);
           if (threadIdx.x == 0) g_L.tree_expand = 0;
           __syncthreads();
           break;
-        } else if (flag_e == 2) {
-          via_chain(C, g_L.ext);
-          if (threadIdx.x == 0) { g_L.tree_expand = 1; g_L.best_nv = g_L.sol[0]; }
-          __syncthreads();
         }
+        e0 = uni(g_L.rw_next) + 1;
+        via_chain(C, g_L.ext);
+        if (threadIdx.x == 0) { g_L.tree_expand = 1; g_L.best_nv = g_L.sol[0]; }
+        __syncthreads();
       }
+      DETAIL_END(_dn, 30);
     }
   }
   insert_via(C, t);

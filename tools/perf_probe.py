@@ -32,7 +32,10 @@ for iters in [int(v) for v in (sys.argv[1:] or ["2000", "10000", "50000"])]:
         rounds = max(raw[30], 1)
         print("   sample_ellipse: %d rounds, stage 1 %.2f us, stage 2 %.2f us per round" % (
             rounds, raw[28] / 1e2 / rounds, raw[29] / 1e2 / rounds), flush=True)
-    if raw[31] > 0:  # SMP_NEAR_PROF build: wave-0 clocks of near_set
+    if os.environ.get("SMP_DETAIL_PROF"):  # SMP_DETAIL_PROF build: serial-section clocks (ticks, slots 28-31)
+        print("   serial sections (us/iter): rewire commit %.2f (cost_update %.2f), connect replay %.2f, insert_via %.2f"
+              % tuple(raw[k] / 1e2 / iters for k in (28, 29, 30, 31)), flush=True)
+    if raw[31] > 0 and not os.environ.get("SMP_DETAIL_PROF"):  # SMP_NEAR_PROF build: wave-0 clocks of near_set
         nc = raw[31] * 1e8
         print("   near_set (%d calls, wave 0): scan %.1f us (insert %.1f us), merge %.1f us per call" % (
             nc, raw[28] * 1e6 / nc, raw[29] * 1e6 / nc, raw[30] * 1e6 / nc), flush=True)
