@@ -106,6 +106,7 @@ typedef struct smp_stats {
   int32_t conn_node_b, conn_node_a;
   int64_t nn_nodes_scanned;      /* nodes streamed by nearest-neighbour scans (64 B each) */
   int64_t near_nodes_scanned;    /* nodes streamed by near-vertex scans (72 B each) */
+  int64_t samples_precomputed;   /* iterations whose sample came from the run-ahead sampler workgroup */
   double phase_seconds[32];      /* device time per planner phase (sample, nn, expand, near, choose-parent,
                                     rewire, connect, collision tiles, #tiles, edge costs, via chains, #via,
                                     tile stages, tile time per calling phase, then counts of checked

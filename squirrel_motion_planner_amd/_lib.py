@@ -56,7 +56,7 @@ class Stats(ctypes.Structure):
                 ("edges_start", _i64), ("edges_goal", _i64), ("rewires_start", _i64), ("rewires_goal", _i64),
                 ("connected_tree_is_start", ctypes.c_int32), ("conn_node_b", ctypes.c_int32),
                 ("conn_node_a", ctypes.c_int32), ("nn_nodes_scanned", _i64), ("near_nodes_scanned", _i64),
-                ("phase_seconds", _d * 32)]
+                ("samples_precomputed", _i64), ("phase_seconds", _d * 32)]
 
 
 class Result(ctypes.Structure):

@@ -516,6 +516,7 @@ static QueryDev make_qdev(QueryBuffers& b, size_t cap, long long rows) {
   d.path_nodes = b.path_nodes.p;
   d.jb = nullptr;
   d.nworkers = 1;
+  d.sampler = 0;
   d.trace = nullptr;
   return d;
 }
@@ -590,7 +591,8 @@ extern "C" int smp_plan_batch(smp_planner* p, const smp_query* qs, int nq, smp_r
   if (nh < 0) nh = 0;
   for (int i = 0; i < nq; ++i) {
     qdev[i].jb = nh > 0 ? p->qb[i].jb.p : nullptr;
-    qdev[i].nworkers = 1 + nh;
+    qdev[i].sampler = nh >= 2;              // with two or more helpers, the last one runs ahead sampling
+    qdev[i].nworkers = nh >= 2 ? nh : 1 + nh;
   }
   static int* trace_host = nullptr;
   const bool debug = std::getenv("SMP_DEBUG") != nullptr;
@@ -724,6 +726,7 @@ extern "C" int smp_plan_batch(smp_planner* p, const smp_query* qs, int nq, smp_r
     st.conn_node_b = s.nB.id; st.conn_node_a = s.nA.id;
     st.nn_nodes_scanned = s.nn_nodes;
     st.near_nodes_scanned = s.near_nodes;
+    st.samples_precomputed = s.smp_hits;
     for (int k = 0; k < 32; ++k)
       st.phase_seconds[k] = (k == 8 || k == 11 || k >= 20) ? (double)s.prof[k] : (double)s.prof[k] / p->wall_rate_hz;
     if (i == 0) { p->last_n[0] = s.n[0]; p->last_n[1] = s.n[1]; }

@@ -115,6 +115,12 @@ struct JobLds {
   int E, np1, nslots, ntiles, self, map, seq, tile, steal, hidx;
   int go[2];  // poll-loop decisions, double-buffered by iteration parity (a slow wave may still read the last one)
 };
+// Sampling scratch (sample_ellipse: first valid inner getRandomConf draw of each outer attempt).
+struct SmpLds {
+  double q[64][NJ];
+  int ok[64];
+  int win;
+};
 constexpr int NEAR_BINS = 256;   // near_set register path: cost histogram bins
 constexpr int NEAR_BUF = 128;    // near_set register path: candidate buffer entries per end
 constexpr int NEAR_NBK = 16;     // near_set register path: 64-node batches per wave held in registers
@@ -136,11 +142,7 @@ struct PlanLds {
       int wli[BLOCK / 64][MAX_NEAR], whi[BLOCK / 64][MAX_NEAR];
       int wtot[BLOCK / 64];
     } nr;
-    struct {  // sample_ellipse: first valid inner getRandomConf draw of 64 outer attempts
-      double q[64][NJ];
-      int ok[64];
-      int win;
-    } smp;
+    SmpLds smp;
     struct {  // near_set, register path: cost histogram and the two candidate buffers
       unsigned hist[NEAR_BINS];
       unsigned long long ck[2][NEAR_BUF];
@@ -159,6 +161,8 @@ struct PlanLds {
   int tile_e[PLAN_CT], tile_i[PLAN_CT], tile_n;
   int count_slot;  // profiling: phase the checked configurations are attributed to
   int job_seq;     // last job published by this leader (this launch)
+  int smp_ver, smp_have_sol, smp_hit;  // run-ahead sampler: published parameter version / snapshot, slot hit
+  double smp_cbest[3];
   // near lists (ascending (cost,id) for the first max_near; last max_near in ascending order)
   int nk;
   unsigned long long near_blo, near_bhi;  // near_set: block-wide bounds on the K-th smallest / largest key
@@ -1245,14 +1249,14 @@ __device__ void insert_via(const Ctx& C, int t) {
 }
 
 // --------------------------------------------------------------------------------------- sampling
-// getRandomConf (control_laws.cpp:1120-1188): draws in chain order until the EE z >= 0.  One lane per
-// inner attempt; the first valid attempt (lowest index) wins.  Used for outer attempt `outer`.
-__device__ void rand_conf_lane(const Ctx& C, const QState& S, uint32_t outer, uint32_t inner, double* q) {
+// getRandomConf (control_laws.cpp:1120-1188) draw `inner` of outer attempt `outer` in iteration `it`; the
+// caller keeps the first draw with EE z >= 0.
+__device__ __forceinline__ void rand_conf_lane(const QState& S, uint32_t it, uint32_t outer, uint32_t inner, double* q) {
   const RobotDev* rb = (&g_rb);
   bool env0 = S.env_x[0] == 0.0 && S.env_x[1] == 0.0 && S.env_y[0] == 0.0 && S.env_y[1] == 0.0;
   double u[NJ];
 #pragma unroll
-  for (int p = 0; p < NJ / 2; ++p) u01_pair(S.seed, S.query, (uint32_t)S.iter, outer, inner, p, &u[2 * p], &u[2 * p + 1]);
+  for (int p = 0; p < NJ / 2; ++p) u01_pair(S.seed, S.query, it, outer, inner, p, &u[2 * p], &u[2 * p + 1]);
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     double lo = rb->q_min[j], hi = rb->q_max[j];
@@ -1262,77 +1266,69 @@ __device__ void rand_conf_lane(const Ctx& C, const QState& S, uint32_t outer, ui
   }
 }
 
-// sampleJointConfig_JntArray (birrt_star.cpp:3832-3878) -> g_L.xr; wave 0 tries 64 attempts at once.
-__device__ void sample_uniform(const Ctx& C) {
+// sampleJointConfig_JntArray (birrt_star.cpp:3832-3878) of iteration `it` -> out[NJ] (LDS); wave 0 tries 64
+// attempts at once.  All threads; returns 0, or -1 if no valid sample was found.
+__device__ __forceinline__ int sample_uniform(const QState& S, uint32_t it, SmpLds& W, double* out) {
   if (wave_id() == 0) {
-    for (uint32_t base = 0;; base += 64) {
-      if (base >= (1u << 24)) {  // no valid sample in 16M attempts: give up loudly
-        if (lane_id() == 0) { g_L.S.status = -1; g_L.S.phase = 2; }
-        break;
-      }
+    int st = -1;
+    for (uint32_t base = 0; base < (1u << 24); base += 64) {  // no valid sample in 16M attempts: give up loudly
       double q[NJ];
-      rand_conf_lane(C, g_L.S, 0, base + lane_id(), q);
+      rand_conf_lane(S, it, 0, base + lane_id(), q);
       bool ok = 0.0 <= ee_z((&g_rb), q);
       unsigned long long m = __ballot(ok);
       if (m) {
         int w = __ffsll((long long)m) - 1;
-        if (lane_id() == w) for (int j = 0; j < NJ; ++j) g_L.xr[j] = q[j];
+        if (lane_id() == w) for (int j = 0; j < NJ; ++j) out[j] = q[j];
+        st = 0;
         break;
       }
     }
+    if (lane_id() == 0) W.win = st;
   }
   __syncthreads();
+  return uni(W.win);
 }
 
-// sampleJointConfigfromEllipse_JntArray (birrt_star.cpp:3607-3829): outer attempt b draws getRandomConf inner
-// attempts 0, 1, ... until one has EE z >= 0, maps it into the informed ellipse, and the lowest outer attempt
-// whose mapped sample is above ground and inside the environment wins.  SE_OUT outer attempts per round:
+// sampleJointConfigfromEllipse_JntArray (birrt_star.cpp:3607-3829) of iteration `it` -> out[NJ] (LDS): outer
+// attempt b draws getRandomConf inner attempts 0, 1, ... until one has EE z >= 0, maps it into the informed
+// ellipse, and the lowest outer attempt whose mapped sample is above ground and inside the environment wins.
+// SE_OUT outer attempts per round:
 //   1. waves 0-3 (one per SIMD: the FK chain is fp64-latency bound, more waves would only queue behind each
 //      other): lane (b, i) evaluates inner attempt i < 8 of outer attempt b; the first valid i of each b goes to
 //      LDS;
 //   2. wave 0, lane b < SE_OUT: an outer attempt without a valid inner attempt in 0..7 continues serially from 8
 //      (p ~ 2^-8 each); ellipse map + EE z + environment test; the lowest valid b wins.
-__device__ void sample_ellipse(const Ctx& C) {
+// All threads; returns 0, or -1 if no valid sample was found.
+__device__ __forceinline__ int sample_ellipse(const QState& S, uint32_t it, SmpLds& W, double* out) {
   const RobotDev* rb = (&g_rb);
-  const QState& S = g_L.S;
   const bool env0 = S.env_x[0] == 0.0 && S.env_x[1] == 0.0 && S.env_y[0] == 0.0 && S.env_y[1] == 0.0;
   const int lane = lane_id();
   constexpr int SE_OUT = 32;
-#ifdef SMP_SAMPLE_PROF
-  unsigned long long _ts = wall_clock64();
-#endif
   for (uint32_t base = 0;; base += SE_OUT) {
-    if (base >= (1u << 20)) {
-      if (threadIdx.x == 0) { g_L.S.status = -1; g_L.S.phase = 2; }
-      __syncthreads();
-      return;
-    }
+    if (base >= (1u << 20)) return -1;
     if (threadIdx.x < SE_OUT * 8) {
       const uint32_t b = base + (threadIdx.x >> 3), inner = threadIdx.x & 7;
       double q[NJ];
-      rand_conf_lane(C, S, 1 + b, inner, q);
+      rand_conf_lane(S, it, 1 + b, inner, q);
       const bool ok = 0.0 <= ee_z(rb, q);
       const unsigned long long m = __ballot(ok);
       const unsigned grp = (unsigned)(m >> (lane & ~7)) & 0xffu;  // the 8 lanes of outer attempt b
       const int first = grp ? __builtin_ctz(grp) : 8;
       if ((int)inner == first)
-        for (int j = 0; j < NJ; ++j) g_L.u.smp.q[threadIdx.x >> 3][j] = q[j];
-      if (inner == 0) g_L.u.smp.ok[threadIdx.x >> 3] = grp != 0;
+        for (int j = 0; j < NJ; ++j) W.q[threadIdx.x >> 3][j] = q[j];
+      if (inner == 0) W.ok[threadIdx.x >> 3] = grp != 0;
     }
     __syncthreads();
-#ifdef SMP_SAMPLE_PROF
-    if (threadIdx.x == 0) { const unsigned long long t = wall_clock64(); g_L.S.prof[28] += t - _ts; _ts = t; g_L.S.prof[30]++; }
-#endif
     if (wave_id() == 0) {
       const uint32_t b = base + lane;
       double q[NJ];
       if (lane >= SE_OUT) {
         for (int j = 0; j < NJ; ++j) q[j] = 1.0;  // idle lanes: excluded from the ballot below
-      } else if (g_L.u.smp.ok[lane]) {
-        for (int j = 0; j < NJ; ++j) q[j] = g_L.u.smp.q[lane][j];
+      } else if (W.ok[lane]) {
+        for (int j = 0; j < NJ; ++j) q[j] = W.q[lane][j];
       } else {
         for (uint32_t inner = 8; inner < (1u << 16); ++inner) {
-          rand_conf_lane(C, S, 1 + b, inner, q);
+          rand_conf_lane(S, it, 1 + b, inner, q);
           if (0.0 <= ee_z(rb, q)) break;
         }
       }
@@ -1342,7 +1338,7 @@ __device__ void sample_ellipse(const Ctx& C) {
       for (int i = 0; i < 6; ++i) sr += br[i] * br[i];
       for (int i = 0; i < 2; ++i) sp += bp[i] * bp[i];
       double nr = sqrt(sr), npn = sqrt(sp);
-      double ps = u01(S.seed, S.query, (uint32_t)S.iter, 1 + b, 0, 8);
+      double ps = u01(S.seed, S.query, it, 1 + b, 0, 8);
       for (int i = 0; i < 6; ++i) br[i] = ps * (br[i] / nr);
       for (int i = 0; i < 2; ++i) bp[i] = ps * (bp[i] / npn);
       double srev = sqrt(S.cbest[1] * S.cbest[1] - S.h0[1] * S.h0[1]) / 2.0;
@@ -1368,15 +1364,55 @@ __device__ void sample_ellipse(const Ctx& C) {
       bool inside = (r[0] < S.env_x[1] && r[0] > S.env_x[0] && r[1] < S.env_y[1] && r[1] > S.env_y[0]) || env0;
       unsigned long long m = __ballot(above && inside && lane < SE_OUT);
       const int w = m ? __ffsll((long long)m) - 1 : -1;
-      if (lane == w) for (int j = 0; j < NJ; ++j) g_L.xr[j] = r[j];
-      if (lane == 0) g_L.u.smp.win = w;
+      if (lane == w) for (int j = 0; j < NJ; ++j) out[j] = r[j];
+      if (lane == 0) W.win = w;
     }
     __syncthreads();
-#ifdef SMP_SAMPLE_PROF
-    if (threadIdx.x == 0) { const unsigned long long t = wall_clock64(); g_L.S.prof[29] += t - _ts; _ts = t; }
-#endif
-    if (uni(g_L.u.smp.win) >= 0) break;
+    if (uni(W.win) >= 0) return 0;
   }
+}
+
+// The sample of iteration `it` for the planner state S (uniform, or informed once a solution exists).
+__device__ __forceinline__ int sample_conf(const QState& S, uint32_t it, SmpLds& W, double* out) {
+  if (uni(S.informed && S.have_sol)) return sample_ellipse(S, it, W, out);
+  return sample_uniform(S, it, W, out);
+}
+
+// Leader: the sample of this iteration -> g_L.xr.  With a run-ahead sampler, first publish the iteration and,
+// when they changed, the informed-sampling parameters (versioned); then take the ring slot if its tag is this
+// iteration at the current version, else draw the sample here.
+__device__ void sample_iteration(const Ctx& C) {
+  QState& S = g_L.S;
+  const uint32_t it = (uint32_t)S.iter;
+  if (C.Q.sampler) {
+    JobBoard* jb = C.Q.jb;
+    if (threadIdx.x == 0) {
+      const bool changed = g_L.smp_ver == 0 || g_L.smp_have_sol != S.have_sol || g_L.smp_cbest[0] != S.cbest[0] ||
+                           g_L.smp_cbest[1] != S.cbest[1] || g_L.smp_cbest[2] != S.cbest[2];
+      if (changed) {
+        g_L.smp_have_sol = S.have_sol;
+        st_agent(&jb->s_have_sol, S.have_sol);
+        for (int k = 0; k < 3; ++k) {
+          g_L.smp_cbest[k] = S.cbest[k];
+          st_agent(&jb->s_cbest[k], (unsigned long long)__double_as_longlong(S.cbest[k]));
+        }
+        drain();
+        st_agent(&jb->s_ver, ++g_L.smp_ver);
+      }
+      st_agent(reinterpret_cast<unsigned long long*>(&jb->s_iter), (unsigned long long)S.iter);
+      const unsigned long long want = ((unsigned long long)it << 32) | (unsigned)g_L.smp_ver;
+      g_L.smp_hit = ld_agent(&jb->ring[it % SMP_RING].tag) == want;
+    }
+    __syncthreads();
+    if (uni(g_L.smp_hit)) {
+      if (threadIdx.x < NJ) g_L.xr[threadIdx.x] = __longlong_as_double((long long)ld_agent(&jb->ring[it % SMP_RING].q[threadIdx.x]));
+      if (threadIdx.x == 0) S.smp_hits++;
+      __syncthreads();
+      return;
+    }
+  }
+  if (sample_conf(S, it, g_L.u.smp, g_L.xr) < 0 && threadIdx.x == 0) { S.status = -1; S.phase = 2; }
+  __syncthreads();
 }
 
 // --------------------------------------------------------------------------------------- tree updates
@@ -1750,7 +1786,7 @@ __device__ void iteration(const Ctx& C) {
   const int A = uni(g_L.S.A), B = 1 - A;
   unsigned long long _t0 = threadIdx.x == 0 ? wall_clock64() : 0, _t1;
 #define PHASE(k) if (threadIdx.x == 0) { _t1 = wall_clock64(); g_L.S.prof[k] += _t1 - _t0; _t0 = _t1; }
-  if (uni(g_L.S.informed && g_L.S.have_sol)) sample_ellipse(C); else sample_uniform(C);
+  sample_iteration(C);
   PHASE(P_SAMPLE);
   int nid = nearest(C, A, g_L.xr);
   PHASE(P_NN);
@@ -1846,6 +1882,7 @@ __global__ void __launch_bounds__(BLOCK) plan_kernel(const RobotDev* __restrict_
     g_L.n_via = 0;
     g_L.near_blo = ~0ull;
     g_L.near_bhi = 0;
+    g_L.smp_ver = 0;
   }
   __syncthreads();
   if (uni(g_L.S.status == 0 && g_L.S.phase == 0)) {
@@ -1876,14 +1913,83 @@ __global__ void __launch_bounds__(BLOCK) plan_kernel(const RobotDev* __restrict_
 // Helper blocks (gridDim = nq * helpers): block b serves query b % nq -- waits for its leader's collision jobs
 // and takes tiles of them until the leader signals stop.  A separate kernel on its own stream, so its
 // resources stay small and a leader never depends on it being resident.
+// LDS of the run-ahead sampler workgroup.
+struct SamplerLds {
+  QState S;        // the query's constants, with have_sol / cbest of the version being served
+  SmpLds W;
+  double out[NJ];
+  long long next;  // next iteration to sample
+  int ver, go[2];
+};
+
+// Run-ahead sampler (DESIGN.md "Sampler"): keeps the samples of the leader's next SMP_RING - 1 iterations in
+// the ring, computed with the latest published parameters and tagged (iteration, version); a parameter change
+// restarts the window.  Never writes the slot of an iteration the leader may be reading: it fills iterations
+// up to (published iteration) + SMP_RING - 1 only.  Leaves on the stop flag or after two idle seconds.
+__device__ void sampler_main(const Ctx& C, SamplerLds& L) {
+  JobBoard* jb = C.Q.jb;
+  {
+    const int* src = reinterpret_cast<const int*>(C.Q.st);
+    int* dst = reinterpret_cast<int*>(&L.S);
+    for (int i = threadIdx.x; i < (int)(sizeof(QState) / sizeof(int)); i += BLOCK) dst[i] = src[i];
+  }
+  if (threadIdx.x == 0) { L.ver = 0; L.next = 0; }
+  __syncthreads();
+  unsigned long long t_last = wall_clock64();
+  for (int k = 0;; k ^= 1) {
+    if (threadIdx.x == 0) {
+      int go = 0;
+      if (ld_agent(&jb->stop)) {
+        go = -1;
+      } else {
+        const int ver = ld_agent(&jb->s_ver);
+        const long long cur = (long long)ld_agent(reinterpret_cast<const unsigned long long*>(&jb->s_iter));
+        if (ver != L.ver) {
+          L.S.have_sol = ld_agent(&jb->s_have_sol);
+          for (int c = 0; c < 3; ++c) L.S.cbest[c] = __longlong_as_double((long long)ld_agent(&jb->s_cbest[c]));
+          if (ld_agent(&jb->s_ver) == ver) { L.ver = ver; L.next = cur + 1; }  // else re-read next poll
+        }
+        if (L.next < cur + 1) L.next = cur + 1;
+        if (L.ver > 0 && ver == L.ver && L.next <= cur + SMP_RING - 1) go = 1;
+        else if (wall_clock64() - t_last > 200000000ull) go = -1;  // 2 s idle
+      }
+      L.go[k] = go;
+    }
+    __syncthreads();
+    const int go = uni(L.go[k]);
+    if (go < 0) break;
+    if (go == 0) {
+      __builtin_amdgcn_s_sleep(2);
+      continue;
+    }
+    const long long it = L.next;
+    const int st = sample_conf(L.S, (uint32_t)it, L.W, L.out);
+    if (st == 0) {
+      if (threadIdx.x < NJ)
+        st_agent(&jb->ring[it % SMP_RING].q[threadIdx.x], (unsigned long long)__double_as_longlong(L.out[threadIdx.x]));
+      drain();
+      __syncthreads();
+      if (threadIdx.x == 0)
+        st_agent(&jb->ring[it % SMP_RING].tag, ((unsigned long long)(uint32_t)it << 32) | (unsigned)L.ver);
+    }
+    if (threadIdx.x == 0) L.next = it + 1;
+    t_last = wall_clock64();
+    __syncthreads();
+  }
+}
+
 __global__ void __launch_bounds__(BLOCK) helper_kernel(const RobotDev* __restrict__ rb, SceneDev sc,
                                                        const MapCfg* __restrict__ mc, QueryDev* qs, int nq) {
   __shared__ JobLds J;
+  __shared__ SamplerLds SL;
   stage_model(rb, mc, &g_rb, &g_mc);
   Ctx C;
   C.sc = sc;
   C.Q = qs[blockIdx.x % nq];
-  if (C.Q.jb) helper_main(C, (int)blockIdx.x / nq, J);
+  const int hidx = (int)blockIdx.x / nq, nh = (int)gridDim.x / nq;
+  if (!C.Q.jb) return;
+  if (C.Q.sampler && hidx == nh - 1) sampler_main(C, SL);
+  else helper_main(C, hidx, J);
 }
 
 __global__ void path_kernel(QueryDev* qs, int* counts) {

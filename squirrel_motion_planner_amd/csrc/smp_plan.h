@@ -39,6 +39,7 @@ struct QState {                // per query, persisted in global memory across l
   long long max_checked;       // > 0: stop once this many configurations were collision-checked
   long long checked, valid, first_iter, last_iter;
   long long nn_nodes, near_nodes;  // nodes streamed by nearest / near scans (algorithmic bytes)
+  long long smp_hits;              // samples taken from the run-ahead sampler
   unsigned long long prof[32];     // device-clock ticks per planner phase (SMP_PROF_* in smp_kernels.hip)
   unsigned long long t0, t_first, t_end, deadline;  // device wall clock (0 deadline = none)
   double cbest[3], h0[3];
@@ -71,6 +72,7 @@ struct ViaNode {               // via node pending insertion (selected_via_nodes
 constexpr int HELPER_CT = SMP_HELPER_CT;          // configurations per job tile
 constexpr int JOB_SLOTS = MAXE * (MAX_PTS + 1); // (edge, point) slots of one job
 constexpr int JOB_TILES = (JOB_SLOTS + HELPER_CT - 1) / HELPER_CT;
+constexpr int SMP_RING = 16;                     // run-ahead sampler: samples kept ahead of the leader
 struct JobBoard {
   int seq;                     // job number; the leader increments it to publish a job
   int stop;                    // 1 once the leader left the launch: helpers exit
@@ -84,6 +86,19 @@ struct JobBoard {
   int pad4[26];
   unsigned tflag[JOB_TILES];   // per tile: the last job that claimed it (atomicMax; see claim_tile)
   int pad5[32 - JOB_TILES % 32];
+  // run-ahead sampler (DESIGN.md "Sampler").  Leader -> sampler: its current iteration and the informed-
+  // sampling parameters, versioned (payload stores drained before the version store).
+  int s_ver, s_have_sol;
+  long long s_iter;
+  unsigned long long s_cbest[3];  // fp64 bit patterns
+  int pad6[22];
+  // sampler -> leader: the sample of iteration i in slot i % SMP_RING, tag = (i << 32) | version, stored after
+  // the drained configuration.
+  struct {
+    unsigned long long tag;
+    unsigned long long q[NJ];     // fp64 bit patterns
+    int pad[14];
+  } ring[SMP_RING];
   unsigned long long start[MAXE][NJ], step[MAXE][NJ];  // fp64 bit patterns
   int slot_e[JOB_SLOTS], slot_i[JOB_SLOTS];
 };
@@ -92,7 +107,8 @@ struct QueryDev {
   QState* st;
   JobBoard* jb;                // null: no helpers
   int* trace;                  // debug only (SMP_DEBUG): host-mapped progress markers of the leader
-  int nworkers;                // leader + helper workgroups of this query (tile w, w + nworkers, ... is worker w's)
+  int nworkers;                // leader + tile helper workgroups (tile w, w + nworkers, ... is worker w's)
+  int sampler;                 // 1: the last helper workgroup is the run-ahead sampler
   TreeDev tr[2];
   ViaNode* via;                // [via_cap]
   int* stack;                  // [cap] DFS stack of recursiveNodeCostUpdate

@@ -24,6 +24,8 @@ for iters in [int(v) for v in (sys.argv[1:] or ["2000", "10000", "50000"])]:
            r["nodes_start"], r["nodes_goal"], r["nn_nodes_scanned"], r["near_nodes_scanned"],
            r["first_solution_iter"], r["time_first_solution"], r["cost_best"][0]), flush=True)
     print("   phases:", {k: round(v, 3) for k, v in r["phases"].items()}, flush=True)
+    print("   samples precomputed by the run-ahead sampler: %d of %d" % (r["samples_precomputed"], r["iterations"]),
+          flush=True)
     raw = r["phase_raw"]
     nj = max(raw[15] * 1e8, 1)
     print("   jobs %d: publish %.1f us, own %.1f us, wait %.1f us per job" % (
