@@ -91,6 +91,10 @@ def main():
     scene = D.broadcast_scene(s0, device="cuda") if world > 1 else s0
 
     gp = GpuPlanner(device=local, path_optimality_threshold=-math.inf, helpers=a.helpers)
+    # helper workgroups per query as the library resolves them (0 = auto: the CUs left over by the queries, at most
+    # 63; with two or more, the last one is the run-ahead sampler)
+    ncu = torch.cuda.get_device_properties(local).multi_processor_count
+    helpers_eff = (min(63, max(0, ncu // a.queries_per_gpu - 1)) if a.helpers == 0 else max(a.helpers, 0))
     gp.set_scene(scene)
 
     def queries(step, samples):
@@ -173,7 +177,7 @@ def main():
             "config": {"workload": "C2: single start->goal query, 10x10x2 m octomap @5 cm, 20 boxes, budget %d "
                                    "collision-checked samples, path_optimality_threshold=-inf" % a.samples,
                        "queries_per_gpu": a.queries_per_gpu, "samples_per_query": a.samples,
-                       "robot": "robotino 8-DoF, 64-sphere model", "helpers_per_query": a.helpers,
+                       "robot": "robotino 8-DoF, 64-sphere model", "helpers_per_query": helpers_eff,
                        "parallelism": "one leader workgroup per query + helper workgroups sharing its collision "
                        "tiles; queries sharded over ranks, scene broadcast once"},
             "valid_configs_per_s": valid / elapsed,

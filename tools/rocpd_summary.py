@@ -2,7 +2,7 @@
 """Summarise rocprofv3 SQLite output (ROCm 7.x `*_results.db`) into the files committed under profiles/.
 
   python tools/rocpd_summary.py stats  <kernel-trace .db>  <out.txt>
-      per-kernel calls / total / average / share (the `--stats` kernel summary)
+      per-kernel calls / total / average (microseconds) / share (the `--stats` kernel summary)
   python tools/rocpd_summary.py pmc    <kernel substring> <out.json> <pmc .db> [<pmc .db> ...]
       FETCH_SIZE / WRITE_SIZE of one kernel, one counter per pass (the two do not fit one pass on gfx950,
       MI355X_MICROARCH.md "rocprofv3 PMC slots") -> HBM bytes per launch
@@ -19,10 +19,11 @@ import sys
 def stats(db, out):
     c = sqlite3.connect(db)
     rows = c.execute("select name, total_calls, total_duration, average, percentage from top_kernels").fetchall()
+    # the rocpd `top_kernels` view reports (end - start) / 1000, i.e. microseconds
     lines = ["# rocprofv3 --kernel-trace --stats summary (%s)" % db,
-             "# %-90s %8s %16s %14s %8s" % ("kernel", "calls", "total_ns", "avg_ns", "pct")]
+             "# %-90s %8s %16s %14s %8s" % ("kernel", "calls", "total_us", "avg_us", "pct")]
     for name, calls, tot, avg, pct in rows:
-        lines.append("%-92s %8d %16.0f %14.0f %8.3f" % (name[:92], calls, tot, avg, pct))
+        lines.append("%-92s %8d %16.1f %14.1f %8.3f" % (name[:92], calls, tot, avg, pct))
     open(out, "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
 
