@@ -644,10 +644,8 @@ extern "C" int smp_plan_batch(smp_planner* p, const smp_query* qs, int nq, smp_r
       while ((qe = hipStreamQuery(p->stream)) == hipErrorNotReady || qe != hipSuccess) {
         if (qe != hipErrorNotReady || std::chrono::duration<double>(std::chrono::steady_clock::now() - tw).count() > 10.0) {
           if (qe != hipErrorNotReady) std::fprintf(stderr, "[smp] launch %lld failed: %s\n", (long long)launches, hipGetErrorString(qe));
-          std::fprintf(stderr, "[smp] launch %lld did not finish in 10 s; trace:", (long long)launches);
+          std::fprintf(stderr, "[smp] launch %lld did not finish in 10 s; leader trace:", (long long)launches);
           for (int i = 0; i < 8; ++i) std::fprintf(stderr, " %d", trace_host[i]);
-          for (int h = 0; h < std::min(nh, 63); ++h)
-            std::fprintf(stderr, " | h%d %d %d %d", h, trace_host[8 + 3 * h], trace_host[9 + 3 * h], trace_host[10 + 3 * h]);
           std::fprintf(stderr, "\n");
           std::_Exit(3);
         }
@@ -660,24 +658,13 @@ extern "C" int smp_plan_batch(smp_planner* p, const smp_query* qs, int nq, smp_r
     float ms = 0;
     HIPCHK(hipEventElapsedTime(&ms, p->ev0, p->ev1));
     total_ms += ms;
-    if (debug) {
-      std::fprintf(stderr, "[smp] scene view: leader d2 %08x%08x nx %d bricks %08x |", trace_host[97], trace_host[96],
-                   trace_host[98], trace_host[99]);
-      for (int h = 0; h < std::min(nh, 30); ++h)
-        std::fprintf(stderr, " h%d d2 %08x%08x nx %d bricks %08x", h, trace_host[101 + 4 * h], trace_host[100 + 4 * h],
-                     trace_host[102 + 4 * h], trace_host[103 + 4 * h]);
-      for (int h = 0; h < std::min(nh, 16); ++h)
-        if (trace_host[200 + 2 * h]) std::fprintf(stderr, " CORRUPT h%d d2lo %08x", h, trace_host[201 + 2 * h]);
-      std::fprintf(stderr, "\n");
-    }
     if (std::getenv("SMP_DEBUG")) {
       JobBoard jbh;
       if (nh > 0) HIPCHK(hipMemcpy(&jbh, qdev[0].jb, sizeof(JobBoard), hipMemcpyDeviceToHost));
       std::fprintf(stderr, "[smp] launch %lld grid %d chunk %d: %.3f ms phase %d status %d iter %lld checked %lld"
-                   " board seq %d stop %d done %d ntiles %d flag0 %u jobs published %d joined %d\n", (long long)launches,
-                   nq * (1 + nh), chunk, ms, S[0].phase, S[0].status, S[0].iter, S[0].checked, nh ? jbh.seq : -1,
-                   nh ? jbh.stop : -1, nh ? jbh.done : -1, nh ? jbh.ntiles : -1, nh ? jbh.tflag[0] : 0u, jbh.pad0[0],
-                   jbh.pad0[1]);
+                   " board stop %d job %u tile0 %llx\n", (long long)launches, nq * (1 + nh), chunk, ms, S[0].phase,
+                   S[0].status, S[0].iter, S[0].checked, nh ? jbh.stop : -1, nh ? (unsigned)(jbh.pay[0] >> 32) : 0u,
+                   nh ? jbh.res[0] : 0ull);
     }
     bool all_done = true;
     for (int i = 0; i < nq; ++i) all_done &= (S[i].phase == 2 || S[i].status != 0);

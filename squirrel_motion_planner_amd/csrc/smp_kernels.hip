@@ -110,9 +110,14 @@ __global__ void sqrt_div_kernel(const double* a, const double* b, int n, double*
 struct JobLds {
   TileLds<HELPER_CT> T;
   double tq[HELPER_CT][NJ];
-  double start[MAXE][NJ], step[MAXE][NJ];
-  int slot_e[JOB_SLOTS], slot_i[JOB_SLOTS];
-  int E, np1, nslots, ntiles, self, map, seq, tile, steal, hidx;
+  double start[MAXE][NJ], step[MAXE][NJ];  // the job's edges (needed edges of the batch, compacted)
+  unsigned words[JOB_WORDS];               // helper: the payload words as received
+  unsigned rmask[JOB_TILES];               // leader: collision mask per tile
+  int rdone[JOB_TILES];                    // leader: tile result known
+  int emap[MAXE];                          // leader: job edge -> batch edge
+  int first[MAXE];                         // leader: first colliding point per job edge
+  int E, np1, nslots, ntiles, self, map, seq, steal, hidx, left;
+  unsigned long long tprof[4];             // SMP_JOB_PROF builds: this helper's tile stage clocks
   int go[2];  // poll-loop decisions, double-buffered by iteration parity (a slow wave may still read the last one)
 };
 // Sampling scratch (sample_ellipse: first valid inner getRandomConf draw of each outer attempt).
@@ -137,21 +142,22 @@ struct PlanLds {
     } tile;
     JobLds job;  // job mode: the leader's LDS copy of its published job + one job tile
     double seg[MAXE][MAX_PTS][3];
-    struct {  // near_set: per-wave sorted low / high ends of the near list
-      unsigned long long wlk[BLOCK / 64][MAX_NEAR], whk[BLOCK / 64][MAX_NEAR];
-      int wli[BLOCK / 64][MAX_NEAR], whi[BLOCK / 64][MAX_NEAR];
-      int wtot[BLOCK / 64];
-    } nr;
     SmpLds smp;
-    struct {  // near_set, register path: cost histogram and the two candidate buffers
-      unsigned hist[NEAR_BINS];
-      unsigned long long ck[2][NEAR_BUF];
-      int ci[2][NEAR_BUF];
-      unsigned long long wmin[BLOCK / 64], wmax[BLOCK / 64];
-      int wtot[BLOCK / 64];
-      int cnt[2], blo, bhi, fast;
-    } nh;
   } u;
+  // near_set scratch (outside the union: a near set may be computed while a collision job holds u.job)
+  struct {  // near_set: per-wave sorted low / high ends of the near list
+    unsigned long long wlk[BLOCK / 64][MAX_NEAR], whk[BLOCK / 64][MAX_NEAR];
+    int wli[BLOCK / 64][MAX_NEAR], whi[BLOCK / 64][MAX_NEAR];
+    int wtot[BLOCK / 64];
+  } nr;
+  struct {  // near_set, register path: cost histogram and the two candidate buffers
+    unsigned hist[NEAR_BINS];
+    unsigned long long ck[2][NEAR_BUF];
+    int ci[2][NEAR_BUF];
+    unsigned long long wmin[BLOCK / 64], wmax[BLOCK / 64];
+    int wtot[BLOCK / 64];
+    int cnt[2], blo, bhi, fast;
+  } nh;
   // edge batch
   double eg_start[MAXE][NJ], eg_target[MAXE][NJ], eg_step[MAXE][NJ], eg_end[MAXE][NJ];
   double eg_base[MAXE][3], eg_cost[MAXE][3];
@@ -162,6 +168,8 @@ struct PlanLds {
   int count_slot;  // profiling: phase the checked configurations are attributed to
   int job_seq;     // last job published by this leader (this launch)
   int smp_ver, smp_have_sol, smp_hit;  // run-ahead sampler: published parameter version / snapshot, slot hit
+  int spec, spec_nn;                   // overlap_work: what was computed during the last collision job, its result
+  long long spec_cnt;                  // ... and the nodes it scanned (counted only if the result is used)
   double smp_cbest[3];
   // near lists (ascending (cost,id) for the first max_near; last max_near in ascending order)
   int nk;
@@ -462,13 +470,13 @@ __device__ __noinline__ void near_set_stream(const Ctx& C, int t, const double* 
     }
   }
   if (lane < K) {
-    g_L.u.nr.wlk[wave][lane] = lk; g_L.u.nr.wli[wave][lane] = li;
-    g_L.u.nr.whk[wave][lane] = hk; g_L.u.nr.whi[wave][lane] = hi;
+    g_L.nr.wlk[wave][lane] = lk; g_L.nr.wli[wave][lane] = li;
+    g_L.nr.whk[wave][lane] = hk; g_L.nr.whi[wave][lane] = hi;
   }
-  if (lane == 0) g_L.u.nr.wtot[wave] = wc;
+  if (lane == 0) g_L.nr.wtot[wave] = wc;
   __syncthreads();
   int tot = 0;
-  for (int w = 0; w < NW; ++w) tot += g_L.u.nr.wtot[w];
+  for (int w = 0; w < NW; ++w) tot += g_L.nr.wtot[w];
   const int take = min(K, tot);
   // threads [0, NW*K): low entries; [256, 256 + NW*K): high entries
   static_assert(NW * K <= 256, "rank merge thread map");
@@ -476,8 +484,8 @@ __device__ __noinline__ void near_set_stream(const Ctx& C, int t, const double* 
   const int e = threadIdx.x - hsel * 256;
   if (e < NW * K) {
     const int w = e / K, k = e - w * K;
-    const unsigned long long ck = hsel ? g_L.u.nr.whk[w][k] : g_L.u.nr.wlk[w][k];
-    const int ci = hsel ? g_L.u.nr.whi[w][k] : g_L.u.nr.wli[w][k];
+    const unsigned long long ck = hsel ? g_L.nr.whk[w][k] : g_L.nr.wlk[w][k];
+    const int ci = hsel ? g_L.nr.whi[w][k] : g_L.nr.wli[w][k];
     if (ci != (hsel ? -1 : 0x7fffffff)) {
       // per list o: number of entries ahead of (ck, ci) in that list's order (ascending low, descending high)
       int lo[NW];
@@ -491,8 +499,8 @@ __device__ __noinline__ void near_set_stream(const Ctx& C, int t, const double* 
         for (int o = 0; o < NW; ++o) {
           const int m = lo[o] + step - 1;
           if (m < K) {
-            const unsigned long long ok = hsel ? g_L.u.nr.whk[o][m] : g_L.u.nr.wlk[o][m];
-            const int oi = hsel ? g_L.u.nr.whi[o][m] : g_L.u.nr.wli[o][m];
+            const unsigned long long ok = hsel ? g_L.nr.whk[o][m] : g_L.nr.wlk[o][m];
+            const int oi = hsel ? g_L.nr.whi[o][m] : g_L.nr.wli[o][m];
             const bool ahead = hsel ? ki_less(ck, ci, ok, oi) : ki_less(ok, oi, ck, ci);
             if (ahead) lo[o] += step;
           }
@@ -610,17 +618,17 @@ __device__ void near_set(const Ctx& C, int t, const double* q, int excl) {
       kmin = min(kmin, (unsigned long long)__shfl_xor(kmin, off));
       kmax = max(kmax, (unsigned long long)__shfl_xor(kmax, off));
     }
-    if (lane == 0) { g_L.u.nh.wmin[wave] = kmin; g_L.u.nh.wmax[wave] = kmax; g_L.u.nh.wtot[wave] = wc; }
-    if (threadIdx.x < NEAR_BINS) g_L.u.nh.hist[threadIdx.x] = 0;
+    if (lane == 0) { g_L.nh.wmin[wave] = kmin; g_L.nh.wmax[wave] = kmax; g_L.nh.wtot[wave] = wc; }
+    if (threadIdx.x < NEAR_BINS) g_L.nh.hist[threadIdx.x] = 0;
     __syncthreads();
     NEAR_CLOCK(1);
     int tot = 0;
     kmin = ~0ull; kmax = 0;
 #pragma unroll
     for (int w = 0; w < NW; ++w) {
-      tot += g_L.u.nh.wtot[w];
-      kmin = min(kmin, g_L.u.nh.wmin[w]);
-      kmax = max(kmax, g_L.u.nh.wmax[w]);
+      tot += g_L.nh.wtot[w];
+      kmin = min(kmin, g_L.nh.wmin[w]);
+      kmax = max(kmax, g_L.nh.wmax[w]);
     }
     tot = uni(tot);
     if (tot == 0) continue;  // nothing near in this chunk: lists unchanged
@@ -634,14 +642,14 @@ __device__ void near_set(const Ctx& C, int t, const double* q, int excl) {
       if (nmask >> b & 1) {
         const int bin = near_bin(key[b], cmin, scale);
         bins[b >> 2] |= (unsigned)bin << (8 * (b & 3));
-        atomicAdd(&g_L.u.nh.hist[bin], 1u);
+        atomicAdd(&g_L.nh.hist[bin], 1u);
       }
     __syncthreads();
     NEAR_CLOCK(2);
     if (wave == 0) {
       // lane l owns bins 4l .. 4l+3: inclusive cumulative counts
-      const unsigned h0 = g_L.u.nh.hist[4 * lane], h1 = g_L.u.nh.hist[4 * lane + 1];
-      const unsigned h2 = g_L.u.nh.hist[4 * lane + 2], h3 = g_L.u.nh.hist[4 * lane + 3];
+      const unsigned h0 = g_L.nh.hist[4 * lane], h1 = g_L.nh.hist[4 * lane + 1];
+      const unsigned h2 = g_L.nh.hist[4 * lane + 2], h3 = g_L.nh.hist[4 * lane + 3];
       int inc = h0 + h1 + h2 + h3;
       for (int off = 1; off < 64; off <<= 1) {
         const int o = __shfl_up(inc, off);
@@ -662,30 +670,30 @@ __device__ void near_set(const Ctx& C, int t, const double* q, int excl) {
       const int bhi = 4 * Lhi + fh;
       const int cnt_hi = tot - __shfl(fhi == 3 ? c2 : fhi == 2 ? c1 : fhi == 1 ? c0b : e0, Lhi);
       if (lane == 0) {
-        g_L.u.nh.blo = blo;
-        g_L.u.nh.bhi = bhi;
-        g_L.u.nh.fast = cnt_lo + prev_lo <= NEAR_BUF && cnt_hi + prev_hi <= NEAR_BUF;
-        g_L.u.nh.cnt[0] = prev_lo;  // the running lists take the first buffer slots
-        g_L.u.nh.cnt[1] = prev_hi;
+        g_L.nh.blo = blo;
+        g_L.nh.bhi = bhi;
+        g_L.nh.fast = cnt_lo + prev_lo <= NEAR_BUF && cnt_hi + prev_hi <= NEAR_BUF;
+        g_L.nh.cnt[0] = prev_lo;  // the running lists take the first buffer slots
+        g_L.nh.cnt[1] = prev_hi;
       }
     }
     if (threadIdx.x < prev_lo) {
-      g_L.u.nh.ck[0][threadIdx.x] = (unsigned long long)__double_as_longlong(g_L.lo_c[threadIdx.x]);
-      g_L.u.nh.ci[0][threadIdx.x] = g_L.lo_i[threadIdx.x];
+      g_L.nh.ck[0][threadIdx.x] = (unsigned long long)__double_as_longlong(g_L.lo_c[threadIdx.x]);
+      g_L.nh.ci[0][threadIdx.x] = g_L.lo_i[threadIdx.x];
     }
     if (threadIdx.x >= 64 && threadIdx.x < 64 + prev_hi) {
-      g_L.u.nh.ck[1][threadIdx.x - 64] = (unsigned long long)__double_as_longlong(g_L.hi_c[threadIdx.x - 64]);
-      g_L.u.nh.ci[1][threadIdx.x - 64] = g_L.hi_i[threadIdx.x - 64];
+      g_L.nh.ck[1][threadIdx.x - 64] = (unsigned long long)__double_as_longlong(g_L.hi_c[threadIdx.x - 64]);
+      g_L.nh.ci[1][threadIdx.x - 64] = g_L.hi_i[threadIdx.x - 64];
     }
     __syncthreads();
     NEAR_CLOCK(3);
-    if (!uni(g_L.u.nh.fast)) {
+    if (!uni(g_L.nh.fast)) {
       NEAR_COUNT(26);
       __syncthreads();
       near_set_stream<K>(C, t, q, excl);
       return;
     }
-    const int blo = g_L.u.nh.blo, bhi = g_L.u.nh.bhi;
+    const int blo = g_L.nh.blo, bhi = g_L.nh.bhi;
     // gather: count the wave's entries per list, one atomic per list, then write
     int nw_lo = 0, nw_hi = 0;
 #pragma unroll
@@ -698,8 +706,8 @@ __device__ void near_set(const Ctx& C, int t, const double* q, int excl) {
       }
     }
     int base_lo = 0, base_hi = 0;
-    if (lane == 0 && nw_lo) base_lo = atomicAdd(&g_L.u.nh.cnt[0], nw_lo);
-    if (lane == 1 && nw_hi) base_hi = atomicAdd(&g_L.u.nh.cnt[1], nw_hi);
+    if (lane == 0 && nw_lo) base_lo = atomicAdd(&g_L.nh.cnt[0], nw_lo);
+    if (lane == 1 && nw_hi) base_hi = atomicAdd(&g_L.nh.cnt[1], nw_hi);
     base_lo = __shfl(base_lo, 0);
     base_hi = __shfl(base_hi, 1);
     const unsigned long long below = (1ull << lane) - 1;
@@ -713,13 +721,13 @@ __device__ void near_set(const Ctx& C, int t, const double* q, int excl) {
         const unsigned long long ml = __ballot(pl), mh = __ballot(ph);
         if (pl) {
           const int slot = base_lo + __popcll(ml & below);
-          g_L.u.nh.ck[0][slot] = key[g];
-          g_L.u.nh.ci[0][slot] = i;
+          g_L.nh.ck[0][slot] = key[g];
+          g_L.nh.ci[0][slot] = i;
         }
         if (ph) {
           const int slot = base_hi + __popcll(mh & below);
-          g_L.u.nh.ck[1][slot] = key[g];
-          g_L.u.nh.ci[1][slot] = i;
+          g_L.nh.ck[1][slot] = key[g];
+          g_L.nh.ci[1][slot] = i;
         }
         base_lo += __popcll(ml);
         base_hi += __popcll(mh);
@@ -732,18 +740,18 @@ __device__ void near_set(const Ctx& C, int t, const double* q, int excl) {
       // rank: threads [0, 256) the low buffer, [256, 512) the high buffer; L lanes per entry
       const int e = threadIdx.x >= 256;
       const int idx = threadIdx.x & 255;
-      const int m = g_L.u.nh.cnt[e];
+      const int m = g_L.nh.cnt[e];
       const int L = m <= 64 ? 4 : 2;
       const int c = L == 4 ? idx >> 2 : idx >> 1, sl = idx & (L - 1);
       int rank = 0;
       unsigned long long ck = 0;
       int ci = 0;
       if (c < m) {
-        ck = g_L.u.nh.ck[e][c];
-        ci = g_L.u.nh.ci[e][c];
+        ck = g_L.nh.ck[e][c];
+        ci = g_L.nh.ci[e][c];
         for (int j = sl; j < m; j += L) {
-          const unsigned long long ok = g_L.u.nh.ck[e][j];
-          const int oi = g_L.u.nh.ci[e][j];
+          const unsigned long long ok = g_L.nh.ck[e][j];
+          const int oi = g_L.nh.ci[e][j];
           rank += e == 0 ? ki_less(ok, oi, ck, ci) : ki_less(ck, ci, ok, oi);
         }
       }
@@ -827,246 +835,294 @@ __device__ __forceinline__ unsigned ld_agent(const unsigned* p) {
 // Waits until this wave's vector-memory operations (stores, atomics) are performed.
 __device__ __forceinline__ void drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// Claims tile t of job `seq`.  Every tile has a flag holding the last job that claimed it (atomicMax), so the
-// claim succeeds iff no worker claimed t in this job.  Flags never decrease and a job is published only after
-// every tile of the previous one was claimed and finished, so a worker still holding an older job's number
-// can never claim a tile of a newer job.
-__device__ __forceinline__ bool claim_tile(JobBoard* jb, int t, int seq) {
-  return (int)__hip_atomic_fetch_max(&jb->tflag[t], (unsigned)seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < seq;
+// Granule = (job << 32) | 32-bit word (smp_plan.h JobBoard).
+__device__ __forceinline__ unsigned long long granule(int seq, unsigned w) {
+  return ((unsigned long long)(unsigned)seq << 32) | w;
 }
 
-// Marks tile t as claimed by job `seq` without waiting for the old value: for tiles no other worker can claim.
-__device__ __forceinline__ void mark_tile(JobBoard* jb, int t, int seq) {
-  __hip_atomic_fetch_max(&jb->tflag[t], (unsigned)seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// One job tile held in g_L.u.job / the helper's LDS: configuration = start + i * step of its (edge, point)
-// slot (the leader's arithmetic), collision tile, then -- only if thread 0's `mine` says the tile is this
-// workgroup's -- first collisions by agent-scope atomicMin into the board and `done` once they are performed.
-// The claim's round trip thus overlaps the tile's first stages.  All threads.
-__device__ __forceinline__ void job_tile(const Ctx& C, JobBoard* jb, JobLds& J, int t, bool mine) {
+// Configurations of job tile t -> J.tq: slot s = job edge s / np1, point s % np1, configuration start + i * step
+// (the leader's arithmetic).  Then the collision tile; returns the tile's collision mask in every thread.
+__device__ __forceinline__ unsigned job_tile_mask(const Ctx& C, JobLds& J, int t, unsigned long long* prof = nullptr) {
   const int base = t * HELPER_CT, nc = min(HELPER_CT, uni(J.nslots) - base);
   if (threadIdx.x < nc * NJ) {
-    int c = threadIdx.x / NJ, j = threadIdx.x - c * NJ;
-    int e = J.slot_e[base + c];
-    J.tq[c][j] = J.start[e][j] + J.slot_i[base + c] * J.step[e][j];
+    const int c = threadIdx.x / NJ, j = threadIdx.x - c * NJ;
+    const int sl = base + c, k = sl / J.np1, i = sl - k * J.np1;
+    J.tq[c][j] = J.start[k][j] + i * J.step[k][j];
   }
   __syncthreads();
-  collide_tile<HELPER_CT>((&g_rb), C.sc, (&g_mc), nc, J.tq, J.self, J.map, J.T);
-  if (threadIdx.x == 0) J.tile = mine;
+  collide_tile<HELPER_CT>((&g_rb), C.sc, (&g_mc), nc, J.tq, J.self, J.map, J.T, nullptr, prof);
+  unsigned m = 0;
+  for (int c = 0; c < nc; ++c) m |= (J.T.coll[c] ? 1u : 0u) << c;
   __syncthreads();
-  if (uni(J.tile)) {
-    if (threadIdx.x < nc && J.T.coll[threadIdx.x])
-      atomicMin(&jb->first[J.slot_e[base + threadIdx.x]], J.slot_i[base + threadIdx.x]);
-    drain();
-    __syncthreads();
-    if (threadIdx.x == 0) atomicAdd(&jb->done, 1);
-  }
+  return m;
 }
 
-// Worker w's share of the job: tiles w, w + W, w + 2W, ... (W = leader + helpers).  A helper claims each one
-// (one atomic, no contention between workers; only the stalled leader competes, see job_steal_one); the
-// leader's own tiles are never stolen, so it only marks them.  All threads.
-__device__ __forceinline__ void job_work(const Ctx& C, JobBoard* jb, JobLds& J, int w, int W) {
-  const int nt = uni(J.ntiles);
-  for (int t = w; t < nt; t += W) {
-    bool mine = true;
-    if (threadIdx.x == 0) {
-      if (w == 0) mark_tile(jb, t, J.seq);
-      else mine = claim_tile(jb, t, J.seq);
-    }
-    job_tile(C, jb, J, t, mine);
+// Work the leader does while a collision job's tiles are checked by the helpers (see edge_validity).
+enum { OV_NONE = 0, OV_NEAR_EXPAND = 1, OV_NN = 2, OV_NEAR_XN = 3 };
+__device__ void overlap_work(const Ctx& C, int ov, int t);
+// Takes the result of overlap_work `ov` if that is what the last job computed: counts its scanned nodes.
+__device__ __forceinline__ bool take_spec(int ov) {
+  const bool hit = uni(g_L.spec) == ov;
+  __syncthreads();
+  if (hit && threadIdx.x == 0) {
+    (ov == OV_NN ? g_L.S.nn_nodes : g_L.S.near_nodes) += g_L.spec_cnt;
+    g_L.spec = OV_NONE;
   }
   __syncthreads();
+  return hit;
 }
 
-// Leader, when the job stops progressing (a helper not resident or late): wave 0 reads the flags of the
-// helpers' tiles, thread 0 claims the first unclaimed one, which the block then checks.  Returns 0 if none
-// was left.
-__device__ __forceinline__ int job_steal_one(const Ctx& C, JobBoard* jb, JobLds& J, int W) {
-  const int nt = uni(J.ntiles);
-  if (threadIdx.x < 64) {
-    int cand = 1 << 30;
-    for (int t = threadIdx.x; t < nt; t += 64)
-      if (t % W != 0 && (int)ld_agent(&jb->tflag[t]) < J.seq) { cand = t; break; }
-    for (int off = 32; off > 0; off >>= 1) cand = min(cand, __shfl_xor(cand, off));
-    if (threadIdx.x == 0) J.steal = cand < nt ? cand : -1;
-  }
-  __syncthreads();
-  const int t = uni(J.steal);
-  if (t >= 0) {
-    bool mine = false;
-    if (threadIdx.x == 0) mine = claim_tile(jb, t, J.seq);
-    job_tile(C, jb, J, t, mine);
-  }
-  __syncthreads();
-  return t >= 0;
-}
-
-// Leader: publishes the needed edges as one job (every point of every needed edge), works on it with the
-// helpers, waits for all its tiles and reads the first collision of each edge into eg_first.
-__device__ __forceinline__ void edge_validity_job(const Ctx& C, int E, int pslot) {
+// Leader: publishes the needed edges of the batch as one job (every point of every needed edge); tile t belongs
+// to worker (t + 1) % W, so the helpers take the first W - 1 tiles and the leader only tiles W - 1, 2W - 1, ...
+// While they are checked, the leader does `ov` (overlap_work), then its own tiles, then collects the helpers'
+// tile results and reduces them to the first collision of each edge (eg_first).  A helper's tile that does not
+// arrive within 8 us of the last progress is checked by the leader itself (a duplicate result is identical, so
+// no claim is needed).
+__device__ __forceinline__ void edge_validity_job(const Ctx& C, int E, int pslot, int ov, int ovt) {
   JobBoard* jb = C.Q.jb;
   auto& J = g_L.u.job;
   const int np1 = g_L.S.n_pts + 1;
+  const int W = C.Q.nworkers;
   if (threadIdx.x < 64) {
     const int e = threadIdx.x;
-    const int cnt = (e < E && g_L.eg_need[e]) ? np1 : 0;
-    int inc = cnt;
-    for (int off = 1; off < 32; off <<= 1) {
-      int v = __shfl_up(inc, off);
-      if (e >= off) inc += v;
-    }
-    const int start = inc - cnt;
-    for (int i = 0; i < cnt; ++i) { J.slot_e[start + i] = e; J.slot_i[start + i] = i; }
-    const int total = __shfl(inc, 31);
+    const bool need = e < E && g_L.eg_need[e];
+    const unsigned long long m = __ballot(need);
+    const int k = __popcll(m & ((1ull << e) - 1));
+    if (need) J.emap[k] = e;
     if (e == 0) {
-      J.nslots = total;
-      J.ntiles = (total + HELPER_CT - 1) / HELPER_CT;
-      J.E = E; J.np1 = np1; J.self = g_L.S.self; J.map = g_L.S.map;
+      const int ne = __popcll(m);
+      J.E = ne;
+      J.np1 = np1;
+      J.nslots = ne * np1;
+      J.ntiles = (ne * np1 + HELPER_CT - 1) / HELPER_CT;
+      J.self = g_L.S.self; J.map = g_L.S.map;
       J.seq = ++g_L.job_seq;
     }
   }
   if (threadIdx.x < E) g_L.eg_first[threadIdx.x] = np1;
   __syncthreads();
-  if (threadIdx.x == 0) { TRACE(C, 0, 1); TRACE(C, 1, J.seq); TRACE(C, 2, J.nslots); TRACE(C, 3, J.ntiles); TRACE(C, 4, E); }
+  const int ne = uni(J.E), nt = uni(J.ntiles), seq = uni(J.seq);
+  if (ne == 0) {
+    overlap_work(C, ov, ovt);
+    return;
+  }
   const unsigned long long tj0 = threadIdx.x == 0 ? wall_clock64() : 0;
-  if (threadIdx.x == 0) J.hidx = -1;
-  if (uni(J.nslots) == 0) return;
-  for (int it = threadIdx.x; it < E * NJ; it += BLOCK) {
-    const int e = it / NJ, j = it - e * NJ;
-    J.start[e][j] = g_L.eg_start[e][j];
-    J.step[e][j] = g_L.eg_step[e][j];
-    st_agent(&jb->start[e][j], (unsigned long long)__double_as_longlong(g_L.eg_start[e][j]));
-    st_agent(&jb->step[e][j], (unsigned long long)__double_as_longlong(g_L.eg_step[e][j]));
+  for (int it = threadIdx.x; it < ne * NJ; it += BLOCK) {
+    const int k = it / NJ, j = it - k * NJ, e = J.emap[k];
+    J.start[k][j] = g_L.eg_start[e][j];
+    J.step[k][j] = g_L.eg_step[e][j];
   }
-  for (int it = threadIdx.x; it < J.nslots; it += BLOCK) {
-    st_agent(&jb->slot_e[it], J.slot_e[it]);
-    st_agent(&jb->slot_i[it], J.slot_i[it]);
-  }
-  if (threadIdx.x < E) st_agent(&jb->first[threadIdx.x], np1);
-  if (threadIdx.x == 0) {
-    st_agent(&jb->E, E); st_agent(&jb->np1, np1); st_agent(&jb->nslots, J.nslots); st_agent(&jb->ntiles, J.ntiles);
-    st_agent(&jb->self, J.self); st_agent(&jb->map, J.map);
-    st_agent(&jb->done, 0);
-  }
-  drain();
+  for (int t = threadIdx.x; t < nt; t += BLOCK) J.rdone[t] = 0;
+  if (threadIdx.x < ne) J.first[threadIdx.x] = np1;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    drain();
-    st_agent(&jb->seq, J.seq);
+  // payload granules (no flag and no drain: each granule carries the job number)
+  for (int i = threadIdx.x; i < 1 + 32 * ne; i += BLOCK) {
+    unsigned w;
+    if (i == 0) {
+      w = (unsigned)ne | (unsigned)np1 << 8 | (unsigned)(J.self != 0) << 16 | (unsigned)(J.map != 0) << 17;
+    } else {
+      const int m = i - 1, k = m >> 5, r = m & 31, j = (r & 15) >> 1;
+      const unsigned long long bits = (unsigned long long)__double_as_longlong(r < 16 ? J.start[k][j] : J.step[k][j]);
+      w = (r & 1) ? (unsigned)(bits >> 32) : (unsigned)bits;
+    }
+    st_agent(&jb->pay[i], granule(seq, w));
   }
+#ifdef SMP_JOB_PROF
+  if (threadIdx.x == 0) st_agent(&jb->dbg[0], wall_clock64());
+#endif
   PROF_BEGIN();
   if (threadIdx.x == 0) { g_L.S.prof[P_TFK] += _pt - tj0; g_L.S.prof[P_TTEST]++; }  // job publication
-  if (threadIdx.x == 0) atomicAdd(&jb->pad0[0], 1);  // diagnostics: jobs published
-  if (threadIdx.x == 0) TRACE(C, 0, 2);
-  job_work(C, jb, J, 0, C.Q.nworkers);  // the leader is worker 0; helpers take their tiles in parallel
-  if (threadIdx.x == 0) TRACE(C, 0, 3);
-  if (threadIdx.x == 0) atomicAdd(&jb->pad0[4], 1);  // diagnostics: leader finished its claims
+  overlap_work(C, ov, ovt);
+  // the leader's own tiles
+  for (int t = W - 1; t < nt; t += W) {
+    const unsigned m = job_tile_mask(C, J, t);
+    if (threadIdx.x == 0) { J.rmask[t] = m; J.rdone[t] = 1; }
+  }
+  __syncthreads();
   const unsigned long long tj1 = threadIdx.x == 0 ? wall_clock64() : 0;
   if (threadIdx.x == 0) g_L.S.prof[P_TCHAIN] += tj1 - _pt;  // the leader's own tiles
-  // wait for the other tiles (block-level loop; thread 0 polls).  Should the job stop progressing for 8 us
-  // (a helper not resident, or late), the leader takes unclaimed tiles itself.
-  const unsigned long long t_wait = wall_clock64();
-  unsigned long long t_prog = t_wait;
-  int last_d = -1;
+  // collect the helpers' results (wave 0 polls the result granules; block-level decision double-buffered)
+  unsigned long long t_prog = tj1, t_wait = tj1;
+  int last_left = 1 << 30;
   for (int k = 0;; k ^= 1) {
-    if (threadIdx.x == 0) {
-      const int d = ld_agent(&jb->done);
-      const unsigned long long now = wall_clock64();
-      if (d != last_d) { last_d = d; t_prog = now; }
-      int st = d >= J.ntiles ? 1 : (now - t_prog > 800ull ? 2 : 0);
-      if (st != 1 && now - t_wait > 200000000ull) {  // 2 s: a job never takes that long -- fail, never hang
-        g_L.S.status = -5;
-        g_L.S.phase = 2;
-        g_L.S.prof[28] = (unsigned long long)d;
-        g_L.S.prof[29] = (unsigned long long)J.ntiles;
-        g_L.S.prof[30] = (unsigned long long)ld_agent(&jb->tflag[0]);
-        g_L.S.prof[31] = (unsigned long long)J.seq;
-        st = 1;
+    if (threadIdx.x < 64) {
+      int left = 0;
+      for (int t = threadIdx.x; t < nt; t += 64) {
+        if (J.rdone[t]) continue;
+        const unsigned long long v = ld_agent(&jb->res[t]);
+        if ((int)(v >> 32) == seq) { J.rmask[t] = (unsigned)v; J.rdone[t] = 1; }
+        else ++left;
       }
-      J.go[k] = st;
+      for (int off = 32; off > 0; off >>= 1) left += __shfl_xor(left, off);
+      if (threadIdx.x == 0) {
+        const unsigned long long now = wall_clock64();
+        if (left != last_left) { last_left = left; t_prog = now; }
+        int st = left == 0 ? 1 : (now - t_prog > 800ull ? 2 : 0);
+        if (st != 1 && now - t_wait > 200000000ull) {  // 2 s: a job never takes that long -- fail, never hang
+          g_L.S.status = -5;
+          g_L.S.phase = 2;
+          g_L.S.prof[28] = (unsigned long long)left;
+          g_L.S.prof[29] = (unsigned long long)nt;
+          g_L.S.prof[31] = (unsigned long long)seq;
+          st = 1;
+        }
+        J.go[k] = st;
+      }
     }
     __syncthreads();
     const int go = uni(J.go[k]);
     if (go == 1) break;
     if (go == 2) {
-      job_steal_one(C, jb, J, C.Q.nworkers);
+      // check the first missing tile here
+      if (threadIdx.x < 64) {
+        int cand = 1 << 30;
+        for (int t = threadIdx.x; t < nt; t += 64)
+          if (!J.rdone[t]) { cand = t; break; }
+        for (int off = 32; off > 0; off >>= 1) cand = min(cand, __shfl_xor(cand, off));
+        if (threadIdx.x == 0) J.steal = cand < nt ? cand : -1;
+      }
+      __syncthreads();
+      const int t = uni(J.steal);
+      if (t >= 0) {
+        const unsigned m = job_tile_mask(C, J, t);
+        if (threadIdx.x == 0) { J.rmask[t] = m; J.rdone[t] = 1; }
+      }
       if (threadIdx.x == 0) t_prog = wall_clock64();
+      __syncthreads();
       continue;
     }
     __builtin_amdgcn_s_sleep(1);
   }
-  if (threadIdx.x == 0) TRACE(C, 0, 4);
   if (threadIdx.x == 0) g_L.S.prof[P_TCENTRE] += wall_clock64() - tj1;  // waiting for helpers' tiles
-  if (threadIdx.x < E) g_L.eg_first[threadIdx.x] = ld_agent(&jb->first[threadIdx.x]);
+  // first collision per job edge from the tile masks
+  for (int t = threadIdx.x; t < nt; t += BLOCK) {
+    unsigned m = J.rmask[t];
+    while (m) {
+      const int c = __builtin_ctz(m);
+      m &= m - 1;
+      const int sl = t * HELPER_CT + c, kk = sl / np1;
+      atomicMin(&J.first[kk], sl - kk * np1);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < ne) g_L.eg_first[J.emap[threadIdx.x]] = J.first[threadIdx.x];
   PROF_END(P_TILES);
   if (threadIdx.x == 0) {
     g_L.S.prof[pslot] += wall_clock64() - _pt;
-    g_L.S.prof[P_NTILES] += J.ntiles;
+    g_L.S.prof[P_NTILES] += nt;
     g_L.S.prof[pslot + 8] += J.nslots;
   }
   __syncthreads();
 }
 
-// Helper workgroup: waits for jobs of its query and works on them until the leader signals stop (or after
-// two idle seconds, should the leader never start).  Never holds a claimed tile while waiting.
+// Helper workgroup w (1 .. W-1): wave 0 polls the first 64 payload granules of its query's board; a new job is
+// taken once every granule it needs carries the header's job number (jobs of one or two edges arrive within the
+// poll itself; longer payloads take one more read).  Then tiles w - 1, w - 1 + W, ... of the job, each result
+// stored as one granule.  Leaves on the stop flag, or after two idle seconds should the leader never start.
 __device__ __forceinline__ void helper_main(const Ctx& C, int hidx, JobLds& J) {
   JobBoard* jb = C.Q.jb;
+  const int w = 1 + hidx, W = C.Q.nworkers;
   int last = 0;
-  J.hidx = hidx;
-  if (threadIdx.x == 0) TRACE(C, 8 + 3 * (hidx & 63), 1);
   unsigned long long t_last = wall_clock64();
   for (int k = 0;; k ^= 1) {
-    // block-level poll (thread 0 reads the board): 0 = nothing yet, > 0 = new job, -1 = leave
-    if (threadIdx.x == 0) {
+    // 0 = nothing new, > 0 = job number complete in J.words, -1 = leave, -2 = payload longer than the poll
+    if (threadIdx.x < 64) {
+      const unsigned long long v = ld_agent(&jb->pay[threadIdx.x]);
+      const unsigned tag = (unsigned)(v >> 32);
+      const unsigned tag0 = __builtin_amdgcn_readfirstlane(tag);
+      const unsigned hdr = __builtin_amdgcn_readfirstlane((unsigned)v);
       int go = 0;
-      const int s = ld_agent(&jb->seq);
-      if (s != last) go = s;
-      else if (ld_agent(&jb->stop) || wall_clock64() - t_last > 200000000ull) go = -1;  // 2 s idle
-      J.go[k] = go;
+      if (tag0 != 0 && (int)tag0 != last) {
+        const int nw = 1 + 32 * (int)(hdr & 255);
+        const bool mine = (int)threadIdx.x < nw;
+        if (!__ballot(mine && tag != tag0)) {
+          if (mine) J.words[threadIdx.x] = (unsigned)v;
+          go = nw <= 64 ? (int)tag0 : -2;
+        }
+      }
+      if (threadIdx.x == 0) {
+        if (go == 0 && (ld_agent(&jb->stop) || wall_clock64() - t_last > 200000000ull)) go = -1;  // 2 s idle
+        J.go[k] = go;
+        J.seq = (int)tag0;
+      }
     }
     __syncthreads();
     const int go = uni(J.go[k]);
-    if (go < 0) break;
+    if (go == -1) break;
     if (go == 0) {
       __builtin_amdgcn_s_sleep(2);
       continue;
     }
-    if (threadIdx.x == 0) TRACE(C, 9 + 3 * (hidx & 63), go);
-    last = go;
-    const int E = min(ld_agent(&jb->E), MAXE), nslots = min(ld_agent(&jb->nslots), JOB_SLOTS);
-    for (int it = threadIdx.x; it < E * NJ; it += BLOCK) {
-      const int e = it / NJ, j = it - e * NJ;
-      J.start[e][j] = __longlong_as_double((long long)ld_agent(&jb->start[e][j]));
-      J.step[e][j] = __longlong_as_double((long long)ld_agent(&jb->step[e][j]));
+    const int seq = uni(J.seq);
+    const unsigned hdr = J.words[0];
+    const int ne = min((int)(hdr & 255), MAXE), nw = 1 + 32 * ne;
+    if (go == -2) {
+      // the rest of a long payload (one read; granules not yet current abandon the job to the next poll, which
+      // sees it again since `last` is unchanged)
+      int bad = 0;
+      for (int i = 64 + threadIdx.x; i < nw; i += BLOCK) {
+        const unsigned long long v = ld_agent(&jb->pay[i]);
+        if ((int)(v >> 32) != seq) bad = 1;
+        J.words[i] = (unsigned)v;
+      }
+      if (threadIdx.x == 0) J.left = 0;
+      __syncthreads();
+      if (bad) J.left = 1;
+      __syncthreads();
+      if (uni(J.left)) continue;
     }
-    for (int it = threadIdx.x; it < nslots; it += BLOCK) {
-      J.slot_e[it] = min(max(ld_agent(&jb->slot_e[it]), 0), MAXE - 1);
-      J.slot_i[it] = ld_agent(&jb->slot_i[it]);
+    for (int it = threadIdx.x; it < ne * 2 * NJ; it += BLOCK) {
+      const int kk = it / (2 * NJ), r = it - kk * 2 * NJ;  // r < NJ: start[j], else step[j - NJ]
+      const int wi = 1 + 32 * kk + 2 * r;
+      const double d = __hiloint2double((int)J.words[wi + 1], (int)J.words[wi]);
+      if (r < NJ) J.start[kk][r] = d; else J.step[kk][r - NJ] = d;
     }
     if (threadIdx.x == 0) {
-      J.nslots = nslots;
-      J.np1 = ld_agent(&jb->np1);
-      J.self = ld_agent(&jb->self);
-      J.map = ld_agent(&jb->map);
-      J.seq = go;
+      J.E = ne;
+      J.np1 = (int)((hdr >> 8) & 255);
+      J.self = (hdr >> 16) & 1;
+      J.map = (hdr >> 17) & 1;
+      J.nslots = ne * J.np1;
+      J.ntiles = (J.nslots + HELPER_CT - 1) / HELPER_CT;
     }
     __syncthreads();
-    if (threadIdx.x == 0) atomicAdd(&jb->pad0[1], 1);  // diagnostics: jobs joined by helpers
-    if (threadIdx.x == 0) J.ntiles = (nslots + HELPER_CT - 1) / HELPER_CT;
-    __syncthreads();
-    job_work(C, jb, J, 1 + hidx, C.Q.nworkers);
+    last = seq;
+    const int nt = uni(J.ntiles);
+#ifdef SMP_JOB_PROF
+    if (threadIdx.x == 0 && w - 1 < nt) {
+      const unsigned long long tp = ld_agent(&jb->dbg[0]);
+      atomicAdd(&jb->dbg[1], wall_clock64() - tp);
+      atomicAdd(&jb->dbg[2], 1ull);
+    }
+#endif
+#ifdef SMP_JOB_PROF
+    if (threadIdx.x == 0) for (int i = 0; i < 4; ++i) J.tprof[i] = 0;
+    unsigned long long* tp = J.tprof;
+#else
+    unsigned long long* tp = nullptr;
+#endif
+    for (int t = w - 1; t < nt; t += W) {
+      const unsigned m = job_tile_mask(C, J, t, tp);
+      if (threadIdx.x == 0) st_agent(&jb->res[t], granule(seq, m));
+#ifdef SMP_JOB_PROF
+      if (threadIdx.x == 0) atomicAdd(&jb->dbg[3], wall_clock64() - ld_agent(&jb->dbg[0]));
+#endif
+    }
+#ifdef SMP_JOB_PROF
+    if (threadIdx.x == 0 && w - 1 < nt) for (int i = 0; i < 4; ++i) atomicAdd(&jb->dbg[4 + i], J.tprof[i]);
+#endif
     t_last = wall_clock64();
   }
-  if (threadIdx.x == 0) TRACE(C, 8 + 3 * (hidx & 63), 2);
 }
 
-__device__ void edge_validity(const Ctx& C, int E, bool stop_first_valid, int pslot) {
+// Validity of the batch's needed edges -> eg_first.  `ov` (OV_*, tree `ovt`): scan work whose inputs are final
+// before the check, done while a collision job runs (after the check without helpers); overlap_work records it
+// in g_L.spec for the caller.
+__device__ void edge_validity(const Ctx& C, int E, bool stop_first_valid, int pslot, int ov = 0, int ovt = 0) {
   const int np1 = g_L.S.n_pts + 1;
   if (threadIdx.x == 0) g_L.count_slot = pslot + 4;
   if (C.Q.jb) {
-    edge_validity_job(C, E, pslot);
+    edge_validity_job(C, E, pslot, ov, ovt);
     return;
   }
   if (threadIdx.x < E) { g_L.eg_first[threadIdx.x] = np1; g_L.eg_ptr[threadIdx.x] = 0; }
@@ -1114,6 +1170,37 @@ __device__ void edge_validity(const Ctx& C, int E, bool stop_first_valid, int ps
       g_L.S.prof[P_NTILES]++;
       g_L.S.prof[pslot + 8] += nc;
     }
+  }
+  __syncthreads();
+  overlap_work(C, ov, ovt);
+}
+
+// Scans whose inputs are final before a collision job, run while its tiles are checked (edge_validity):
+//   OV_NEAR_EXPAND  near set of the expand edge's end in tree t (x_new if the edge is valid);
+//   OV_NN           nearest node of tree t to x_new (connect's tree_B lookup, during the rewire job);
+//   OV_NEAR_XN      near set of x_new in tree t (connect's near loop, during its direct-edge job).
+// The nodes a scan streams are held back (spec_cnt) and counted by the caller only if it uses the result.
+__device__ void overlap_work(const Ctx& C, int ov, int t) {
+  ov = uni(ov);
+  t = uni(t);
+  if (ov == OV_NONE) {
+    if (threadIdx.x == 0) g_L.spec = OV_NONE;
+    __syncthreads();
+    return;
+  }
+  const long long c0 = ov == OV_NN ? g_L.S.nn_nodes : g_L.S.near_nodes;
+  __syncthreads();
+  if (ov == OV_NEAR_EXPAND) near_set<20>(C, t, g_L.eg_end[0], g_L.S.n[t]);
+  else if (ov == OV_NEAR_XN) near_set<20>(C, t, g_L.xn.q, g_L.xn.id);
+  else {
+    const int id = nearest(C, t, g_L.xn.q);
+    if (threadIdx.x == 0) g_L.spec_nn = id;
+  }
+  if (threadIdx.x == 0) {
+    long long& cnt = ov == OV_NN ? g_L.S.nn_nodes : g_L.S.near_nodes;
+    g_L.spec_cnt = cnt - c0;
+    cnt = c0;
+    g_L.spec = ov;
   }
   __syncthreads();
 }
@@ -1554,7 +1641,7 @@ __device__ void rewire(const Ctx& C, int t) {
   }
   for (int e = cnt + threadIdx.x; e < MAXE; e += BLOCK) g_L.eg_need[e] = 0;
   __syncthreads();
-  edge_validity(C, cnt, false, P_XREWIRE);
+  edge_validity(C, cnt, false, P_XREWIRE, OV_NN, 1 - t);
   DETAIL_BEGIN(_dr);
   // Sequential commits (birrt_star.cpp:5096-5228).  The candidates' parents and costs are gathered into LDS by
   // one thread each; thread 0 walks the candidates from the resume point and stops after a commit, which may
@@ -1637,8 +1724,10 @@ __device__ void connect_graphs(const Ctx& C, int t) {
     g_L.eg_need[0] = g_L.sol[0] < g_L.csp[0];
   }
   __syncthreads();
+  if (threadIdx.x == 0) g_L.spec = OV_NONE;
+  __syncthreads();
   if (uni(g_L.eg_need[0])) {
-    edge_validity(C, 1, false, P_XCONNECT);
+    edge_validity(C, 1, false, P_XCONNECT, g_L.S.have_sol ? OV_NEAR_XN : OV_NONE, t);
     if (threadIdx.x == 0) {
       int f = g_L.eg_first[0];
       count_edge(f);
@@ -1668,7 +1757,7 @@ __device__ void connect_graphs(const Ctx& C, int t) {
     __syncthreads();
   }
   if (uni(g_L.S.have_sol)) {
-    near_set<20>(C, t, g_L.xn.q, g_L.xn.id);
+    if (!take_spec(OV_NEAR_XN)) near_set<20>(C, t, g_L.xn.q, g_L.xn.id);
     if (threadIdx.x == 0) {
       int m = min(g_L.n_lo, g_L.S.max_near);
       g_L.cnt = m;
@@ -1800,8 +1889,9 @@ __device__ void iteration(const Ctx& C) {
     g_L.eg_need[0] = 1;
   }
   __syncthreads();
+  const bool opt = uni(g_L.S.tree_opt && g_L.S.have_sol);
   edge_costs(C, 1);
-  edge_validity(C, 1, false, P_XEXPAND);
+  edge_validity(C, 1, false, P_XEXPAND, opt ? OV_NEAR_EXPAND : OV_NONE, A);
   if (threadIdx.x == 0) {
     int f = g_L.eg_first[0];
     count_edge(f);
@@ -1818,13 +1908,12 @@ __device__ void iteration(const Ctx& C) {
       g_L.xn.parent = g_L.nn.id;
     }
     g_L.ext_bp = 0;
-    g_L.nk = 0;
   }
   __syncthreads();
   PHASE(P_EXPAND);
-  const bool opt = uni(g_L.S.tree_opt && g_L.S.have_sol);
   if (opt) {
-    near_set<20>(C, A, g_L.xn.q, g_L.xn.id);
+    // x_new is the expand edge's end exactly when the edge is valid: then its near set was computed during the job
+    if (!(uni(g_L.ext_nn) && take_spec(OV_NEAR_EXPAND))) near_set<20>(C, A, g_L.xn.q, g_L.xn.id);
     PHASE(P_NEAR);
     choose_parent(C, A);
     PHASE(P_CHOOSE);
@@ -1832,9 +1921,11 @@ __device__ void iteration(const Ctx& C) {
   if (uni(g_L.ext_nn || g_L.ext_bp)) {
     if (threadIdx.x == 0) insert_node(C, A, g_L.en_start, g_L.en_target, g_L.xn);
     __syncthreads();
+    if (threadIdx.x == 0) g_L.spec = OV_NONE;
+    __syncthreads();
     if (opt) rewire(C, A);
     PHASE(P_REWIRE);
-    int cid = nearest(C, B, g_L.xn.q);
+    const int cid = take_spec(OV_NN) ? uni(g_L.spec_nn) : nearest(C, B, g_L.xn.q);
     if (threadIdx.x == 0) load_node(C, B, cid, &g_L.xc);
     __syncthreads();
     PHASE(P_NN);
@@ -1871,10 +1962,6 @@ __global__ void __launch_bounds__(BLOCK) plan_kernel(const RobotDev* __restrict_
   C.sc = sc;
   C.Q = qs[blockIdx.x];
   if (threadIdx.x == 0) {
-    TRACE(C, 96, (int)(reinterpret_cast<unsigned long long>(C.sc.d2) & 0xffffffffu));
-    TRACE(C, 97, (int)(reinterpret_cast<unsigned long long>(C.sc.d2) >> 32));
-    TRACE(C, 98, C.sc.nx);
-    TRACE(C, 99, (int)(reinterpret_cast<unsigned long long>(C.sc.bricks) & 0xffffffffu));
     g_L.count_slot = 0;
     g_L.job_seq = 0;
     g_L.S = *C.Q.st;
@@ -1903,6 +1990,14 @@ __global__ void __launch_bounds__(BLOCK) plan_kernel(const RobotDev* __restrict_
   }
   if (threadIdx.x == 0) {
     if (g_L.S.phase == 2 && g_L.S.t_end == 0) g_L.S.t_end = wall_clock64();
+#ifdef SMP_JOB_PROF
+    if (C.Q.jb) {
+      g_L.S.prof[28] += ld_agent(&C.Q.jb->dbg[1]);
+      g_L.S.prof[29] += ld_agent(&C.Q.jb->dbg[2]);
+      g_L.S.prof[30] += ld_agent(&C.Q.jb->dbg[3]);
+      for (int i = 0; i < 4; ++i) g_L.S.prof[P_TFK + i] += ld_agent(&C.Q.jb->dbg[4 + i]);  // helper tile stages
+    }
+#endif
     *C.Q.st = g_L.S;
     if (C.Q.jb) st_agent(&C.Q.jb->stop, 1);
   }

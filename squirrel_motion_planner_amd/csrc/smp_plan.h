@@ -63,29 +63,31 @@ struct ViaNode {               // via node pending insertion (selected_via_nodes
 };
 
 // Collision-check job of one query, shared by its leader workgroup and its helper workgroups through HBM
-// (DESIGN.md "Helpers").  Control words sit on their own 128-byte lines.  Hand-off (MI355X_MICROARCH.md,
-// valid forms): payload and flags are agent-scope (sc1) stores drained with s_waitcnt vmcnt(0) behind a
-// workgroup barrier before the flag store; readers poll with sc1 loads and read the payload with sc1 loads.
+// (DESIGN.md "Helpers").  Both directions use data-tagged 8-byte granules (MI355X_MICROARCH.md hand-off table:
+// "data-tagged granules"; an aligned 8-byte store is single-copy atomic): the high 32 bits of every granule are
+// the job number, the low 32 bits data, so a reader knows a granule is current without any flag, fence or
+// drain.  Granules are stored and read with agent-scope (sc1) relaxed atomics.
 #ifndef SMP_HELPER_CT
 #define SMP_HELPER_CT 8
 #endif
 constexpr int HELPER_CT = SMP_HELPER_CT;          // configurations per job tile
+static_assert(HELPER_CT <= 32, "a tile's collision mask is one 32-bit word");
 constexpr int JOB_SLOTS = MAXE * (MAX_PTS + 1); // (edge, point) slots of one job
 constexpr int JOB_TILES = (JOB_SLOTS + HELPER_CT - 1) / HELPER_CT;
+constexpr int JOB_WORDS = 1 + 4 * NJ * MAXE;     // payload words: header + (start, step) halves per edge
 constexpr int SMP_RING = 16;                     // run-ahead sampler: samples kept ahead of the leader
 struct JobBoard {
-  int seq;                     // job number; the leader increments it to publish a job
   int stop;                    // 1 once the leader left the launch: helpers exit
-  int pad0[30];
-  int pad1[32];
-  int done;                    // tiles of the current job finished
-  int pad2[31];
-  int first[MAXE];             // first colliding point per edge (atomicMin); np1 = free
-  int pad3[32 - MAXE % 32];
-  int E, np1, nslots, ntiles, self, map;
-  int pad4[26];
-  unsigned tflag[JOB_TILES];   // per tile: the last job that claimed it (atomicMax; see claim_tile)
-  int pad5[32 - JOB_TILES % 32];
+  int pad0[7];
+  unsigned long long dbg[12];  // SMP_JOB_PROF builds: publish time, helper pickup / finish delay sums and counts,
+                               // helper tile stage clocks (collide_tile A, B, C-centres, C)
+  // leader -> helpers: word 0 = header (edges | np1 << 8 | self << 16 | map << 17); word 1 + 32k + 2j (+1) =
+  // low (high) half of edge k's start[j], word 1 + 32k + 16 + 2j (+1) = of its step[j]
+  unsigned long long pay[JOB_WORDS];
+  int pad1[32 - (2 * JOB_WORDS) % 32];
+  // helpers -> leader: tile t's collision mask (bit c = configuration c of the tile collides)
+  unsigned long long res[JOB_TILES];
+  int pad2[32 - (2 * JOB_TILES) % 32];
   // run-ahead sampler (DESIGN.md "Sampler").  Leader -> sampler: its current iteration and the informed-
   // sampling parameters, versioned (payload stores drained before the version store).
   int s_ver, s_have_sol;
@@ -99,8 +101,6 @@ struct JobBoard {
     unsigned long long q[NJ];     // fp64 bit patterns
     int pad[14];
   } ring[SMP_RING];
-  unsigned long long start[MAXE][NJ], step[MAXE][NJ];  // fp64 bit patterns
-  int slot_e[JOB_SLOTS], slot_i[JOB_SLOTS];
 };
 
 struct QueryDev {

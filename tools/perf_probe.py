@@ -34,6 +34,13 @@ for iters in [int(v) for v in (sys.argv[1:] or ["2000", "10000", "50000"])]:
         rounds = max(raw[30], 1)
         print("   sample_ellipse: %d rounds, stage 1 %.2f us, stage 2 %.2f us per round" % (
             rounds, raw[28] / 1e2 / rounds, raw[29] / 1e2 / rounds), flush=True)
+    if os.environ.get("SMP_JOB_PROF"):  # SMP_JOB_PROF build: helper pickup / tile-finish delay after publication
+        n = max(raw[29], 1)
+        print("   helpers: %d pickups, pickup %.2f us, tile finished %.2f us after publication (mean)" % (
+            raw[29], raw[28] / 1e2 / n, raw[30] / 1e2 / n), flush=True)
+        nt = max(r["phases"]["n_tiles"], 1)
+        print("   helper tile stages (us per tile, approx.): A %.2f B %.2f C-centres %.2f C %.2f" % tuple(
+            raw[12 + i] * 1e6 / nt for i in range(4)), flush=True)
     if os.environ.get("SMP_DETAIL_PROF"):  # SMP_DETAIL_PROF build: serial-section clocks (ticks, slots 28-31)
         print("   serial sections (us/iter): rewire commit %.2f (cost_update %.2f), connect replay %.2f, insert_via %.2f"
               % tuple(raw[k] / 1e2 / iters for k in (28, 29, 30, 31)), flush=True)
