@@ -74,7 +74,10 @@ typedef struct smp_params {
   int informed_sampling;   /* m_informed_sampling_active (default 1) */
   int64_t node_capacity;   /* per-tree node capacity on the device (0: derived from the budget) */
   int helpers;             /* helper workgroups per query that share its collision tiles across CUs
-                              (0: automatic, up to 63; -1: none, the query runs on its own workgroup) */
+                              (0: automatic, up to 127 with the scout / 63 without; -1: none, the query runs on
+                              its own workgroup) */
+  int scout;               /* 1 (default): a scout workgroup per query computes the next iteration's scans and
+                              collision jobs ahead (needs >= 4 helpers); 0: off.  Results are identical either way */
 } smp_params;
 
 typedef struct smp_query {
@@ -111,6 +114,15 @@ typedef struct smp_stats {
                                     rewire, connect, collision tiles, #tiles, edge costs, via chains, #via,
                                     tile stages, tile time per calling phase, then counts of checked
                                     configurations and of tile slots per calling phase) */
+  int64_t scout_nn_hits;         /* nearest-neighbour scans answered from the scout's record */
+  int64_t scout_near_hits;       /* near-vertex scans answered from the scout's record */
+  int64_t scout_edge_hits;       /* needed edges whose collision check the scout had done */
+  int64_t scout_edge_misses;     /* needed edges checked by the leader's own jobs while the scout was asked */
+  double scout_wait_seconds;     /* time the leader waited for the scout */
+  double scout_phase_seconds[32]; /* the scout's time per stage (0 sample, 1 nearest, 2 expand, 3 near, 4 choose,
+                                    5 via chain, 6 rewire, 28 idle, 29 publishing, 31 busy; 30 = iterations) */
+  int32_t helpers;               /* helper workgroups per query used */
+  int32_t scout;                 /* 1 if the scout ran */
 } smp_stats;
 
 typedef struct smp_result {

@@ -40,7 +40,7 @@ class SceneOpts(ctypes.Structure):
 class Params(ctypes.Structure):
     _fields_ = [("near_threshold", _d), ("step_factor", _d), ("num_traj_segments", _i), ("max_near_nodes", _i),
                 ("path_optimality_threshold", _d), ("tree_optimization", _i), ("informed_sampling", _i),
-                ("node_capacity", _i64), ("helpers", _i)]
+                ("node_capacity", _i64), ("helpers", _i), ("scout", _i)]
 
 
 class Query(ctypes.Structure):
@@ -56,7 +56,10 @@ class Stats(ctypes.Structure):
                 ("edges_start", _i64), ("edges_goal", _i64), ("rewires_start", _i64), ("rewires_goal", _i64),
                 ("connected_tree_is_start", ctypes.c_int32), ("conn_node_b", ctypes.c_int32),
                 ("conn_node_a", ctypes.c_int32), ("nn_nodes_scanned", _i64), ("near_nodes_scanned", _i64),
-                ("samples_precomputed", _i64), ("phase_seconds", _d * 32)]
+                ("samples_precomputed", _i64), ("phase_seconds", _d * 32), ("scout_nn_hits", _i64),
+                ("scout_near_hits", _i64), ("scout_edge_hits", _i64), ("scout_edge_misses", _i64),
+                ("scout_wait_seconds", _d), ("scout_phase_seconds", _d * 32), ("helpers", ctypes.c_int32),
+                ("scout", ctypes.c_int32)]
 
 
 class Result(ctypes.Structure):

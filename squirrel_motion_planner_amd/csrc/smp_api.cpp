@@ -11,6 +11,7 @@
 #include <set>
 #include <stdexcept>
 #include <string>
+#include <array>
 #include <vector>
 
 #include "../../include/smp_gpu.h"
@@ -22,7 +23,8 @@
 namespace smp {
 void launch_check(int ct, int grid, hipStream_t st, const RobotDev* rb, SceneDev sc, const MapCfg* mc, const double* q,
                   long long n, int self, int map, uint8_t* valid, unsigned long long* prof);
-__global__ void plan_kernel(const RobotDev* rb, SceneDev sc, const MapCfg* mc, QueryDev* qs, int iters);
+__global__ void plan_kernel(const RobotDev* rb, SceneDev sc, const MapCfg* mc, QueryDev* qs, int nq, int scout_base,
+                            int iters);
 __global__ void helper_kernel(const RobotDev* rb, SceneDev sc, const MapCfg* mc, QueryDev* qs, int nq);
 __global__ void path_kernel(QueryDev* qs, int* counts);
 __global__ void sincos_kernel(const double* x, int n, double* s, double* c);
@@ -80,12 +82,14 @@ struct QueryBuffers {
   DBuf<double> q, cost, e_start, e_target, rows;
   DBuf<int> parent, first_child, next_sib, prev_sib, stack, path_nodes;
   DBuf<ViaNode> via;
-  DBuf<JobBoard> jb;
+  DBuf<JobBoard> jb, sjb;          // the leader's and the scout's collision-job boards
+  DBuf<ScoutBoard> scb;
+  DBuf<ViaNode> svia;
   size_t cap = 0;
   void release() {
     st.release(); q.release(); cost.release(); e_start.release(); e_target.release(); rows.release();
     parent.release(); first_child.release(); next_sib.release(); prev_sib.release(); stack.release();
-    path_nodes.release(); via.release(); jb.release();
+    path_nodes.release(); via.release(); jb.release(); sjb.release(); scb.release(); svia.release();
     cap = 0;
   }
 };
@@ -148,6 +152,7 @@ void smp_params_default(smp_params* p) {
   p->informed_sampling = 1;
   p->node_capacity = 0;
   p->helpers = 0;
+  p->scout = 1;
 }
 
 void smp_scene_opts_default(smp_scene_opts* o) {
@@ -491,6 +496,9 @@ static hipError_t alloc_query(QueryBuffers& b, size_t cap, int via_cap, long lon
   if ((e = b.via.reserve(via_cap))) return e;
   if ((e = b.rows.reserve(std::max<long long>(rows, 1) * 5))) return e;
   if ((e = b.jb.reserve(1))) return e;
+  if ((e = b.sjb.reserve(1))) return e;
+  if ((e = b.scb.reserve(1))) return e;
+  if ((e = b.svia.reserve(via_cap))) return e;
   b.cap = cap;
   return hipSuccess;
 }
@@ -515,6 +523,11 @@ static QueryDev make_qdev(QueryBuffers& b, size_t cap, long long rows) {
   d.rows_cap = rows;
   d.path_nodes = b.path_nodes.p;
   d.jb = nullptr;
+  d.sjb = nullptr;
+  d.sampler_jb = nullptr;
+  d.scb = nullptr;
+  d.svia = nullptr;
+  d.sworkers = 1;
   d.nworkers = 1;
   d.sampler = 0;
   d.trace = nullptr;
@@ -585,14 +598,25 @@ extern "C" int smp_plan_batch(smp_planner* p, const smp_query* qs, int nq, smp_r
     if (st) return st;
     HIPCHK(hipMemcpyAsync(qdev[i].st, &S[i], sizeof(QState), hipMemcpyHostToDevice, p->stream));
   }
-  // helper workgroups per query (DESIGN.md "Helpers"): one workgroup per CU, leaders first
+  // helper workgroups per query (DESIGN.md "Helpers", "Scout"): one workgroup per CU, leaders (and scouts) first.
+  // With a scout the helpers are the leader's tile helpers, the scout's tile helpers and the run-ahead sampler.
   int nh = p->params.helpers;
-  if (nh == 0) nh = std::min(63, std::max(0, p->num_cus / nq - 1));
+  const bool want_scout = p->params.scout != 0;
+  if (nh == 0) nh = want_scout ? std::min(127, std::max(0, p->num_cus / nq - 2)) : std::min(63, std::max(0, p->num_cus / nq - 1));
   if (nh < 0) nh = 0;
+  const bool scout = want_scout && nh >= 4;
+  const int h_lead = scout ? (nh - 1) / 2 : 0, h_scout = scout ? nh - 1 - h_lead : 0;
   for (int i = 0; i < nq; ++i) {
     qdev[i].jb = nh > 0 ? p->qb[i].jb.p : nullptr;
     qdev[i].sampler = nh >= 2;              // with two or more helpers, the last one runs ahead sampling
-    qdev[i].nworkers = nh >= 2 ? nh : 1 + nh;
+    qdev[i].nworkers = scout ? 1 + h_lead : (nh >= 2 ? nh : 1 + nh);
+    if (scout) {
+      qdev[i].sjb = p->qb[i].sjb.p;
+      qdev[i].scb = p->qb[i].scb.p;
+      qdev[i].svia = p->qb[i].svia.p;
+      qdev[i].sampler_jb = p->qb[i].jb.p;
+      qdev[i].sworkers = 1 + h_scout;
+    }
   }
   static int* trace_host = nullptr;
   const bool debug = std::getenv("SMP_DEBUG") != nullptr;
@@ -613,6 +637,8 @@ extern "C" int smp_plan_batch(smp_planner* p, const smp_query* qs, int nq, smp_r
   for (int i = 0; i < nq; ++i) if (qs[i].budget_kind == SMP_BUDGET_SECONDS) tmax = std::max(tmax, qs[i].budget);
   auto t_begin = std::chrono::steady_clock::now();
   int chunk = 256;
+  std::vector<std::array<unsigned long long, 32>> scout_prof(nq);
+  for (auto& a : scout_prof) a.fill(0);
   float total_ms = 0;
   int64_t launches = 0;
   bool deadline_set = false;
@@ -626,7 +652,13 @@ extern "C" int smp_plan_batch(smp_planner* p, const smp_query* qs, int nq, smp_r
     if (nh > 0) {
       // fresh boards, then the helpers on their own (high-priority, separate hardware queue) stream; they wait
       // for the reset and leave when the leader signals stop
-      for (int i = 0; i < nq; ++i) HIPCHK(hipMemsetAsync(qdev[i].jb, 0, sizeof(JobBoard), p->stream));
+      for (int i = 0; i < nq; ++i) {
+        HIPCHK(hipMemsetAsync(qdev[i].jb, 0, sizeof(JobBoard), p->stream));
+        if (scout) {
+          HIPCHK(hipMemsetAsync(qdev[i].sjb, 0, sizeof(JobBoard), p->stream));
+          HIPCHK(hipMemsetAsync(qdev[i].scb, 0, sizeof(ScoutBoard), p->stream));
+        }
+      }
       HIPCHK(hipEventRecord(p->ev_board, p->stream));
       HIPCHK(hipStreamWaitEvent(p->hstream, p->ev_board, 0));
       hipLaunchKernelGGL(helper_kernel, dim3(nq * nh), dim3(BLOCK), 0, p->hstream, p->d_rb, p->sc, p->d_mc,
@@ -634,7 +666,10 @@ extern "C" int smp_plan_batch(smp_planner* p, const smp_query* qs, int nq, smp_r
       HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(p->ev0, p->stream));
-    hipLaunchKernelGGL(plan_kernel, dim3(nq), dim3(BLOCK), 0, p->stream, p->d_rb, p->sc, p->d_mc, p->d_qdev.p, chunk);
+    // scouts at block scout_base + q, scout_base a multiple of 8: blocks b and b + 8 are dealt to the same XCD
+    const int scout_base = scout ? (nq + 7) / 8 * 8 : 0;
+    hipLaunchKernelGGL(plan_kernel, dim3(scout ? scout_base + nq : nq), dim3(BLOCK), 0, p->stream, p->d_rb, p->sc,
+                       p->d_mc, p->d_qdev.p, nq, scout_base, chunk);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(p->ev1, p->stream));
     launches++;
@@ -653,6 +688,14 @@ extern "C" int smp_plan_batch(smp_planner* p, const smp_query* qs, int nq, smp_r
     }
     for (int i = 0; i < nq; ++i)
       HIPCHK(hipMemcpyAsync(&S[i], qdev[i].st, sizeof(QState), hipMemcpyDeviceToHost, p->stream));
+    if (scout) {
+      HIPCHK(hipStreamSynchronize(p->stream));
+      for (int i = 0; i < nq; ++i) {
+        unsigned long long sp[32];
+        HIPCHK(hipMemcpy(sp, qdev[i].scb->prof, sizeof(sp), hipMemcpyDeviceToHost));
+        for (int k = 0; k < 32; ++k) scout_prof[i][k] += sp[k];
+      }
+    }
     HIPCHK(hipStreamSynchronize(p->stream));
     if (nh > 0) HIPCHK(hipStreamSynchronize(p->hstream));
     float ms = 0;
@@ -714,6 +757,17 @@ extern "C" int smp_plan_batch(smp_planner* p, const smp_query* qs, int nq, smp_r
     st.nn_nodes_scanned = s.nn_nodes;
     st.near_nodes_scanned = s.near_nodes;
     st.samples_precomputed = s.smp_hits;
+    st.scout_nn_hits = s.sc_nn;
+    st.scout_near_hits = s.sc_near;
+    st.scout_edge_hits = s.sc_edge_hit;
+    st.scout_edge_misses = s.sc_edge_miss;
+    st.scout_wait_seconds = (double)s.sc_wait / p->wall_rate_hz;
+    for (int k = 0; k < 32; ++k) {
+      const bool count = k == 8 || k == 11 || (k >= 20 && k < 28) || k == 30;
+      st.scout_phase_seconds[k] = count ? (double)scout_prof[i][k] : (double)scout_prof[i][k] / p->wall_rate_hz;
+    }
+    st.helpers = nh;
+    st.scout = scout ? 1 : 0;
     for (int k = 0; k < 32; ++k)
       st.phase_seconds[k] = (k == 8 || k == 11 || k >= 20) ? (double)s.prof[k] : (double)s.prof[k] / p->wall_rate_hz;
     if (i == 0) { p->last_n[0] = s.n[0]; p->last_n[1] = s.n[1]; }
@@ -864,7 +918,7 @@ extern "C" int smp_probe_check_latency(smp_planner* p, const double* q_soa, int6
   float f = 0;
   HIPCHK(hipEventElapsedTime(&f, p->ev0, p->ev1));
   *ms = f;
-  HIPCHK(hipMemcpy(ticks, dprof, 6 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(ticks, dprof, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   (void)hipFree(dprof);
   *clock_hz = p->wall_rate_hz;
   return SMP_OK;

@@ -281,7 +281,7 @@ template <int CT>
 __device__ __forceinline__ void collide_tile(const RobotDev* __restrict__ rb, const SceneDev& sc,
                                              const MapCfg* __restrict__ mc, int nc, const double (*q_lds)[NJ],
                                              int self, int map, TileLds<CT>& L, const TileOrder* ord = nullptr,
-                                             unsigned long long* prof = nullptr) {
+                                             unsigned long long* prof = nullptr, unsigned long long* prof2 = nullptr) {
   static_assert(CT % NWAVE == 0, "tile size");
   constexpr int CPW = TileLds<CT>::CPW, SW = TileLds<CT>::SW;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -302,31 +302,25 @@ __device__ __forceinline__ void collide_tile(const RobotDev* __restrict__ rb, co
   if (tid < nc) L.coll[tid] = 0;
   __syncthreads();
   unsigned long long ta = (prof && tid == 0) ? wall_clock64() : 0;
-  // B: 12 lanes per configuration, one frame element each (fmul's evaluation order), steps in chain order
-  {
-    constexpr int G = 64 / 12;  // configurations per wave per round
-    const int e = lane % 12, g = lane / 12;
-    for (int c0 = 0; c0 < nc; c0 += NWAVE * G) {
-      const int c = c0 + wave * G + g;
-      const bool act = g < G && c < nc;
-      const bool rot = e < 9;
-      const int r = rot ? e / 3 : e - 9, col = rot ? e - r * 3 : 0;
-      if (act) L.tf[c][0][e] = (e == 0 || e == 4 || e == 8) ? 1.0 : (e == 11 ? rb->root_z : 0.0);
-      wave_sync();
-      int cur = 0;
-      for (int k = 0; k < nch; ++k) {
-        if (act) {
-          const double* A = L.tf[c][cur];
-          const double* l = L.u.lf[c][k];
-          const double b0 = rot ? l[col] : l[9], b1 = rot ? l[3 + col] : l[10], b2 = rot ? l[6 + col] : l[11];
-          const double m = A[r * 3 + 0] * b0 + A[r * 3 + 1] * b1 + A[r * 3 + 2] * b2;
-          const double v = rot ? m : m + A[9 + r];
-          L.tf[c][cur ^ 1][e] = v;
-          const int bd = rb->ch_body[k];
-          if (bd >= 0) L.fr[c][bd][e] = v;
-        }
-        wave_sync();
-        cur ^= 1;
+  // B: 3 lanes per configuration, one row each.  Row r of T * L needs only row r of T (and all of the local
+  // frame L), so each lane carries its row through the whole chain in registers, no exchange between lanes;
+  // fmul's evaluation order.
+  if (tid < nc * 3) {
+    const int c = tid / 3, r = tid - c * 3;
+    double t0 = r == 0 ? 1.0 : 0.0, t1 = r == 1 ? 1.0 : 0.0, t2 = r == 2 ? 1.0 : 0.0;
+    double tp = r == 2 ? rb->root_z : 0.0;
+    for (int k = 0; k < nch; ++k) {
+      const double* l = L.u.lf[c][k];
+      const double n0 = t0 * l[0] + t1 * l[3] + t2 * l[6];
+      const double n1 = t0 * l[1] + t1 * l[4] + t2 * l[7];
+      const double n2 = t0 * l[2] + t1 * l[5] + t2 * l[8];
+      const double m = t0 * l[9] + t1 * l[10] + t2 * l[11];
+      tp = m + tp;
+      t0 = n0; t1 = n1; t2 = n2;
+      const int bd = rb->ch_body[k];
+      if (bd >= 0) {
+        double* o = L.fr[c][bd];
+        o[r * 3 + 0] = t0; o[r * 3 + 1] = t1; o[r * 3 + 2] = t2; o[9 + r] = tp;
       }
     }
   }
@@ -391,6 +385,7 @@ __device__ __forceinline__ void collide_tile(const RobotDev* __restrict__ rb, co
       }
       if (hit) hitm |= 1u << k;
     }
+    const unsigned long long tm = (prof2 && tid == 0) ? wall_clock64() : 0;
     if (self) {
       // every sphere pair of the enabled link pairs, the CPW configurations of this wave interleaved
       const uint32_t todo = live & ~hitm;
@@ -412,6 +407,11 @@ __device__ __forceinline__ void collide_tile(const RobotDev* __restrict__ rb, co
         for (int k = 0; k < CPW; ++k)
           if (((todo >> k) & 1u) && __ballot((sh >> k) & 1u)) hitm |= 1u << k;
       }
+    }
+    if (prof2 && tid == 0) {
+      const unsigned long long ts = wall_clock64();
+      prof2[0] += tm - t1;  // wave 0: centres + map sweeps
+      prof2[1] += ts - tm;  // wave 0: self test
     }
     if (lane == 0) {
       for (int k = 0; k < CPW; ++k) {

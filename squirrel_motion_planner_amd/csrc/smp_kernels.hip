@@ -57,7 +57,7 @@ __global__ void __launch_bounds__(BLOCK) check_kernel_t(const RobotDev* __restri
       ql[c][j] = q[(long long)j * n + base + c];
     }
     __syncthreads();
-    collide_tile<CT>(&g_rb, sc, &g_mc, nc, ql, self, map, L, nullptr, pr);
+    collide_tile<CT>(&g_rb, sc, &g_mc, nc, ql, self, map, L, nullptr, pr, pr ? pr + 6 : nullptr);
     if (threadIdx.x < nc) valid[base + threadIdx.x] = L.coll[threadIdx.x] ? 0 : 1;
     __syncthreads();
   }
@@ -193,6 +193,13 @@ struct PlanLds {
   double wd[BLOCK / 64];
   int wi[BLOCK / 64];
   long long wcount[BLOCK / 64];
+  // scout (DESIGN.md "Scout").  Leader: the scout's record of this iteration as far as received (sp_stage), sp_on =
+  // still worth asking; eg_hit[e] = first colliding point of batch edge e taken from the record, -2 = none.
+  // Scout: the record it builds.
+  ScoutRec sr;
+  int sp_on, sp_stage, sp_go[2];
+  int sc_same;                  // leader: the scout runs on this XCD (1), another (0), not yet known (-1)
+  int eg_hit[MAXE];
 };
 
 // The planner's LDS objects live at namespace scope so that every device function addresses them as LDS
@@ -234,6 +241,21 @@ __device__ __forceinline__ gcdptr uni_gptr(const double* p) {
   return (gcdptr)(((unsigned long long)hi << 32) | lo);
 }
 
+// Stores into the tree arrays that the scout reads (q, cost, parent).  Plain stores: the lines stay in this XCD's
+// L2, where a scout on the same XCD (the usual placement, plan_kernel) and the leader's own scans find them;
+// scout_request publishes them (drain, plus an agent release when the scout runs on another XCD).
+__device__ __forceinline__ void st_tree(double* p, double v) { *p = v; }
+__device__ __forceinline__ void st_tree(int* p, int v) { *p = v; }
+// XCD of this workgroup (HW_REG_XCC_ID): placement knowledge for speed only.
+__device__ __forceinline__ int xcc_id() { return __builtin_amdgcn_s_getreg((3 << 11) | 20); }
+// Bitwise equality of two configurations (cache keys of the scout's records).
+__device__ __forceinline__ bool same8(const double* a, const double* b) {
+  bool s = true;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) s &= __double_as_longlong(a[j]) == __double_as_longlong(b[j]);
+  return s;
+}
+
 // --------------------------------------------------------------------------------------- node access
 __device__ __forceinline__ void load_node(const Ctx& C, int t, int id, NodeRef* o) {
   const TreeDev& T = C.Q.tr[t];
@@ -252,12 +274,12 @@ __device__ void insert_node(const Ctx& C, int t, const double* e_start, const do
   const TreeDev& T = C.Q.tr[t];
   int cap = S.cap;
   for (int j = 0; j < NJ; ++j) {
-    T.q[(size_t)j * cap + i] = x.q[j];
+    st_tree(&T.q[(size_t)j * cap + i], x.q[j]);
     T.e_start[(size_t)j * cap + i] = e_start[j];
     T.e_target[(size_t)j * cap + i] = e_target[j];
   }
-  for (int k = 0; k < 3; ++k) T.cost[(size_t)k * cap + i] = x.c[k];
-  T.parent[i] = x.parent;
+  for (int k = 0; k < 3; ++k) st_tree(&T.cost[(size_t)k * cap + i], x.c[k]);
+  st_tree(&T.parent[i], x.parent);
   T.first_child[i] = -1;
   int p = x.parent;
   int f = T.first_child[p];
@@ -290,15 +312,17 @@ __device__ int block_argmin(double d, int i) {
 // find_nearest_neighbour_interpolation: first strict minimum of the Euclidean joint distance (DH:128-156).
 // sqrt is monotone, so a node can only beat the running minimum if its squared distance is below the minimum's
 // squared distance; the (correctly rounded) sqrt is taken only then and compared exactly as the reference does.
-__device__ int nearest(const Ctx& C, int t, const double* q) {
+__device__ bool spec_stage(const Ctx& C, int s);
+// Block argmin of the nodes [i_begin, n) of tree t: the first strict minimum (d, id) of the distances, d = 10000
+// if none is below it.  All threads; result in (g_L.wd[0], g_L.wi[0]) via nearest_scan's return.
+__device__ int nearest_scan(const Ctx& C, int t, const double* q, int i_begin, double* d_out) {
   const gcdptr tq = uni_gptr(C.Q.tr[t].q);
   const int n = uni(g_L.S.n[t]), cap = uni(g_L.S.cap);
-  if (threadIdx.x == 0) g_L.S.nn_nodes += n;
   double qq[NJ];
   for (int j = 0; j < NJ; ++j) qq[j] = q[j];
   double best = 10000.0, best_s = 1e300;
   int bid = 0x7fffffff;
-  for (int i0 = threadIdx.x; i0 < n; i0 += 2 * BLOCK) {
+  for (int i0 = i_begin + threadIdx.x; i0 < n; i0 += 2 * BLOCK) {
     const int i1 = i0 + BLOCK;
     const bool v1 = i1 < n;
     double a[NJ], b[NJ];
@@ -324,7 +348,41 @@ __device__ int nearest(const Ctx& C, int t, const double* q) {
       if (dist < best) { best = dist; bid = i1; best_s = sb; }
     }
   }
-  return block_argmin(best, bid);
+  for (int off = 32; off > 0; off >>= 1) {
+    double od = __shfl_xor(best, off);
+    int oi = __shfl_xor(bid, off);
+    if (od < best || (od == best && oi < bid)) { best = od; bid = oi; }
+  }
+  if (lane_id() == 0) { g_L.wd[wave_id()] = best; g_L.wi[wave_id()] = bid; }
+  __syncthreads();
+  double bd = g_L.wd[0];
+  int bi = g_L.wi[0];
+  for (int w = 1; w < BLOCK / 64; ++w)
+    if (g_L.wd[w] < bd || (g_L.wd[w] == bd && g_L.wi[w] < bi)) { bd = g_L.wd[w]; bi = g_L.wi[w]; }
+  __syncthreads();
+  *d_out = bd;
+  return bi;
+}
+
+// find_nearest_neighbour_interpolation (birrt_star.cpp:4076-4133).  With `spec`, the scout's scan of the same
+// sample over the tree's first X nodes is taken if it matches, and only the nodes appended since are scanned: one
+// of them replaces the scout's node only with a strictly smaller distance (it has a larger index).
+__device__ int nearest(const Ctx& C, int t, const double* q, bool spec = false) {
+  const int n = uni(g_L.S.n[t]);
+  if (threadIdx.x == 0) g_L.S.nn_nodes += n;
+  if (spec && spec_stage(C, SC_NN)) {
+    const ScoutNN& R = g_L.sr.nn;
+    if (uni(R.ok && R.t == t && R.X <= n && same8(q, R.q))) {
+      double dp;
+      const int ip = nearest_scan(C, t, q, R.X, &dp);
+      if (threadIdx.x == 0) g_L.S.sc_nn++;
+      if (dp < R.d) return ip;
+      return R.d < 10000.0 ? R.id : 0;
+    }
+  }
+  double bd;
+  const int bi = nearest_scan(C, t, q, 0, &bd);
+  return bd < 10000.0 ? bi : 0;
 }
 
 // (cost,id) lexicographic order of the near list (std::sort order made total).  Costs are
@@ -548,11 +606,12 @@ __device__ __forceinline__ int near_bin(unsigned long long key, double cmin, dou
 }
 
 template <int K>
-__device__ void near_set(const Ctx& C, int t, const double* q, int excl) {
+__device__ void near_set(const Ctx& C, int t, const double* q, int excl, bool spec = false) {
 #ifdef SMP_NEAR_PROF
   unsigned long long _tn = 0;
 #endif
   static_assert(K <= 64 && NEAR_BUF == 128 && NEAR_BINS == 4 * 64, "register path layout");
+  static_assert(K <= MAX_NEAR, "scout record lists");
   constexpr int NW = BLOCK / 64, CH = NEAR_NBK * BLOCK;
   const int n = uni(g_L.S.n[t]);
   const gcdptr tq = uni_gptr(C.Q.tr[t].q), tc = uni_gptr(C.Q.tr[t].cost);
@@ -560,6 +619,38 @@ __device__ void near_set(const Ctx& C, int t, const double* q, int excl) {
   const double r = g_L.S.near_r;
   const double r2 = r * r, r2lo = r2 * (1.0 - 1e-12), r2hi = r2 * (1.0 + 1e-12);
   const int lane = lane_id(), wave = wave_id();
+  if (spec && spec_stage(C, SC_NEAR)) {
+    // the scout's near set of the same configuration over the tree's first X nodes is the answer if none of the
+    // nodes appended since is near (else the full scan below)
+    const ScoutNear& R = g_L.sr.nr;
+    if (uni(R.ok && R.t == t && R.X <= n && same8(q, R.q))) {
+      bool any = false;
+      for (int i = R.X + (int)threadIdx.x; i < n; i += BLOCK) {
+        double sb = 0.0;
+        for (int j = 0; j < NJ; ++j) {
+          double d = q[j] - (tq + (size_t)j * cap)[(unsigned)i];
+          sb += d * d;
+        }
+        bool amb;
+        bool nr = near_radius(i != excl, sb, r, r2lo, r2hi, amb);
+        if (amb) nr = sqrt(sb) < r;
+        any |= nr;
+      }
+      if (!__syncthreads_or(any)) {
+        if (threadIdx.x < K) {
+          g_L.lo_i[threadIdx.x] = R.lo_i[threadIdx.x]; g_L.lo_c[threadIdx.x] = R.lo_c[threadIdx.x];
+          g_L.hi_i[threadIdx.x] = R.hi_i[threadIdx.x]; g_L.hi_c[threadIdx.x] = R.hi_c[threadIdx.x];
+        }
+        if (threadIdx.x == 0) {
+          g_L.nk = R.nk; g_L.n_lo = R.n_lo; g_L.n_hi = R.n_hi;
+          g_L.S.near_nodes += n;
+          g_L.S.sc_near++;
+        }
+        __syncthreads();
+        return;
+      }
+    }
+  }
   double qq[NJ];
   for (int j = 0; j < NJ; ++j) qq[j] = q[j];
   int tot_all = 0;  // near nodes of the chunks before this one (block-uniform)
@@ -885,7 +976,7 @@ __device__ __forceinline__ void edge_validity_job(const Ctx& C, int E, int pslot
   const int W = C.Q.nworkers;
   if (threadIdx.x < 64) {
     const int e = threadIdx.x;
-    const bool need = e < E && g_L.eg_need[e];
+    const bool need = e < E && g_L.eg_need[e] && g_L.eg_hit[e] < 0;  // edges the scout checked are not published
     const unsigned long long m = __ballot(need);
     const int k = __popcll(m & ((1ull << e) - 1));
     if (need) J.emap[k] = e;
@@ -1115,14 +1206,135 @@ __device__ __forceinline__ void helper_main(const Ctx& C, int hidx, JobLds& J) {
   }
 }
 
+// --------------------------------------------------------------------------------------- scout hand-off
+// Copies nbytes of LDS record section p (inside g_L.sr) to / from record `par` of the scout board, 8-byte words
+// with agent-scope (sc1) stores / loads.  All threads.
+__device__ __forceinline__ void sc_copy_out(ScoutBoard* sb, int par, const void* p, int nbytes) {
+  const size_t off = (const char*)p - (const char*)&g_L.sr;
+  const unsigned long long* src = (const unsigned long long*)p;
+  unsigned long long* dst = (unsigned long long*)((char*)&sb->rec[par] + off);
+  for (int w = threadIdx.x; w < nbytes / 8; w += BLOCK) st_agent(&dst[w], src[w]);
+}
+__device__ __forceinline__ void sc_copy_in(const ScoutBoard* sb, int par, void* p, int nbytes) {
+  const size_t off = (const char*)p - (const char*)&g_L.sr;
+  unsigned long long* dst = (unsigned long long*)p;
+  const unsigned long long* src = (const unsigned long long*)((const char*)&sb->rec[par] + off);
+  for (int w = threadIdx.x; w < nbytes / 8; w += BLOCK) dst[w] = ld_agent(&src[w]);
+}
+static_assert(sizeof(ScoutNN) % 8 == 0 && sizeof(ScoutNear) % 8 == 0 && sizeof(ScoutEdge) % 8 == 0 &&
+              offsetof(ScoutRec, nr) % 8 == 0 && offsetof(ScoutRec, n_choose) % 8 == 0 && offsetof(ScoutRec, e) % 8 == 0,
+              "scout record sections are 8-byte words");
+
+constexpr unsigned long long SCOUT_WAIT = 6000;  // device-clock ticks (60 us) the leader waits for one scout stage
+
+// Leader: waits until the scout's record of this iteration reached stage s (or the scout is not working on this
+// iteration, or SCOUT_WAIT passes: then the scout is not asked again this iteration) and copies the sections of
+// the stages received since the last call into g_L.sr.  All threads; returns whether stage s is there.
+__device__ bool spec_stage(const Ctx& C, int s) {
+  if (!uni(g_L.sp_on)) return false;
+  const int have = uni(g_L.sp_stage);
+  if (have >= s) return true;
+  const ScoutBoard* sb = C.Q.scb;
+  const int par = (int)(g_L.S.iter & 1);
+  const unsigned tag = (unsigned)(g_L.S.iter + 1);
+  const unsigned long long t0 = threadIdx.x == 0 ? wall_clock64() : 0;
+  int got;
+  for (int k = 0;; k ^= 1) {
+    if (threadIdx.x == 0) {
+      const unsigned long long v = ld_agent(&sb->stage[par]);
+      int go = 0;
+      if ((unsigned)(v >> 32) != tag) go = -1;           // the scout is not on this iteration
+      else if ((int)(unsigned)v >= s) go = 1 + (int)(unsigned)v;
+      else if (wall_clock64() - t0 > SCOUT_WAIT) go = -1;
+      g_L.sp_go[k] = go;
+    }
+    __syncthreads();
+    got = uni(g_L.sp_go[k]);
+    if (got != 0) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  if (threadIdx.x == 0) g_L.S.sc_wait += wall_clock64() - t0;
+  if (got < 0) {
+    if (threadIdx.x == 0) g_L.sp_on = 0;
+    __syncthreads();
+    return false;
+  }
+  const int st = got - 1;  // stages (have, st] arrived
+  ScoutRec& R = g_L.sr;
+  if (have < SC_NN && st >= SC_NN) sc_copy_in(sb, par, &R.nn, sizeof(ScoutNN));
+  if (have < SC_EXPAND && st >= SC_EXPAND) sc_copy_in(sb, par, &R.e[0], sizeof(ScoutEdge));
+  if (have < SC_NEAR && st >= SC_NEAR) sc_copy_in(sb, par, &R.nr, sizeof(ScoutNear));
+  if ((have < SC_CHOOSE && st >= SC_CHOOSE) || (have < SC_DONE && st >= SC_DONE))
+    sc_copy_in(sb, par, &R.n_choose, 4 * sizeof(int));
+  if (have < SC_CHOOSE && st >= SC_CHOOSE) sc_copy_in(sb, par, &R.e[SCOUT_CHOOSE0], MAX_NEAR * sizeof(ScoutEdge));
+  if (have < SC_DONE && st >= SC_DONE) sc_copy_in(sb, par, &R.e[SCOUT_REWIRE0], MAX_NEAR * sizeof(ScoutEdge));
+  __syncthreads();
+  if (threadIdx.x == 0) g_L.sp_stage = st;
+  __syncthreads();
+  return true;
+}
+
+// Leader, at the start of iteration i (after its sample): asks the scout for iteration i + 1, which expands tree
+// `t` (= tree_B of iteration i).  Its first n[t] nodes stay as they are until then (iteration i only appends to
+// it), and their stores are drained here, so the scout reads them as the leader will.
+__device__ void scout_request(const Ctx& C, int t) {
+  drain();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (g_L.sc_same < 0) {
+      const int x = ld_agent(&C.Q.scb->xcc);
+      if (x > 0) g_L.sc_same = (x - 1) == xcc_id() ? 1 : 0;
+    }
+    // a scout on another XCD reads through its own L2: write this XCD's dirty lines back first
+    if (g_L.sc_same != 1) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      drain();
+    }
+    const QState& S = g_L.S;
+    const unsigned tag = (unsigned)(S.iter + 2);
+    const unsigned w0 = (unsigned)S.n[t] | (unsigned)t << 28 | (unsigned)(S.tree_opt && S.have_sol) << 29;
+    st_agent(&C.Q.scb->req[1], granule(tag, (unsigned)g_L.smp_ver));
+    st_agent(&C.Q.scb->req[0], granule(tag, w0));
+    g_L.sp_on = 1;
+    g_L.sp_stage = -1;
+  }
+  __syncthreads();
+}
+
 // Validity of the batch's needed edges -> eg_first.  `ov` (OV_*, tree `ovt`): scan work whose inputs are final
 // before the check, done while a collision job runs (after the check without helpers); overlap_work records it
 // in g_L.spec for the caller.
-__device__ void edge_validity(const Ctx& C, int E, bool stop_first_valid, int pslot, int ov = 0, int ovt = 0) {
+// `sgrp` (leader, job mode): the scout record stage whose candidate edges may hold these edges' results
+// (SC_EXPAND: the expand edge, SC_CHOOSE: choose-parent candidates, SC_DONE: rewire candidates).  A needed edge
+// whose start and target equal a checked record edge bit for bit takes that edge's first collision (a pure
+// function of the two configurations) and is left out of the job.
+__device__ void edge_validity(const Ctx& C, int E, bool stop_first_valid, int pslot, int ov = 0, int ovt = 0,
+                              int sgrp = -1) {
   const int np1 = g_L.S.n_pts + 1;
   if (threadIdx.x == 0) g_L.count_slot = pslot + 4;
   if (C.Q.jb) {
+    if (threadIdx.x < MAXE) g_L.eg_hit[threadIdx.x] = -2;
+    __syncthreads();
+    if (sgrp >= 0 && spec_stage(C, sgrp)) {
+      const int g0 = sgrp == SC_EXPAND ? 0 : sgrp == SC_CHOOSE ? SCOUT_CHOOSE0 : SCOUT_REWIRE0;
+      const int gn = sgrp == SC_EXPAND ? 1 : sgrp == SC_CHOOSE ? g_L.sr.n_choose : g_L.sr.n_rewire;
+      for (int it = threadIdx.x; it < E * gn; it += BLOCK) {
+        const int e = it / gn, k = g0 + it - (it / gn) * gn;
+        const ScoutEdge& R = g_L.sr.e[k];
+        if (g_L.eg_need[e] && R.first >= 0 && same8(g_L.eg_start[e], R.s) && same8(g_L.eg_target[e], R.g))
+          g_L.eg_hit[e] = R.first;  // equal edges have equal results: concurrent writers agree
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        for (int e = 0; e < E; ++e) {
+          if (!g_L.eg_need[e]) continue;
+          if (g_L.eg_hit[e] >= 0) g_L.S.sc_edge_hit++; else g_L.S.sc_edge_miss++;
+        }
+      }
+    }
     edge_validity_job(C, E, pslot, ov, ovt);
+    if (threadIdx.x < E && g_L.eg_hit[threadIdx.x] >= 0) g_L.eg_first[threadIdx.x] = g_L.eg_hit[threadIdx.x];
+    __syncthreads();
     return;
   }
   if (threadIdx.x < E) { g_L.eg_first[threadIdx.x] = np1; g_L.eg_ptr[threadIdx.x] = 0; }
@@ -1190,7 +1402,7 @@ __device__ void overlap_work(const Ctx& C, int ov, int t) {
   }
   const long long c0 = ov == OV_NN ? g_L.S.nn_nodes : g_L.S.near_nodes;
   __syncthreads();
-  if (ov == OV_NEAR_EXPAND) near_set<20>(C, t, g_L.eg_end[0], g_L.S.n[t]);
+  if (ov == OV_NEAR_EXPAND) near_set<20>(C, t, g_L.eg_end[0], g_L.S.n[t], true);
   else if (ov == OV_NEAR_XN) near_set<20>(C, t, g_L.xn.q, g_L.xn.id);
   else {
     const int id = nearest(C, t, g_L.xn.q);
@@ -1303,12 +1515,12 @@ __device__ void insert_via(const Ctx& C, int t) {
         const int i = n0 + k;
         if (w.id != i || (k > 0 && w.parent != i - 1)) S.status = -7;  // not the chain insert_node expects
         for (int j = 0; j < NJ; ++j) {
-          T.q[(size_t)j * cap + i] = w.q[j];
+          st_tree(&T.q[(size_t)j * cap + i], w.q[j]);
           T.e_start[(size_t)j * cap + i] = w.e_start[j];
           T.e_target[(size_t)j * cap + i] = w.e_target[j];
         }
-        for (int c = 0; c < 3; ++c) T.cost[(size_t)c * cap + i] = w.c[c];
-        T.parent[i] = w.parent;
+        for (int c = 0; c < 3; ++c) st_tree(&T.cost[(size_t)c * cap + i], w.c[c]);
+        st_tree(&T.parent[i], w.parent);
         T.first_child[i] = k + 1 < nv ? i + 1 : -1;
         T.prev_sib[i] = -1;
         if (k > 0) {
@@ -1517,7 +1729,7 @@ __device__ void cost_update(const Ctx& C, int t, int v, const double* red) {
     if (++visits > S.n[t]) { S.status = -7; S.phase = 2; return; }  // a loop in the tree: fail loudly
     int id = stack[--sp];
     double nc[3];
-    for (int k = 0; k < 3; ++k) { nc[k] = T.cost[(size_t)k * cap + id] + red[k]; T.cost[(size_t)k * cap + id] = nc[k]; }
+    for (int k = 0; k < 3; ++k) { nc[k] = T.cost[(size_t)k * cap + id] + red[k]; st_tree(&T.cost[(size_t)k * cap + id], nc[k]); }
     if (S.have_sol) {
       if (id == S.nB.id && connected) {
         for (int k = 0; k < 3; ++k) { S.cbest[k] = S.cbest[k] + red[k]; S.nB.c[k] = nc[k]; }
@@ -1570,7 +1782,7 @@ __device__ void choose_parent(const Ctx& C, int t) {
     if (threadIdx.x < E) g_L.eg_need[threadIdx.x] = g_L.eg_cost[threadIdx.x][0] <= g_L.xn.c[0];
     for (int e = E + threadIdx.x; e < MAXE; e += BLOCK) g_L.eg_need[e] = 0;
     __syncthreads();
-    edge_validity(C, E, true, P_XCHOOSE);
+    edge_validity(C, E, true, P_XCHOOSE, 0, 0, SC_CHOOSE);
     if (threadIdx.x == 0) {
       for (int e = 0; e < E; ++e) {
         if (!g_L.eg_need[e]) continue;
@@ -1602,23 +1814,27 @@ __device__ void choose_parent(const Ctx& C, int t) {
   __syncthreads();
 }
 
+// rewireTreeInterpolation's candidates (birrt_star.cpp:5088-5096): the last min(k, max_near) near nodes, from the
+// end, whose cost exceeds x_new's -> g_L.cnt.  The hi list is in ascending (cost, id) order, so they are a suffix
+// of it; wave 0 tests them with one load each (lane l: position n_hi - 1 - l) and counts by ballot.
+__device__ void rewire_count(const TreeDev& T) {
+  if (threadIdx.x < 64) {
+    const int n = g_L.nk, lane = threadIdx.x;
+    const int m = n >= g_L.S.max_near ? g_L.S.max_near : n;
+    bool ok = false;
+    if (lane < m) ok = g_L.xn.c[0] < T.cost[g_L.hi_i[g_L.n_hi - 1 - lane]];
+    const int cnt = __popcll(__ballot(ok));
+    if (lane == 0) g_L.cnt = cnt;
+  }
+  __syncthreads();
+}
+
 // rewireTreeInterpolation, unconstrained (birrt_star.cpp:5056-5230).  Validity of every candidate edge
 // x_new -> near is independent of the tree state, so all are checked at once; commits stay sequential.
 __device__ void rewire(const Ctx& C, int t) {
   const int cap = g_L.S.cap;
   const TreeDev& T = C.Q.tr[t];
-  if (threadIdx.x == 0) {
-    int n = g_L.nk;
-    int lower = n >= g_L.S.max_near ? n - g_L.S.max_near : 0;
-    int cnt = 0;
-    // g_L.hi_* holds positions n-n_hi .. n-1 in ascending order
-    for (int k = n - 1; k >= lower; --k) {
-      int pos = k - (n - g_L.n_hi);
-      if (g_L.xn.c[0] < T.cost[g_L.hi_i[pos]]) cnt++;
-    }
-    g_L.cnt = cnt;
-  }
-  __syncthreads();
+  rewire_count(T);
   const int cnt = uni(g_L.cnt);
   if (cnt == 0) return;
   // candidates k = n-1 .. n-cnt  ->  edge slot e = n-1-k
@@ -1641,7 +1857,7 @@ __device__ void rewire(const Ctx& C, int t) {
   }
   for (int e = cnt + threadIdx.x; e < MAXE; e += BLOCK) g_L.eg_need[e] = 0;
   __syncthreads();
-  edge_validity(C, cnt, false, P_XREWIRE, OV_NN, 1 - t);
+  edge_validity(C, cnt, false, P_XREWIRE, OV_NN, 1 - t, SC_DONE);
   DETAIL_BEGIN(_dr);
   // Sequential commits (birrt_star.cpp:5096-5228).  The candidates' parents and costs are gathered into LDS by
   // one thread each; thread 0 walks the candidates from the resume point and stops after a commit, which may
@@ -1670,14 +1886,14 @@ __device__ void rewire(const Ctx& C, int t) {
         if (pv >= 0) T.next_sib[pv] = nx; else T.first_child[p] = nx;
         if (nx >= 0) T.prev_sib[nx] = pv;
         S.edges[t]--;
-        T.parent[v] = g_L.xn.id;
+        st_tree(&T.parent[v], g_L.xn.id);
         if (S.have_sol) {
           bool connected = (t == 0) == (S.conn_start != 0);
           if (v == S.nB.id && connected) S.nB.parent = g_L.xn.id;
           else if (v == S.nA.id && !connected) S.nA.parent = g_L.xn.id;
         }
         for (int j = 0; j < NJ; ++j) {
-          T.q[(size_t)j * cap + v] = g_L.eg_end[e][j];
+          st_tree(&T.q[(size_t)j * cap + v], g_L.eg_end[e][j]);
           T.e_start[(size_t)j * cap + v] = g_L.eg_start[e][j];
           T.e_target[(size_t)j * cap + v] = g_L.eg_target[e][j];
         }
@@ -1876,8 +2092,9 @@ __device__ void iteration(const Ctx& C) {
   unsigned long long _t0 = threadIdx.x == 0 ? wall_clock64() : 0, _t1;
 #define PHASE(k) if (threadIdx.x == 0) { _t1 = wall_clock64(); g_L.S.prof[k] += _t1 - _t0; _t0 = _t1; }
   sample_iteration(C);
+  if (C.Q.scb) scout_request(C, B);
   PHASE(P_SAMPLE);
-  int nid = nearest(C, A, g_L.xr);
+  int nid = nearest(C, A, g_L.xr, true);
   PHASE(P_NN);
   if (threadIdx.x == 0) {
     load_node(C, A, nid, &g_L.nn);
@@ -1891,7 +2108,7 @@ __device__ void iteration(const Ctx& C) {
   __syncthreads();
   const bool opt = uni(g_L.S.tree_opt && g_L.S.have_sol);
   edge_costs(C, 1);
-  edge_validity(C, 1, false, P_XEXPAND, opt ? OV_NEAR_EXPAND : OV_NONE, A);
+  edge_validity(C, 1, false, P_XEXPAND, opt ? OV_NEAR_EXPAND : OV_NONE, A, SC_EXPAND);
   if (threadIdx.x == 0) {
     int f = g_L.eg_first[0];
     count_edge(f);
@@ -1913,7 +2130,7 @@ __device__ void iteration(const Ctx& C) {
   PHASE(P_EXPAND);
   if (opt) {
     // x_new is the expand edge's end exactly when the edge is valid: then its near set was computed during the job
-    if (!(uni(g_L.ext_nn) && take_spec(OV_NEAR_EXPAND))) near_set<20>(C, A, g_L.xn.q, g_L.xn.id);
+    if (!(uni(g_L.ext_nn) && take_spec(OV_NEAR_EXPAND))) near_set<20>(C, A, g_L.xn.q, g_L.xn.id, true);
     PHASE(P_NEAR);
     choose_parent(C, A);
     PHASE(P_CHOOSE);
@@ -1952,16 +2169,338 @@ __device__ void iteration(const Ctx& C) {
   __syncthreads();
 }
 
+// ----------------------------------------------------------------------------------------------- scout
+// Scout: publishes `nbytes` of section p of its record, then (stage >= 0) the stage granule once every wave's
+// stores are drained.
+__device__ void sc_publish(const Ctx& C, int par, unsigned tag, int stage) {
+  const unsigned long long t0 = threadIdx.x == 0 ? wall_clock64() : 0;
+  drain();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    st_agent(&C.Q.scb->stage[par], granule(tag, (unsigned)stage));
+    g_L.S.prof[29] += wall_clock64() - t0;
+  }
+  __syncthreads();
+}
+#define SC_PHASE(k) if (threadIdx.x == 0) { const unsigned long long _t = wall_clock64(); g_L.S.prof[k] += _t - _ts; _ts = _t; }
+// True (block-uniform) once the leader has moved past the iteration with record tag `tag` (its newest request is
+// for a later one than tag + 1): the rest of the record would not be used.
+__device__ bool sc_stale(const Ctx& C, unsigned tag) {
+  if (threadIdx.x == 0) g_L.sp_go[0] = (unsigned)(ld_agent(&C.Q.scb->req[0]) >> 32) > tag + 1 || ld_agent(&C.Q.scb->stop);
+  __syncthreads();
+  const int s = uni(g_L.sp_go[0]);
+  __syncthreads();
+  return s != 0;
+}
+
+// The scout's pass for iteration `it` of the leader, which expands tree t from a snapshot of its first X nodes:
+// the leader's steps up to its rewire collision job (iteration / choose_parent / rewire, same functions on the
+// scout's own LDS, job board, helpers and via-node scratch), recording the results the leader keys on; nothing is
+// written to the trees.  The sample is the run-ahead sampler's for (it, ver).
+__device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int opt, unsigned ver) {
+  QState& S = g_L.S;
+  ScoutRec& R = g_L.sr;
+  ScoutBoard* sb = C.Q.scb;
+  JobBoard* jb = C.Q.jb;  // this Ctx's board is the scout's; the sampler ring lives on the leader's (sampler_jb)
+  const int par = (int)(it & 1);
+  const unsigned tag = (unsigned)(it + 1);
+  (void)jb;
+  unsigned long long _ts = threadIdx.x == 0 ? wall_clock64() : 0;
+  if (threadIdx.x == 0) {
+    S.prof[30]++;
+    S.n[t] = X;
+    R.nn.ok = 0; R.nr.ok = 0; R.n_choose = 0; R.n_rewire = 0;
+  }
+  sc_publish(C, par, tag, SC_STARTED);
+  // the sample: the sampler's ring slot for (it, ver), if it is there within ~20 us
+  if (threadIdx.x == 0) {
+    const JobBoard* lb = C.Q.sampler_jb;
+    const unsigned long long want = ((unsigned long long)(uint32_t)it << 32) | ver;
+    const unsigned long long t0 = wall_clock64();
+    int ok = 0;
+    for (;;) {
+      if (ld_agent(&lb->ring[it % SMP_RING].tag) == want) {
+        for (int j = 0; j < NJ; ++j) g_L.xr[j] = __longlong_as_double((long long)ld_agent(&lb->ring[it % SMP_RING].q[j]));
+        ok = ld_agent(&lb->ring[it % SMP_RING].tag) == want;  // not overwritten while read
+        break;
+      }
+      if (wall_clock64() - t0 > 2000) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+    g_L.flag = ok;
+  }
+  __syncthreads();
+  SC_PHASE(0);
+  if (!uni(g_L.flag)) {
+    sc_copy_out(sb, par, &R.nn, sizeof(ScoutNN));
+    sc_copy_out(sb, par, &R.nr, sizeof(ScoutNear));
+    sc_copy_out(sb, par, &R.n_choose, 4 * sizeof(int));
+    sc_publish(C, par, tag, SC_DONE);
+    return;
+  }
+  // nearest + expand edge (iteration())
+  const int nid = nearest(C, t, g_L.xr);
+  if (threadIdx.x == 0) {
+    load_node(C, t, nid, &g_L.nn);
+    double s = 0.0;
+    for (int j = 0; j < NJ; ++j) { double d = g_L.xr[j] - g_L.nn.q[j]; s += d * d; }
+    const double d = sqrt(s);
+    for (int j = 0; j < NJ; ++j) R.nn.q[j] = g_L.xr[j];
+    R.nn.d = d < 10000.0 ? d : 10000.0;
+    R.nn.id = nid; R.nn.X = X; R.nn.t = t; R.nn.ok = 1;
+    for (int j = 0; j < NJ; ++j) g_L.ext[j] = g_L.xr[j];
+    step_towards((&g_rb), g_L.nn.q, g_L.ext, S.step);
+    for (int j = 0; j < NJ; ++j) { g_L.eg_start[0][j] = g_L.nn.q[j]; g_L.eg_target[0][j] = g_L.ext[j]; }
+    for (int k = 0; k < 3; ++k) g_L.eg_base[0][k] = g_L.nn.c[k];
+    g_L.eg_need[0] = 1;
+  }
+  __syncthreads();
+  sc_copy_out(sb, par, &R.nn, sizeof(ScoutNN));
+  sc_publish(C, par, tag, SC_NN);
+  SC_PHASE(1);
+  edge_costs(C, 1);
+  edge_validity(C, 1, false, P_XEXPAND);
+  if (threadIdx.x == 0) {
+    for (int j = 0; j < NJ; ++j) { R.e[0].s[j] = g_L.eg_start[0][j]; R.e[0].g[j] = g_L.eg_target[0][j]; }
+    R.e[0].first = g_L.eg_first[0];
+    const int f = g_L.eg_first[0];
+    g_L.ext_nn = f > S.n_pts;
+    if (g_L.ext_nn) {
+      for (int j = 0; j < NJ; ++j) g_L.xn.q[j] = g_L.eg_end[0][j];
+      for (int k = 0; k < 3; ++k) g_L.xn.c[k] = g_L.eg_cost[0][k];
+    } else {
+      for (int j = 0; j < NJ; ++j) g_L.xn.q[j] = g_L.xr[j];
+      g_L.xn.c[0] = 10000.0; g_L.xn.c[1] = 0.0; g_L.xn.c[2] = 0.0;
+    }
+    g_L.xn.id = X;
+    g_L.xn.parent = g_L.nn.id;
+    g_L.ext_bp = 0;
+  }
+  __syncthreads();
+  sc_copy_out(sb, par, &R.e[0], sizeof(ScoutEdge));
+  if (!opt || sc_stale(C, tag)) {
+    sc_copy_out(sb, par, &R.nr, sizeof(ScoutNear));
+    sc_copy_out(sb, par, &R.n_choose, 4 * sizeof(int));
+    sc_publish(C, par, tag, SC_DONE);
+    return;
+  }
+  sc_publish(C, par, tag, SC_EXPAND);
+  SC_PHASE(2);
+  // near set of x_new (the leader's, before choose_parent)
+  near_set<20>(C, t, g_L.xn.q, X);
+  if (threadIdx.x < 20) {
+    R.nr.lo_i[threadIdx.x] = g_L.lo_i[threadIdx.x]; R.nr.lo_c[threadIdx.x] = g_L.lo_c[threadIdx.x];
+    R.nr.hi_i[threadIdx.x] = g_L.hi_i[threadIdx.x]; R.nr.hi_c[threadIdx.x] = g_L.hi_c[threadIdx.x];
+  }
+  if (threadIdx.x == 0) {
+    for (int j = 0; j < NJ; ++j) R.nr.q[j] = g_L.xn.q[j];
+    R.nr.nk = g_L.nk; R.nr.n_lo = g_L.n_lo; R.nr.n_hi = g_L.n_hi;
+    R.nr.X = X; R.nr.t = t; R.nr.ok = 1;
+  }
+  __syncthreads();
+  sc_copy_out(sb, par, &R.nr, sizeof(ScoutNear));
+  sc_publish(C, par, tag, SC_NEAR);
+  SC_PHASE(3);
+  // choose_parent's candidate edges (all needed ones checked: the job computes every tile)
+  if (threadIdx.x == 0) {
+    int E = 0;
+    if (g_L.nk > 0) {
+      const int m = min(g_L.n_lo, S.max_near);
+      for (int i = 0; i < m; ++i) {
+        if (!(g_L.lo_c[i] < g_L.xn.c[0])) break;
+        E++;
+      }
+    }
+    g_L.cnt = E;
+    g_L.found = -1;
+  }
+  __syncthreads();
+  const int E = uni(g_L.cnt);
+  if (E > 0) {
+    if (threadIdx.x < E) {
+      const int e = threadIdx.x;
+      NodeRef nd;
+      load_node(C, t, g_L.lo_i[e], &nd);
+      for (int j = 0; j < NJ; ++j) { g_L.eg_start[e][j] = nd.q[j]; g_L.eg_target[e][j] = g_L.xn.q[j]; }
+      for (int k = 0; k < 3; ++k) g_L.eg_base[e][k] = nd.c[k];
+      g_L.eg_near[e] = nd.id;
+    }
+    __syncthreads();
+    edge_costs(C, E);
+    if (threadIdx.x < E) g_L.eg_need[threadIdx.x] = g_L.eg_cost[threadIdx.x][0] <= g_L.xn.c[0];
+    for (int e = E + threadIdx.x; e < MAXE; e += BLOCK) g_L.eg_need[e] = 0;
+    __syncthreads();
+    edge_validity(C, E, false, P_XCHOOSE);
+    if (threadIdx.x < E) {
+      const int e = threadIdx.x;
+      ScoutEdge& w = R.e[SCOUT_CHOOSE0 + e];
+      for (int j = 0; j < NJ; ++j) { w.s[j] = g_L.eg_start[e][j]; w.g[j] = g_L.eg_target[e][j]; }
+      w.first = g_L.eg_need[e] ? g_L.eg_first[e] : -1;
+    }
+    if (threadIdx.x == 0) {
+      R.n_choose = E;
+      for (int e = 0; e < E; ++e)
+        if (g_L.eg_need[e] && g_L.eg_first[e] > S.n_pts) { g_L.found = e; break; }
+    }
+    __syncthreads();
+  }
+  sc_copy_out(sb, par, &R.n_choose, 4 * sizeof(int));
+  sc_copy_out(sb, par, &R.e[SCOUT_CHOOSE0], E * (int)sizeof(ScoutEdge));
+  if (sc_stale(C, tag)) { sc_publish(C, par, tag, SC_DONE); return; }
+  sc_publish(C, par, tag, SC_CHOOSE);
+  SC_PHASE(4);
+  if (uni(g_L.found) >= 0) {
+    // x_new <- the last edge of the via chain from the chosen parent (choose_parent)
+    if (threadIdx.x == 0) {
+      g_L.n_via = 0;
+      g_L.nn_t = X;
+      load_node(C, t, g_L.eg_near[g_L.found], &g_L.cur);
+    }
+    __syncthreads();
+    via_chain(C, g_L.xn.q);
+    if (threadIdx.x == 0) {
+      g_L.xn.id = g_L.sel.id;
+      g_L.xn.parent = g_L.sel.parent;
+      for (int j = 0; j < NJ; ++j) g_L.xn.q[j] = g_L.sel.q[j];
+      for (int k = 0; k < 3; ++k) g_L.xn.c[k] = g_L.sel.c[k];
+      g_L.ext_bp = 1;
+      g_L.n_via = 0;
+    }
+    __syncthreads();
+  }
+  SC_PHASE(5);
+  if (!uni(g_L.ext_nn || g_L.ext_bp)) { sc_publish(C, par, tag, SC_DONE); return; }
+  // rewire's candidate edges (rewire())
+  const TreeDev& T = C.Q.tr[t];
+  rewire_count(T);
+  const int cnt = uni(g_L.cnt);
+  if (cnt > 0) {
+    if (threadIdx.x < cnt) {
+      const int e = threadIdx.x, v = g_L.hi_i[g_L.n_hi - 1 - e];
+      NodeRef nd;
+      load_node(C, t, v, &nd);
+      for (int j = 0; j < NJ; ++j) { g_L.eg_start[e][j] = g_L.xn.q[j]; g_L.eg_target[e][j] = nd.q[j]; }
+      for (int k = 0; k < 3; ++k) g_L.eg_base[e][k] = g_L.xn.c[k];
+      g_L.eg_near[e] = v;
+    }
+    __syncthreads();
+    edge_costs(C, cnt);
+    if (threadIdx.x < cnt) {
+      const int e = threadIdx.x, v = g_L.eg_near[e];
+      g_L.eg_need[e] = (v != g_L.xn.parent) && (T.parent[v] != 0) && (g_L.eg_cost[e][0] < T.cost[v]);
+    }
+    for (int e = cnt + threadIdx.x; e < MAXE; e += BLOCK) g_L.eg_need[e] = 0;
+    __syncthreads();
+    edge_validity(C, cnt, false, P_XREWIRE);
+    if (threadIdx.x < cnt) {
+      const int e = threadIdx.x;
+      ScoutEdge& w = R.e[SCOUT_REWIRE0 + e];
+      for (int j = 0; j < NJ; ++j) { w.s[j] = g_L.eg_start[e][j]; w.g[j] = g_L.eg_target[e][j]; }
+      w.first = g_L.eg_need[e] ? g_L.eg_first[e] : -1;
+    }
+    if (threadIdx.x == 0) R.n_rewire = cnt;
+    __syncthreads();
+  }
+  sc_copy_out(sb, par, &R.n_choose, 4 * sizeof(int));
+  sc_copy_out(sb, par, &R.e[SCOUT_REWIRE0], cnt * (int)sizeof(ScoutEdge));
+  sc_publish(C, par, tag, SC_DONE);
+  SC_PHASE(6);
+}
+#undef SC_PHASE
+
+// Scout workgroup of a query (plan_kernel blocks nq .. 2nq-1): takes the leader's newest request, runs
+// scout_iteration on it, repeats; leaves on the stop flag (then stops its helpers) or after two idle seconds.
+__device__ void scout_main(Ctx& C) {
+  {
+    const int* src = reinterpret_cast<const int*>(C.Q.st);
+    int* dst = reinterpret_cast<int*>(&g_L.S);
+    for (int i = threadIdx.x; i < (int)(sizeof(QState) / sizeof(int)); i += BLOCK) dst[i] = src[i];
+  }
+  __syncthreads();
+  if (threadIdx.x < 32) g_L.S.prof[threadIdx.x] = 0;
+  C.Q.sampler_jb = C.Q.jb;  // the run-ahead sampler's ring
+  C.Q.jb = C.Q.sjb;         // collision jobs go to the scout's own board and helpers
+  C.Q.nworkers = C.Q.sworkers;
+  C.Q.via = C.Q.svia;
+  C.Q.rows = nullptr;
+  C.Q.trace = nullptr;
+  if (threadIdx.x == 0) {
+    g_L.count_slot = 0;
+    g_L.job_seq = 0;
+    g_L.n_via = 0;
+    g_L.near_blo = ~0ull;
+    g_L.near_bhi = 0;
+    g_L.spec = OV_NONE;
+    g_L.sp_on = 0;
+    st_agent(&C.Q.scb->xcc, xcc_id() + 1);
+  }
+  __syncthreads();
+  unsigned last = 0;
+  unsigned long long t_last = wall_clock64();
+  for (int k = 0;; k ^= 1) {
+    if (threadIdx.x == 0) {
+      int go = 0;
+      if (ld_agent(&C.Q.scb->stop)) {
+        go = -1;
+      } else {
+        const unsigned long long r0 = ld_agent(&C.Q.scb->req[0]), r1 = ld_agent(&C.Q.scb->req[1]);
+        const unsigned tag = (unsigned)(r0 >> 32);
+        if (tag > last && (unsigned)(r1 >> 32) == tag) {
+          go = 1;
+          g_L.cnt = (int)(unsigned)r0;        // X | t << 28 | opt << 29
+          g_L.nn_t = (int)(unsigned)r1;       // sampler parameter version
+          g_L.tree_expand = (int)tag;
+        } else if (wall_clock64() - t_last > 200000000ull) {
+          go = -1;  // 2 s idle
+        }
+      }
+      g_L.sp_go[k] = go;
+    }
+    __syncthreads();
+    const int go = uni(g_L.sp_go[k]);
+    if (go < 0) break;
+    if (go == 0) {
+      __builtin_amdgcn_s_sleep(2);
+      continue;
+    }
+    const unsigned w0 = (unsigned)uni(g_L.cnt), ver = (unsigned)uni(g_L.nn_t), tag = (unsigned)uni(g_L.tree_expand);
+    __syncthreads();
+    // tree words stored by the leader since this CU / XCD last cached them: drop stale copies
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const unsigned long long tb = wall_clock64();
+    if (threadIdx.x == 0) g_L.S.prof[28] += tb - t_last;  // idle: waiting for a request
+    scout_iteration(C, (long long)tag - 1, (int)(w0 >> 28) & 1, (int)(w0 & ((1u << 28) - 1)), (int)(w0 >> 29) & 1, ver);
+    last = tag;
+    t_last = wall_clock64();
+    if (threadIdx.x == 0) g_L.S.prof[31] += t_last - tb;
+  }
+  if (threadIdx.x == 0) {
+    st_agent(&C.Q.jb->stop, 1);
+    for (int k = 0; k < 32; ++k) st_agent(&C.Q.scb->prof[k], g_L.S.prof[k]);
+  }
+}
+
 // Advances every query (one workgroup each) by at most `iters` planner iterations.
 // One block per query: the planner loop.  Its collision jobs are shared with helper_kernel's blocks when the
 // query has a job board (DESIGN.md "Helpers").
 __global__ void __launch_bounds__(BLOCK) plan_kernel(const RobotDev* __restrict__ rb, SceneDev sc,
-                                                     const MapCfg* __restrict__ mc, QueryDev* qs, int iters) {
+                                                     const MapCfg* __restrict__ mc, QueryDev* qs, int nq, int scout_base,
+                                                     int iters) {
+  // blocks [0, nq): leaders; [scout_base, scout_base + nq): their scouts (scout_base a multiple of 8, so that query
+  // q's two blocks are dealt to the same XCD); any other block has nothing to do
+  const int b = (int)blockIdx.x;
+  if (b >= nq && !(scout_base > 0 && b >= scout_base && b < scout_base + nq)) return;
   stage_model(rb, mc, &g_rb, &g_mc);
   Ctx C;
   C.sc = sc;
-  C.Q = qs[blockIdx.x];
+  C.Q = qs[b < nq ? b : b - scout_base];
+  if (b >= nq) {
+    if (C.Q.scb) scout_main(C);
+    return;
+  }
   if (threadIdx.x == 0) {
+    g_L.sp_on = 0;
+    g_L.sc_same = -1;
     g_L.count_slot = 0;
     g_L.job_seq = 0;
     g_L.S = *C.Q.st;
@@ -2000,6 +2539,7 @@ __global__ void __launch_bounds__(BLOCK) plan_kernel(const RobotDev* __restrict_
 #endif
     *C.Q.st = g_L.S;
     if (C.Q.jb) st_agent(&C.Q.jb->stop, 1);
+    if (C.Q.scb) st_agent(&C.Q.scb->stop, 1);
   }
 }
 
@@ -2083,8 +2623,16 @@ __global__ void __launch_bounds__(BLOCK) helper_kernel(const RobotDev* __restric
   C.Q = qs[blockIdx.x % nq];
   const int hidx = (int)blockIdx.x / nq, nh = (int)gridDim.x / nq;
   if (!C.Q.jb) return;
-  if (C.Q.sampler && hidx == nh - 1) sampler_main(C, SL);
-  else helper_main(C, hidx, J);
+  if (C.Q.sampler && hidx == nh - 1) {
+    sampler_main(C, SL);
+  } else if (hidx < C.Q.nworkers - 1) {
+    helper_main(C, hidx, J);                 // the leader's tile helpers
+  } else if (C.Q.sjb && hidx - (C.Q.nworkers - 1) < C.Q.sworkers - 1) {
+    const int h = hidx - (C.Q.nworkers - 1);  // the scout's tile helpers
+    C.Q.jb = C.Q.sjb;
+    C.Q.nworkers = C.Q.sworkers;
+    helper_main(C, h, J);
+  }
 }
 
 __global__ void path_kernel(QueryDev* qs, int* counts) {

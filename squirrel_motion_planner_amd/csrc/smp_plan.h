@@ -40,6 +40,8 @@ struct QState {                // per query, persisted in global memory across l
   long long checked, valid, first_iter, last_iter;
   long long nn_nodes, near_nodes;  // nodes streamed by nearest / near scans (algorithmic bytes)
   long long smp_hits;              // samples taken from the run-ahead sampler
+  long long sc_nn, sc_near, sc_edge_hit, sc_edge_miss;  // scout results used: nearest, near sets, edges (+ misses)
+  unsigned long long sc_wait;      // device-clock ticks the leader waited for the scout
   unsigned long long prof[32];     // device-clock ticks per planner phase (SMP_PROF_* in smp_kernels.hip)
   unsigned long long t0, t_first, t_end, deadline;  // device wall clock (0 deadline = none)
   double cbest[3], h0[3];
@@ -103,9 +105,58 @@ struct JobBoard {
   } ring[SMP_RING];
 };
 
+// Scout (DESIGN.md "Scout"): a second workgroup per query computes the expand / near / choose-parent / rewire
+// scans and collision jobs of the leader's NEXT iteration on a snapshot of the tree that iteration expands (its
+// first X nodes, which no step of the current iteration modifies; the current iteration only appends to it).  The
+// leader takes a result only if its key matches exactly (same tree, same query configuration, same edge end
+// points) and patches the scans with the nodes appended since the snapshot, so its trees are the ones it would
+// have built alone.  Records are double-buffered by iteration parity; every word is written with sc1 stores and
+// drained before the record's stage granule, (tag << 32) | stage with tag = iteration + 1.
+constexpr int SCOUT_EDGES = 1 + 2 * MAX_NEAR;  // expand edge, choose-parent candidates, rewire candidates
+constexpr int SCOUT_CHOOSE0 = 1, SCOUT_REWIRE0 = 1 + MAX_NEAR;
+enum { SC_STARTED = 0, SC_NN = 1, SC_EXPAND = 2, SC_NEAR = 3, SC_CHOOSE = 4, SC_DONE = 5 };
+struct ScoutNN {               // stage SC_NN: nearest node of the sample in the snapshot
+  double q[NJ];                // the sample scanned
+  double d;                    // its distance (the running minimum of the reference scan, 10000 if none)
+  int id, X, t, ok;            // node id, snapshot size, tree, 1 = valid
+};
+struct ScoutNear {             // stage SC_NEAR: near set of x_new in the snapshot
+  double q[NJ];
+  int nk, n_lo, n_hi, ok, X, t;  // count, list lengths, 1 = valid, snapshot size, tree
+  int lo_i[MAX_NEAR], hi_i[MAX_NEAR];
+  double lo_c[MAX_NEAR], hi_c[MAX_NEAR];
+};
+struct ScoutEdge {             // one candidate edge: interpolation start / target, first colliding point
+  double s[NJ], g[NJ];
+  int first, pad;              // first: as eg_first (n_pts + 1 = free), -1 = not checked
+};
+struct ScoutRec {
+  ScoutNN nn;
+  ScoutNear nr;
+  int n_choose, n_rewire, pad[2];
+  ScoutEdge e[SCOUT_EDGES];    // [0] expand, [SCOUT_CHOOSE0 ..) choose-parent, [SCOUT_REWIRE0 ..) rewire
+};
+struct ScoutBoard {
+  // leader -> scout, at the start of iteration i: tag i + 2 (the request is for iteration i + 1);
+  // req[0] low word = X | t << 28 | opt << 29, req[1] low word = the sampler parameter version
+  unsigned long long req[2];
+  int stop;                    // the leader left the launch
+  int xcc;                     // the scout's XCD (XCC_ID) + 1, 0 = not yet known
+  int pad0[10];
+  unsigned long long stage[2]; // scout -> leader, by iteration parity
+  int pad1[28];
+  unsigned long long prof[32]; // the scout's phase clocks of the launch (written when it leaves)
+  ScoutRec rec[2];
+};
+
 struct QueryDev {
   QState* st;
   JobBoard* jb;                // null: no helpers
+  JobBoard* sjb;               // the scout's collision-job board (null: no scout)
+  JobBoard* sampler_jb;        // scout: the leader's board (run-ahead sampler ring)
+  ScoutBoard* scb;
+  ViaNode* svia;               // the scout's via-node scratch [via_cap]
+  int sworkers;                // scout + its tile helper workgroups
   int* trace;                  // debug only (SMP_DEBUG): host-mapped progress markers of the leader
   int nworkers;                // leader + tile helper workgroups (tile w, w + nworkers, ... is worker w's)
   int sampler;                 // 1: the last helper workgroup is the run-ahead sampler

@@ -219,6 +219,7 @@ def _result_dict(r):
              "slots_expand", "slots_choose", "slots_rewire", "slots_connect"]
     d["phases"] = {n: s.phase_seconds[i] for i, n in enumerate(names)}
     d["phase_raw"] = list(s.phase_seconds)
+    d["scout_phases"] = list(s.scout_phase_seconds)
     d["status"] = r.status
     n = r.n_waypoints
     d["path"] = np.ctypeslib.as_array(r.waypoints, shape=(n, 8)).copy() if n else np.zeros((0, 8))

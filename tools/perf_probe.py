@@ -26,6 +26,15 @@ for iters in [int(v) for v in (sys.argv[1:] or ["2000", "10000", "50000"])]:
     print("   phases:", {k: round(v, 3) for k, v in r["phases"].items()}, flush=True)
     print("   samples precomputed by the run-ahead sampler: %d of %d" % (r["samples_precomputed"], r["iterations"]),
           flush=True)
+    print("   helpers %d scout %d: nn hits %d, near hits %d, edge hits %d misses %d, leader waited %.1f us/iter" % (
+        r["helpers"], r["scout"], r["scout_nn_hits"], r["scout_near_hits"], r["scout_edge_hits"],
+        r["scout_edge_misses"], r["scout_wait_seconds"] * 1e6 / max(r["iterations"], 1)), flush=True)
+    sp = r["scout_phases"]
+    if sp[30] > 0:
+        ns = sp[30]
+        print("   scout (us per pass, %d passes): sample %.1f nn %.1f expand %.1f near %.1f choose %.1f via %.1f rewire %.1f"
+              " | publish %.1f busy %.1f idle %.1f | edge_costs %.1f tiles(job) %.1f" % (
+                  ns, *[sp[k] * 1e6 / ns for k in (0, 1, 2, 3, 4, 5, 6, 29, 31, 28, 9, 7)]), flush=True)
     raw = r["phase_raw"]
     nj = max(raw[15] * 1e8, 1)
     print("   jobs %d: publish %.1f us, own %.1f us, wait %.1f us per job" % (

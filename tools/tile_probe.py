@@ -34,7 +34,7 @@ for name, X in (("tree-edges", Q), ("random", R)):
     for tile, grid in ((32, 1), (16, 1), (8, 1), (32, 2048)):
         ms = ctypes.c_double()
         hz = ctypes.c_double()
-        ticks = (ctypes.c_uint64 * 6)()
+        ticks = (ctypes.c_uint64 * 8)()
         L.check(lib.smp_probe_check_latency(gp.h, soa.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), n, 1, 1, grid, tile,
                                             ctypes.byref(ms), ticks, ctypes.byref(hz)))
         tiles = (n + tile - 1) // tile
@@ -42,4 +42,5 @@ for name, X in (("tree-edges", Q), ("random", R)):
         print("%-10s tile %2d n %7d grid %5d: %.2f ms  %.3g configs/s  per tile %.2f us  stages(us) A %.2f B %.2f C0 %.2f C %.2f"
               % (name, tile, n, grid, ms.value, n / (ms.value * 1e-3), ms.value * 1e3 / tiles * (grid if grid > 1 else 1) /
                  (1 if grid == 1 else min(grid, tiles)), *per_tile_us[:4]), flush=True)
-        print("   shader clock %.3f GHz" % (ticks[4] / (ticks[5] / hz.value) / 1e9 if ticks[5] else 0), flush=True)
+        print("   shader clock %.3f GHz; wave 0 in C: centres + map sweeps %.2f us, self test %.2f us per tile" % (
+            ticks[4] / (ticks[5] / hz.value) / 1e9 if ticks[5] else 0, per_tile_us[6], per_tile_us[7]), flush=True)
