@@ -2259,7 +2259,9 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
   sc_publish(C, par, tag, SC_NN);
   SC_PHASE(1);
   edge_costs(C, 1);
-  edge_validity(C, 1, false, P_XEXPAND);
+  // the near set of the edge's end (x_new if the edge is valid) is scanned while the helpers check the edge
+  if (threadIdx.x == 0) g_L.spec = OV_NONE;
+  edge_validity(C, 1, false, P_XEXPAND, opt ? OV_NEAR_EXPAND : OV_NONE, t);
   if (threadIdx.x == 0) {
     for (int j = 0; j < NJ; ++j) { R.e[0].s[j] = g_L.eg_start[0][j]; R.e[0].g[j] = g_L.eg_target[0][j]; }
     R.e[0].first = g_L.eg_first[0];
@@ -2287,7 +2289,7 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
   sc_publish(C, par, tag, SC_EXPAND);
   SC_PHASE(2);
   // near set of x_new (the leader's, before choose_parent)
-  near_set<20>(C, t, g_L.xn.q, X);
+  if (!(uni(g_L.ext_nn) && take_spec(OV_NEAR_EXPAND))) near_set<20>(C, t, g_L.xn.q, X);
   if (threadIdx.x < 20) {
     R.nr.lo_i[threadIdx.x] = g_L.lo_i[threadIdx.x]; R.nr.lo_c[threadIdx.x] = g_L.lo_c[threadIdx.x];
     R.nr.hi_i[threadIdx.x] = g_L.hi_i[threadIdx.x]; R.nr.hi_c[threadIdx.x] = g_L.hi_c[threadIdx.x];
