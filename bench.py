@@ -39,20 +39,39 @@ def parse():
                     help="helper workgroups per query (0 automatic, -1 none: e.g. for counter passes, which "
                          "serialise dispatches)")
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--workload", choices=("c2", "c3", "c5"), default="c2",
+                    help="c2 (default, BASELINE configs[1]): the single C2 query; c3: random (start, goal) pairs on "
+                         "the C2 scene, 8 per GPU (configs[2]); c5: 2 cm dense clutter, 8 random queries per GPU "
+                         "(configs[4])")
+    ap.add_argument("--iterations", type=int, default=None,
+                    help="iteration budget per query instead of --samples (C3: 1e5 in SURVEY.md 8d)")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
 
 
-def cpu_baseline(sc, samples, seed):
-    """The oracle (sequential C++ restatement of the reference loop, 1 thread) on the same query and budget.
+def workload_name(a, sc):
+    if a.workload == "c2":
+        return ("C2: single start->goal query, 10x10x2 m octomap @5 cm, 20 boxes, budget %s, "
+                "path_optimality_threshold=-inf" % (("%d iterations" % a.iterations) if a.iterations else
+                                                   ("%d collision-checked samples" % a.samples)))
+    if a.workload == "c3":
+        return ("C3: random collision-free start/goal pairs (seed 7) on the C2 scene, %d queries per GPU, "
+                "path_optimality_threshold=-inf" % a.queries_per_gpu)
+    return ("C5: 10x10x2 m @2 cm dense clutter voxelised from a 2e6-point synthetic cloud (seed 11), %d random "
+            "queries per GPU, path_optimality_threshold=-inf" % a.queries_per_gpu)
 
-    Same seed, scene and sample budget as GPU step 0, so the CPU run plans the identical trees; the bench
+
+def cpu_baseline(sc, pair, a, step0_seed):
+    """The oracle (sequential C++ restatement of the reference loop, 1 thread) on query 0 of GPU step 0.
+
+    Same scene, (start, goal), seed, query id and budget, so the CPU run plans the identical trees; the bench
     records whether its counters match the GPU's (a parity check of the measured run itself)."""
     from oracle import oracle as O
     rob = O.OracleRobot(os.path.join(ROOT, "squirrel_motion_planner_amd", "data", "robotino_model.json"))
     orc = O.Oracle(rob, O.OracleScene(sc.keys, sc.res))
-    r = orc.plan(sc.start, sc.goal, env_x=sc.env_x, env_y=sc.env_y, max_checked=samples, seed=seed,
-                 opt_thresh=-math.inf)
+    budget = dict(max_iter=a.iterations) if a.iterations else dict(max_checked=a.samples, max_iter=0)
+    r = orc.plan(pair[0], pair[1], env_x=sc.env_x, env_y=sc.env_y, seed=step0_seed, query=0,
+                 opt_thresh=-math.inf, **budget)
     cpu = "unknown"
     try:
         for line in open("/proc/cpuinfo"):
@@ -62,9 +81,9 @@ def cpu_baseline(sc, samples, seed):
     except OSError:
         pass
     return {"value": r["checked"] / r["t_total"], "unit": "configs/s", "cores": 1, "kind": "port",
-            "sample": "C2 query (seed %d), oracle/smp_oracle.cpp single thread, budget %d samples: %d iterations, "
-                      "%d configs checked in %.2f s on %s" % (seed, samples, r["iterations"], r["checked"],
-                                                           r["t_total"], cpu),
+            "sample": "%s query 0 (seed %d), oracle/smp_oracle.cpp single thread, same budget: %d iterations, "
+                      "%d configs checked in %.2f s on %s" % (a.workload.upper(), step0_seed, r["iterations"],
+                                                           r["checked"], r["t_total"], cpu),
             "valid_configs_per_s": r["valid"] / r["t_total"],
             "iterations": r["iterations"], "checked": r["checked"], "time_first_solution_s": r["t_first"],
             "iters_per_s": r["iterations"] / r["t_total"], "cost_best": r["cost"][0]}
@@ -85,24 +104,35 @@ def main():
     from squirrel_motion_planner_amd import distributed as D, scenes
     from squirrel_motion_planner_amd.planner import GpuPlanner, Scene
 
-    sc = scenes.box_room()
+    if a.workload != "c2" and a.queries_per_gpu == 1:
+        a.queries_per_gpu = 8
+    # every rank builds the same scene description (seeded); only rank 0 turns it into the grid
+    sc = scenes.clutter_cloud() if a.workload == "c5" else scenes.box_room()
     # scene: rank 0 builds the grid (octomap keys -> bitset + box-gap field) and broadcasts it once (RCCL/xGMI)
     s0 = Scene.from_keys(sc.keys, sc.res) if rank == 0 else None
     scene = D.broadcast_scene(s0, device="cuda") if world > 1 else s0
 
     gp = GpuPlanner(device=local, path_optimality_threshold=-math.inf, helpers=a.helpers)
-    # helper workgroups per query as the library resolves them (0 = auto: the CUs left over by the queries, at most
-    # 63; with two or more, the last one is the run-ahead sampler)
-    ncu = torch.cuda.get_device_properties(local).multi_processor_count
-    helpers_eff = (min(63, max(0, ncu // a.queries_per_gpu - 1)) if a.helpers == 0 else max(a.helpers, 0))
     gp.set_scene(scene)
+
+    # (start, goal) of every query of the job: C2 repeats its own pair; C3/C5 draw world * queries_per_gpu
+    # collision-free pairs (scenes.random_queries, seed 7) and each rank takes its own slice (no collective)
+    n_job = world * a.queries_per_gpu
+    if a.workload == "c2":
+        pairs = [(sc.start, sc.goal)] * n_job
+    else:
+        pairs = scenes.random_queries(sc, n_job, seed=7, check=lambda q: bool(gp.check_configs([q])[0]))
+        if len(pairs) < n_job:
+            raise RuntimeError("only %d collision-free query pairs" % len(pairs))
 
     def queries(step, samples):
         out = []
         for k in range(a.queries_per_gpu):
             qid = rank * a.queries_per_gpu + k
-            out.append(GpuPlanner.make_query(sc.start, sc.goal, sc.env_x, sc.env_y, samples=samples,
-                                             seed=a.seed + 1000 * step, query_id=qid))
+            s, g = pairs[qid]
+            budget = dict(iterations=a.iterations) if a.iterations else dict(samples=samples)
+            out.append(GpuPlanner.make_query(s, g, sc.env_x, sc.env_y, seed=a.seed + 1000 * step, query_id=qid,
+                                             **budget))
         return out
 
     for w in range(a.warmup):
@@ -174,10 +204,14 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (seeded box scene + seeded Philox samples)",
-            "config": {"workload": "C2: single start->goal query, 10x10x2 m octomap @5 cm, 20 boxes, budget %d "
-                                   "collision-checked samples, path_optimality_threshold=-inf" % a.samples,
-                       "queries_per_gpu": a.queries_per_gpu, "samples_per_query": a.samples,
-                       "robot": "robotino 8-DoF, 64-sphere model", "helpers_per_query": helpers_eff,
+            "config": {"workload": workload_name(a, sc),
+                       "queries_per_gpu": a.queries_per_gpu,
+                       "budget_per_query": ("%d iterations" % a.iterations) if a.iterations else
+                                           ("%d collision-checked samples" % a.samples),
+                       "robot": "robotino 8-DoF, 64-sphere model",
+                       # helper workgroups per query as the library resolved them (0 = auto: the CUs left over by
+                       # the queries; with a scout, split between the leader's and the scout's tiles + the sampler)
+                       "helpers_per_query": int(step0["helpers"]), "scout": int(step0["scout"]),
                        "parallelism": "one leader workgroup per query + helper workgroups sharing its collision "
                        "tiles; queries sharded over ranks, scene broadcast once"},
             "valid_configs_per_s": valid / elapsed,
@@ -191,7 +225,7 @@ def main():
                          "algorithmic_bytes_rank0": alg_bytes_rank0},
         }
         if not a.no_cpu and world == 1:
-            cb = cpu_baseline(sc, a.samples, a.seed)
+            cb = cpu_baseline(sc, pairs[0], a, step0_seed=a.seed)
             cb["same_result_as_gpu_step0"] = bool(cb["checked"] == step0["configs_checked"] and
                                                   cb["iterations"] == step0["iterations"] and
                                                   cb["cost_best"] == step0["cost_best"][0])

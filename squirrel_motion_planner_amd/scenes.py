@@ -117,9 +117,14 @@ def box_room(seed=42, res=0.05, n_boxes=20, start=None, goal=None):
 
 
 def narrow_passage(res=0.05, slot=0.24):
-    """C4: wall at x = 0 with a slot `slot` m wide (2 x ~0.12 m arm-link width) at z 0.55-0.79."""
+    """C4: wall at x = 0 with a slot `slot` m wide (2 x ~0.12 m arm-link width) at z 0.55-0.79.
+
+    Start: folded arm 0.9 m in front of the wall.  Goal: the hand inside the slot (hand_wrist_link at x 0.027,
+    y -0.024, z 0.613), one of the few collision-free configurations that reach into it (found by rejection
+    sampling with the oracle); the straight start->goal edge collides, so the query is planned, not connected
+    directly (birrt_star.cpp:1072-1075)."""
     start = [-0.9, 0.0, 0.0] + ARM_FOLDED
-    goal = [-0.55, 0.0, 0.0] + [0.0, 1.45, 0.0, 0.1, 0.0]
+    goal = [-0.351, -0.064, 1.074, -0.445, 0.83, -0.28, 0.395, -0.119]
     wall = _box_keys([0.0, -5.0, 0.0], [0.1, 5.0, 2.0], res)
     rel = (wall - KEY_OFFSET + 0.5) * res
     hole = (np.abs(rel[:, 1]) < slot / 2) & (rel[:, 2] > 0.55) & (rel[:, 2] < 0.79)

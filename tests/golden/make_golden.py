@@ -24,7 +24,7 @@ PLAN_CASES = {
     "c1_direct": (scenes.empty_room, dict(max_iter=50, seed=1)),
     "c2_boxes_300": (scenes.box_room, dict(max_iter=300, seed=3)),
     "c2_boxes_yaml": (scenes.box_room, dict(max_iter=200, seed=5, near_r=1.5, step=0.6)),
-    "c4_passage": (scenes.narrow_passage, dict(max_iter=150, seed=2)),
+    "c4_passage": (scenes.narrow_passage, dict(max_iter=400, seed=2)),
 }
 
 
