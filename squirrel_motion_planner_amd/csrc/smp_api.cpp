@@ -108,6 +108,7 @@ struct smp_planner {
   MapCfg* d_mc = nullptr;
   DBuf<uint64_t> d_bricks;
   DBuf<uint16_t> d_d2;
+  DBuf<uint8_t> d_d2b;
   SceneDev sc{};
   bool have_scene = false;
   double scene_res = 0.05;
@@ -139,6 +140,8 @@ static int update_mapcfg(smp_planner* p) {
   HIPCHK(hipStreamSynchronize(p->stream));
   return SMP_OK;
 }
+
+extern "C" int smp_debug_bounds(int* out);
 
 extern "C" {
 
@@ -340,7 +343,7 @@ void smp_planner_destroy(smp_planner* p) {
   (void)hipStreamSynchronize(p->stream);
   for (auto& q : p->qb) q.release();
   p->d_qdev.release(); p->d_counts.release(); p->d_cq.release(); p->d_valid.release();
-  p->d_bricks.release(); p->d_d2.release();
+  p->d_bricks.release(); p->d_d2.release(); p->d_d2b.release();
   if (p->d_rb) (void)hipFree(p->d_rb);
   if (p->d_mc) (void)hipFree(p->d_mc);
   if (p->ev0) (void)hipEventDestroy(p->ev0);
@@ -363,6 +366,18 @@ int smp_planner_set_scene(smp_planner* p, const smp_scene* s) {
   p->sc.ox = s->h.ox; p->sc.oy = s->h.oy; p->sc.oz = s->h.oz; p->sc.res = s->h.res; p->sc.inv_res = 1.0 / s->h.res;
   p->sc.bricks = p->d_bricks.p;
   p->sc.d2 = p->d_d2.p;
+  // byte copy of the field when every sphere's threshold is below 255 (SceneDev.d2b)
+  uint32_t tmax = 0;
+  for (int k = 0; k < p->robot.dev.n_sph; ++k) tmax = std::max(tmax, sphere_threshold(p->robot.dev.sph_r[k], s->h.res));
+  p->sc.d2b = nullptr;
+  if (tmax < 255) {
+    std::vector<uint8_t> b(s->h.d2.size());
+    for (size_t i = 0; i < b.size(); ++i) b[i] = (uint8_t)std::min<uint16_t>(s->h.d2[i], 255);
+    HIPCHK(p->d_d2b.reserve(b.size()));
+    HIPCHK(hipMemcpyAsync(p->d_d2b.p, b.data(), b.size(), hipMemcpyHostToDevice, p->stream));
+    HIPCHK(hipStreamSynchronize(p->stream));  // b is released on return
+    p->sc.d2b = p->d_d2b.p;
+  }
   p->have_scene = true;
   p->scene_res = s->h.res;
   return update_mapcfg(p);
@@ -698,6 +713,12 @@ extern "C" int smp_plan_batch(smp_planner* p, const smp_query* qs, int nq, smp_r
     }
     HIPCHK(hipStreamSynchronize(p->stream));
     if (nh > 0) HIPCHK(hipStreamSynchronize(p->hstream));
+    if (std::getenv("SMP_BOUNDS")) {
+      int dbg[8];
+      if (smp_debug_bounds(dbg) == 0 && dbg[0])
+        std::fprintf(stderr, "[smp] bounds: line %d id %d block %d tree %d limit %d (launch %lld)\n", dbg[0], dbg[1],
+                     dbg[2], dbg[3], dbg[4], (long long)launches);
+    }
     float ms = 0;
     HIPCHK(hipEventElapsedTime(&ms, p->ev0, p->ev1));
     total_ms += ms;

@@ -304,24 +304,35 @@ __device__ __forceinline__ void collide_tile(const RobotDev* __restrict__ rb, co
   unsigned long long ta = (prof && tid == 0) ? wall_clock64() : 0;
   // B: 3 lanes per configuration, one row each.  Row r of T * L needs only row r of T (and all of the local
   // frame L), so each lane carries its row through the whole chain in registers, no exchange between lanes;
-  // fmul's evaluation order.
+  // fmul's evaluation order.  The next step's local frame is loaded before this step's products (software
+  // pipelining: the LDS latency hides behind the dependent fp64 chain instead of adding to it).
   if (tid < nc * 3) {
     const int c = tid / 3, r = tid - c * 3;
     double t0 = r == 0 ? 1.0 : 0.0, t1 = r == 1 ? 1.0 : 0.0, t2 = r == 2 ? 1.0 : 0.0;
     double tp = r == 2 ? rb->root_z : 0.0;
+    double l[12];
+    int bd = rb->ch_body[0];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) l[i] = L.u.lf[c][0][i];
     for (int k = 0; k < nch; ++k) {
-      const double* l = L.u.lf[c][k];
+      const int kn = k + 1 < nch ? k + 1 : k;
+      double ln[12];
+#pragma unroll
+      for (int i = 0; i < 12; ++i) ln[i] = L.u.lf[c][kn][i];
+      const int bdn = rb->ch_body[kn];
       const double n0 = t0 * l[0] + t1 * l[3] + t2 * l[6];
       const double n1 = t0 * l[1] + t1 * l[4] + t2 * l[7];
       const double n2 = t0 * l[2] + t1 * l[5] + t2 * l[8];
       const double m = t0 * l[9] + t1 * l[10] + t2 * l[11];
       tp = m + tp;
       t0 = n0; t1 = n1; t2 = n2;
-      const int bd = rb->ch_body[k];
       if (bd >= 0) {
         double* o = L.fr[c][bd];
         o[r * 3 + 0] = t0; o[r * 3 + 1] = t1; o[r * 3 + 2] = t2; o[9 + r] = tp;
       }
+#pragma unroll
+      for (int i = 0; i < 12; ++i) l[i] = ln[i];
+      bd = bdn;
     }
   }
   __syncthreads();
@@ -358,8 +369,13 @@ __device__ __forceinline__ void collide_tile(const RobotDev* __restrict__ rb, co
       }
     }
     uint32_t dv[MAXU];
+    if (sc.d2b) {
 #pragma unroll
-    for (int u = 0; u < MAXU; ++u) dv[u] = cell[u] >= 0 ? (uint32_t)sc.d2[cell[u]] : 0xffffffffu;
+      for (int u = 0; u < MAXU; ++u) dv[u] = cell[u] >= 0 ? (uint32_t)sc.d2b[cell[u]] : 0xffffffffu;
+    } else {
+#pragma unroll
+      for (int u = 0; u < MAXU; ++u) dv[u] = cell[u] >= 0 ? (uint32_t)sc.d2[cell[u]] : 0xffffffffu;
+    }
 #pragma unroll
     for (int u = 0; u < MAXU; ++u) {
       const int it = u * 64 + lane;
@@ -392,6 +408,7 @@ __device__ __forceinline__ void collide_tile(const RobotDev* __restrict__ rb, co
       if (todo) {
         const int nsp = rb->n_spairs;
         uint32_t sh = 0;
+#pragma unroll 4
         for (int p = lane; p < nsp; p += 64) {
           const uint32_t ab = rb->sp_ab[p];
           const int a = ab & 0xff, b = ab >> 8;

@@ -257,9 +257,24 @@ __device__ __forceinline__ bool same8(const double* a, const double* b) {
 }
 
 // --------------------------------------------------------------------------------------- node access
-__device__ __forceinline__ void load_node(const Ctx& C, int t, int id, NodeRef* o) {
+// SMP_BOUNDS builds (debugging): out-of-range node ids are recorded in g_dbg (first one: source line, id, block,
+// tree) and replaced by 0 instead of being dereferenced; smp_debug_bounds() reads the record.
+#ifdef SMP_BOUNDS
+__device__ int g_dbg[8];
+#define BCHK(id, lim, line, t)                                                                          \
+  if ((unsigned)(id) >= (unsigned)(lim)) {                                                             \
+    if (atomicCAS(&g_dbg[0], 0, (line)) == 0) { g_dbg[1] = (id); g_dbg[2] = blockIdx.x; g_dbg[3] = (t); g_dbg[4] = (lim); } \
+    id = 0;                                                                                            \
+  }
+#else
+#define BCHK(id, lim, line, t)
+#endif
+#define load_node(C, t, id, o) load_node_at(C, t, id, o, __LINE__)
+__device__ __forceinline__ void load_node_at(const Ctx& C, int t, int id, NodeRef* o, int line) {
   const TreeDev& T = C.Q.tr[t];
   int cap = C.Q.st->cap;
+  BCHK(id, cap, line, t);
+  (void)line;
   for (int j = 0; j < NJ; ++j) o->q[j] = T.q[(size_t)j * cap + id];
   for (int k = 0; k < 3; ++k) o->c[k] = T.cost[(size_t)k * cap + id];
   o->id = id;
@@ -322,30 +337,36 @@ __device__ int nearest_scan(const Ctx& C, int t, const double* q, int i_begin, d
   for (int j = 0; j < NJ; ++j) qq[j] = q[j];
   double best = 10000.0, best_s = 1e300;
   int bid = 0x7fffffff;
-  for (int i0 = i_begin + threadIdx.x; i0 < n; i0 += 2 * BLOCK) {
-    const int i1 = i0 + BLOCK;
-    const bool v1 = i1 < n;
-    double a[NJ], b[NJ];
+  // NPT nodes per thread per round, all loads of a round issued together: a round costs about one memory latency
+  // plus one 8-term dependent sum, so few rounds matter more than few loads (a 4k-node tree is 2 rounds)
+  constexpr int NPT = 4;
+  for (int i0 = i_begin + threadIdx.x; i0 < n; i0 += NPT * BLOCK) {
+    double a[NPT][NJ];
+#pragma unroll
+    for (int u = 0; u < NPT; ++u) {
+      const int i = i0 + u * BLOCK;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) a[u][j] = i < n ? (tq + (size_t)j * cap)[(unsigned)i] : 0.0;
+    }
+    double s[NPT];
+#pragma unroll
+    for (int u = 0; u < NPT; ++u) s[u] = 0.0;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-      a[j] = (tq + (size_t)j * cap)[(unsigned)i0];
-      b[j] = v1 ? (tq + (size_t)j * cap)[(unsigned)i1] : 0.0;
-    }
-    double sa = 0.0, sb = 0.0;
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      double d = qq[j] - a[j];
-      sa += d * d;
-      double e = qq[j] - b[j];
-      sb += e * e;
+      for (int u = 0; u < NPT; ++u) {
+        const double d = qq[j] - a[u][j];
+        s[u] += d * d;
+      }
     }
-    if (sa < best_s) {
-      double dist = sqrt(sa);
-      if (dist < best) { best = dist; bid = i0; best_s = sa; }
-    }
-    if (v1 && sb < best_s) {
-      double dist = sqrt(sb);
-      if (dist < best) { best = dist; bid = i1; best_s = sb; }
+    // this thread's nodes in increasing index order (first strict minimum)
+#pragma unroll
+    for (int u = 0; u < NPT; ++u) {
+      const int i = i0 + u * BLOCK;
+      if (i < n && s[u] < best_s) {
+        const double dist = sqrt(s[u]);
+        if (dist < best) { best = dist; bid = i; best_s = s[u]; }
+      }
     }
   }
   for (int off = 32; off > 0; off >>= 1) {
@@ -1728,6 +1749,7 @@ __device__ void cost_update(const Ctx& C, int t, int v, const double* red) {
   while (sp > 0) {
     if (++visits > S.n[t]) { S.status = -7; S.phase = 2; return; }  // a loop in the tree: fail loudly
     int id = stack[--sp];
+    BCHK(id, cap, __LINE__, t);
     double nc[3];
     for (int k = 0; k < 3; ++k) { nc[k] = T.cost[(size_t)k * cap + id] + red[k]; st_tree(&T.cost[(size_t)k * cap + id], nc[k]); }
     if (S.have_sol) {
@@ -1822,7 +1844,13 @@ __device__ void rewire_count(const TreeDev& T) {
     const int n = g_L.nk, lane = threadIdx.x;
     const int m = n >= g_L.S.max_near ? g_L.S.max_near : n;
     bool ok = false;
-    if (lane < m) ok = g_L.xn.c[0] < T.cost[g_L.hi_i[g_L.n_hi - 1 - lane]];
+    if (lane < m) {
+      int hv = g_L.n_hi - 1 - lane;
+      BCHK(hv, MAX_NEAR, __LINE__, 9);
+      int v = g_L.hi_i[hv];
+      BCHK(v, g_L.S.cap, __LINE__, 9);
+      ok = g_L.xn.c[0] < T.cost[v];
+    }
     const int cnt = __popcll(__ballot(ok));
     if (lane == 0) g_L.cnt = cnt;
   }
@@ -1853,7 +1881,9 @@ __device__ void rewire(const Ctx& C, int t) {
   if (threadIdx.x < cnt) {
     int e = threadIdx.x, v = g_L.eg_near[e];
     // costs only decrease during the loop, so a candidate failing against the current cost never passes
-    g_L.eg_need[e] = (v != g_L.xn.parent) && (T.parent[v] != 0) && (g_L.eg_cost[e][0] < T.cost[v]);
+    int vv = v;
+    BCHK(vv, g_L.S.cap, __LINE__, t);
+    g_L.eg_need[e] = (vv != g_L.xn.parent) && (T.parent[vv] != 0) && (g_L.eg_cost[e][0] < T.cost[vv]);
   }
   for (int e = cnt + threadIdx.x; e < MAXE; e += BLOCK) g_L.eg_need[e] = 0;
   __syncthreads();
@@ -1865,8 +1895,10 @@ __device__ void rewire(const Ctx& C, int t) {
   for (int e0 = 0;;) {
     if (threadIdx.x >= e0 && threadIdx.x < cnt) {
       const int e = threadIdx.x, v = g_L.eg_near[e];
-      g_L.rw_par[e] = T.parent[v];
-      for (int k = 0; k < 3; ++k) g_L.rw_cost[e][k] = T.cost[(size_t)k * cap + v];
+      int vv = v;
+      BCHK(vv, g_L.S.cap, __LINE__, t);
+      g_L.rw_par[e] = T.parent[vv];
+      for (int k = 0; k < 3; ++k) g_L.rw_cost[e][k] = T.cost[(size_t)k * cap + vv];
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -2703,3 +2735,11 @@ __global__ void __launch_bounds__(BLOCK) near_probe_kernel(const double* tq, con
 }
 
 }  // namespace smp
+
+#ifdef SMP_BOUNDS
+extern "C" int smp_debug_bounds(int* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(smp::g_dbg), 8 * sizeof(int)) == hipSuccess ? 0 : -1;
+}
+#else
+extern "C" int smp_debug_bounds(int* out) { for (int i = 0; i < 8; ++i) out[i] = 0; return 1; }
+#endif

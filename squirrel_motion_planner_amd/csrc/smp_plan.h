@@ -8,7 +8,10 @@ namespace smp {
 
 constexpr int MAX_PTS = 32;    // num_traj_segments_interp upper bound (reference default 20)
 constexpr int MAX_NEAR = 32;   // max_near_nodes upper bound (reference default 20)
-constexpr int MAXE = 24;       // edges per validity / cost batch
+#ifndef SMP_MAXE
+#define SMP_MAXE 24
+#endif
+constexpr int MAXE = SMP_MAXE;  // edges per validity / cost batch 
 
 struct NodeRef {               // what the reference passes by value (Node, data_structs.h:29-45)
   double q[NJ];

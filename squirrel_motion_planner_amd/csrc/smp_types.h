@@ -41,11 +41,15 @@ struct RobotDev {
 // axis.  bricks: one 64-bit occupancy mask per 4x4x4 cells, bit (k&3)*16 + (j&3)*4 + (i&3) of brick
 // ((k>>2)*bny + (j>>2))*bnx + (i>>2).  d2: per cell the squared box-to-box gap (voxel units, clamped to
 // 65535) to the nearest occupied cell -- a lower bound of (distance to any occupied box / res)^2.
+// d2b: the same field clamped to 255, one byte per cell (half the bytes, so a 5 cm 10x10x2 m grid stays
+// resident in one XCD's 4 MB L2); set only when every sphere threshold T is below 255, where
+// min(d2, 255) > T  <=>  d2 > T, so the prefilter decides identically.
 struct SceneDev {
   int nx, ny, nz, bnx, bny;
   double ox, oy, oz, res, inv_res;
   const uint64_t* bricks;
   const uint16_t* d2;
+  const uint8_t* d2b;
 };
 
 // Per (scene, disabled-link set) sphere constants.
