@@ -175,6 +175,44 @@ class BiRRTstarPlanner {
           "smp_set_disabled_map_links");
   }
 
+  // The node's keyframe loops over isConfigValid (fold / unfold arm, squirrel_8dof_planner.cpp:759-784, 814-823) as
+  // one batched check: index of the first pose in collision, or -1 when all are valid.
+  long long firstInvalidConfig(const vector<vector<double> >& configs, bool check_self_collision,
+                               bool check_map_collision) {
+    need();
+    vector<double> rows;
+    rows.reserve(configs.size() * 8);
+    for (size_t i = 0; i < configs.size(); ++i) {
+      if (configs[i].size() != 8) return (long long)i;  // isConfigValid rejects a wrong dimension
+      rows.insert(rows.end(), configs[i].begin(), configs[i].end());
+    }
+    int64_t first = -1;
+    check(smp_check_sequence(planner_, rows.data(), (int64_t)configs.size(), check_self_collision, check_map_collision,
+                             &first), "smp_check_sequence");
+    return first;
+  }
+
+  // An octomap_msgs/Octomap straight from the octomap server (squirrel_8dof_planner.cpp:875-883: binaryMsgToMap /
+  // fullMsgToMap), optionally with the node's floor square around (floor_x, floor_y) (SP:886-904).
+  void setOctreeMsg(const std::string& id, double resolution, bool binary, const std::vector<int8_t>& data,
+                    bool insert_floor = false, double floor_x = 0.0, double floor_y = 0.0, double floor_distance = 3.0) {
+    need();
+    smp_scene_opts o;
+    smp_scene_opts_default(&o);
+    o.insert_floor = insert_floor ? 1 : 0;
+    o.floor_center[0] = floor_x;
+    o.floor_center[1] = floor_y;
+    o.floor_distance = floor_distance;
+    smp_scene* s = nullptr;
+    check(smp_scene_from_octomap_msg(id.c_str(), resolution, binary ? 1 : 0,
+                                     reinterpret_cast<const uint8_t*>(data.empty() ? nullptr : data.data()),
+                                     data.size(), &o, &s),
+          "smp_scene_from_octomap_msg");
+    int st = smp_planner_set_scene(planner_, s);
+    smp_scene_destroy(s);
+    check(st, "smp_planner_set_scene");
+  }
+
   bool isConfigValid(const vector<double>& config, bool check_self_collision, bool check_map_collision) {
     need();
     if (config.size() != 8) return false;
@@ -226,5 +264,35 @@ class BiRRTstarPlanner {
 };
 
 }  // namespace birrt_star_motion_planning
+
+namespace smp_node {
+
+// Planner::normalizeTrajectory (squirrel_8dof_planner.cpp:1557-1637), same signature and the same behaviour: the
+// output is left untouched for an empty normalized pose, a single pose or a dimension mismatch.  Host only.
+inline void normalizeTrajectory(const std::vector<std::vector<double> >& trajectoryRaw,
+                                std::vector<std::vector<double> >& trajectoryNormalized,
+                                const std::vector<double>& normalizedPose) {
+  const size_t dim = normalizedPose.size();
+  if (dim < 1 || trajectoryRaw.size() <= 1 || trajectoryRaw[0].size() != dim) return;
+  std::vector<double> raw;
+  raw.reserve(trajectoryRaw.size() * dim);
+  for (size_t i = 0; i < trajectoryRaw.size(); ++i) {
+    if (trajectoryRaw[i].size() != dim) throw std::runtime_error("smp: normalizeTrajectory: ragged trajectory");
+    raw.insert(raw.end(), trajectoryRaw[i].begin(), trajectoryRaw[i].end());
+  }
+  int64_t n = 0;
+  int st = smp_normalize_trajectory(raw.data(), (int64_t)trajectoryRaw.size(), (int)dim, normalizedPose.data(), nullptr,
+                                    0, &n);
+  std::vector<double> out((size_t)n * dim);
+  if (st == SMP_OK)
+    st = smp_normalize_trajectory(raw.data(), (int64_t)trajectoryRaw.size(), (int)dim, normalizedPose.data(),
+                                  out.data(), n, &n);
+  if (st != SMP_OK) throw std::runtime_error(std::string("smp: normalizeTrajectory: ") + smp_strerror(st));
+  trajectoryNormalized.clear();
+  for (int64_t i = 0; i < n; ++i)
+    trajectoryNormalized.push_back(std::vector<double>(out.begin() + i * dim, out.begin() + (i + 1) * dim));
+}
+
+}  // namespace smp_node
 
 #endif  // SMP_BIRRT_STAR_HPP

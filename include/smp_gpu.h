@@ -10,6 +10,10 @@
  *                              (birrt_star.cpp:1621-1624, collision_checker.hpp:76-88) for occupied leaf keys
  *   smp_scene_from_bt          the same from an octomap binary (.bt / binary octomap_msgs payload), with the
  *                              node's floor insertion (squirrel_8dof_planner.cpp:862-917)
+ *   smp_scene_from_ot          the same from an octomap full-format file (.ot, the octomap_server's input,
+ *                              launch/simulation.launch:51)
+ *   smp_scene_from_octomap_msg the same from an octomap_msgs/Octomap payload (id, resolution, binary flag, data):
+ *                              binaryMsgToMap / fullMsgToMap (squirrel_8dof_planner.cpp:875-883)
  *   smp_scene_from_grid        the same from a broadcast grid (multi-GPU: one RCCL broadcast per scene)
  *   smp_planner_create         BiRRTstarPlanner::initialize (birrt_star.cpp:11-326) on one GPU
  *   smp_planner_set_scene      BiRRTstarPlanner::setOctree (copies; caller keeps ownership)
@@ -20,6 +24,9 @@
  *   smp_plan_batch             independent queries against one scene (one workgroup each)
  *   smp_check_configs          batched isConfigValid (birrt_star.cpp:6897-6908) -> valid flags
  *   smp_is_config_valid        BiRRTstarPlanner::isConfigValid for one configuration
+ *   smp_check_sequence         the node's keyframe loops over isConfigValid (fold / unfold arm,
+ *                              squirrel_8dof_planner.cpp:759-784, 814-823): first invalid pose, one kernel launch
+ *   smp_normalize_trajectory   Planner::normalizeTrajectory (squirrel_8dof_planner.cpp:1557-1637), host only
  *   smp_result_free            releases library-owned result buffers
  *   smp_strerror               text of a status code
  *
@@ -145,6 +152,14 @@ const char* smp_robot_link_name(const smp_robot* r, int i);
 
 int smp_scene_from_keys(const uint16_t* keys_xyz, int64_t n, const smp_scene_opts* opts, smp_scene** out);
 int smp_scene_from_bt(const uint8_t* data, size_t size, const smp_scene_opts* opts, smp_scene** out);
+/* Octomap full format (.ot): per node a float log-odds and a child-existence byte; leaves with log-odds >= 0 are
+ * occupied.  Floor insertion (opts->insert_floor) leaves cells of free leaves free when one hit does not make them
+ * occupied, as updateNode(key, true) does. */
+int smp_scene_from_ot(const uint8_t* data, size_t size, const smp_scene_opts* opts, smp_scene** out);
+/* octomap_msgs/Octomap fields: id must be "OcTree" (other tree types: SMP_ERR_PARSE, the node's "empty octomap"),
+ * binary != 0: writeBinaryData payload, else writeData payload; neither carries a text header. */
+int smp_scene_from_octomap_msg(const char* id, double resolution, int binary, const uint8_t* data, size_t size,
+                               const smp_scene_opts* opts, smp_scene** out);
 /* A scene from an exported grid (bitset + d2), e.g. after the RCCL broadcast of rank 0's scene. */
 int smp_scene_from_grid(const uint64_t* bits, const uint16_t* d2, const int dims[3], const double origin[3],
                         double resolution, smp_scene** out);
@@ -172,6 +187,14 @@ int64_t smp_get_tree(smp_planner* p, int which, int32_t* parent, double* conf, d
 
 int smp_check_configs(smp_planner* p, const double* q_soa, int64_t n, int check_self, int check_map, uint8_t* valid);
 int smp_is_config_valid(smp_planner* p, const double q[8], int check_self, int check_map, int* valid);
+/* n poses, row-major n x 8: *first_invalid = index of the first pose in collision, -1 if all are valid. */
+int smp_check_sequence(smp_planner* p, const double* q_rows, int64_t n, int check_self, int check_map,
+                       int64_t* first_invalid);
+/* n poses of `dim` values, row-major.  *n_out = rows of the normalized trajectory; with out == NULL only counts,
+ * else writes them (SMP_ERR_CAPACITY if out_cap < *n_out).  For dim < 1 or n <= 1 the reference leaves its output
+ * untouched: *n_out = 0.  Host only (no GPU needed). */
+int smp_normalize_trajectory(const double* raw, int64_t n, int dim, const double* normalized_pose, double* out,
+                             int64_t out_cap, int64_t* n_out);
 
 /* Kernel timing of the last smp_check_configs / smp_plan call: milliseconds on the launch stream. */
 int smp_last_kernel_ms(const smp_planner* p, double* check_ms, double* plan_ms, int64_t* plan_launches);

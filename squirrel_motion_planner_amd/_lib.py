@@ -78,6 +78,9 @@ EXPORTS = [
     ("smp_robot_link_name", ctypes.c_char_p, [_p, _i]),
     ("smp_scene_from_keys", _i, [_p, _i64, ctypes.POINTER(SceneOpts), ctypes.POINTER(_p)]),
     ("smp_scene_from_bt", _i, [_p, ctypes.c_size_t, ctypes.POINTER(SceneOpts), ctypes.POINTER(_p)]),
+    ("smp_scene_from_ot", _i, [_p, ctypes.c_size_t, ctypes.POINTER(SceneOpts), ctypes.POINTER(_p)]),
+    ("smp_scene_from_octomap_msg", _i, [ctypes.c_char_p, _d, _i, _p, ctypes.c_size_t, ctypes.POINTER(SceneOpts),
+                                        ctypes.POINTER(_p)]),
     ("smp_scene_from_grid", _i, [_p, _p, ctypes.POINTER(_i), _pd, _d, ctypes.POINTER(_p)]),
     ("smp_scene_destroy", None, [_p]),
     ("smp_scene_info", _i, [_p, ctypes.POINTER(_i), _pd, _pd, ctypes.POINTER(_i64), _pd, _pd]),
@@ -94,6 +97,8 @@ EXPORTS = [
     ("smp_get_tree", _i64, [_p, _i, _p, _p, _p]),
     ("smp_check_configs", _i, [_p, _pd, _i64, _i, _i, _p]),
     ("smp_is_config_valid", _i, [_p, _pd, _i, _i, ctypes.POINTER(_i)]),
+    ("smp_check_sequence", _i, [_p, _pd, _i64, _i, _i, ctypes.POINTER(_i64)]),
+    ("smp_normalize_trajectory", _i, [_pd, _i64, _i, _pd, _pd, _i64, ctypes.POINTER(_i64)]),
     ("smp_last_kernel_ms", _i, [_p, _pd, _pd, ctypes.POINTER(_i64)]),
     ("smp_strerror", ctypes.c_char_p, [_i]),
 ]

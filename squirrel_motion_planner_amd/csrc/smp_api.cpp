@@ -226,21 +226,43 @@ int smp_scene_from_keys(const uint16_t* keys, int64_t n, const smp_scene_opts* o
   return SMP_OK;
 }
 
-int smp_scene_from_bt(const uint8_t* data, size_t size, const smp_scene_opts* o, smp_scene** out) {
-  if (!data || !o || !out) return SMP_ERR_ARG;
+// Occupied keys + free leaves of an octomap stream -> scene (with the node's floor insertion when asked).
+static int scene_from_octomap(bool full, bool header, const uint8_t* data, size_t size, double res,
+                              const smp_scene_opts* o, smp_scene** out) {
   std::vector<uint16_t> k;
-  double res = 0;
+  std::vector<FreeLeaf> fl;
   try {
-    octomap_bt_keys(data, size, &res, &k);
+    if (full) octomap_ot_keys(data, size, &res, &k, &fl, header);
+    else octomap_bt_keys(data, size, &res, &k, &fl, header);
   } catch (const std::exception& e) {
     fprintf(stderr, "smp_gpu: %s\n", e.what());
     return SMP_ERR_PARSE;
   }
-  if (o->insert_floor) floor_keys(o->floor_center[0], o->floor_center[1], res, o->floor_distance, &k);
+  if (!(res > 0)) return SMP_ERR_ARG;
+  if (o->insert_floor) floor_keys(o->floor_center[0], o->floor_center[1], res, o->floor_distance, &k, &fl);
   smp_scene* s = new smp_scene();
   scene_from_keys(k.data(), (int64_t)k.size() / 3, res, o->z_offset, &s->h);
   *out = s;
   return SMP_OK;
+}
+
+int smp_scene_from_bt(const uint8_t* data, size_t size, const smp_scene_opts* o, smp_scene** out) {
+  if (!data || !o || !out) return SMP_ERR_ARG;
+  return scene_from_octomap(false, true, data, size, 0.0, o, out);
+}
+
+int smp_scene_from_ot(const uint8_t* data, size_t size, const smp_scene_opts* o, smp_scene** out) {
+  if (!data || !o || !out) return SMP_ERR_ARG;
+  return scene_from_octomap(true, true, data, size, 0.0, o, out);
+}
+
+int smp_scene_from_octomap_msg(const char* id, double resolution, int binary, const uint8_t* data, size_t size,
+                               const smp_scene_opts* o, smp_scene** out) {
+  if (!id || !o || !out || (size > 0 && !data) || !(resolution > 0)) return SMP_ERR_ARG;
+  // binaryMsgToMap / fullMsgToMap + dynamic_cast<octomap::OcTree*> (squirrel_8dof_planner.cpp:875-883): any
+  // other tree type is an empty octomap for the node
+  if (std::strcmp(id, "OcTree") != 0) return SMP_ERR_PARSE;
+  return scene_from_octomap(binary == 0, false, data, size, resolution, o, out);
 }
 
 int smp_scene_from_grid(const uint64_t* bits, const uint16_t* d2, const int dims[3], const double origin[3],
@@ -410,6 +432,22 @@ int smp_check_configs(smp_planner* p, const double* q_soa, int64_t n, int check_
   float ms = 0;
   HIPCHK(hipEventElapsedTime(&ms, p->ev0, p->ev1));
   p->last_check_ms = ms;
+  return SMP_OK;
+}
+
+int smp_check_sequence(smp_planner* p, const double* q_rows, int64_t n, int check_self, int check_map,
+                       int64_t* first_invalid) {
+  if (!p || !first_invalid || n < 0 || (n > 0 && !q_rows)) return SMP_ERR_ARG;
+  *first_invalid = -1;
+  if (n == 0) return SMP_OK;
+  std::vector<double> soa((size_t)n * NJ);
+  for (int64_t i = 0; i < n; ++i)
+    for (int j = 0; j < NJ; ++j) soa[(size_t)j * n + i] = q_rows[i * NJ + j];
+  std::vector<uint8_t> v((size_t)n);
+  const int st = smp_check_configs(p, soa.data(), n, check_self, check_map, v.data());
+  if (st != SMP_OK) return st;
+  for (int64_t i = 0; i < n; ++i)
+    if (!v[i]) { *first_invalid = i; break; }
   return SMP_OK;
 }
 

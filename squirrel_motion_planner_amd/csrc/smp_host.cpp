@@ -277,73 +277,133 @@ void scene_from_keys(const uint16_t* keys, int64_t n, double res, double z_offse
   build_bricks(out);
 }
 
-void floor_keys(double cx, double cy, double res, double distance, std::vector<uint16_t>* keys) {
-  // octree->coordToKey(x, y, -res/2): key = floor(coord / res) + 32768 (octomap OcTreeBaseImpl::coordToKey)
-  int kx = (int)std::floor(cx / res) + KEY_OFFSET;
-  int ky = (int)std::floor(cy / res) + KEY_OFFSET;
-  int kz = (int)std::floor((-res * 0.5) / res) + KEY_OFFSET;
+void floor_keys(double cx, double cy, double res, double distance, std::vector<uint16_t>* keys,
+                const std::vector<FreeLeaf>* free) {
+  // octree->coordToKey(x, y, -res/2): key = floor(coord * (1 / res)) + 32768 (octomap OcTreeBaseImpl::coordToKey,
+  // resolution_factor = 1.0 / resolution)
+  const double f = 1.0 / res;
+  int kx = (int)std::floor(f * cx) + KEY_OFFSET;
+  int ky = (int)std::floor(f * cy) + KEY_OFFSET;
+  int kz = (int)std::floor(f * (-res * 0.5)) + KEY_OFFSET;
   int nd = (int)(distance / res);
+  // updateNode(key, true) adds prob_hit_log (logodds(0.7), float) to an existing leaf: a free leaf stays free
+  // when its log-odds plus the hit stay below the occupancy threshold (logodds(0.5) = 0).  Only the free leaves
+  // whose key range holds the floor plane matter.
+  // a leaf at depth d with centre key k covers keys [k - h, k - h + s), h = 32768 >> d, s = 65536 >> d
+  auto inside = [](const FreeLeaf& l, int a, int v) {
+    const int lo = l.k[a] - (KEY_OFFSET >> l.depth);
+    return v >= lo && v < lo + ((2 * KEY_OFFSET) >> l.depth);
+  };
+  std::vector<FreeLeaf> fl;
+  if (free)
+    for (const FreeLeaf& l : *free)
+      if (inside(l, 2, kz) && !(l.v + kHitLogOdds >= 0.0f)) fl.push_back(l);
   for (int x = kx - nd; x <= kx + nd; ++x)
     for (int y = ky - nd; y <= ky + nd; ++y) {
+      bool stays_free = false;
+      for (const FreeLeaf& l : fl)
+        if (inside(l, 0, x) && inside(l, 1, y)) { stays_free = true; break; }
+      if (stays_free) continue;
       keys->push_back((uint16_t)x);
       keys->push_back((uint16_t)y);
       keys->push_back((uint16_t)kz);
     }
 }
 
-// Octomap binary format (OcTreeBase::writeBinaryNode): per inner node two bytes, 2 bits per child
-// (00 unknown, 01 occupied leaf, 10 free leaf, 11 inner), then the inner children recursively.
+// Occupied leaf (depth, centre key) -> its depth-16 keys; a pruned leaf at depth d covers [k - h, k + h - 1],
+// h = 32768 >> d, on every axis.
 namespace {
+void emit_leaf(std::vector<uint16_t>* keys, int depth, int kx, int ky, int kz) {
+  if (depth < 6) throw std::runtime_error("octomap: occupied leaf too coarse to expand");
+  if (depth >= 16) {
+    keys->push_back((uint16_t)kx); keys->push_back((uint16_t)ky); keys->push_back((uint16_t)kz);
+    return;
+  }
+  int h = KEY_OFFSET >> depth;
+  for (int z = kz - h; z < kz + h; ++z)
+    for (int y = ky - h; y < ky + h; ++y)
+      for (int x = kx - h; x < kx + h; ++x) {
+        keys->push_back((uint16_t)x); keys->push_back((uint16_t)y); keys->push_back((uint16_t)z);
+      }
+}
+
+// Child i of a node at depth d with centre key k (octomap computeChildKey): bit 0/1/2 of i selects +x/+y/+z.
+inline void child_key(int depth, int i, const int* k, int* c) {
+  const int half = KEY_OFFSET >> (depth + 1);
+  for (int a = 0; a < 3; ++a) c[a] = k[a] + (((i >> a) & 1) ? half : -half - (half ? 0 : 1));
+}
+
+// Octomap binary format (OccupancyOcTreeBase::readBinaryNode): per inner node two bytes, 2 bits per child --
+// 00 unknown, bit 2i only: free leaf (log-odds clamping_thres_min), bit 2i+1 only: occupied leaf
+// (clamping_thres_max), both: inner node -- then the inner children recursively in child order.
 struct BtReader {
   const uint8_t* p;
   const uint8_t* end;
   std::vector<uint16_t>* keys;
-  void node(int depth, int kx, int ky, int kz) {
+  std::vector<FreeLeaf>* free;
+  void node(int depth, const int* k) {
     if (end - p < 2) throw std::runtime_error("octomap: truncated binary stream");
-    uint8_t c14 = *p++, c58 = *p++;
-    int half = 32768 >> (depth + 1);  // center offset of the children
+    const uint8_t c14 = *p++, c58 = *p++;
     int inner[8];
     for (int i = 0; i < 8; ++i) {
-      uint8_t byte = i < 4 ? c14 : c58;
-      int b = (i & 3) * 2;
-      int b0 = (byte >> b) & 1, b1 = (byte >> (b + 1)) & 1;
-      inner[i] = (b0 && b1);
-      int cx = kx + ((i & 1) ? half : -half - (half ? 0 : 1));
-      int cy = ky + ((i & 2) ? half : -half - (half ? 0 : 1));
-      int cz = kz + ((i & 4) ? half : -half - (half ? 0 : 1));
-      if (!b0 && b1) emit(depth + 1, cx, cy, cz);
+      const uint8_t byte = i < 4 ? c14 : c58;
+      const int b = (i & 3) * 2;
+      const int b0 = (byte >> b) & 1, b1 = (byte >> (b + 1)) & 1;
+      inner[i] = b0 && b1;
+      int c[3];
+      child_key(depth, i, k, c);
+      if (!b0 && b1) emit_leaf(keys, depth + 1, c[0], c[1], c[2]);
+      else if (b0 && !b1 && free) free->push_back({depth + 1, {c[0], c[1], c[2]}, kClampMinLogOdds});
     }
     for (int i = 0; i < 8; ++i) {
       if (!inner[i]) continue;
       if (depth + 1 >= 16) throw std::runtime_error("octomap: inner node below max depth");
-      int cx = kx + ((i & 1) ? half : -half - (half ? 0 : 1));
-      int cy = ky + ((i & 2) ? half : -half - (half ? 0 : 1));
-      int cz = kz + ((i & 4) ? half : -half - (half ? 0 : 1));
-      node(depth + 1, cx, cy, cz);
+      int c[3];
+      child_key(depth, i, k, c);
+      node(depth + 1, c);
     }
-  }
-  void emit(int depth, int kx, int ky, int kz) {
-    if (depth >= 16) {
-      keys->push_back((uint16_t)kx); keys->push_back((uint16_t)ky); keys->push_back((uint16_t)kz);
-      return;
-    }
-    int h = 32768 >> depth;  // pruned leaf covers [k - h, k + h - 1]
-    for (int z = kz - h; z < kz + h; ++z)
-      for (int y = ky - h; y < ky + h; ++y)
-        for (int x = kx - h; x < kx + h; ++x) {
-          keys->push_back((uint16_t)x); keys->push_back((uint16_t)y); keys->push_back((uint16_t)z);
-        }
   }
 };
-}  // namespace
 
-void octomap_bt_keys(const uint8_t* data, size_t size, double* res, std::vector<uint16_t>* keys) {
+// Octomap full format (OcTreeDataNode::readData / OcTreeBaseImpl::readNodesRecurs): per node its value (float
+// log-odds) and one byte whose bit i says child i exists, then the existing children recursively in child order.
+// A node without children is a leaf, occupied iff log-odds >= occ_prob_thres_log = logodds(0.5) = 0
+// (OccupancyOcTreeBase::isNodeOccupied).
+struct OtReader {
+  const uint8_t* p;
+  const uint8_t* end;
+  std::vector<uint16_t>* keys;
+  std::vector<FreeLeaf>* free;
+  void node(int depth, const int* k) {
+    if (end - p < 5) throw std::runtime_error("octomap: truncated full stream");
+    float v;
+    std::memcpy(&v, p, 4);
+    const uint8_t m = p[4];
+    p += 5;
+    if (m == 0) {
+      if (v >= 0.0f) emit_leaf(keys, depth, k[0], k[1], k[2]);
+      else if (free) free->push_back({depth, {k[0], k[1], k[2]}, v});
+      return;
+    }
+    if (depth >= 16) throw std::runtime_error("octomap: children below max depth");
+    for (int i = 0; i < 8; ++i) {
+      if (!((m >> i) & 1)) continue;
+      int c[3];
+      child_key(depth, i, k, c);
+      node(depth + 1, c);
+    }
+  }
+};
+
+// Text header of .bt / .ot files (AbstractOcTree::readHeader): comment lines, "id", "size", "res", then "data".
+// Returns the first byte after the "data" line; *nodes = -1 when no size line was given.
+const uint8_t* octomap_header(const uint8_t* data, size_t size, double* res, long long* nodes) {
   const uint8_t* p = data;
   const uint8_t* end = data + size;
-  bool have_res = false, in_header = true;
+  bool have_res = false;
   std::string id;
-  long long nodes = -1;
-  while (in_header) {
+  *nodes = -1;
+  for (;;) {
     const uint8_t* nl = (const uint8_t*)memchr(p, '\n', end - p);
     if (!nl) throw std::runtime_error("octomap: header not terminated");
     std::string line((const char*)p, nl - p);
@@ -351,14 +411,41 @@ void octomap_bt_keys(const uint8_t* data, size_t size, double* res, std::vector<
     if (!line.empty() && line.back() == '\r') line.pop_back();
     if (line.empty() || line[0] == '#') continue;
     if (line.rfind("id ", 0) == 0) id = line.substr(3);
-    else if (line.rfind("size ", 0) == 0) nodes = atoll(line.c_str() + 5);
+    else if (line.rfind("size ", 0) == 0) *nodes = atoll(line.c_str() + 5);
     else if (line.rfind("res ", 0) == 0) { *res = strtod(line.c_str() + 4, nullptr); have_res = true; }
-    else if (line == "data") in_header = false;
+    else if (line == "data") break;
   }
-  if (!have_res || (id != "OcTree" && !id.empty())) throw std::runtime_error("octomap: unsupported header");
-  if (nodes == 0) return;
-  BtReader r{p, end, keys};
-  r.node(0, 32768, 32768, 32768);
+  if (!have_res || !(*res > 0) || (id != "OcTree" && !id.empty())) throw std::runtime_error("octomap: unsupported header");
+  return p;
+}
+}  // namespace
+
+void octomap_bt_keys(const uint8_t* data, size_t size, double* res, std::vector<uint16_t>* keys,
+                     std::vector<FreeLeaf>* free, bool header) {
+  const uint8_t* p = data;
+  if (header) {
+    long long nodes;
+    p = octomap_header(data, size, res, &nodes);
+    if (nodes == 0) return;
+  }
+  if (p == data + size) return;  // empty tree
+  BtReader r{p, data + size, keys, free};
+  const int root[3] = {KEY_OFFSET, KEY_OFFSET, KEY_OFFSET};
+  r.node(0, root);
+}
+
+void octomap_ot_keys(const uint8_t* data, size_t size, double* res, std::vector<uint16_t>* keys,
+                     std::vector<FreeLeaf>* free, bool header) {
+  const uint8_t* p = data;
+  if (header) {
+    long long nodes;
+    p = octomap_header(data, size, res, &nodes);
+    if (nodes == 0) return;
+  }
+  if (p == data + size) return;  // empty tree
+  OtReader r{p, data + size, keys, free};
+  const int root[3] = {KEY_OFFSET, KEY_OFFSET, KEY_OFFSET};
+  r.node(0, root);
 }
 
 }  // namespace smp

@@ -33,10 +33,26 @@ constexpr int KEY_OFFSET = 32768;  // octomap tree_max_val
 
 int grid_pad_cells(double res);
 void scene_from_keys(const uint16_t* keys, int64_t n, double res, double z_offset, SceneHost* out);
-// Octomap binary stream (.bt file or octomap_msgs binary payload) -> occupied leaf keys (expanded to depth 16).
-void octomap_bt_keys(const uint8_t* data, size_t size, double* res, std::vector<uint16_t>* keys);
-// squirrel_8dof_planner.cpp:889-902 floor square around (cx, cy) at the key of z = -res/2.
-void floor_keys(double cx, double cy, double res, double distance, std::vector<uint16_t>* keys);
+// A free octree leaf (depth, centre key, float log-odds): kept for the floor insertion, which leaves a floor cell
+// free when it falls in a free leaf whose log-odds plus one hit stay below 0.
+struct FreeLeaf {
+  int depth;
+  int k[3];
+  float v;
+};
+constexpr float kHitLogOdds = 0.847297860387203f;        // octomap prob_hit 0.7: logodds(0.7)
+constexpr float kClampMinLogOdds = -2.000027830777221f;   // clamping_thres_min 0.1192: logodds(0.1192)
+// Octomap binary stream (.bt file, or with header = false an octomap_msgs binary payload) -> occupied leaf keys
+// (expanded to depth 16) and, if `free` is given, the free leaves.  *res is read from the header.
+void octomap_bt_keys(const uint8_t* data, size_t size, double* res, std::vector<uint16_t>* keys,
+                     std::vector<FreeLeaf>* free = nullptr, bool header = true);
+// Octomap full stream (.ot file, or with header = false an octomap_msgs full payload), same outputs.
+void octomap_ot_keys(const uint8_t* data, size_t size, double* res, std::vector<uint16_t>* keys,
+                     std::vector<FreeLeaf>* free = nullptr, bool header = true);
+// squirrel_8dof_planner.cpp:889-902 floor square around (cx, cy) at the key of z = -res/2 (updateNode(key, true)
+// on each cell; cells inside a free leaf that one hit does not make occupied are skipped).
+void floor_keys(double cx, double cy, double res, double distance, std::vector<uint16_t>* keys,
+                const std::vector<FreeLeaf>* free = nullptr);
 // Exact squared Euclidean distance transform (voxel units) of a dense occupancy mask (x fastest).
 void edt_squared(const std::vector<uint8_t>& occ, int nx, int ny, int nz, std::vector<uint16_t>* d2);
 // Squared box-to-box gap field (voxel units): EDT of the 3x3x3-dilated occupancy.

@@ -68,9 +68,8 @@ class Scene:
                                         ctypes.byref(h)), "smp_scene_from_keys")
         return cls(h)
 
-    @classmethod
-    def from_bt(cls, data, z_offset=-0.02, floor_center=None, floor_distance=3.0):
-        buf = ctypes.create_string_buffer(bytes(data), len(data))
+    @staticmethod
+    def _opts(z_offset, floor_center, floor_distance):
         o = L.SceneOpts()
         lib().smp_scene_opts_default(ctypes.byref(o))
         o.z_offset = z_offset
@@ -78,8 +77,36 @@ class Scene:
             o.insert_floor = 1
             o.floor_center[0], o.floor_center[1] = floor_center
             o.floor_distance = floor_distance
+        return o
+
+    @classmethod
+    def from_bt(cls, data, z_offset=-0.02, floor_center=None, floor_distance=3.0):
+        """Octomap binary file (.bt) bytes."""
+        buf = ctypes.create_string_buffer(bytes(data), len(data))
+        o = cls._opts(z_offset, floor_center, floor_distance)
         h = ctypes.c_void_p()
         check(lib().smp_scene_from_bt(buf, len(data), ctypes.byref(o), ctypes.byref(h)), "smp_scene_from_bt")
+        return cls(h)
+
+    @classmethod
+    def from_ot(cls, data, z_offset=-0.02, floor_center=None, floor_distance=3.0):
+        """Octomap full-format file (.ot) bytes (the octomap_server's map, launch/simulation.launch:51)."""
+        buf = ctypes.create_string_buffer(bytes(data), len(data))
+        o = cls._opts(z_offset, floor_center, floor_distance)
+        h = ctypes.c_void_p()
+        check(lib().smp_scene_from_ot(buf, len(data), ctypes.byref(o), ctypes.byref(h)), "smp_scene_from_ot")
+        return cls(h)
+
+    @classmethod
+    def from_octomap_msg(cls, id, resolution, binary, data, z_offset=-0.02, floor_center=None, floor_distance=3.0):
+        """octomap_msgs/Octomap fields (squirrel_8dof_planner.cpp:875-883): binaryMsgToMap / fullMsgToMap."""
+        data = bytes(data)
+        buf = ctypes.create_string_buffer(data, max(len(data), 1))
+        o = cls._opts(z_offset, floor_center, floor_distance)
+        h = ctypes.c_void_p()
+        check(lib().smp_scene_from_octomap_msg(id.encode() if isinstance(id, str) else id, float(resolution),
+                                               int(bool(binary)), buf, len(data), ctypes.byref(o), ctypes.byref(h)),
+              "smp_scene_from_octomap_msg")
         return cls(h)
 
     @classmethod
@@ -146,6 +173,14 @@ class GpuPlanner:
         check(lib().smp_check_configs(self.h, soa.ctypes.data_as(_pd), len(q), int(check_self), int(check_map),
                                       out.ctypes.data_as(ctypes.c_void_p)), "smp_check_configs")
         return out
+
+    def check_sequence(self, poses, check_self=True, check_map=True):
+        """Index of the first pose in collision (-1: all valid), one batched check (fold / unfold keyframes)."""
+        q = np.ascontiguousarray(np.asarray(poses, np.float64).reshape(-1, 8))
+        first = ctypes.c_int64()
+        check(lib().smp_check_sequence(self.h, q.ctypes.data_as(_pd), len(q), int(check_self), int(check_map),
+                                       ctypes.byref(first)), "smp_check_sequence")
+        return first.value
 
     def last_kernel_ms(self):
         a, b = ctypes.c_double(), ctypes.c_double()
@@ -256,9 +291,12 @@ class BiRRTstarPlanner:
         self._gpu = GpuPlanner(device=self.device, **params)
 
     def setOctree(self, octree, resolution=None, floor_center=None, floor_distance=3.0):
-        """octree: .bt bytes or an (n, 3) array of occupied octomap keys (then `resolution` is required)."""
+        """octree: .bt or .ot file bytes, or an (n, 3) array of occupied octomap keys (then `resolution` is
+        required).  The first line tells the formats apart (AbstractOcTree::read / OcTree::readBinary)."""
         if isinstance(octree, (bytes, bytearray)):
-            sc = Scene.from_bt(octree, floor_center=floor_center, floor_distance=floor_distance)
+            full = bytes(octree).startswith(b"# Octomap OcTree file")
+            sc = (Scene.from_ot if full else Scene.from_bt)(octree, floor_center=floor_center,
+                                                            floor_distance=floor_distance)
         else:
             sc = Scene.from_keys(octree, resolution, floor_center=floor_center, floor_distance=floor_distance)
         self._gpu.set_scene(sc)
@@ -303,3 +341,21 @@ class BiRRTstarPlanner:
 
     def getJointTrajectoryRef(self):
         return self._traj
+
+
+def normalize_trajectory(raw, normalized_pose):
+    """Planner::normalizeTrajectory (squirrel_8dof_planner.cpp:1557-1637) through the C ABI: the resampled poses as
+    an (m, dim) array, or None where the reference returns without touching its output (dim < 1, <= 1 pose)."""
+    np_ = np.ascontiguousarray(np.asarray(normalized_pose, np.float64).reshape(-1))
+    raw = np.ascontiguousarray(np.asarray(raw, np.float64))
+    dim = len(np_)
+    if raw.ndim != 2 or len(raw) <= 1 or dim < 1 or raw.shape[1] != dim:
+        return None
+    n_out = ctypes.c_int64()
+    check(lib().smp_normalize_trajectory(raw.ctypes.data_as(_pd), len(raw), dim, np_.ctypes.data_as(_pd), None, 0,
+                                         ctypes.byref(n_out)), "smp_normalize_trajectory")
+    out = np.zeros((n_out.value, dim))
+    check(lib().smp_normalize_trajectory(raw.ctypes.data_as(_pd), len(raw), dim, np_.ctypes.data_as(_pd),
+                                         out.ctypes.data_as(_pd), n_out.value, ctypes.byref(n_out)),
+          "smp_normalize_trajectory")
+    return out

@@ -24,7 +24,8 @@ ARM_REACH = [0.6, 0.9, 0.4, 0.8, 0.0]
 
 
 def coord_to_key(c, res):
-    return np.floor(np.asarray(c, np.float64) / res).astype(np.int64) + KEY_OFFSET
+    """octomap OcTreeBaseImpl::coordToKey: floor(resolution_factor * c) + 32768, resolution_factor = 1.0 / res."""
+    return np.floor((1.0 / res) * np.asarray(c, np.float64)).astype(np.int64) + KEY_OFFSET
 
 
 def _box_keys(lo, hi, res):

@@ -321,3 +321,46 @@ def test_reference_call_sequence():
     assert p.init_planner(sc.start, sc.goal, 1, True, True)
     ok = p.run_planner(1, 1, 0.5, False, 0.0, 1)
     assert ok and p.stats["time_total"] <= 1.5
+
+
+# ------------------------------------------------------------------------------------------ fold / unfold (§8f)
+def test_check_sequence_fold_keyframes(gp, orobot):
+    """The node's fold / unfold loops (squirrel_8dof_planner.cpp:759-784, 814-823): normalized folding keyframes
+    (60-67) copied into robot poses, first invalid pose from one batched check, on the reference's room3.ot map
+    with the node's floor; checked against the oracle's per-pose validity."""
+    from oracle import trajectory as OT
+    from squirrel_motion_planner_amd.planner import normalize_trajectory
+    kf = np.load(os.path.join(GOLD, "folding_poses_tuw-robotino2.npz"))["keyframes"]
+    arm = normalize_trajectory(kf, [0.08] * 5)
+    assert np.array_equal(arm, np.array(OT.normalize_trajectory(kf.tolist(), [0.08] * 5)))
+    fc = (0.0, 0.0)
+    gs = Scene.from_ot(open(os.path.join(GOLD, "room3.ot"), "rb").read(), floor_center=fc)
+    keys = np.concatenate([np.load(os.path.join(GOLD, "room3_keys.npz"))["keys"].astype(np.int64),
+                           scenes.floor_keys(fc, 0.05, 3.0)])
+    gp.set_scene(gs)
+    gp.set_disabled_map_links([])
+    orc = O.Oracle(orobot, O.OracleScene(keys, 0.05))
+    # the sphere model is conservative around the tightest folding keyframes (arm_joint2 2.26 rad): keep the
+    # keyframes from the first one after which every pose is self-collision free
+    ok = orc.check_configs(np.array([[0.0, 0.0, 0.0] + list(a) for a in arm]), True, False)
+    i0 = int(np.flatnonzero(ok == 0)[-1]) + 1 if (ok == 0).any() else 0
+    assert i0 < len(arm) // 2, i0
+    arm = arm[i0:]
+    rng = np.random.default_rng(4)
+    firsts = []
+    for k in range(48):
+        base = [rng.uniform(-3.0, 3.0), rng.uniform(-3.0, 3.0), rng.uniform(-np.pi, np.pi)]
+        poses = np.array([base + list(a) for a in (arm if k % 2 else arm[::-1])])
+        flags = (True, k % 3 != 0)   # some sequences self-collision only
+        first = gp.check_sequence(poses, *flags)
+        ov = orc.check_configs(poses, *flags)
+        bad = np.flatnonzero(ov == 0)
+        assert first == (bad[0] if len(bad) else -1), (k, first, bad[:3])
+        firsts.append((first, poses, flags))
+    free = [p for f, p, fl in firsts if f < 0 and fl[1]]
+    hit = [p for f, p, fl in firsts if f >= 0 and fl[1]]
+    assert free and hit, [f for f, _, _ in firsts]
+    # a collision in the middle of a sequence: valid poses, then a colliding one
+    seq = np.concatenate([free[0], hit[0][:1], free[1 % len(free)]])
+    assert gp.check_sequence(seq) == len(free[0])
+    assert gp.check_sequence(np.zeros((0, 8))) == -1

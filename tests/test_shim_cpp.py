@@ -72,3 +72,42 @@ def test_shim_node_sequence_matches_oracle(tmp_path):
     assert checked == o["checked"]
     assert path.shape == o["path"].reshape(-1, 8).shape
     assert np.array_equal(path, o["path"].reshape(-1, 8))
+
+
+def test_shim_normalize_trajectory_matches_oracle(tmp_path):
+    """smp_node::normalizeTrajectory (the node's Planner::normalizeTrajectory, SP:1557-1637) through the C++ shim,
+    bit for bit against oracle/trajectory.py; host only, no GPU."""
+    from oracle import trajectory as OT
+    exe = os.path.join(str(tmp_path), "shim_normalize")
+    subprocess.run(["g++", "-std=c++11", "-O2", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "cpp", "shim_normalize.cpp"), "-L", LIBDIR, "-lsmp_gpu",
+                    "-Wl,-rpath," + LIBDIR, "-o", exe], check=True, capture_output=True, text=True)
+    rng = np.random.default_rng(2)
+    cases = []
+    for k in range(12):
+        dim = 8 if k % 3 else 5
+        n = int(rng.integers(1, 7))
+        raw = np.cumsum(rng.normal(0, 0.2, (n, dim)), 0)
+        if dim == 8:
+            raw[:, 2] = rng.uniform(-3.5, 3.5, n)
+        npose = [0.02, 0.02, 0.08, 0.08, 0.08, 0.08, 0.08, 0.08][:dim] if dim == 8 else [0.08] * 5
+        cases.append((raw, npose))
+    txt = ""
+    for raw, npose in cases:
+        txt += "%d %d\n" % (raw.shape[1], len(raw))
+        txt += "\n".join(" ".join("%.17g" % v for v in r) for r in raw) + "\n"
+        txt += " ".join("%.17g" % v for v in npose) + "\n"
+    p = subprocess.run([exe], input=txt, capture_output=True, text=True, timeout=60)
+    assert p.returncode == 0, p.stderr
+    lines = p.stdout.splitlines()
+    i = 0
+    for raw, npose in cases:
+        want = OT.normalize_trajectory(raw.tolist(), npose)
+        if want is None:
+            assert lines[i] == "untouched"
+            i += 1
+            continue
+        assert lines[i] == "rows %d" % len(want)
+        got = np.array([[float(v) for v in ln.split()] for ln in lines[i + 1:i + 1 + len(want)]])
+        assert np.array_equal(got, np.array(want))
+        i += 1 + len(want)
