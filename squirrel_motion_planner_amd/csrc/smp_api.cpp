@@ -27,6 +27,7 @@ __global__ void plan_kernel(const RobotDev* rb, SceneDev sc, const MapCfg* mc, Q
                             int iters);
 __global__ void helper_kernel(const RobotDev* rb, SceneDev sc, const MapCfg* mc, QueryDev* qs, int nq);
 __global__ void path_kernel(QueryDev* qs, int* counts);
+size_t check_kernels_private_bytes();
 __global__ void sincos_kernel(const double* x, int n, double* s, double* c);
 __global__ void u01_kernel(unsigned long long seed, unsigned query, const uint32_t* ctr, int n, double* out);
 __global__ void fk_kernel(const RobotDev* rb, const double* q, int n, double* frames, double* eez);
@@ -335,6 +336,27 @@ int smp_planner_create(int device, const smp_robot* robot, const smp_params* par
   if (!params_ok(p->params)) {
     delete p;
     return SMP_ERR_ARG;
+  }
+  // The runtime sizes a dispatch's scratch from the device stack limit (hipLimitStackSize, 1 KB per work-item by
+  // default), not from the kernel's private segment: a kernel whose fixed private segment exceeds the limit reads
+  // and writes scratch beyond its allocation (HSA_STATUS_ERROR_MEMORY_APERTURE_VIOLATION).  Raise the limit to the
+  // largest private segment of the planner's kernels.
+  {
+    size_t need = 0;
+    hipFuncAttributes fa;
+    const void* ks[] = {reinterpret_cast<const void*>(&plan_kernel), reinterpret_cast<const void*>(&helper_kernel),
+                        reinterpret_cast<const void*>(&path_kernel)};
+    for (const void* k : ks)
+      if (hipFuncGetAttributes(&fa, k) == hipSuccess) need = std::max(need, (size_t)fa.localSizeBytes);
+    need = std::max(need, check_kernels_private_bytes());
+    size_t cur = 0;
+    if (hipDeviceGetLimit(&cur, hipLimitStackSize) == hipSuccess && cur < need) {
+      need = (need + 255) / 256 * 256;
+      if (hipDeviceSetLimit(hipLimitStackSize, need) != hipSuccess) {
+        delete p;
+        return SMP_ERR_HIP;
+      }
+    }
   }
   HIPCHK(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
   int prio_lo = 0, prio_hi = 0;

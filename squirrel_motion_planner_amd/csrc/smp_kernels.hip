@@ -65,6 +65,18 @@ __global__ void __launch_bounds__(BLOCK) check_kernel_t(const RobotDev* __restri
 }
 
 // Batched isConfigValid (birrt_star.cpp:6897-6908): grid-stride over tiles of CT configurations.
+// Largest per-work-item private segment (scratch) of the batch check kernels (smp_planner_create raises the
+// device stack limit to cover every kernel of the library).
+size_t check_kernels_private_bytes() {
+  size_t need = 0;
+  hipFuncAttributes fa;
+  const void* ks[] = {reinterpret_cast<const void*>(&check_kernel_t<8>), reinterpret_cast<const void*>(&check_kernel_t<16>),
+                      reinterpret_cast<const void*>(&check_kernel_t<CHECK_CT>)};
+  for (const void* k : ks)
+    if (hipFuncGetAttributes(&fa, k) == hipSuccess && (size_t)fa.localSizeBytes > need) need = fa.localSizeBytes;
+  return need;
+}
+
 void launch_check(int ct, int grid, hipStream_t st, const RobotDev* rb, SceneDev sc, const MapCfg* mc, const double* q,
                   long long n, int self, int map, uint8_t* valid, unsigned long long* prof) {
   switch (ct) {
