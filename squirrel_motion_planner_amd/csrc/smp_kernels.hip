@@ -2130,8 +2130,10 @@ __device__ void connect_graphs(const Ctx& C, int t) {
   __syncthreads();
 }
 
-// One C-space iteration of run_planner (birrt_star.cpp:1163-1338).
-__device__ void iteration(const Ctx& C) {
+// One C-space iteration of run_planner (birrt_star.cpp:1163-1338).  Always inlined into plan_kernel: builds in
+// which the inliner outlined it (a larger scout) fault the GPU with a memory-aperture violation in the first
+// iterations (tools/experiments/README.md), builds that inline it run clean.
+__device__ __forceinline__ void iteration(const Ctx& C) {
   const int A = uni(g_L.S.A), B = 1 - A;
   unsigned long long _t0 = threadIdx.x == 0 ? wall_clock64() : 0, _t1;
 #define PHASE(k) if (threadIdx.x == 0) { _t1 = wall_clock64(); g_L.S.prof[k] += _t1 - _t0; _t0 = _t1; }
