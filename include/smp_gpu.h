@@ -84,7 +84,9 @@ typedef struct smp_params {
                               (0: automatic, up to 127 with the scout / 63 without; -1: none, the query runs on
                               its own workgroup) */
   int scout;               /* 1 (default): a scout workgroup per query computes the next iteration's scans and
-                              collision jobs ahead (needs >= 4 helpers); 0: off.  Results are identical either way */
+                              collision jobs ahead (needs >= 4 helpers), and with >= 16 helpers a second one takes
+                              every other iteration two ahead until the first solution; 0: off.  Results are
+                              identical either way */
 } smp_params;
 
 typedef struct smp_query {

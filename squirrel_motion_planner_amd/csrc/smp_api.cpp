@@ -83,14 +83,15 @@ struct QueryBuffers {
   DBuf<double> q, cost, e_start, e_target, rows;
   DBuf<int> parent, first_child, next_sib, prev_sib, stack, path_nodes;
   DBuf<ViaNode> via;
-  DBuf<JobBoard> jb, sjb;          // the leader's and the scout's collision-job boards
-  DBuf<ScoutBoard> scb;
-  DBuf<ViaNode> svia;
+  DBuf<JobBoard> jb, sjb, sjb2;    // the leader's and the scouts' collision-job boards
+  DBuf<ScoutBoard> scb, scb2;
+  DBuf<ViaNode> svia, svia2;
   size_t cap = 0;
   void release() {
     st.release(); q.release(); cost.release(); e_start.release(); e_target.release(); rows.release();
     parent.release(); first_child.release(); next_sib.release(); prev_sib.release(); stack.release();
     path_nodes.release(); via.release(); jb.release(); sjb.release(); scb.release(); svia.release();
+    sjb2.release(); scb2.release(); svia2.release();
     cap = 0;
   }
 };
@@ -574,6 +575,9 @@ static hipError_t alloc_query(QueryBuffers& b, size_t cap, int via_cap, long lon
   if ((e = b.sjb.reserve(1))) return e;
   if ((e = b.scb.reserve(1))) return e;
   if ((e = b.svia.reserve(via_cap))) return e;
+  if ((e = b.sjb2.reserve(1))) return e;
+  if ((e = b.scb2.reserve(1))) return e;
+  if ((e = b.svia2.reserve(via_cap))) return e;
   b.cap = cap;
   return hipSuccess;
 }
@@ -603,6 +607,10 @@ static QueryDev make_qdev(QueryBuffers& b, size_t cap, long long rows) {
   d.scb = nullptr;
   d.svia = nullptr;
   d.sworkers = 1;
+  d.sjb2 = nullptr;
+  d.scb2 = nullptr;
+  d.svia2 = nullptr;
+  d.sworkers2 = 1;
   d.nworkers = 1;
   d.sampler = 0;
   d.trace = nullptr;
@@ -680,7 +688,10 @@ extern "C" int smp_plan_batch(smp_planner* p, const smp_query* qs, int nq, smp_r
   if (nh == 0) nh = want_scout ? std::min(127, std::max(0, p->num_cus / nq - 2)) : std::min(63, std::max(0, p->num_cus / nq - 1));
   if (nh < 0) nh = 0;
   const bool scout = want_scout && nh >= 4;
-  const int h_lead = scout ? (nh - 1) / 2 : 0, h_scout = scout ? nh - 1 - h_lead : 0;
+  // a second scout (pre-solution iterations, two ahead) with a few helpers of its own: its jobs are one edge
+  const bool scout2 = scout && nh >= 16;
+  const int h_s2 = scout2 ? 4 : 0;
+  const int h_lead = scout ? (nh - 1 - h_s2) / 2 : 0, h_scout = scout ? nh - 1 - h_s2 - h_lead : 0;
   for (int i = 0; i < nq; ++i) {
     qdev[i].jb = nh > 0 ? p->qb[i].jb.p : nullptr;
     qdev[i].sampler = nh >= 2;              // with two or more helpers, the last one runs ahead sampling
@@ -691,6 +702,12 @@ extern "C" int smp_plan_batch(smp_planner* p, const smp_query* qs, int nq, smp_r
       qdev[i].svia = p->qb[i].svia.p;
       qdev[i].sampler_jb = p->qb[i].jb.p;
       qdev[i].sworkers = 1 + h_scout;
+      if (scout2) {
+        qdev[i].sjb2 = p->qb[i].sjb2.p;
+        qdev[i].scb2 = p->qb[i].scb2.p;
+        qdev[i].svia2 = p->qb[i].svia2.p;
+        qdev[i].sworkers2 = 1 + h_s2;
+      }
     }
   }
   static int* trace_host = nullptr;
@@ -733,6 +750,10 @@ extern "C" int smp_plan_batch(smp_planner* p, const smp_query* qs, int nq, smp_r
           HIPCHK(hipMemsetAsync(qdev[i].sjb, 0, sizeof(JobBoard), p->stream));
           HIPCHK(hipMemsetAsync(qdev[i].scb, 0, sizeof(ScoutBoard), p->stream));
         }
+        if (scout2) {
+          HIPCHK(hipMemsetAsync(qdev[i].sjb2, 0, sizeof(JobBoard), p->stream));
+          HIPCHK(hipMemsetAsync(qdev[i].scb2, 0, sizeof(ScoutBoard), p->stream));
+        }
       }
       HIPCHK(hipEventRecord(p->ev_board, p->stream));
       HIPCHK(hipStreamWaitEvent(p->hstream, p->ev_board, 0));
@@ -743,7 +764,9 @@ extern "C" int smp_plan_batch(smp_planner* p, const smp_query* qs, int nq, smp_r
     HIPCHK(hipEventRecord(p->ev0, p->stream));
     // scouts at block scout_base + q, scout_base a multiple of 8: blocks b and b + 8 are dealt to the same XCD
     const int scout_base = scout ? (nq + 7) / 8 * 8 : 0;
-    hipLaunchKernelGGL(plan_kernel, dim3(scout ? scout_base + nq : nq), dim3(BLOCK), 0, p->stream, p->d_rb, p->sc,
+    // second scouts at scout_base + round8(nq) + q (plan_kernel)
+    const int grid = scout2 ? scout_base + (nq + 7) / 8 * 8 + nq : (scout ? scout_base + nq : nq);
+    hipLaunchKernelGGL(plan_kernel, dim3(grid), dim3(BLOCK), 0, p->stream, p->d_rb, p->sc,
                        p->d_mc, p->d_qdev.p, nq, scout_base, chunk);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(p->ev1, p->stream));
@@ -848,7 +871,7 @@ extern "C" int smp_plan_batch(smp_planner* p, const smp_query* qs, int nq, smp_r
       st.scout_phase_seconds[k] = count ? (double)scout_prof[i][k] : (double)scout_prof[i][k] / p->wall_rate_hz;
     }
     st.helpers = nh;
-    st.scout = scout ? 1 : 0;
+    st.scout = scout2 ? 2 : (scout ? 1 : 0);
     for (int k = 0; k < 32; ++k)
       st.phase_seconds[k] = (k == 8 || k == 11 || k >= 20) ? (double)s.prof[k] : (double)s.prof[k] / p->wall_rate_hz;
     if (i == 0) { p->last_n[0] = s.n[0]; p->last_n[1] = s.n[1]; }

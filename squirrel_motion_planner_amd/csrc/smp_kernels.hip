@@ -210,7 +210,8 @@ struct PlanLds {
   // Scout: the record it builds.
   ScoutRec sr;
   int sp_on, sp_stage, sp_go[2];
-  int sc_same;                  // leader: the scout runs on this XCD (1), another (0), not yet known (-1)
+  int sc_same[2];               // leader: scout 1 / 2 runs on this XCD (1), another (0), not yet known (-1)
+  int asked[4];                 // leader: scout (1, 2) asked for iteration k in slot k % 4, 0 = none
   int eg_hit[MAXE];
 };
 
@@ -1267,8 +1268,8 @@ __device__ bool spec_stage(const Ctx& C, int s) {
   if (!uni(g_L.sp_on)) return false;
   const int have = uni(g_L.sp_stage);
   if (have >= s) return true;
-  const ScoutBoard* sb = C.Q.scb;
-  const int par = (int)(g_L.S.iter & 1);
+  const ScoutBoard* sb = uni(g_L.asked[g_L.S.iter & 3]) == 2 ? C.Q.scb2 : C.Q.scb;
+  const int par = (int)(g_L.S.iter & 3);
   const unsigned tag = (unsigned)(g_L.S.iter + 1);
   const unsigned long long t0 = threadIdx.x == 0 ? wall_clock64() : 0;
   int got;
@@ -1307,28 +1308,50 @@ __device__ bool spec_stage(const Ctx& C, int s) {
   return true;
 }
 
-// Leader, at the start of iteration i (after its sample): asks the scout for iteration i + 1, which expands tree
-// `t` (= tree_B of iteration i).  Its first n[t] nodes stay as they are until then (iteration i only appends to
-// it), and their stores are drained here, so the scout reads them as the leader will.
+// Leader, at the start of iteration j (after its sample): asks a scout for iteration j + 1, which expands tree `t`
+// (= tree_B of iteration j), unless it was asked already.  Before the first solution (no choose-parent / rewire,
+// so the trees only grow) and with a second scout, it also asks for iteration j + 2, which expands tree_A of
+// iteration j: the scouts alternate by iteration parity, each with two leader iterations for its pass, since a
+// pre-solution pass (nearest + expand job) is longer than the leader's own iteration.  The first n[t] nodes of a
+// requested tree stay as they are until the record is used (only appends before then), and their stores are
+// drained here, so the scout reads them as the leader will.  Iteration j looks a record up only if it was asked
+// for (asked[j % 4]); every scout also gets the leader's current iteration (its staleness test).
 __device__ void scout_request(const Ctx& C, int t) {
   drain();
   __syncthreads();
   if (threadIdx.x == 0) {
-    if (g_L.sc_same < 0) {
-      const int x = ld_agent(&C.Q.scb->xcc);
-      if (x > 0) g_L.sc_same = (x - 1) == xcc_id() ? 1 : 0;
-    }
-    // a scout on another XCD reads through its own L2: write this XCD's dirty lines back first
-    if (g_L.sc_same != 1) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      drain();
-    }
     const QState& S = g_L.S;
-    const unsigned tag = (unsigned)(S.iter + 2);
-    const unsigned w0 = (unsigned)S.n[t] | (unsigned)t << 28 | (unsigned)(S.tree_opt && S.have_sol) << 29;
-    st_agent(&C.Q.scb->req[1], granule(tag, (unsigned)g_L.smp_ver));
-    st_agent(&C.Q.scb->req[0], granule(tag, w0));
-    g_L.sp_on = 1;
+    const long long j = S.iter;
+    const bool pre = !(S.tree_opt && S.have_sol);
+    const bool two = pre && C.Q.scb2 != nullptr;
+    g_L.asked[(j + 3) & 3] = 0;  // iteration j - 1's slot
+    st_agent(&C.Q.scb->cur, (unsigned long long)j);
+    if (C.Q.scb2) st_agent(&C.Q.scb2->cur, (unsigned long long)j);
+    bool fenced = false;
+    for (int ahead = 1; ahead <= (two ? 2 : 1); ++ahead) {
+      const long long k = j + ahead;
+      if (g_L.asked[k & 3]) continue;
+      const int which = two && !(k & 1) ? 2 : 1;  // pre-solution: scout 2 takes the even iterations
+      ScoutBoard* sb = which == 2 ? C.Q.scb2 : C.Q.scb;
+      int& same = g_L.sc_same[which - 1];
+      if (same < 0) {
+        const int x = ld_agent(&sb->xcc);
+        if (x > 0) same = (x - 1) == xcc_id() ? 1 : 0;
+      }
+      // a scout on another XCD reads through its own L2: write this XCD's dirty lines back first
+      if (same != 1 && !fenced) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        drain();
+        fenced = true;
+      }
+      const int tree = ahead == 1 ? t : 1 - t;
+      const unsigned tag = (unsigned)(k + 1);
+      const unsigned w0 = (unsigned)S.n[tree] | (unsigned)tree << 28 | (unsigned)(!pre) << 29;
+      st_agent(&sb->req[1], granule(tag, (unsigned)g_L.smp_ver));
+      st_agent(&sb->req[0], granule(tag, w0));
+      g_L.asked[k & 3] = which;
+    }
+    g_L.sp_on = g_L.asked[j & 3] != 0;
     g_L.sp_stage = -1;
   }
   __syncthreads();
@@ -2229,10 +2252,10 @@ __device__ void sc_publish(const Ctx& C, int par, unsigned tag, int stage) {
   __syncthreads();
 }
 #define SC_PHASE(k) if (threadIdx.x == 0) { const unsigned long long _t = wall_clock64(); g_L.S.prof[k] += _t - _ts; _ts = _t; }
-// True (block-uniform) once the leader has moved past the iteration with record tag `tag` (its newest request is
-// for a later one than tag + 1): the rest of the record would not be used.
+// True (block-uniform) once the leader has moved past the iteration with record tag `tag` (iteration tag - 1):
+// the rest of the record would not be used.
 __device__ bool sc_stale(const Ctx& C, unsigned tag) {
-  if (threadIdx.x == 0) g_L.sp_go[0] = (unsigned)(ld_agent(&C.Q.scb->req[0]) >> 32) > tag + 1 || ld_agent(&C.Q.scb->stop);
+  if (threadIdx.x == 0) g_L.sp_go[0] = (long long)ld_agent(&C.Q.scb->cur) > (long long)tag - 1 || ld_agent(&C.Q.scb->stop);
   __syncthreads();
   const int s = uni(g_L.sp_go[0]);
   __syncthreads();
@@ -2248,7 +2271,7 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
   ScoutRec& R = g_L.sr;
   ScoutBoard* sb = C.Q.scb;
   JobBoard* jb = C.Q.jb;  // this Ctx's board is the scout's; the sampler ring lives on the leader's (sampler_jb)
-  const int par = (int)(it & 1);
+  const int par = (int)(it & 3);
   const unsigned tag = (unsigned)(it + 1);
   (void)jb;
   unsigned long long _ts = threadIdx.x == 0 ? wall_clock64() : 0;
@@ -2458,7 +2481,13 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
 
 // Scout workgroup of a query (plan_kernel blocks nq .. 2nq-1): takes the leader's newest request, runs
 // scout_iteration on it, repeats; leaves on the stop flag (then stops its helpers) or after two idle seconds.
-__device__ void scout_main(Ctx& C) {
+__device__ __forceinline__ void scout_main(Ctx& C, int which) {
+  if (which == 2) {  // the second scout: its own record board, job board, helpers and via scratch
+    C.Q.scb = C.Q.scb2;
+    C.Q.sjb = C.Q.sjb2;
+    C.Q.svia = C.Q.svia2;
+    C.Q.sworkers = C.Q.sworkers2;
+  }
   {
     const int* src = reinterpret_cast<const int*>(C.Q.st);
     int* dst = reinterpret_cast<int*>(&g_L.S);
@@ -2536,19 +2565,24 @@ __global__ void __launch_bounds__(BLOCK) plan_kernel(const RobotDev* __restrict_
                                                      int iters) {
   // blocks [0, nq): leaders; [scout_base, scout_base + nq): their scouts (scout_base a multiple of 8, so that query
   // q's two blocks are dealt to the same XCD); any other block has nothing to do
+  // second scouts at scout_base2 + q (again a multiple of 8 apart: same XCD as their leader)
   const int b = (int)blockIdx.x;
-  if (b >= nq && !(scout_base > 0 && b >= scout_base && b < scout_base + nq)) return;
+  const int scout_base2 = scout_base + (nq + 7) / 8 * 8;
+  const bool s1 = scout_base > 0 && b >= scout_base && b < scout_base + nq;
+  const bool s2 = scout_base > 0 && b >= scout_base2 && b < scout_base2 + nq;
+  if (b >= nq && !s1 && !s2) return;
   stage_model(rb, mc, &g_rb, &g_mc);
   Ctx C;
   C.sc = sc;
-  C.Q = qs[b < nq ? b : b - scout_base];
+  C.Q = qs[b < nq ? b : (s1 ? b - scout_base : b - scout_base2)];
   if (b >= nq) {
-    if (C.Q.scb) scout_main(C);
+    if ((s1 && C.Q.scb) || (s2 && C.Q.scb2)) scout_main(C, s2 ? 2 : 1);  // one call site: inlined
     return;
   }
   if (threadIdx.x == 0) {
     g_L.sp_on = 0;
-    g_L.sc_same = -1;
+    g_L.sc_same[0] = g_L.sc_same[1] = -1;
+    for (int k = 0; k < 4; ++k) g_L.asked[k] = 0;
     g_L.count_slot = 0;
     g_L.job_seq = 0;
     g_L.S = *C.Q.st;
@@ -2588,6 +2622,7 @@ __global__ void __launch_bounds__(BLOCK) plan_kernel(const RobotDev* __restrict_
     *C.Q.st = g_L.S;
     if (C.Q.jb) st_agent(&C.Q.jb->stop, 1);
     if (C.Q.scb) st_agent(&C.Q.scb->stop, 1);
+    if (C.Q.scb2) st_agent(&C.Q.scb2->stop, 1);
   }
 }
 
@@ -2679,6 +2714,11 @@ __global__ void __launch_bounds__(BLOCK) helper_kernel(const RobotDev* __restric
     const int h = hidx - (C.Q.nworkers - 1);  // the scout's tile helpers
     C.Q.jb = C.Q.sjb;
     C.Q.nworkers = C.Q.sworkers;
+    helper_main(C, h, J);
+  } else if (C.Q.sjb2 && hidx - (C.Q.nworkers - 1) - (C.Q.sworkers - 1) < C.Q.sworkers2 - 1) {
+    const int h = hidx - (C.Q.nworkers - 1) - (C.Q.sworkers - 1);  // the second scout's tile helpers
+    C.Q.jb = C.Q.sjb2;
+    C.Q.nworkers = C.Q.sworkers2;
     helper_main(C, h, J);
   }
 }

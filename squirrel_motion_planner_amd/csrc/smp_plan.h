@@ -140,16 +140,18 @@ struct ScoutRec {
   ScoutEdge e[SCOUT_EDGES];    // [0] expand, [SCOUT_CHOOSE0 ..) choose-parent, [SCOUT_REWIRE0 ..) rewire
 };
 struct ScoutBoard {
-  // leader -> scout, at the start of iteration i: tag i + 2 (the request is for iteration i + 1);
-  // req[0] low word = X | t << 28 | opt << 29, req[1] low word = the sampler parameter version
+  // leader -> scout: the request for iteration k carries tag k + 1; req[0] low word = X | t << 28 | opt << 29,
+  // req[1] low word = the sampler parameter version
   unsigned long long req[2];
   int stop;                    // the leader left the launch
   int xcc;                     // the scout's XCD (XCC_ID) + 1, 0 = not yet known
   int pad0[10];
-  unsigned long long stage[2]; // scout -> leader, by iteration parity
-  int pad1[28];
+  unsigned long long cur;      // leader -> scout: the leader's current iteration (a record of an earlier one is stale)
+  int pad2[30];
+  unsigned long long stage[4]; // scout -> leader, by iteration mod 4 (a scout may work two iterations ahead)
+  int pad1[24];
   unsigned long long prof[32]; // the scout's phase clocks of the launch (written when it leaves)
-  ScoutRec rec[2];
+  ScoutRec rec[4];
 };
 
 struct QueryDev {
@@ -160,6 +162,11 @@ struct QueryDev {
   ScoutBoard* scb;
   ViaNode* svia;               // the scout's via-node scratch [via_cap]
   int sworkers;                // scout + its tile helper workgroups
+  // second scout (pre-solution iterations, two ahead of the leader; null: none) and its board / helpers
+  JobBoard* sjb2;
+  ScoutBoard* scb2;
+  ViaNode* svia2;
+  int sworkers2;
   int* trace;                  // debug only (SMP_DEBUG): host-mapped progress markers of the leader
   int nworkers;                // leader + tile helper workgroups (tile w, w + nworkers, ... is worker w's)
   int sampler;                 // 1: the last helper workgroup is the run-ahead sampler
