@@ -173,6 +173,7 @@ struct PlanLds {
   // edge batch
   double eg_start[MAXE][NJ], eg_target[MAXE][NJ], eg_step[MAXE][NJ], eg_end[MAXE][NJ];
   double eg_base[MAXE][3], eg_cost[MAXE][3];
+  double eg_acc[MAXE][3];             // edge_costs: the segment-norm sums (eg_cost = eg_base + eg_acc)
   int eg_first[MAXE], eg_need[MAXE], eg_near[MAXE], eg_ptr[MAXE];
   int rw_par[MAXE], rw_next;          // rewire: candidates' parents (refreshed after every commit), resume point
   double rw_cost[MAXE][3];            // rewire: candidates' costs
@@ -931,6 +932,7 @@ __device__ void edge_costs(const Ctx& C, int E) {
     int e = threadIdx.x / 3, k = threadIdx.x - e * 3;
     double acc = 0.0;
     for (int s = 0; s < np; ++s) acc += g_L.u.seg[e][s][k];
+    g_L.eg_acc[e][k] = acc;
     g_L.eg_cost[e][k] = g_L.eg_base[e][k] + acc;
   }
   __syncthreads();
@@ -1256,7 +1258,7 @@ __device__ __forceinline__ void sc_copy_in(const ScoutBoard* sb, int par, void* 
   for (int w = threadIdx.x; w < nbytes / 8; w += BLOCK) dst[w] = ld_agent(&src[w]);
 }
 static_assert(sizeof(ScoutNN) % 8 == 0 && sizeof(ScoutNear) % 8 == 0 && sizeof(ScoutEdge) % 8 == 0 &&
-              offsetof(ScoutRec, nr) % 8 == 0 && offsetof(ScoutRec, n_choose) % 8 == 0 && offsetof(ScoutRec, e) % 8 == 0,
+              sizeof(ScoutExpand) % 8 == 0 && offsetof(ScoutRec, ex) % 8 == 0 && offsetof(ScoutRec, nr) % 8 == 0 && offsetof(ScoutRec, n_choose) % 8 == 0 && offsetof(ScoutRec, e) % 8 == 0,
               "scout record sections are 8-byte words");
 
 constexpr unsigned long long SCOUT_WAIT = 6000;  // device-clock ticks (60 us) the leader waits for one scout stage
@@ -1296,12 +1298,17 @@ __device__ bool spec_stage(const Ctx& C, int s) {
   const int st = got - 1;  // stages (have, st] arrived
   ScoutRec& R = g_L.sr;
   if (have < SC_NN && st >= SC_NN) sc_copy_in(sb, par, &R.nn, sizeof(ScoutNN));
-  if (have < SC_EXPAND && st >= SC_EXPAND) sc_copy_in(sb, par, &R.e[0], sizeof(ScoutEdge));
+  if (have < SC_EXPAND && st >= SC_EXPAND) {
+    sc_copy_in(sb, par, &R.e[0], sizeof(ScoutEdge));
+    sc_copy_in(sb, par, &R.ex, sizeof(ScoutExpand));
+  }
+  // choose-parent / rewire candidates only in iterations that have those steps (tree optimisation, a solution)
+  const bool opt_now = uni(g_L.S.tree_opt && g_L.S.have_sol) != 0;
   if (have < SC_NEAR && st >= SC_NEAR) sc_copy_in(sb, par, &R.nr, sizeof(ScoutNear));
   if ((have < SC_CHOOSE && st >= SC_CHOOSE) || (have < SC_DONE && st >= SC_DONE))
     sc_copy_in(sb, par, &R.n_choose, 4 * sizeof(int));
-  if (have < SC_CHOOSE && st >= SC_CHOOSE) sc_copy_in(sb, par, &R.e[SCOUT_CHOOSE0], MAX_NEAR * sizeof(ScoutEdge));
-  if (have < SC_DONE && st >= SC_DONE) sc_copy_in(sb, par, &R.e[SCOUT_REWIRE0], MAX_NEAR * sizeof(ScoutEdge));
+  if (opt_now && have < SC_CHOOSE && st >= SC_CHOOSE) sc_copy_in(sb, par, &R.e[SCOUT_CHOOSE0], MAX_NEAR * sizeof(ScoutEdge));
+  if (opt_now && have < SC_DONE && st >= SC_DONE) sc_copy_in(sb, par, &R.e[SCOUT_REWIRE0], MAX_NEAR * sizeof(ScoutEdge));
   __syncthreads();
   if (threadIdx.x == 0) g_L.sp_stage = st;
   __syncthreads();
@@ -2167,16 +2174,36 @@ __device__ __forceinline__ void iteration(const Ctx& C) {
   PHASE(P_NN);
   if (threadIdx.x == 0) {
     load_node(C, A, nid, &g_L.nn);
-    // expandTree single step (birrt_star.cpp:2224-2256)
-    for (int j = 0; j < NJ; ++j) g_L.ext[j] = g_L.xr[j];
-    step_towards((&g_rb), g_L.nn.q, g_L.ext, g_L.S.step);
-    for (int j = 0; j < NJ; ++j) { g_L.eg_start[0][j] = g_L.nn.q[j]; g_L.eg_target[0][j] = g_L.ext[j]; }
-    for (int k = 0; k < 3; ++k) g_L.eg_base[0][k] = g_L.nn.c[k];
+    // expandTree single step (birrt_star.cpp:2224-2256).  If the scout's record of this iteration already holds
+    // its expand stage for the same sample, tree and nearest node, the step target and the interpolation data are
+    // its (the same function of the same inputs); else computed here.
+    const ScoutRec& R = g_L.sr;
+    bool rec = g_L.sp_on && g_L.sp_stage >= SC_EXPAND && R.ex.ok && R.nn.ok && R.nn.t == A && R.nn.id == nid &&
+               same8(R.nn.q, g_L.xr) && same8(R.e[0].s, g_L.nn.q) && same8(R.e[0].g, R.ex.ext);
+    g_L.flag = rec;
+    if (rec) {
+      for (int j = 0; j < NJ; ++j) {
+        g_L.eg_start[0][j] = g_L.nn.q[j];
+        g_L.eg_target[0][j] = R.ex.ext[j];
+        g_L.eg_step[0][j] = R.ex.step[j];
+        g_L.eg_end[0][j] = R.ex.end[j];
+      }
+      for (int k = 0; k < 3; ++k) {
+        g_L.eg_base[0][k] = g_L.nn.c[k];
+        g_L.eg_acc[0][k] = R.ex.acc[k];
+        g_L.eg_cost[0][k] = g_L.nn.c[k] + R.ex.acc[k];
+      }
+    } else {
+      for (int j = 0; j < NJ; ++j) g_L.ext[j] = g_L.xr[j];
+      step_towards((&g_rb), g_L.nn.q, g_L.ext, g_L.S.step);
+      for (int j = 0; j < NJ; ++j) { g_L.eg_start[0][j] = g_L.nn.q[j]; g_L.eg_target[0][j] = g_L.ext[j]; }
+      for (int k = 0; k < 3; ++k) g_L.eg_base[0][k] = g_L.nn.c[k];
+    }
     g_L.eg_need[0] = 1;
   }
   __syncthreads();
   const bool opt = uni(g_L.S.tree_opt && g_L.S.have_sol);
-  edge_costs(C, 1);
+  if (!uni(g_L.flag)) edge_costs(C, 1);
   edge_validity(C, 1, false, P_XEXPAND, opt ? OV_NEAR_EXPAND : OV_NONE, A, SC_EXPAND);
   if (threadIdx.x == 0) {
     int f = g_L.eg_first[0];
@@ -2278,7 +2305,7 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
   if (threadIdx.x == 0) {
     S.prof[30]++;
     S.n[t] = X;
-    R.nn.ok = 0; R.nr.ok = 0; R.n_choose = 0; R.n_rewire = 0;
+    R.nn.ok = 0; R.ex.ok = 0; R.nr.ok = 0; R.n_choose = 0; R.n_rewire = 0;
   }
   sc_publish(C, par, tag, SC_STARTED);
   // the sample: the sampler's ring slot for (it, ver), if it is there within ~20 us
@@ -2328,6 +2355,11 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
   sc_publish(C, par, tag, SC_NN);
   SC_PHASE(1);
   edge_costs(C, 1);
+  if (threadIdx.x == 0) {  // the expand edge's interpolation data, for the leader (published with SC_EXPAND)
+    for (int j = 0; j < NJ; ++j) { R.ex.ext[j] = g_L.eg_target[0][j]; R.ex.step[j] = g_L.eg_step[0][j]; R.ex.end[j] = g_L.eg_end[0][j]; }
+    for (int k = 0; k < 3; ++k) R.ex.acc[k] = g_L.eg_acc[0][k];
+    R.ex.ok = 1;
+  }
   // the near set of the edge's end (x_new if the edge is valid) is scanned while the helpers check the edge
   if (threadIdx.x == 0) g_L.spec = OV_NONE;
   edge_validity(C, 1, false, P_XEXPAND, opt ? OV_NEAR_EXPAND : OV_NONE, t);
@@ -2349,6 +2381,7 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
   }
   __syncthreads();
   sc_copy_out(sb, par, &R.e[0], sizeof(ScoutEdge));
+  sc_copy_out(sb, par, &R.ex, sizeof(ScoutExpand));
   if (!opt || sc_stale(C, tag)) {
     sc_copy_out(sb, par, &R.nr, sizeof(ScoutNear));
     sc_copy_out(sb, par, &R.n_choose, 4 * sizeof(int));

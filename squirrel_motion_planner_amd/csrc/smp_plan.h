@@ -133,8 +133,15 @@ struct ScoutEdge {             // one candidate edge: interpolation start / targ
   double s[NJ], g[NJ];
   int first, pad;              // first: as eg_first (n_pts + 1 = free), -1 = not checked
 };
+struct ScoutExpand {           // stage SC_EXPAND: the expand edge's interpolation data (edge_costs of edge 0)
+  double ext[NJ];              // step target (stepTowardsRandSample from the nearest node towards the sample)
+  double step[NJ], end[NJ];    // interpolation step and end point
+  double acc[3];               // segment-norm sums (cost = nearest node's cost + acc)
+  int ok, pad;
+};
 struct ScoutRec {
   ScoutNN nn;
+  ScoutExpand ex;
   ScoutNear nr;
   int n_choose, n_rewire, pad[2];
   ScoutEdge e[SCOUT_EDGES];    // [0] expand, [SCOUT_CHOOSE0 ..) choose-parent, [SCOUT_REWIRE0 ..) rewire
