@@ -1258,7 +1258,8 @@ __device__ __forceinline__ void sc_copy_in(const ScoutBoard* sb, int par, void* 
   for (int w = threadIdx.x; w < nbytes / 8; w += BLOCK) dst[w] = ld_agent(&src[w]);
 }
 static_assert(sizeof(ScoutNN) % 8 == 0 && sizeof(ScoutNear) % 8 == 0 && sizeof(ScoutEdge) % 8 == 0 &&
-              sizeof(ScoutExpand) % 8 == 0 && offsetof(ScoutRec, ex) % 8 == 0 && offsetof(ScoutRec, nr) % 8 == 0 && offsetof(ScoutRec, n_choose) % 8 == 0 && offsetof(ScoutRec, e) % 8 == 0,
+              sizeof(ScoutExpand) % 8 == 0 && offsetof(ScoutRec, ex) % 8 == 0 && offsetof(ScoutRec, nr) % 8 == 0 &&
+              sizeof(ScoutConnect) % 8 == 0 && offsetof(ScoutRec, cn) % 8 == 0 && offsetof(ScoutRec, n_choose) % 8 == 0 && offsetof(ScoutRec, e) % 8 == 0,
               "scout record sections are 8-byte words");
 
 constexpr unsigned long long SCOUT_WAIT = 6000;  // device-clock ticks (60 us) the leader waits for one scout stage
@@ -1309,6 +1310,7 @@ __device__ bool spec_stage(const Ctx& C, int s) {
     sc_copy_in(sb, par, &R.n_choose, 4 * sizeof(int));
   if (opt_now && have < SC_CHOOSE && st >= SC_CHOOSE) sc_copy_in(sb, par, &R.e[SCOUT_CHOOSE0], MAX_NEAR * sizeof(ScoutEdge));
   if (opt_now && have < SC_DONE && st >= SC_DONE) sc_copy_in(sb, par, &R.e[SCOUT_REWIRE0], MAX_NEAR * sizeof(ScoutEdge));
+  if (!opt_now && have < SC_DONE && st >= SC_DONE) sc_copy_in(sb, par, &R.cn, sizeof(ScoutConnect));
   __syncthreads();
   if (threadIdx.x == 0) g_L.sp_stage = st;
   __syncthreads();
@@ -1354,6 +1356,7 @@ __device__ void scout_request(const Ctx& C, int t) {
       const int tree = ahead == 1 ? t : 1 - t;
       const unsigned tag = (unsigned)(k + 1);
       const unsigned w0 = (unsigned)S.n[tree] | (unsigned)tree << 28 | (unsigned)(!pre) << 29;
+      st_agent(&sb->req[2], granule(tag, (unsigned)S.n[1 - tree]));
       st_agent(&sb->req[1], granule(tag, (unsigned)g_L.smp_ver));
       st_agent(&sb->req[0], granule(tag, w0));
       g_L.asked[k & 3] = which;
@@ -2017,7 +2020,14 @@ __device__ void connect_graphs(const Ctx& C, int t) {
   if (threadIdx.x == 0) g_L.spec = OV_NONE;
   __syncthreads();
   if (uni(g_L.eg_need[0])) {
-    edge_validity(C, 1, false, P_XCONNECT, g_L.S.have_sol ? OV_NEAR_XN : OV_NONE, t);
+    if (uni(!g_L.S.have_sol && g_L.sp_on && g_L.sp_stage >= SC_DONE && g_L.sr.cn.ok && g_L.sr.cn.t == t &&
+            same8(g_L.sr.cn.e.s, g_L.eg_start[0]) && same8(g_L.sr.cn.e.g, g_L.eg_target[0]))) {
+      // the scout checked this edge (before the first solution: no near set to overlap)
+      if (threadIdx.x == 0) { g_L.eg_first[0] = g_L.sr.cn.e.first; g_L.S.sc_edge_hit++; }
+      __syncthreads();
+    } else {
+      edge_validity(C, 1, false, P_XCONNECT, g_L.S.have_sol ? OV_NEAR_XN : OV_NONE, t);
+    }
     if (threadIdx.x == 0) {
       int f = g_L.eg_first[0];
       count_edge(f);
@@ -2238,7 +2248,21 @@ __device__ __forceinline__ void iteration(const Ctx& C) {
     __syncthreads();
     if (opt) rewire(C, A);
     PHASE(P_REWIRE);
-    const int cid = take_spec(OV_NN) ? uni(g_L.spec_nn) : nearest(C, B, g_L.xn.q);
+    int cid;
+    if (take_spec(OV_NN)) {
+      cid = uni(g_L.spec_nn);
+    } else if (uni(!opt && g_L.sp_on && g_L.sp_stage >= SC_DONE && g_L.sr.cn.ok && g_L.sr.cn.t == B &&
+                   g_L.sr.cn.X <= g_L.S.n[B] && same8(g_L.sr.cn.q, g_L.xn.q))) {
+      // the scout's nearest node over the first X nodes; only the nodes appended since are scanned (one of them
+      // replaces it only with a strictly smaller distance: it has a larger index)
+      const int n = uni(g_L.S.n[B]);
+      double dp;
+      const int ip = nearest_scan(C, B, g_L.xn.q, g_L.sr.cn.X, &dp);
+      if (threadIdx.x == 0) { g_L.S.nn_nodes += n; g_L.S.sc_nn++; }
+      cid = uni(dp < g_L.sr.cn.d ? ip : (g_L.sr.cn.d < 10000.0 ? g_L.sr.cn.id : 0));
+    } else {
+      cid = nearest(C, B, g_L.xn.q);
+    }
     if (threadIdx.x == 0) load_node(C, B, cid, &g_L.xc);
     __syncthreads();
     PHASE(P_NN);
@@ -2293,7 +2317,7 @@ __device__ bool sc_stale(const Ctx& C, unsigned tag) {
 // the leader's steps up to its rewire collision job (iteration / choose_parent / rewire, same functions on the
 // scout's own LDS, job board, helpers and via-node scratch), recording the results the leader keys on; nothing is
 // written to the trees.  The sample is the run-ahead sampler's for (it, ver).
-__device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int opt, unsigned ver) {
+__device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int opt, unsigned ver, int XB) {
   QState& S = g_L.S;
   ScoutRec& R = g_L.sr;
   ScoutBoard* sb = C.Q.scb;
@@ -2305,6 +2329,8 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
   if (threadIdx.x == 0) {
     S.prof[30]++;
     S.n[t] = X;
+    S.n[1 - t] = XB;
+    R.cn.ok = 0;
     R.nn.ok = 0; R.ex.ok = 0; R.nr.ok = 0; R.n_choose = 0; R.n_rewire = 0;
   }
   sc_publish(C, par, tag, SC_STARTED);
@@ -2382,6 +2408,37 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
   __syncthreads();
   sc_copy_out(sb, par, &R.e[0], sizeof(ScoutEdge));
   sc_copy_out(sb, par, &R.ex, sizeof(ScoutExpand));
+  if (!opt && uni(g_L.ext_nn) && !sc_stale(C, tag)) {
+    // before the first solution the iteration goes on with connect (connectGraphs): x_new is the expand edge's
+    // end; its nearest node in the other tree over that tree's first XB nodes (the tree only grows until then)
+    // and the direct edge to it, whose check always runs while there is no solution (c_best = inf)
+    sc_publish(C, par, tag, SC_EXPAND);
+    const int tb = 1 - t;
+    const int cid = nearest(C, tb, g_L.xn.q);
+    if (threadIdx.x == 0) {
+      load_node(C, tb, cid, &g_L.xc);
+      double s = 0.0;
+      for (int j = 0; j < NJ; ++j) { double d = g_L.xn.q[j] - g_L.xc.q[j]; s += d * d; }
+      const double d = sqrt(s);
+      for (int j = 0; j < NJ; ++j) R.cn.q[j] = g_L.xn.q[j];
+      R.cn.d = d < 10000.0 ? d : 10000.0;
+      R.cn.id = cid; R.cn.X = XB; R.cn.t = tb;
+      for (int j = 0; j < NJ; ++j) { g_L.eg_start[0][j] = g_L.xc.q[j]; g_L.eg_target[0][j] = g_L.xn.q[j]; }
+      for (int k = 0; k < 3; ++k) g_L.eg_base[0][k] = g_L.xc.c[k];
+      g_L.eg_need[0] = 1;
+    }
+    for (int e = 1 + threadIdx.x; e < MAXE; e += BLOCK) g_L.eg_need[e] = 0;
+    __syncthreads();
+    edge_costs(C, 1);
+    edge_validity(C, 1, false, P_XCONNECT);
+    if (threadIdx.x == 0) {
+      for (int j = 0; j < NJ; ++j) { R.cn.e.s[j] = g_L.eg_start[0][j]; R.cn.e.g[j] = g_L.eg_target[0][j]; }
+      R.cn.e.first = g_L.eg_first[0];
+      R.cn.ok = 1;
+    }
+    __syncthreads();
+    sc_copy_out(sb, par, &R.cn, sizeof(ScoutConnect));
+  }
   if (!opt || sc_stale(C, tag)) {
     sc_copy_out(sb, par, &R.nr, sizeof(ScoutNear));
     sc_copy_out(sb, par, &R.n_choose, 4 * sizeof(int));
@@ -2554,11 +2611,13 @@ __device__ __forceinline__ void scout_main(Ctx& C, int which) {
         go = -1;
       } else {
         const unsigned long long r0 = ld_agent(&C.Q.scb->req[0]), r1 = ld_agent(&C.Q.scb->req[1]);
+        const unsigned long long r2 = ld_agent(&C.Q.scb->req[2]);
         const unsigned tag = (unsigned)(r0 >> 32);
-        if (tag > last && (unsigned)(r1 >> 32) == tag) {
+        if (tag > last && (unsigned)(r1 >> 32) == tag && (unsigned)(r2 >> 32) == tag) {
           go = 1;
           g_L.cnt = (int)(unsigned)r0;        // X | t << 28 | opt << 29
           g_L.nn_t = (int)(unsigned)r1;       // sampler parameter version
+          g_L.found = (int)(unsigned)r2;      // XB
           g_L.tree_expand = (int)tag;
         } else if (wall_clock64() - t_last > 200000000ull) {
           go = -1;  // 2 s idle
@@ -2574,12 +2633,14 @@ __device__ __forceinline__ void scout_main(Ctx& C, int which) {
       continue;
     }
     const unsigned w0 = (unsigned)uni(g_L.cnt), ver = (unsigned)uni(g_L.nn_t), tag = (unsigned)uni(g_L.tree_expand);
+    const int XB = uni(g_L.found);
     __syncthreads();
     // tree words stored by the leader since this CU / XCD last cached them: drop stale copies
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     const unsigned long long tb = wall_clock64();
     if (threadIdx.x == 0) g_L.S.prof[28] += tb - t_last;  // idle: waiting for a request
-    scout_iteration(C, (long long)tag - 1, (int)(w0 >> 28) & 1, (int)(w0 & ((1u << 28) - 1)), (int)(w0 >> 29) & 1, ver);
+    scout_iteration(C, (long long)tag - 1, (int)(w0 >> 28) & 1, (int)(w0 & ((1u << 28) - 1)), (int)(w0 >> 29) & 1, ver,
+                    XB);
     last = tag;
     t_last = wall_clock64();
     if (threadIdx.x == 0) g_L.S.prof[31] += t_last - tb;

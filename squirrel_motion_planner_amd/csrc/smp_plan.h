@@ -139,20 +139,27 @@ struct ScoutExpand {           // stage SC_EXPAND: the expand edge's interpolati
   double acc[3];               // segment-norm sums (cost = nearest node's cost + acc)
   int ok, pad;
 };
+struct ScoutConnect {          // stage SC_DONE, before the first solution: connect's nearest node and direct edge
+  double q[NJ];                // x_new (the expand edge's end)
+  double d;                    // its nearest node's distance over the other tree's first X nodes (10000 if none)
+  int id, X, t, ok;            // that node, the snapshot size, the tree, 1 = valid
+  ScoutEdge e;                 // the direct edge nearest -> x_new and its first colliding point
+};
 struct ScoutRec {
   ScoutNN nn;
   ScoutExpand ex;
+  ScoutConnect cn;
   ScoutNear nr;
   int n_choose, n_rewire, pad[2];
   ScoutEdge e[SCOUT_EDGES];    // [0] expand, [SCOUT_CHOOSE0 ..) choose-parent, [SCOUT_REWIRE0 ..) rewire
 };
 struct ScoutBoard {
   // leader -> scout: the request for iteration k carries tag k + 1; req[0] low word = X | t << 28 | opt << 29,
-  // req[1] low word = the sampler parameter version
-  unsigned long long req[2];
+  // req[1] low word = the sampler parameter version, req[2] low word = XB (nodes of the other tree)
+  unsigned long long req[3];
   int stop;                    // the leader left the launch
   int xcc;                     // the scout's XCD (XCC_ID) + 1, 0 = not yet known
-  int pad0[10];
+  int pad0[8];
   unsigned long long cur;      // leader -> scout: the leader's current iteration (a record of an earlier one is stale)
   int pad2[30];
   unsigned long long stage[4]; // scout -> leader, by iteration mod 4 (a scout may work two iterations ahead)
