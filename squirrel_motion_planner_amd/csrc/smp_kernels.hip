@@ -1765,16 +1765,21 @@ __device__ void sample_iteration(const Ctx& C) {
         st_agent(&jb->s_ver, ++g_L.smp_ver);
       }
       st_agent(reinterpret_cast<unsigned long long*>(&jb->s_iter), (unsigned long long)S.iter);
-      const unsigned long long want = ((unsigned long long)it << 32) | (unsigned)g_L.smp_ver;
-      g_L.smp_hit = ld_agent(&jb->ring[it % SMP_RING].tag) == want;
+    }
+    // the slot's 16 granules in one round; current iff every tag is this iteration's with the current version
+    if (threadIdx.x < 64) {
+      const unsigned want = ring_tag(it, (unsigned)__builtin_amdgcn_readfirstlane(g_L.smp_ver));
+      unsigned long long v = 0;
+      if (threadIdx.x < 2 * NJ) v = ld_agent(&jb->ring[it % SMP_RING].g[threadIdx.x]);
+      const bool ok = threadIdx.x >= 2 * NJ || (unsigned)(v >> 32) == want;
+      const unsigned hi = (unsigned)__shfl((int)(unsigned)v, (threadIdx.x | 1) & 63);
+      if (threadIdx.x < 2 * NJ && !(threadIdx.x & 1))
+        g_L.xr[threadIdx.x >> 1] = __longlong_as_double((long long)(((unsigned long long)hi << 32) | (unsigned)v));
+      const bool all = __ballot(!ok) == 0;
+      if (threadIdx.x == 0) { g_L.smp_hit = all; if (all) S.smp_hits++; }
     }
     __syncthreads();
-    if (uni(g_L.smp_hit)) {
-      if (threadIdx.x < NJ) g_L.xr[threadIdx.x] = __longlong_as_double((long long)ld_agent(&jb->ring[it % SMP_RING].q[threadIdx.x]));
-      if (threadIdx.x == 0) S.smp_hits++;
-      __syncthreads();
-      return;
-    }
+    if (uni(g_L.smp_hit)) return;
   }
   if (sample_conf(S, it, g_L.u.smp, g_L.xr) < 0 && threadIdx.x == 0) { S.status = -1; S.phase = 2; }
   __syncthreads();
@@ -2335,21 +2340,26 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
   }
   sc_publish(C, par, tag, SC_STARTED);
   // the sample: the sampler's ring slot for (it, ver), if it is there within ~20 us
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < 64) {  // wave 0 polls the slot's 16 granules (one round each time)
     const JobBoard* lb = C.Q.sampler_jb;
-    const unsigned long long want = ((unsigned long long)(uint32_t)it << 32) | ver;
+    const unsigned want = ring_tag(it, ver);
     const unsigned long long t0 = wall_clock64();
     int ok = 0;
     for (;;) {
-      if (ld_agent(&lb->ring[it % SMP_RING].tag) == want) {
-        for (int j = 0; j < NJ; ++j) g_L.xr[j] = __longlong_as_double((long long)ld_agent(&lb->ring[it % SMP_RING].q[j]));
-        ok = ld_agent(&lb->ring[it % SMP_RING].tag) == want;  // not overwritten while read
+      unsigned long long v = 0;
+      if (threadIdx.x < 2 * NJ) v = ld_agent(&lb->ring[it % SMP_RING].g[threadIdx.x]);
+      const bool cur = threadIdx.x >= 2 * NJ || (unsigned)(v >> 32) == want;
+      if (__ballot(!cur) == 0) {
+        const unsigned hi = (unsigned)__shfl((int)(unsigned)v, (threadIdx.x | 1) & 63);
+        if (threadIdx.x < 2 * NJ && !(threadIdx.x & 1))
+          g_L.xr[threadIdx.x >> 1] = __longlong_as_double((long long)(((unsigned long long)hi << 32) | (unsigned)v));
+        ok = 1;
         break;
       }
-      if (wall_clock64() - t0 > 2000) break;
+      if (__builtin_amdgcn_readfirstlane((int)(wall_clock64() - t0 > 2000))) break;
       __builtin_amdgcn_s_sleep(2);
     }
-    g_L.flag = ok;
+    if (threadIdx.x == 0) g_L.flag = ok;
   }
   __syncthreads();
   SC_PHASE(0);
@@ -2776,13 +2786,10 @@ __device__ void sampler_main(const Ctx& C, SamplerLds& L) {
     }
     const long long it = L.next;
     const int st = sample_conf(L.S, (uint32_t)it, L.W, L.out);
-    if (st == 0) {
-      if (threadIdx.x < NJ)
-        st_agent(&jb->ring[it % SMP_RING].q[threadIdx.x], (unsigned long long)__double_as_longlong(L.out[threadIdx.x]));
-      drain();
-      __syncthreads();
-      if (threadIdx.x == 0)
-        st_agent(&jb->ring[it % SMP_RING].tag, ((unsigned long long)(uint32_t)it << 32) | (unsigned)L.ver);
+    if (st == 0 && threadIdx.x < 2 * NJ) {
+      const unsigned long long bits = (unsigned long long)__double_as_longlong(L.out[threadIdx.x >> 1]);
+      const unsigned w = (threadIdx.x & 1) ? (unsigned)(bits >> 32) : (unsigned)bits;
+      st_agent(&jb->ring[it % SMP_RING].g[threadIdx.x], granule((int)ring_tag(it, L.ver), w));
     }
     if (threadIdx.x == 0) L.next = it + 1;
     t_last = wall_clock64();

@@ -81,6 +81,12 @@ constexpr int JOB_SLOTS = MAXE * (MAX_PTS + 1); // (edge, point) slots of one jo
 constexpr int JOB_TILES = (JOB_SLOTS + HELPER_CT - 1) / HELPER_CT;
 constexpr int JOB_WORDS = 1 + 4 * NJ * MAXE;     // payload words: header + (start, step) halves per edge
 constexpr int SMP_RING = 16;                     // run-ahead sampler: samples kept ahead of the leader
+// Tag of the run-ahead sampler's ring granules: iteration (low 24 bits) and parameter version (low 8 bits).  A slot
+// holds only iteration i (mod SMP_RING) and the version changes at most once per iteration, so the short fields
+// cannot alias within a run of fewer than 2^24 iterations.
+__host__ __device__ inline unsigned ring_tag(long long it, unsigned ver) {
+  return ((unsigned)it & 0xffffffu) << 8 | (ver & 0xffu);
+}
 struct JobBoard {
   int stop;                    // 1 once the leader left the launch: helpers exit
   int pad0[7];
@@ -101,10 +107,10 @@ struct JobBoard {
   int pad6[22];
   // sampler -> leader: the sample of iteration i in slot i % SMP_RING, tag = (i << 32) | version, stored after
   // the drained configuration.
+  // Each configuration value travels as two data-tagged granules (low, high 32 bits) whose tag is
+  // ring_tag(iteration, version), so one round of 16 loads both reads a slot and tells whether it is current.
   struct {
-    unsigned long long tag;
-    unsigned long long q[NJ];     // fp64 bit patterns
-    int pad[14];
+    unsigned long long g[2 * NJ];
   } ring[SMP_RING];
 };
 
