@@ -408,10 +408,12 @@ __device__ int nearest(const Ctx& C, int t, const double* q, bool spec = false) 
   if (spec && spec_stage(C, SC_NN)) {
     const ScoutNN& R = g_L.sr.nn;
     if (uni(R.ok && R.t == t && R.X <= n && same8(q, R.q))) {
-      double dp;
-      const int ip = nearest_scan(C, t, q, R.X, &dp);
       if (threadIdx.x == 0) g_L.S.sc_nn++;
-      if (dp < R.d) return ip;
+      if (uni(R.X < n)) {  // nodes appended since the snapshot (none: the scout's answer stands)
+        double dp;
+        const int ip = nearest_scan(C, t, q, R.X, &dp);
+        if (dp < R.d) return ip;
+      }
       return R.d < 10000.0 ? R.id : 0;
     }
   }
@@ -2261,8 +2263,9 @@ __device__ __forceinline__ void iteration(const Ctx& C) {
       // the scout's nearest node over the first X nodes; only the nodes appended since are scanned (one of them
       // replaces it only with a strictly smaller distance: it has a larger index)
       const int n = uni(g_L.S.n[B]);
-      double dp;
-      const int ip = nearest_scan(C, B, g_L.xn.q, g_L.sr.cn.X, &dp);
+      double dp = 10000.0;
+      int ip = 0;
+      if (uni(g_L.sr.cn.X < n)) ip = nearest_scan(C, B, g_L.xn.q, g_L.sr.cn.X, &dp);
       if (threadIdx.x == 0) { g_L.S.nn_nodes += n; g_L.S.sc_nn++; }
       cid = uni(dp < g_L.sr.cn.d ? ip : (g_L.sr.cn.d < 10000.0 ? g_L.sr.cn.id : 0));
     } else {
