@@ -1269,6 +1269,7 @@ constexpr unsigned long long SCOUT_WAIT = 6000;  // device-clock ticks (60 us) t
 // Leader: waits until the scout's record of this iteration reached stage s (or the scout is not working on this
 // iteration, or SCOUT_WAIT passes: then the scout is not asked again this iteration) and copies the sections of
 // the stages received since the last call into g_L.sr.  All threads; returns whether stage s is there.
+__device__ void spec_copy(const ScoutBoard* sb, int par, int have, int st);
 __device__ bool spec_stage(const Ctx& C, int s) {
   if (!uni(g_L.sp_on)) return false;
   const int have = uni(g_L.sp_stage);
@@ -1298,7 +1299,12 @@ __device__ bool spec_stage(const Ctx& C, int s) {
     __syncthreads();
     return false;
   }
-  const int st = got - 1;  // stages (have, st] arrived
+  spec_copy(sb, par, have, got - 1);  // stages (have, st] arrived
+  return true;
+}
+
+// Copies the sections of record stages (have, st] of record slot par into g_L.sr; all threads.
+__device__ void spec_copy(const ScoutBoard* sb, int par, int have, int st) {
   ScoutRec& R = g_L.sr;
   if (have < SC_NN && st >= SC_NN) sc_copy_in(sb, par, &R.nn, sizeof(ScoutNN));
   if (have < SC_EXPAND && st >= SC_EXPAND) {
@@ -1316,7 +1322,6 @@ __device__ bool spec_stage(const Ctx& C, int s) {
   __syncthreads();
   if (threadIdx.x == 0) g_L.sp_stage = st;
   __syncthreads();
-  return true;
 }
 
 // Leader, at the start of iteration j (after its sample): asks a scout for iteration j + 1, which expands tree `t`
@@ -1748,43 +1753,68 @@ __device__ __forceinline__ int sample_conf(const QState& S, uint32_t it, SmpLds&
 // Leader: the sample of this iteration -> g_L.xr.  With a run-ahead sampler, first publish the iteration and,
 // when they changed, the informed-sampling parameters (versioned); then take the ring slot if its tag is this
 // iteration at the current version, else draw the sample here.
-__device__ void sample_iteration(const Ctx& C) {
+// Leader, first part of its sample step: publishes its iteration and (on a change) the informed-sampling
+// parameters for the run-ahead sampler.
+__device__ void sample_publish(const Ctx& C) {
+  QState& S = g_L.S;
+  if (C.Q.sampler && threadIdx.x == 0) {
+    JobBoard* jb = C.Q.jb;
+    const bool changed = g_L.smp_ver == 0 || g_L.smp_have_sol != S.have_sol || g_L.smp_cbest[0] != S.cbest[0] ||
+                         g_L.smp_cbest[1] != S.cbest[1] || g_L.smp_cbest[2] != S.cbest[2];
+    if (changed) {
+      g_L.smp_have_sol = S.have_sol;
+      st_agent(&jb->s_have_sol, S.have_sol);
+      for (int k = 0; k < 3; ++k) {
+        g_L.smp_cbest[k] = S.cbest[k];
+        st_agent(&jb->s_cbest[k], (unsigned long long)__double_as_longlong(S.cbest[k]));
+      }
+      drain();
+      st_agent(&jb->s_ver, ++g_L.smp_ver);
+    }
+    st_agent(reinterpret_cast<unsigned long long*>(&jb->s_iter), (unsigned long long)S.iter);
+  }
+}
+
+// Second part: the sample from the ring (one round of tagged granules, wave 0) -- and, in the same round (wave 1),
+// a look at the stage of this iteration's scout record, whose sections are then copied ahead of the steps that
+// use them -- else drawn here.
+__device__ void sample_read(const Ctx& C) {
   QState& S = g_L.S;
   const uint32_t it = (uint32_t)S.iter;
-  if (C.Q.sampler) {
-    JobBoard* jb = C.Q.jb;
-    if (threadIdx.x == 0) {
-      const bool changed = g_L.smp_ver == 0 || g_L.smp_have_sol != S.have_sol || g_L.smp_cbest[0] != S.cbest[0] ||
-                           g_L.smp_cbest[1] != S.cbest[1] || g_L.smp_cbest[2] != S.cbest[2];
-      if (changed) {
-        g_L.smp_have_sol = S.have_sol;
-        st_agent(&jb->s_have_sol, S.have_sol);
-        for (int k = 0; k < 3; ++k) {
-          g_L.smp_cbest[k] = S.cbest[k];
-          st_agent(&jb->s_cbest[k], (unsigned long long)__double_as_longlong(S.cbest[k]));
-        }
-        drain();
-        st_agent(&jb->s_ver, ++g_L.smp_ver);
-      }
-      st_agent(reinterpret_cast<unsigned long long*>(&jb->s_iter), (unsigned long long)S.iter);
+  const bool pre = uni(g_L.sp_on && g_L.sp_stage < 0) != 0;
+  const ScoutBoard* sb = uni(g_L.asked[S.iter & 3]) == 2 ? C.Q.scb2 : C.Q.scb;
+  const int par = (int)(S.iter & 3);
+  if (threadIdx.x == 64) {
+    int st = -1;
+    if (pre) {
+      const unsigned long long v = ld_agent(&sb->stage[par]);
+      if ((unsigned)(v >> 32) == (unsigned)(S.iter + 1)) st = (int)(unsigned)v;
     }
-    // the slot's 16 granules in one round; current iff every tag is this iteration's with the current version
-    if (threadIdx.x < 64) {
-      const unsigned want = ring_tag(it, (unsigned)__builtin_amdgcn_readfirstlane(g_L.smp_ver));
-      unsigned long long v = 0;
-      if (threadIdx.x < 2 * NJ) v = ld_agent(&jb->ring[it % SMP_RING].g[threadIdx.x]);
-      const bool ok = threadIdx.x >= 2 * NJ || (unsigned)(v >> 32) == want;
-      const unsigned hi = (unsigned)__shfl((int)(unsigned)v, (threadIdx.x | 1) & 63);
-      if (threadIdx.x < 2 * NJ && !(threadIdx.x & 1))
-        g_L.xr[threadIdx.x >> 1] = __longlong_as_double((long long)(((unsigned long long)hi << 32) | (unsigned)v));
-      const bool all = __ballot(!ok) == 0;
-      if (threadIdx.x == 0) { g_L.smp_hit = all; if (all) S.smp_hits++; }
-    }
-    __syncthreads();
-    if (uni(g_L.smp_hit)) return;
+    g_L.sp_go[0] = st;
   }
-  if (sample_conf(S, it, g_L.u.smp, g_L.xr) < 0 && threadIdx.x == 0) { S.status = -1; S.phase = 2; }
+  if (C.Q.sampler && threadIdx.x < 64) {
+    JobBoard* jb = C.Q.jb;
+    // the slot's 16 granules in one round; current iff every tag is this iteration's with the current version
+    const unsigned want = ring_tag(it, (unsigned)__builtin_amdgcn_readfirstlane(g_L.smp_ver));
+    unsigned long long v = 0;
+    if (threadIdx.x < 2 * NJ) v = ld_agent(&jb->ring[it % SMP_RING].g[threadIdx.x]);
+    const bool ok = threadIdx.x >= 2 * NJ || (unsigned)(v >> 32) == want;
+    const unsigned hi = (unsigned)__shfl((int)(unsigned)v, (threadIdx.x | 1) & 63);
+    if (threadIdx.x < 2 * NJ && !(threadIdx.x & 1))
+      g_L.xr[threadIdx.x >> 1] = __longlong_as_double((long long)(((unsigned long long)hi << 32) | (unsigned)v));
+    const bool all = __ballot(!ok) == 0;
+    if (threadIdx.x == 0) { g_L.smp_hit = all; if (all) S.smp_hits++; }
+  } else if (threadIdx.x == 0) {
+    g_L.smp_hit = 0;
+  }
   __syncthreads();
+  const int st = uni(g_L.sp_go[0]);
+  __syncthreads();
+  if (pre && st >= 0) spec_copy(sb, par, -1, st);
+  if (!uni(g_L.smp_hit)) {
+    if (sample_conf(S, it, g_L.u.smp, g_L.xr) < 0 && threadIdx.x == 0) { S.status = -1; S.phase = 2; }
+    __syncthreads();
+  }
 }
 
 // --------------------------------------------------------------------------------------- tree updates
@@ -2184,8 +2214,9 @@ __device__ __forceinline__ void iteration(const Ctx& C) {
   const int A = uni(g_L.S.A), B = 1 - A;
   unsigned long long _t0 = threadIdx.x == 0 ? wall_clock64() : 0, _t1;
 #define PHASE(k) if (threadIdx.x == 0) { _t1 = wall_clock64(); g_L.S.prof[k] += _t1 - _t0; _t0 = _t1; }
-  sample_iteration(C);
+  sample_publish(C);
   if (C.Q.scb) scout_request(C, B);
+  sample_read(C);
   PHASE(P_SAMPLE);
   int nid = nearest(C, A, g_L.xr, true);
   PHASE(P_NN);
