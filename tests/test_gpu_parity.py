@@ -195,6 +195,21 @@ def test_planner_parity_sample_budget(orobot, robot, name, seed, samples):
     assert_same_run(gp2, r, o)
 
 
+@pytest.mark.parametrize("seed", [1, 1001])
+def test_planner_parity_bench_workload(orobot, robot, seed):
+    """bench.py's C2 step at full size (steps 0 and 1: seeds 1, 1001; 1e6 collision-checked samples,
+    path_optimality_threshold = -inf, default helpers and scouts): both trees, costs and path bit for bit."""
+    gp2 = GpuPlanner(robot, path_optimality_threshold=-np.inf)
+    sc, gscene, osc = scene_pair("c2")
+    gp2.set_scene(gscene)
+    r = gp2.plan(GpuPlanner.make_query(sc.start, sc.goal, sc.env_x, sc.env_y, samples=1_000_000, seed=seed))
+    o = O.Oracle(orobot, osc).plan(sc.start, sc.goal, env_x=sc.env_x, env_y=sc.env_y, max_checked=1_000_000,
+                                   seed=seed, opt_thresh=-np.inf)
+    assert o["checked"] >= 1_000_000 and r["status"] == 0
+    assert r["scout"] >= 1 and r["helpers"] > 0  # the run-ahead path the bench measures
+    assert_same_run(gp2, r, o)
+
+
 @pytest.mark.parametrize("helpers", [-1, 1, 7])
 def test_planner_parity_helper_counts(orobot, robot, helpers):
     """The query alone on its workgroup (-1) and with helper workgroups sharing its collision tiles."""
