@@ -296,6 +296,24 @@ def test_c3_random_queries_batch(orobot, robot):
         _same_query_result(r, o)
 
 
+def test_c3_bench_share_full_budget(orobot, robot):
+    """bench.py --workload c3 step 0 at full size: the 8 queries of one GPU's share (seed 1, query_id k), 1e6
+    collision-checked samples each, path_optimality_threshold = -inf, queries sharing the chip's helpers."""
+    gp2 = GpuPlanner(robot, path_optimality_threshold=-np.inf)
+    sc, gscene, osc = scene_pair("c2")
+    gp2.set_scene(gscene)
+    pairs = scenes.random_queries(sc, 8, seed=7, check=lambda q: bool(gp2.check_configs([q])[0]))
+    qs = [GpuPlanner.make_query(s, g, sc.env_x, sc.env_y, samples=1_000_000, seed=1, query_id=k)
+          for k, (s, g) in enumerate(pairs)]
+    rs = gp2.plan_batch(qs)
+    orc = O.Oracle(orobot, osc)
+    for k, ((s, g), r) in enumerate(zip(pairs, rs)):
+        o = orc.plan(s, g, env_x=sc.env_x, env_y=sc.env_y, max_checked=1_000_000, seed=1, query=k,
+                     opt_thresh=-np.inf)
+        assert o["checked"] >= 1_000_000 or o["iterations"] == 0
+        _same_query_result(r, o)
+
+
 @pytest.fixture(scope="module")
 def c5_pair():
     sc = scenes.clutter_cloud()
