@@ -335,6 +335,24 @@ def test_c5_clutter_2cm_check_and_plan(orobot, robot, c5_pair):
     assert_same_run(gp2, r, o)
 
 
+def test_c5_bench_share_full_budget(orobot, robot, c5_pair):
+    """bench.py --workload c5 step 0 at full size: 8 random queries on the 2 cm clutter scene (seed 7), 1e6
+    collision-checked samples each, path_optimality_threshold = -inf; every query equals its oracle run."""
+    sc, gscene, osc = c5_pair
+    gp2 = GpuPlanner(robot, path_optimality_threshold=-np.inf)
+    gp2.set_scene(gscene)
+    pairs = scenes.random_queries(sc, 8, seed=7, check=lambda q: bool(gp2.check_configs([q])[0]))
+    assert len(pairs) == 8
+    qs = [GpuPlanner.make_query(s, g, sc.env_x, sc.env_y, samples=1_000_000, seed=1, query_id=k)
+          for k, (s, g) in enumerate(pairs)]
+    rs = gp2.plan_batch(qs)
+    orc = O.Oracle(orobot, osc)
+    for k, ((s, g), r) in enumerate(zip(pairs, rs)):
+        o = orc.plan(s, g, env_x=sc.env_x, env_y=sc.env_y, max_checked=1_000_000, seed=1, query=k,
+                     opt_thresh=-np.inf)
+        _same_query_result(r, o)
+
+
 def test_reference_call_sequence():
     """squirrel_8dof_planner.cpp:1221-1248 through the BiRRTstarPlanner mirror."""
     sc = scenes.box_room()
