@@ -27,8 +27,8 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8 TB/s
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=1)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--samples", type=int, default=int(os.environ.get("SMP_BENCH_SAMPLES", 1_000_000)),
                     help="budget of collision-checked configurations per query")
     ap.add_argument("--warmup-samples", type=int, default=None,

@@ -195,9 +195,9 @@ def test_planner_parity_sample_budget(orobot, robot, name, seed, samples):
     assert_same_run(gp2, r, o)
 
 
-@pytest.mark.parametrize("seed", [1, 1001])
+@pytest.mark.parametrize("seed", [1, 1001, 2001])
 def test_planner_parity_bench_workload(orobot, robot, seed):
-    """bench.py's C2 step at full size (steps 0 and 1: seeds 1, 1001; 1e6 collision-checked samples,
+    """bench.py's C2 step at full size (default steps 0-2: seeds 1, 1001, 2001; 1e6 collision-checked samples,
     path_optimality_threshold = -inf, default helpers and scouts): both trees, costs and path bit for bit."""
     gp2 = GpuPlanner(robot, path_optimality_threshold=-np.inf)
     sc, gscene, osc = scene_pair("c2")
