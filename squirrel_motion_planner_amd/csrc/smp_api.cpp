@@ -688,10 +688,13 @@ extern "C" int smp_plan_batch(smp_planner* p, const smp_query* qs, int nq, smp_r
   if (nh == 0) nh = want_scout ? std::min(127, std::max(0, p->num_cus / nq - 2)) : std::min(63, std::max(0, p->num_cus / nq - 1));
   if (nh < 0) nh = 0;
   const bool scout = want_scout && nh >= 4;
-  // a second scout (pre-solution iterations, two ahead) with a few helpers of its own: its jobs are one edge
+  // a second scout (iterations of the other parity, two ahead of the leader) with as many helpers as the first:
+  // after the first solution both check choose-parent / rewire candidate batches; the leader's own jobs (edges no
+  // record had) are rare, so it keeps a fifth
   const bool scout2 = scout && nh >= 16;
-  const int h_s2 = scout2 ? 4 : 0;
-  const int h_lead = scout ? (nh - 1 - h_s2) / 2 : 0, h_scout = scout ? nh - 1 - h_s2 - h_lead : 0;
+  const int h_lead = scout ? (scout2 ? (nh - 1) / 5 : (nh - 1) / 2) : 0;
+  const int h_s2 = scout2 ? (nh - 1 - h_lead) / 2 : 0;
+  const int h_scout = scout ? nh - 1 - h_s2 - h_lead : 0;
   for (int i = 0; i < nq; ++i) {
     qdev[i].jb = nh > 0 ? p->qb[i].jb.p : nullptr;
     qdev[i].sampler = nh >= 2;              // with two or more helpers, the last one runs ahead sampling

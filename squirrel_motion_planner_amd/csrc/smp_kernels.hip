@@ -12,10 +12,17 @@
 // bounded number of iterations and persists the state (QState) in HBM.
 #include <hip/hip_runtime.h>
 
+#include <vector>
+
 #include "smp_collide.h"
 #include "smp_math.h"
 #include "smp_plan.h"
 #include "smp_types.h"
+
+// Wave reductions of the device library (ockl, DPP-based); hip's header declares the 64-bit ones only under
+// HIP_ENABLE_EXTRA_WARP_SYNC_TYPES.
+extern "C" __device__ __attribute__((const)) unsigned long long __ockl_wfred_min_u64(unsigned long long);
+extern "C" __device__ __attribute__((const)) unsigned long long __ockl_wfred_max_u64(unsigned long long);
 
 namespace smp {
 
@@ -204,12 +211,18 @@ struct PlanLds {
   double sol[3];
   // wave reductions
   double wd[BLOCK / 64];
+  unsigned long long wk[BLOCK / 64];
   int wi[BLOCK / 64];
   long long wcount[BLOCK / 64];
   // scout (DESIGN.md "Scout").  Leader: the scout's record of this iteration as far as received (sp_stage), sp_on =
   // still worth asking; eg_hit[e] = first colliding point of batch edge e taken from the record, -2 = none.
   // Scout: the record it builds.
   ScoutRec sr;
+#ifdef SMP_TRACE
+  int trole;                    // SMP_TRACE builds: 0 leader, 1 / 2 scout (trace records of this workgroup)
+  unsigned tn;                  // records of this role so far
+  long long tit;                // iteration the records belong to
+#endif
   int sp_on, sp_stage, sp_go[2];
   int sc_same[2];               // leader: scout 1 / 2 runs on this XCD (1), another (0), not yet known (-1)
   int asked[4];                 // leader: scout (1, 2) asked for iteration k in slot k % 4, 0 = none
@@ -224,6 +237,31 @@ struct Ctx {
   SceneDev sc;
   QueryDev Q;
 };
+
+// SMP_TRACE builds (tools/trace_probe.py): thread 0 of the leader and of the scouts appends (role, source line,
+// device clock) records for the iterations [SMP_TRACE_IT0, SMP_TRACE_IT1) of query 0; smp_debug_tlog reads them.
+#ifdef SMP_TRACE
+#ifndef SMP_TRACE_IT0
+#define SMP_TRACE_IT0 3000
+#endif
+#ifndef SMP_TRACE_IT1
+#define SMP_TRACE_IT1 3040
+#endif
+constexpr unsigned TLOG_CAP = 1u << 18, TLOG_ROLE = TLOG_CAP / 4;  // records per role (0 leader, 1-2 scouts)
+__device__ unsigned long long g_tlog[TLOG_CAP];
+__device__ unsigned g_tlog_n[4];
+// No atomics: each workgroup keeps its role's record count in LDS (loaded at launch start by tlog_begin) and
+// stores it back after every record (plain stores, nothing waited on), so tracing adds ~0.1 us per record.
+#define TR()                                                                                                  \
+  if (threadIdx.x == 0 && g_L.tit >= SMP_TRACE_IT0 && g_L.tit < SMP_TRACE_IT1 && g_L.tn < TLOG_ROLE) {        \
+    g_tlog[g_L.trole * TLOG_ROLE + g_L.tn] =                                                                   \
+        ((unsigned long long)g_L.trole << 62) | ((unsigned long long)((g_L.tit - SMP_TRACE_IT0) & 0xff) << 54) | \
+        ((unsigned long long)(__LINE__ & 0x3fff) << 40) | (wall_clock64() & 0xffffffffffull);                  \
+    g_tlog_n[g_L.trole] = ++g_L.tn;                                                                            \
+  }
+#else
+#define TR()
+#endif
 
 // Phase clocks (thread 0, s_memrealtime ticks): where an iteration spends its time.
 enum { P_SAMPLE, P_NN, P_EXPAND, P_NEAR, P_CHOOSE, P_REWIRE, P_CONNECT, P_TILES, P_NTILES, P_COSTS, P_VIA, P_NVIA,
@@ -321,23 +359,6 @@ __device__ void insert_node(const Ctx& C, int t, const double* e_start, const do
 }
 
 // --------------------------------------------------------------------------------------- scans
-// Block argmin of (d, i): smallest d, then smallest i; d >= 10000 never wins (birrt_star.cpp:4090,4122).
-__device__ int block_argmin(double d, int i) {
-  for (int off = 32; off > 0; off >>= 1) {
-    double od = __shfl_xor(d, off);
-    int oi = __shfl_xor(i, off);
-    if (od < d || (od == d && oi < i)) { d = od; i = oi; }
-  }
-  if (lane_id() == 0) { g_L.wd[wave_id()] = d; g_L.wi[wave_id()] = i; }
-  __syncthreads();
-  double bd = g_L.wd[0];
-  int bi = g_L.wi[0];
-  for (int w = 1; w < BLOCK / 64; ++w)
-    if (g_L.wd[w] < bd || (g_L.wd[w] == bd && g_L.wi[w] < bi)) { bd = g_L.wd[w]; bi = g_L.wi[w]; }
-  __syncthreads();
-  return bd < 10000.0 ? bi : 0;
-}
-
 // find_nearest_neighbour_interpolation: first strict minimum of the Euclidean joint distance (DH:128-156).
 // sqrt is monotone, so a node can only beat the running minimum if its squared distance is below the minimum's
 // squared distance; the (correctly rounded) sqrt is taken only then and compared exactly as the reference does.
@@ -345,6 +366,7 @@ __device__ bool spec_stage(const Ctx& C, int s);
 // Block argmin of the nodes [i_begin, n) of tree t: the first strict minimum (d, id) of the distances, d = 10000
 // if none is below it.  All threads; result in (g_L.wd[0], g_L.wi[0]) via nearest_scan's return.
 __device__ int nearest_scan(const Ctx& C, int t, const double* q, int i_begin, double* d_out) {
+  TR();
   const gcdptr tq = uni_gptr(C.Q.tr[t].q);
   const int n = uni(g_L.S.n[t]), cap = uni(g_L.S.cap);
   double qq[NJ];
@@ -352,8 +374,8 @@ __device__ int nearest_scan(const Ctx& C, int t, const double* q, int i_begin, d
   double best = 10000.0, best_s = 1e300;
   int bid = 0x7fffffff;
   // NPT nodes per thread per round, all loads of a round issued together: a round costs about one memory latency
-  // plus one 8-term dependent sum, so few rounds matter more than few loads (a 4k-node tree is 2 rounds)
-  constexpr int NPT = 4;
+  // plus one 8-term dependent sum, so few rounds matter more than few loads (a 4k-node tree is 1 round)
+  constexpr int NPT = 8;
   for (int i0 = i_begin + threadIdx.x; i0 < n; i0 += NPT * BLOCK) {
     double a[NPT][NJ];
 #pragma unroll
@@ -383,19 +405,26 @@ __device__ int nearest_scan(const Ctx& C, int t, const double* q, int i_begin, d
       }
     }
   }
-  for (int off = 32; off > 0; off >>= 1) {
-    double od = __shfl_xor(best, off);
-    int oi = __shfl_xor(bid, off);
-    if (od < best || (od == best && oi < bid)) { best = od; bid = oi; }
-  }
-  if (lane_id() == 0) { g_L.wd[wave_id()] = best; g_L.wi[wave_id()] = bid; }
+  TR();
+  // (distance, id) lexicographic minimum: distances are non-negative doubles, whose bit patterns order like the
+  // values, so the wave minimum is two DPP integer reductions (distance bits, then the lowest id among the lanes
+  // holding that distance) instead of fp64 compares through shuffles
+  const unsigned long long key = (unsigned long long)__double_as_longlong(best);
+  const unsigned long long wk = __ockl_wfred_min_u64(key);
+  const int wi = __ockl_wfred_min_i32(key == wk ? bid : 0x7fffffff);
+  if (lane_id() == 0) { g_L.wk[wave_id()] = wk; g_L.wi[wave_id()] = wi; }
   __syncthreads();
-  double bd = g_L.wd[0];
+  unsigned long long bk = g_L.wk[0];
   int bi = g_L.wi[0];
-  for (int w = 1; w < BLOCK / 64; ++w)
-    if (g_L.wd[w] < bd || (g_L.wd[w] == bd && g_L.wi[w] < bi)) { bd = g_L.wd[w]; bi = g_L.wi[w]; }
+#pragma unroll
+  for (int w = 1; w < BLOCK / 64; ++w) {
+    const unsigned long long k = g_L.wk[w];
+    const int i = g_L.wi[w];
+    if (k < bk || (k == bk && i < bi)) { bk = k; bi = i; }
+  }
   __syncthreads();
-  *d_out = bd;
+  *d_out = __longlong_as_double((long long)bk);
+  TR();
   return bi;
 }
 
@@ -634,6 +663,9 @@ __device__ __noinline__ void near_set_stream(const Ctx& C, int t, const double* 
     _tn = _t;                                                                            \
   }
 #define NEAR_COUNT(k) if (threadIdx.x == 0) g_L.S.prof[k]++
+#elif defined(SMP_TRACE)
+#define NEAR_CLOCK(k) TR()
+#define NEAR_COUNT(k)
 #else
 #define NEAR_CLOCK(k)
 #define NEAR_COUNT(k)
@@ -656,6 +688,7 @@ __device__ void near_set(const Ctx& C, int t, const double* q, int excl, bool sp
   const double r = g_L.S.near_r;
   const double r2 = r * r, r2lo = r2 * (1.0 - 1e-12), r2hi = r2 * (1.0 + 1e-12);
   const int lane = lane_id(), wave = wave_id();
+  TR();
   if (spec && spec_stage(C, SC_NEAR)) {
     // the scout's near set of the same configuration over the tree's first X nodes is the answer if none of the
     // nodes appended since is near (else the full scan below)
@@ -684,6 +717,7 @@ __device__ void near_set(const Ctx& C, int t, const double* q, int excl, bool sp
           g_L.S.sc_near++;
         }
         __syncthreads();
+        TR();
         return;
       }
     }
@@ -742,10 +776,8 @@ __device__ void near_set(const Ctx& C, int t, const double* q, int excl, bool sp
         }
       }
     }
-    for (int off = 32; off > 0; off >>= 1) {
-      kmin = min(kmin, (unsigned long long)__shfl_xor(kmin, off));
-      kmax = max(kmax, (unsigned long long)__shfl_xor(kmax, off));
-    }
+    kmin = __ockl_wfred_min_u64(kmin);
+    kmax = __ockl_wfred_max_u64(kmax);
     if (lane == 0) { g_L.nh.wmin[wave] = kmin; g_L.nh.wmax[wave] = kmax; g_L.nh.wtot[wave] = wc; }
     if (threadIdx.x < NEAR_BINS) g_L.nh.hist[threadIdx.x] = 0;
     __syncthreads();
@@ -898,6 +930,7 @@ __device__ void near_set(const Ctx& C, int t, const double* q, int excl, bool sp
   }
   if (threadIdx.x == 0) { g_L.nk = tot_all; g_L.S.near_nodes += n; }
   __syncthreads();
+  TR();
 }
 
 // --------------------------------------------------------------------------------------- edges
@@ -905,6 +938,7 @@ __device__ void near_set(const Ctx& C, int t, const double* q, int excl, bool sp
 // 4162-4242) for E <= MAXE edges eg_start -> eg_target, base costs eg_base.  Segment norms in parallel,
 // ordered sums per edge.  Fills eg_step, eg_end (the child configuration) and eg_cost.
 __device__ void edge_costs(const Ctx& C, int E) {
+  TR();
   PROF_BEGIN();
   const int np = g_L.S.n_pts;
   const RobotDev* rb = (&g_rb);
@@ -939,6 +973,7 @@ __device__ void edge_costs(const Ctx& C, int E) {
   }
   __syncthreads();
   PROF_END(P_COSTS);
+  TR();
 }
 
 // isEdgeValid for the edges with eg_need[e] set: eg_first[e] = index of the first colliding configuration,
@@ -1032,7 +1067,9 @@ __device__ __forceinline__ void edge_validity_job(const Ctx& C, int E, int pslot
   __syncthreads();
   const int ne = uni(J.E), nt = uni(J.ntiles), seq = uni(J.seq);
   if (ne == 0) {
-    overlap_work(C, ov, ovt);
+    // nothing to check (the scout's record had every edge): no job whose latency the scan would hide, and its
+    // result may not be needed (OV_NEAR_EXPAND when the expand edge collides) -- the caller scans if it must
+    overlap_work(C, OV_NONE, ovt);
     return;
   }
   const unsigned long long tj0 = threadIdx.x == 0 ? wall_clock64() : 0;
@@ -1061,7 +1098,9 @@ __device__ __forceinline__ void edge_validity_job(const Ctx& C, int E, int pslot
 #endif
   PROF_BEGIN();
   if (threadIdx.x == 0) { g_L.S.prof[P_TFK] += _pt - tj0; g_L.S.prof[P_TTEST]++; }  // job publication
+  TR();
   overlap_work(C, ov, ovt);
+  TR();
   // the leader's own tiles
   for (int t = W - 1; t < nt; t += W) {
     const unsigned m = job_tile_mask(C, J, t);
@@ -1122,6 +1161,7 @@ __device__ __forceinline__ void edge_validity_job(const Ctx& C, int E, int pslot
     }
     __builtin_amdgcn_s_sleep(1);
   }
+  TR();
   if (threadIdx.x == 0) g_L.S.prof[P_TCENTRE] += wall_clock64() - tj1;  // waiting for helpers' tiles
   // first collision per job edge from the tile masks
   for (int t = threadIdx.x; t < nt; t += BLOCK) {
@@ -1278,6 +1318,7 @@ __device__ bool spec_stage(const Ctx& C, int s) {
   const int par = (int)(g_L.S.iter & 3);
   const unsigned tag = (unsigned)(g_L.S.iter + 1);
   const unsigned long long t0 = threadIdx.x == 0 ? wall_clock64() : 0;
+  TR();
   int got;
   for (int k = 0;; k ^= 1) {
     if (threadIdx.x == 0) {
@@ -1294,6 +1335,7 @@ __device__ bool spec_stage(const Ctx& C, int s) {
     __builtin_amdgcn_s_sleep(1);
   }
   if (threadIdx.x == 0) g_L.S.sc_wait += wall_clock64() - t0;
+  TR();
   if (got < 0) {
     if (threadIdx.x == 0) g_L.sp_on = 0;
     __syncthreads();
@@ -1332,6 +1374,31 @@ __device__ void spec_copy(const ScoutBoard* sb, int par, int have, int st) {
 // requested tree stay as they are until the record is used (only appends before then), and their stores are
 // drained here, so the scout reads them as the leader will.  Iteration j looks a record up only if it was asked
 // for (asked[j % 4]); every scout also gets the leader's current iteration (its staleness test).
+// Thread 0: asks the scout for iteration k (expanding `tree`, whose first n[tree] nodes are final for it); with a
+// second scout the two alternate by parity (scout 2 takes the even iterations).
+__device__ void scout_ask(const Ctx& C, long long k, int tree, bool pre, bool& fenced) {
+  const QState& S = g_L.S;
+  const int which = C.Q.scb2 && !(k & 1) ? 2 : 1;
+  ScoutBoard* sb = which == 2 ? C.Q.scb2 : C.Q.scb;
+  int& same = g_L.sc_same[which - 1];
+  if (same < 0) {
+    const int x = ld_agent(&sb->xcc);
+    if (x > 0) same = (x - 1) == xcc_id() ? 1 : 0;
+  }
+  // a scout on another XCD reads through its own L2: write this XCD's dirty lines back first
+  if (same != 1 && !fenced) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    drain();
+    fenced = true;
+  }
+  const unsigned tag = (unsigned)(k + 1);
+  const unsigned w0 = (unsigned)S.n[tree] | (unsigned)tree << 28 | (unsigned)(!pre) << 29;
+  st_agent(&sb->req[2], granule(tag, (unsigned)S.n[1 - tree]));
+  st_agent(&sb->req[1], granule(tag, (unsigned)g_L.smp_ver));
+  st_agent(&sb->req[0], granule(tag, w0));
+  g_L.asked[k & 3] = which;
+}
+
 __device__ void scout_request(const Ctx& C, int t) {
   drain();
   __syncthreads();
@@ -1347,29 +1414,26 @@ __device__ void scout_request(const Ctx& C, int t) {
     for (int ahead = 1; ahead <= (two ? 2 : 1); ++ahead) {
       const long long k = j + ahead;
       if (g_L.asked[k & 3]) continue;
-      const int which = two && !(k & 1) ? 2 : 1;  // pre-solution: scout 2 takes the even iterations
-      ScoutBoard* sb = which == 2 ? C.Q.scb2 : C.Q.scb;
-      int& same = g_L.sc_same[which - 1];
-      if (same < 0) {
-        const int x = ld_agent(&sb->xcc);
-        if (x > 0) same = (x - 1) == xcc_id() ? 1 : 0;
-      }
-      // a scout on another XCD reads through its own L2: write this XCD's dirty lines back first
-      if (same != 1 && !fenced) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        drain();
-        fenced = true;
-      }
-      const int tree = ahead == 1 ? t : 1 - t;
-      const unsigned tag = (unsigned)(k + 1);
-      const unsigned w0 = (unsigned)S.n[tree] | (unsigned)tree << 28 | (unsigned)(!pre) << 29;
-      st_agent(&sb->req[2], granule(tag, (unsigned)S.n[1 - tree]));
-      st_agent(&sb->req[1], granule(tag, (unsigned)g_L.smp_ver));
-      st_agent(&sb->req[0], granule(tag, w0));
-      g_L.asked[k & 3] = which;
+      scout_ask(C, k, ahead == 1 ? t : 1 - t, pre, fenced);
     }
     g_L.sp_on = g_L.asked[j & 3] != 0;
     g_L.sp_stage = -1;
+  }
+  __syncthreads();
+}
+
+// After the first solution, with two scouts: iteration j asks for iteration j + 2 once its own rewire commits are
+// done (or where they would be).  j + 2 expands tree_A of iteration j, which no later step of iteration j changes
+// and iteration j + 1 only appends to (its connect step), so the record stays exact up to the appended nodes, which
+// the leader patches in as before; each scout gets two leader iterations for its pass.
+__device__ void scout_request_ahead2(const Ctx& C, int tA) {
+  if (!C.Q.scb2) return;
+  drain();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const long long k = g_L.S.iter + 2;
+    bool fenced = false;
+    if (!g_L.asked[k & 3]) scout_ask(C, k, tA, false, fenced);
   }
   __syncthreads();
 }
@@ -1385,29 +1449,39 @@ __device__ void edge_validity(const Ctx& C, int E, bool stop_first_valid, int ps
                               int sgrp = -1) {
   const int np1 = g_L.S.n_pts + 1;
   if (threadIdx.x == 0) g_L.count_slot = pslot + 4;
+  TR();
   if (C.Q.jb) {
     if (threadIdx.x < MAXE) g_L.eg_hit[threadIdx.x] = -2;
     __syncthreads();
     if (sgrp >= 0 && spec_stage(C, sgrp)) {
+      TR();
       const int g0 = sgrp == SC_EXPAND ? 0 : sgrp == SC_CHOOSE ? SCOUT_CHOOSE0 : SCOUT_REWIRE0;
       const int gn = sgrp == SC_EXPAND ? 1 : sgrp == SC_CHOOSE ? g_L.sr.n_choose : g_L.sr.n_rewire;
-      for (int it = threadIdx.x; it < E * gn; it += BLOCK) {
-        const int e = it / gn, k = g0 + it - (it / gn) * gn;
-        const ScoutEdge& R = g_L.sr.e[k];
-        if (g_L.eg_need[e] && R.first >= 0 && same8(g_L.eg_start[e], R.s) && same8(g_L.eg_target[e], R.g))
-          g_L.eg_hit[e] = R.first;  // equal edges have equal results: concurrent writers agree
+      // wave 0, lane e = batch edge e: the record edge at the same position first (the scout builds its candidate
+      // lists with the leader's code, so they usually line up), then any other record edge
+      if (threadIdx.x < 64) {
+        const int e = threadIdx.x;
+        const bool need = e < E && g_L.eg_need[e];
+        int hit = -2;
+        if (need) {
+          const int d = e < gn ? e : -1;
+          for (int u = 0; u < gn; ++u) {
+            const int k = g0 + (d < 0 ? u : (u == 0 ? d : (u <= d ? u - 1 : u)));
+            const ScoutEdge& R = g_L.sr.e[k];
+            if (R.first >= 0 && same8(g_L.eg_start[e], R.s) && same8(g_L.eg_target[e], R.g)) { hit = R.first; break; }
+          }
+          g_L.eg_hit[e] = hit;
+        }
+        const unsigned long long mh = __ballot(need && hit >= 0), mm = __ballot(need && hit < 0);
+        if (e == 0) { g_L.S.sc_edge_hit += __popcll(mh); g_L.S.sc_edge_miss += __popcll(mm); }
       }
       __syncthreads();
-      if (threadIdx.x == 0) {
-        for (int e = 0; e < E; ++e) {
-          if (!g_L.eg_need[e]) continue;
-          if (g_L.eg_hit[e] >= 0) g_L.S.sc_edge_hit++; else g_L.S.sc_edge_miss++;
-        }
-      }
     }
+    TR();
     edge_validity_job(C, E, pslot, ov, ovt);
     if (threadIdx.x < E && g_L.eg_hit[threadIdx.x] >= 0) g_L.eg_first[threadIdx.x] = g_L.eg_hit[threadIdx.x];
     __syncthreads();
+    TR();
     return;
   }
   if (threadIdx.x < E) { g_L.eg_first[threadIdx.x] = np1; g_L.eg_ptr[threadIdx.x] = 0; }
@@ -1498,6 +1572,29 @@ __device__ __forceinline__ void count_edge(int first) {
   else { g_L.S.checked += first + 1; g_L.S.valid += first; }
 }
 
+// count_edge over the needed edges of a batch, wave-parallel: every needed edge e < E (stop_first: up to and
+// including the first needed one that is free, which is returned; -1 if none).  All threads.
+__device__ int count_edges(int E, bool stop_first) {
+  if (threadIdx.x < 64) {
+    const int e = threadIdx.x, np1 = g_L.S.n_pts + 1;
+    const bool need = e < E && g_L.eg_need[e];
+    const int f = need ? g_L.eg_first[e] : 0;
+    const unsigned long long mfree = __ballot(need && f >= np1);
+    const int ev = (stop_first && mfree) ? __builtin_ctzll(mfree) : 64;
+    int chk = 0, val = 0;
+    if (need && e <= ev) { chk = f >= np1 ? np1 : f + 1; val = f >= np1 ? np1 : f; }
+    for (int off = 32; off > 0; off >>= 1) { chk += __shfl_xor(chk, off); val += __shfl_xor(val, off); }
+    if (e == 0) {
+      g_L.S.prof[g_L.count_slot] += chk;
+      g_L.S.checked += chk;
+      g_L.S.valid += val;
+      g_L.found = ev < 64 ? ev : -1;
+    }
+  }
+  __syncthreads();
+  return uni(g_L.found);
+}
+
 // stepTowardsRandSample (birrt_star.cpp:5712-5868), single lane.
 __device__ bool step_towards(const RobotDev* rb, const double* nn, double* x, double f) {
   double ed[NJ], srev = 0.0, spr = 0.0;
@@ -1530,6 +1627,7 @@ __device__ bool step_towards(const RobotDev* rb, const double* nn, double* x, do
 // unconstraint_extend_step_factor, collecting via nodes (ids nn_t, nn_t+1, ...) until the target is
 // reached; the last edge becomes `sel` (id nn_t at that point).  No collision checks (reference behaviour).
 __device__ void via_chain(const Ctx& C, const double* target) {
+  TR();
   PROF_BEGIN();
   for (;;) {
     if (threadIdx.x == 0) g_L.S.prof[P_NVIA]++;
@@ -1567,6 +1665,7 @@ __device__ void via_chain(const Ctx& C, const double* target) {
     if (uni(g_L.reached)) break;
   }
   PROF_END(P_VIA);
+  TR();
 }
 
 // Inserts the pending via nodes (insertNode, birrt_star.cpp:3298-3322, once per node in order).  They form a
@@ -1574,6 +1673,7 @@ __device__ void via_chain(const Ctx& C, const double* target) {
 // inserts is known up front: node n0+k gets first child n0+k+1 (none for the last), and only p0's child list
 // changes among the existing nodes.  One thread per node; thread 0 also links the first node under p0.
 __device__ void insert_via(const Ctx& C, int t) {
+  TR();
   DETAIL_BEGIN(_di);
   const int nv = uni(g_L.n_via);
   if (nv > 0) {
@@ -1618,6 +1718,7 @@ __device__ void insert_via(const Ctx& C, int t) {
   }
   DETAIL_END(_di, 31);
   __syncthreads();
+  TR();
 }
 
 // --------------------------------------------------------------------------------------- sampling
@@ -1779,6 +1880,7 @@ __device__ void sample_publish(const Ctx& C) {
 // a look at the stage of this iteration's scout record, whose sections are then copied ahead of the steps that
 // use them -- else drawn here.
 __device__ void sample_read(const Ctx& C) {
+  TR();
   QState& S = g_L.S;
   const uint32_t it = (uint32_t)S.iter;
   const bool pre = uni(g_L.sp_on && g_L.sp_stage < 0) != 0;
@@ -1887,12 +1989,8 @@ __device__ void choose_parent(const Ctx& C, int t) {
     for (int e = E + threadIdx.x; e < MAXE; e += BLOCK) g_L.eg_need[e] = 0;
     __syncthreads();
     edge_validity(C, E, true, P_XCHOOSE, 0, 0, SC_CHOOSE);
+    count_edges(E, true);  // -> g_L.found
     if (threadIdx.x == 0) {
-      for (int e = 0; e < E; ++e) {
-        if (!g_L.eg_need[e]) continue;
-        count_edge(g_L.eg_first[e]);
-        if (g_L.eg_first[e] > g_L.S.n_pts) { g_L.found = e; break; }
-      }
       if (g_L.found >= 0) {
         g_L.ext_bp = 1;
         g_L.n_via = 0;
@@ -1970,6 +2068,7 @@ __device__ void rewire(const Ctx& C, int t) {
   for (int e = cnt + threadIdx.x; e < MAXE; e += BLOCK) g_L.eg_need[e] = 0;
   __syncthreads();
   edge_validity(C, cnt, false, P_XREWIRE, OV_NN, 1 - t, SC_DONE);
+  TR();
   DETAIL_BEGIN(_dr);
   // Sequential commits (birrt_star.cpp:5096-5228).  The candidates' parents and costs are gathered into LDS by
   // one thread each; thread 0 walks the candidates from the resume point and stops after a commit, which may
@@ -1983,15 +2082,32 @@ __device__ void rewire(const Ctx& C, int t) {
       for (int k = 0; k < 3; ++k) g_L.rw_cost[e][k] = T.cost[(size_t)k * cap + vv];
     }
     __syncthreads();
+    // wave 0: the candidates from e0 on that act (birrt_star.cpp:5094-5110: not x_new's parent, not a child of the
+    // root, cheaper through x_new), the first acting one that is free commits; every acting candidate up to it is
+    // counted as the sequential loop counts it
+    if (threadIdx.x < 64) {
+      const int e = threadIdx.x, np1 = g_L.S.n_pts + 1;
+      const bool act = e >= e0 && e < cnt && g_L.S.status == 0 && g_L.eg_near[e] != g_L.xn.parent &&
+                       g_L.rw_par[e] != 0 && g_L.eg_cost[e][0] < g_L.rw_cost[e][0];
+      const int f = act ? g_L.eg_first[e] : 0;
+      const unsigned long long mc = __ballot(act && f >= np1);
+      const int ec = mc ? __builtin_ctzll(mc) : 64;
+      int chk = 0, val = 0;
+      if (act && e <= ec) { chk = f >= np1 ? np1 : f + 1; val = f >= np1 ? np1 : f; }
+      for (int off = 32; off > 0; off >>= 1) { chk += __shfl_xor(chk, off); val += __shfl_xor(val, off); }
+      if (e == 0) {
+        g_L.S.prof[g_L.count_slot] += chk;
+        g_L.S.checked += chk;
+        g_L.S.valid += val;
+        g_L.rw_next = ec;
+      }
+    }
+    __syncthreads();
     if (threadIdx.x == 0) {
       QState& S = g_L.S;
       int next = cnt;
-      for (int e = e0; e < cnt && S.status == 0; ++e) {
+      for (int e = g_L.rw_next; e < cnt; ++e) {  // at most one pass: e is the committing candidate
         const int v = g_L.eg_near[e];
-        if (!(v != g_L.xn.parent && g_L.rw_par[e] != 0)) continue;
-        if (!(g_L.eg_cost[e][0] < g_L.rw_cost[e][0])) continue;
-        count_edge(g_L.eg_first[e]);
-        if (g_L.eg_first[e] <= S.n_pts) continue;
         double red[3];
         for (int k = 0; k < 3; ++k) red[k] = g_L.eg_cost[e][k] - g_L.rw_cost[e][k];
         // unlink from the old parent (the reference erases the outgoing edge, birrt_star.cpp:5124-5169)
@@ -2033,6 +2149,7 @@ __device__ void rewire(const Ctx& C, int t) {
   }
   DETAIL_END(_dr, 28);
   __syncthreads();
+  TR();
 }
 
 // connectGraphsInterpolation, unconstrained branch + commit (birrt_star.cpp:2608-3046, 3219-3288).
@@ -2213,12 +2330,20 @@ __device__ void connect_graphs(const Ctx& C, int t) {
 __device__ __forceinline__ void iteration(const Ctx& C) {
   const int A = uni(g_L.S.A), B = 1 - A;
   unsigned long long _t0 = threadIdx.x == 0 ? wall_clock64() : 0, _t1;
+#ifdef SMP_TRACE
+  if (threadIdx.x == 0) g_L.tit = g_L.S.iter;
+#endif
+  TR();
 #define PHASE(k) if (threadIdx.x == 0) { _t1 = wall_clock64(); g_L.S.prof[k] += _t1 - _t0; _t0 = _t1; }
   sample_publish(C);
+  TR();
   if (C.Q.scb) scout_request(C, B);
+  TR();
   sample_read(C);
+  TR();
   PHASE(P_SAMPLE);
   int nid = nearest(C, A, g_L.xr, true);
+  TR();
   PHASE(P_NN);
   if (threadIdx.x == 0) {
     load_node(C, A, nid, &g_L.nn);
@@ -2250,9 +2375,11 @@ __device__ __forceinline__ void iteration(const Ctx& C) {
     g_L.eg_need[0] = 1;
   }
   __syncthreads();
+  TR();
   const bool opt = uni(g_L.S.tree_opt && g_L.S.have_sol);
   if (!uni(g_L.flag)) edge_costs(C, 1);
   edge_validity(C, 1, false, P_XEXPAND, opt ? OV_NEAR_EXPAND : OV_NONE, A, SC_EXPAND);
+  TR();
   if (threadIdx.x == 0) {
     int f = g_L.eg_first[0];
     count_edge(f);
@@ -2274,9 +2401,12 @@ __device__ __forceinline__ void iteration(const Ctx& C) {
   PHASE(P_EXPAND);
   if (opt) {
     // x_new is the expand edge's end exactly when the edge is valid: then its near set was computed during the job
+    TR();
     if (!(uni(g_L.ext_nn) && take_spec(OV_NEAR_EXPAND))) near_set<20>(C, A, g_L.xn.q, g_L.xn.id, true);
+    TR();
     PHASE(P_NEAR);
     choose_parent(C, A);
+    TR();
     PHASE(P_CHOOSE);
   }
   if (uni(g_L.ext_nn || g_L.ext_bp)) {
@@ -2284,7 +2414,12 @@ __device__ __forceinline__ void iteration(const Ctx& C) {
     __syncthreads();
     if (threadIdx.x == 0) g_L.spec = OV_NONE;
     __syncthreads();
-    if (opt) rewire(C, A);
+    TR();
+    if (opt) {
+      rewire(C, A);
+      scout_request_ahead2(C, A);
+    }
+    TR();
     PHASE(P_REWIRE);
     int cid;
     if (take_spec(OV_NN)) {
@@ -2304,9 +2439,14 @@ __device__ __forceinline__ void iteration(const Ctx& C) {
     }
     if (threadIdx.x == 0) load_node(C, B, cid, &g_L.xc);
     __syncthreads();
+    TR();
     PHASE(P_NN);
     connect_graphs(C, B);
+    TR();
     PHASE(P_CONNECT);
+  }
+  else if (opt) {
+    scout_request_ahead2(C, A);
   }
 #undef PHASE
   if (threadIdx.x == 0) {
@@ -2365,6 +2505,10 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
   const unsigned tag = (unsigned)(it + 1);
   (void)jb;
   unsigned long long _ts = threadIdx.x == 0 ? wall_clock64() : 0;
+#ifdef SMP_TRACE
+  if (threadIdx.x == 0) g_L.tit = it;
+#endif
+  TR();
   if (threadIdx.x == 0) {
     S.prof[30]++;
     S.n[t] = X;
@@ -2397,6 +2541,7 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
   }
   __syncthreads();
   SC_PHASE(0);
+  TR();
   if (!uni(g_L.flag)) {
     sc_copy_out(sb, par, &R.nn, sizeof(ScoutNN));
     sc_copy_out(sb, par, &R.nr, sizeof(ScoutNear));
@@ -2424,6 +2569,7 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
   sc_copy_out(sb, par, &R.nn, sizeof(ScoutNN));
   sc_publish(C, par, tag, SC_NN);
   SC_PHASE(1);
+  TR();
   edge_costs(C, 1);
   if (threadIdx.x == 0) {  // the expand edge's interpolation data, for the leader (published with SC_EXPAND)
     for (int j = 0; j < NJ; ++j) { R.ex.ext[j] = g_L.eg_target[0][j]; R.ex.step[j] = g_L.eg_step[0][j]; R.ex.end[j] = g_L.eg_end[0][j]; }
@@ -2491,6 +2637,7 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
   }
   sc_publish(C, par, tag, SC_EXPAND);
   SC_PHASE(2);
+  TR();
   // near set of x_new (the leader's, before choose_parent)
   if (!(uni(g_L.ext_nn) && take_spec(OV_NEAR_EXPAND))) near_set<20>(C, t, g_L.xn.q, X);
   if (threadIdx.x < 20) {
@@ -2506,6 +2653,7 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
   sc_copy_out(sb, par, &R.nr, sizeof(ScoutNear));
   sc_publish(C, par, tag, SC_NEAR);
   SC_PHASE(3);
+  TR();
   // choose_parent's candidate edges (all needed ones checked: the job computes every tile)
   if (threadIdx.x == 0) {
     int E = 0;
@@ -2554,6 +2702,7 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
   if (sc_stale(C, tag)) { sc_publish(C, par, tag, SC_DONE); return; }
   sc_publish(C, par, tag, SC_CHOOSE);
   SC_PHASE(4);
+  TR();
   if (uni(g_L.found) >= 0) {
     // x_new <- the last edge of the via chain from the chosen parent (choose_parent)
     if (threadIdx.x == 0) {
@@ -2574,6 +2723,7 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
     __syncthreads();
   }
   SC_PHASE(5);
+  TR();
   if (!uni(g_L.ext_nn || g_L.ext_bp)) { sc_publish(C, par, tag, SC_DONE); return; }
   // rewire's candidate edges (rewire())
   const TreeDev& T = C.Q.tr[t];
@@ -2610,6 +2760,7 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
   sc_copy_out(sb, par, &R.e[SCOUT_REWIRE0], cnt * (int)sizeof(ScoutEdge));
   sc_publish(C, par, tag, SC_DONE);
   SC_PHASE(6);
+  TR();
 }
 #undef SC_PHASE
 
@@ -2644,6 +2795,11 @@ __device__ __forceinline__ void scout_main(Ctx& C, int which) {
     g_L.spec = OV_NONE;
     g_L.sp_on = 0;
     st_agent(&C.Q.scb->xcc, xcc_id() + 1);
+#ifdef SMP_TRACE
+    g_L.trole = which;
+    g_L.tit = -1;
+    g_L.tn = g_tlog_n[which];
+#endif
   }
   __syncthreads();
   unsigned last = 0;
@@ -2729,6 +2885,11 @@ __global__ void __launch_bounds__(BLOCK) plan_kernel(const RobotDev* __restrict_
     g_L.near_blo = ~0ull;
     g_L.near_bhi = 0;
     g_L.smp_ver = 0;
+#ifdef SMP_TRACE
+    g_L.trole = 0;
+    g_L.tit = -1;
+    g_L.tn = g_tlog_n[0];
+#endif
   }
   __syncthreads();
   if (uni(g_L.S.status == 0 && g_L.S.phase == 0)) {
@@ -2924,6 +3085,26 @@ __global__ void __launch_bounds__(BLOCK) near_probe_kernel(const double* tq, con
 }
 
 }  // namespace smp
+
+#ifdef SMP_TRACE
+// Copies the records of every role (out: cap >= TLOG_CAP words, roles in blocks of TLOG_ROLE, unused words 0).
+extern "C" int smp_debug_tlog(unsigned long long* out, int cap, int reset) {
+  if (cap < (int)smp::TLOG_CAP) return -1;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(smp::g_tlog), smp::TLOG_CAP * sizeof(unsigned long long)) != hipSuccess) return -1;
+  unsigned n[4];
+  if (hipMemcpyFromSymbol(n, HIP_SYMBOL(smp::g_tlog_n), sizeof(n)) != hipSuccess) return -1;
+  if (reset) {
+    std::vector<unsigned long long> z(smp::TLOG_CAP, 0);
+    unsigned zn[4] = {0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(smp::g_tlog), z.data(), z.size() * sizeof(unsigned long long)) != hipSuccess) return -1;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(smp::g_tlog_n), zn, sizeof(zn)) != hipSuccess) return -1;
+  }
+  return (int)(n[0] + n[1] + n[2]);
+}
+#else
+extern "C" int smp_debug_tlog(unsigned long long*, int, int) { return -1; }
+#endif
 
 #ifdef SMP_BOUNDS
 extern "C" int smp_debug_bounds(int* out) {
