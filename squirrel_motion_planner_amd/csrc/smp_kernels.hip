@@ -226,7 +226,13 @@ struct PlanLds {
   int sp_on, sp_stage, sp_go[2];
   int sc_same[2];               // leader: scout 1 / 2 runs on this XCD (1), another (0), not yet known (-1)
   int asked[4];                 // leader: scout (1, 2) asked for iteration k in slot k % 4, 0 = none
+  int asked_conn[4];            // leader: that record will carry connect's scans (stage SC_CONN)
+  int conn_rec;                 // leader: connect of this iteration takes its scans from the record (g_L.sr.cc)
+  int two_scouts;               // scout: two scouts share the iterations (post-solution records get SC_CONN)
   int eg_hit[MAXE];
+  int eg_rec[MAXE];             // leader: record edge (index into sr.e) equal to batch edge e, -1 = none
+  int rec_grp;                  // leader: the record stage eg_rec was matched against (-1 = not matched)
+  int rec_all, ev_job;          // rec_match: every edge matched; edge_validity: a job is needed
 };
 
 // The planner's LDS objects live at namespace scope so that every device function addresses them as LDS
@@ -362,7 +368,7 @@ __device__ void insert_node(const Ctx& C, int t, const double* e_start, const do
 // find_nearest_neighbour_interpolation: first strict minimum of the Euclidean joint distance (DH:128-156).
 // sqrt is monotone, so a node can only beat the running minimum if its squared distance is below the minimum's
 // squared distance; the (correctly rounded) sqrt is taken only then and compared exactly as the reference does.
-__device__ bool spec_stage(const Ctx& C, int s);
+__device__ bool spec_stage(const Ctx& C, int s, unsigned long long wait = 0);
 // Block argmin of the nodes [i_begin, n) of tree t: the first strict minimum (d, id) of the distances, d = 10000
 // if none is below it.  All threads; result in (g_L.wd[0], g_L.wi[0]) via nearest_scan's return.
 __device__ int nearest_scan(const Ctx& C, int t, const double* q, int i_begin, double* d_out) {
@@ -976,6 +982,24 @@ __device__ void edge_costs(const Ctx& C, int E) {
   TR();
 }
 
+// edge_costs for E edges whose segment-norm sums the scout computed (acc[e], the same function of the same two
+// configurations): only the interpolation step / end point are formed here.
+__device__ void edge_costs_acc(int E, const double (*acc)[3]) {
+  const int np = g_L.S.n_pts;
+  if (threadIdx.x < E * NJ) {
+    const int e = threadIdx.x / NJ, j = threadIdx.x - e * NJ;
+    const double st = (g_L.eg_target[e][j] - g_L.eg_start[e][j]) / double(np);
+    g_L.eg_step[e][j] = st;
+    g_L.eg_end[e][j] = g_L.eg_start[e][j] + np * st;
+  } else if (threadIdx.x >= 256 && threadIdx.x < 256 + E * 3) {
+    const int i = threadIdx.x - 256, e = i / 3, k = i - e * 3;
+    const double a = acc[e][k];
+    g_L.eg_acc[e][k] = a;
+    g_L.eg_cost[e][k] = g_L.eg_base[e][k] + a;
+  }
+  __syncthreads();
+}
+
 // isEdgeValid for the edges with eg_need[e] set: eg_first[e] = index of the first colliding configuration,
 // or n_pts + 1 if the edge is free.  Each 32-configuration tile takes the next unchecked points of the
 // unresolved needed edges in edge order, so an edge leaves the schedule at its first collision and every
@@ -1301,7 +1325,8 @@ __device__ __forceinline__ void sc_copy_in(const ScoutBoard* sb, int par, void* 
 }
 static_assert(sizeof(ScoutNN) % 8 == 0 && sizeof(ScoutNear) % 8 == 0 && sizeof(ScoutEdge) % 8 == 0 &&
               sizeof(ScoutExpand) % 8 == 0 && offsetof(ScoutRec, ex) % 8 == 0 && offsetof(ScoutRec, nr) % 8 == 0 &&
-              sizeof(ScoutConnect) % 8 == 0 && offsetof(ScoutRec, cn) % 8 == 0 && offsetof(ScoutRec, n_choose) % 8 == 0 && offsetof(ScoutRec, e) % 8 == 0,
+              sizeof(ScoutConnect) % 8 == 0 && offsetof(ScoutRec, cn) % 8 == 0 && sizeof(ScoutConn) % 8 == 0 &&
+              offsetof(ScoutRec, cc) % 8 == 0 && offsetof(ScoutRec, n_choose) % 8 == 0 && offsetof(ScoutRec, e) % 8 == 0,
               "scout record sections are 8-byte words");
 
 constexpr unsigned long long SCOUT_WAIT = 6000;  // device-clock ticks (60 us) the leader waits for one scout stage
@@ -1310,8 +1335,9 @@ constexpr unsigned long long SCOUT_WAIT = 6000;  // device-clock ticks (60 us) t
 // iteration, or SCOUT_WAIT passes: then the scout is not asked again this iteration) and copies the sections of
 // the stages received since the last call into g_L.sr.  All threads; returns whether stage s is there.
 __device__ void spec_copy(const ScoutBoard* sb, int par, int have, int st);
-__device__ bool spec_stage(const Ctx& C, int s) {
+__device__ bool spec_stage(const Ctx& C, int s, unsigned long long wait) {
   if (!uni(g_L.sp_on)) return false;
+  if (wait == 0) wait = SCOUT_WAIT;
   const int have = uni(g_L.sp_stage);
   if (have >= s) return true;
   const ScoutBoard* sb = uni(g_L.asked[g_L.S.iter & 3]) == 2 ? C.Q.scb2 : C.Q.scb;
@@ -1326,7 +1352,7 @@ __device__ bool spec_stage(const Ctx& C, int s) {
       int go = 0;
       if ((unsigned)(v >> 32) != tag) go = -1;           // the scout is not on this iteration
       else if ((int)(unsigned)v >= s) go = 1 + (int)(unsigned)v;
-      else if (wall_clock64() - t0 > SCOUT_WAIT) go = -1;
+      else if (wall_clock64() - t0 > wait) go = -1;
       g_L.sp_go[k] = go;
     }
     __syncthreads();
@@ -1361,6 +1387,7 @@ __device__ void spec_copy(const ScoutBoard* sb, int par, int have, int st) {
   if (opt_now && have < SC_CHOOSE && st >= SC_CHOOSE) sc_copy_in(sb, par, &R.e[SCOUT_CHOOSE0], MAX_NEAR * sizeof(ScoutEdge));
   if (opt_now && have < SC_DONE && st >= SC_DONE) sc_copy_in(sb, par, &R.e[SCOUT_REWIRE0], MAX_NEAR * sizeof(ScoutEdge));
   if (!opt_now && have < SC_DONE && st >= SC_DONE) sc_copy_in(sb, par, &R.cn, sizeof(ScoutConnect));
+  if (have < SC_CONN && st >= SC_CONN) sc_copy_in(sb, par, &R.cc, sizeof(ScoutConn));
   __syncthreads();
   if (threadIdx.x == 0) g_L.sp_stage = st;
   __syncthreads();
@@ -1397,6 +1424,7 @@ __device__ void scout_ask(const Ctx& C, long long k, int tree, bool pre, bool& f
   st_agent(&sb->req[1], granule(tag, (unsigned)g_L.smp_ver));
   st_agent(&sb->req[0], granule(tag, w0));
   g_L.asked[k & 3] = which;
+  g_L.asked_conn[k & 3] = !pre && C.Q.scb2 != nullptr;
 }
 
 __device__ void scout_request(const Ctx& C, int t) {
@@ -1408,6 +1436,7 @@ __device__ void scout_request(const Ctx& C, int t) {
     const bool pre = !(S.tree_opt && S.have_sol);
     const bool two = pre && C.Q.scb2 != nullptr;
     g_L.asked[(j + 3) & 3] = 0;  // iteration j - 1's slot
+    g_L.asked_conn[(j + 3) & 3] = 0;
     st_agent(&C.Q.scb->cur, (unsigned long long)j);
     if (C.Q.scb2) st_agent(&C.Q.scb2->cur, (unsigned long long)j);
     bool fenced = false;
@@ -1431,9 +1460,64 @@ __device__ void scout_request_ahead2(const Ctx& C, int tA) {
   drain();
   __syncthreads();
   if (threadIdx.x == 0) {
-    const long long k = g_L.S.iter + 2;
+    const long long j = g_L.S.iter, k = j + 2;
     bool fenced = false;
     if (!g_L.asked[k & 3]) scout_ask(C, k, tA, false, fenced);
+    // tree_A of this iteration is tree_B of iteration j + 1 and final for its connect step (which comes before any
+    // other write to it): the scout of record j + 1 may run connect's scans now
+    const long long k1 = j + 1;
+    if (g_L.asked[k1 & 3] && g_L.asked_conn[k1 & 3]) {
+      ScoutBoard* sb = g_L.asked[k1 & 3] == 2 ? C.Q.scb2 : C.Q.scb;
+      if (!fenced && g_L.sc_same[g_L.asked[k1 & 3] - 1] != 1) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        drain();
+      }
+      st_agent(&sb->cgo, granule((int)(k1 + 1), (unsigned)g_L.S.n[tA]));
+    }
+  }
+  __syncthreads();
+}
+
+// Leader: matches the batch's first E edges against the candidate edges of scout record stage sgrp (SC_CHOOSE:
+// choose-parent candidates, SC_DONE: rewire candidates; equal start and target bit for bit) -> eg_rec[e], and
+// returns whether every one of them has a record edge.  Wave 0, lane e: the record edge at the same position first
+// (the scout builds its candidate lists with the leader's code, so they usually line up), then the others.
+__device__ bool rec_match(const Ctx& C, int E, int sgrp) {
+  const bool rec = spec_stage(C, sgrp);
+  if (threadIdx.x < 64) {
+    const int e = threadIdx.x;
+    const int g0 = sgrp == SC_EXPAND ? 0 : sgrp == SC_CHOOSE ? SCOUT_CHOOSE0 : SCOUT_REWIRE0;
+    const int gn = !rec ? 0 : sgrp == SC_EXPAND ? 1 : sgrp == SC_CHOOSE ? g_L.sr.n_choose : g_L.sr.n_rewire;
+    int m = -1;
+    if (e < E) {
+      const int d = e < gn ? e : -1;
+      for (int u = 0; u < gn; ++u) {
+        const int k = g0 + (d < 0 ? u : (u == 0 ? d : (u <= d ? u - 1 : u)));
+        const ScoutEdge& R = g_L.sr.e[k];
+        if (same8(g_L.eg_start[e], R.s) && same8(g_L.eg_target[e], R.g)) { m = k; break; }
+      }
+    }
+    if (e < MAXE) g_L.eg_rec[e] = m;
+    const unsigned long long miss = __ballot(e < E && m < 0);
+    if (e == 0) { g_L.rec_grp = sgrp; g_L.rec_all = miss == 0; }
+  }
+  __syncthreads();
+  return uni(g_L.rec_all) != 0;
+}
+
+// edge_costs of E batch edges that all have record edges (rec_match): the record's segment-norm sums.
+__device__ void edge_costs_rec(int E) {
+  const int np = g_L.S.n_pts;
+  if (threadIdx.x < E * NJ) {
+    const int e = threadIdx.x / NJ, j = threadIdx.x - e * NJ;
+    const double st = (g_L.eg_target[e][j] - g_L.eg_start[e][j]) / double(np);
+    g_L.eg_step[e][j] = st;
+    g_L.eg_end[e][j] = g_L.eg_start[e][j] + np * st;
+  } else if (threadIdx.x >= 256 && threadIdx.x < 256 + E * 3) {
+    const int i = threadIdx.x - 256, e = i / 3, k = i - e * 3;
+    const double a = g_L.sr.e[g_L.eg_rec[e]].acc[k];
+    g_L.eg_acc[e][k] = a;
+    g_L.eg_cost[e][k] = g_L.eg_base[e][k] + a;
   }
   __syncthreads();
 }
@@ -1451,33 +1535,42 @@ __device__ void edge_validity(const Ctx& C, int E, bool stop_first_valid, int ps
   if (threadIdx.x == 0) g_L.count_slot = pslot + 4;
   TR();
   if (C.Q.jb) {
-    if (threadIdx.x < MAXE) g_L.eg_hit[threadIdx.x] = -2;
-    __syncthreads();
-    if (sgrp >= 0 && spec_stage(C, sgrp)) {
-      TR();
-      const int g0 = sgrp == SC_EXPAND ? 0 : sgrp == SC_CHOOSE ? SCOUT_CHOOSE0 : SCOUT_REWIRE0;
-      const int gn = sgrp == SC_EXPAND ? 1 : sgrp == SC_CHOOSE ? g_L.sr.n_choose : g_L.sr.n_rewire;
-      // wave 0, lane e = batch edge e: the record edge at the same position first (the scout builds its candidate
-      // lists with the leader's code, so they usually line up), then any other record edge
-      if (threadIdx.x < 64) {
-        const int e = threadIdx.x;
-        const bool need = e < E && g_L.eg_need[e];
-        int hit = -2;
-        if (need) {
+    // the record's results for the needed edges (matched by rec_match for this batch, else here)
+    const bool matched = uni(g_L.rec_grp) == sgrp && sgrp >= 0;
+    const bool rec = sgrp >= 0 && (matched || spec_stage(C, sgrp));
+    TR();
+    if (threadIdx.x < 64) {
+      const int e = threadIdx.x;
+      const bool need = e < E && g_L.eg_need[e];
+      int hit = -2;
+      if (rec && need) {
+        if (matched) {
+          const int k = g_L.eg_rec[e];
+          if (k >= 0 && g_L.sr.e[k].first >= 0) hit = g_L.sr.e[k].first;
+        } else {
+          const int g0 = sgrp == SC_EXPAND ? 0 : sgrp == SC_CHOOSE ? SCOUT_CHOOSE0 : SCOUT_REWIRE0;
+          const int gn = sgrp == SC_EXPAND ? 1 : sgrp == SC_CHOOSE ? g_L.sr.n_choose : g_L.sr.n_rewire;
           const int d = e < gn ? e : -1;
           for (int u = 0; u < gn; ++u) {
             const int k = g0 + (d < 0 ? u : (u == 0 ? d : (u <= d ? u - 1 : u)));
             const ScoutEdge& R = g_L.sr.e[k];
             if (R.first >= 0 && same8(g_L.eg_start[e], R.s) && same8(g_L.eg_target[e], R.g)) { hit = R.first; break; }
           }
-          g_L.eg_hit[e] = hit;
         }
-        const unsigned long long mh = __ballot(need && hit >= 0), mm = __ballot(need && hit < 0);
-        if (e == 0) { g_L.S.sc_edge_hit += __popcll(mh); g_L.S.sc_edge_miss += __popcll(mm); }
       }
-      __syncthreads();
+      if (e < MAXE) g_L.eg_hit[e] = hit;
+      const unsigned long long mh = __ballot(need && hit >= 0), mm = __ballot(need && hit < 0);
+      if (rec && e == 0) { g_L.S.sc_edge_hit += __popcll(mh); g_L.S.sc_edge_miss += __popcll(mm); }
+      // every needed edge answered by the record: no job
+      if (mm == 0 && e < E) g_L.eg_first[e] = need ? hit : np1;
+      if (e == 0) {
+        g_L.ev_job = mm != 0;
+        g_L.rec_grp = -1;
+        if (mm == 0) g_L.spec = OV_NONE;
+      }
     }
-    TR();
+    __syncthreads();
+    if (!uni(g_L.ev_job)) { TR(); return; }
     edge_validity_job(C, E, pslot, ov, ovt);
     if (threadIdx.x < E && g_L.eg_hit[threadIdx.x] >= 0) g_L.eg_first[threadIdx.x] = g_L.eg_hit[threadIdx.x];
     __syncthreads();
@@ -1984,7 +2077,8 @@ __device__ void choose_parent(const Ctx& C, int t) {
       g_L.eg_near[e] = nd.id;
     }
     __syncthreads();
-    edge_costs(C, E);
+    if (C.Q.jb && rec_match(C, E, SC_CHOOSE)) edge_costs_rec(E);
+    else edge_costs(C, E);
     if (threadIdx.x < E) g_L.eg_need[threadIdx.x] = g_L.eg_cost[threadIdx.x][0] <= g_L.xn.c[0];
     for (int e = E + threadIdx.x; e < MAXE; e += BLOCK) g_L.eg_need[e] = 0;
     __syncthreads();
@@ -2057,7 +2151,8 @@ __device__ void rewire(const Ctx& C, int t) {
     g_L.eg_near[e] = v;
   }
   __syncthreads();
-  edge_costs(C, cnt);
+  if (C.Q.jb && rec_match(C, cnt, SC_DONE)) edge_costs_rec(cnt);
+  else edge_costs(C, cnt);
   if (threadIdx.x < cnt) {
     int e = threadIdx.x, v = g_L.eg_near[e];
     // costs only decrease during the loop, so a candidate failing against the current cost never passes
@@ -2165,7 +2260,9 @@ __device__ void connect_graphs(const Ctx& C, int t) {
     g_L.sel.id = -1;
   }
   __syncthreads();
-  edge_costs(C, 1);
+  const bool crec = uni(g_L.conn_rec) != 0;
+  if (crec) edge_costs_acc(1, (const double (*)[3])g_L.sr.cc.acc0);
+  else edge_costs(C, 1);
   if (threadIdx.x == 0) {
     for (int k = 0; k < 3; ++k) g_L.sol[k] = g_L.eg_cost[0][k] + g_L.xn.c[k];
     g_L.eg_need[0] = g_L.sol[0] < g_L.csp[0];
@@ -2180,7 +2277,7 @@ __device__ void connect_graphs(const Ctx& C, int t) {
       if (threadIdx.x == 0) { g_L.eg_first[0] = g_L.sr.cn.e.first; g_L.S.sc_edge_hit++; }
       __syncthreads();
     } else {
-      edge_validity(C, 1, false, P_XCONNECT, g_L.S.have_sol ? OV_NEAR_XN : OV_NONE, t);
+      edge_validity(C, 1, false, P_XCONNECT, (g_L.S.have_sol && !crec) ? OV_NEAR_XN : OV_NONE, t);
     }
     if (threadIdx.x == 0) {
       int f = g_L.eg_first[0];
@@ -2211,7 +2308,23 @@ __device__ void connect_graphs(const Ctx& C, int t) {
     __syncthreads();
   }
   if (uni(g_L.S.have_sol)) {
-    if (!take_spec(OV_NEAR_XN)) near_set<20>(C, t, g_L.xn.q, g_L.xn.id);
+    if (!take_spec(OV_NEAR_XN)) {
+      if (crec) {  // the record's near set of x_new over the same final tree
+        const ScoutConn& R = g_L.sr.cc;
+        if (threadIdx.x < MAX_NEAR) {
+          g_L.lo_i[threadIdx.x] = R.lo_i[threadIdx.x]; g_L.lo_c[threadIdx.x] = R.lo_c[threadIdx.x];
+          g_L.hi_i[threadIdx.x] = R.hi_i[threadIdx.x]; g_L.hi_c[threadIdx.x] = R.hi_c[threadIdx.x];
+        }
+        if (threadIdx.x == 0) {
+          g_L.nk = R.nk; g_L.n_lo = R.n_lo; g_L.n_hi = R.n_hi;
+          g_L.S.near_nodes += g_L.S.n[t];
+          g_L.S.sc_near++;
+        }
+        __syncthreads();
+      } else {
+        near_set<20>(C, t, g_L.xn.q, g_L.xn.id);
+      }
+    }
     if (threadIdx.x == 0) {
       int m = min(g_L.n_lo, g_L.S.max_near);
       g_L.cnt = m;
@@ -2228,7 +2341,8 @@ __device__ void connect_graphs(const Ctx& C, int t) {
         g_L.eg_near[e] = nd.id;
       }
       __syncthreads();
-      edge_costs(C, E);
+      if (crec) edge_costs_acc(E, g_L.sr.cc.acc);
+      else edge_costs(C, E);
       if (threadIdx.x < E) {
         int e = threadIdx.x;
         double s0 = g_L.eg_cost[e][0] + g_L.xn.c[0];
@@ -2324,6 +2438,21 @@ __device__ void connect_graphs(const Ctx& C, int t) {
   __syncthreads();
 }
 
+// Leader, connect step of an iteration after the first solution: takes connect's scans from the scout's record
+// (stage SC_CONN) if it is there within 10 us and was made for this x_new over the final tree_B (same size, same
+// configuration, same excluded id) -> g_L.conn_rec.  All threads.
+__device__ bool conn_stage(const Ctx& C, int B) {
+  if (threadIdx.x == 0) g_L.conn_rec = 0;
+  __syncthreads();
+  if (!uni(g_L.asked_conn[g_L.S.iter & 3])) return false;
+  if (!spec_stage(C, SC_CONN, 1000)) return false;
+  const ScoutConn& R = g_L.sr.cc;
+  const bool ok = uni(R.ok && R.t == B && R.X == g_L.S.n[B] && R.excl == g_L.xn.id && same8(R.q, g_L.xn.q));
+  if (ok && threadIdx.x == 0) g_L.conn_rec = 1;
+  __syncthreads();
+  return ok;
+}
+
 // One C-space iteration of run_planner (birrt_star.cpp:1163-1338).  Always inlined into plan_kernel: builds in
 // which the inliner outlined it (a larger scout) fault the GPU with a memory-aperture violation in the first
 // iterations (tools/experiments/README.md), builds that inline it run clean.
@@ -2333,6 +2462,7 @@ __device__ __forceinline__ void iteration(const Ctx& C) {
 #ifdef SMP_TRACE
   if (threadIdx.x == 0) g_L.tit = g_L.S.iter;
 #endif
+  if (threadIdx.x == 0) g_L.conn_rec = 0;
   TR();
 #define PHASE(k) if (threadIdx.x == 0) { _t1 = wall_clock64(); g_L.S.prof[k] += _t1 - _t0; _t0 = _t1; }
   sample_publish(C);
@@ -2422,8 +2552,12 @@ __device__ __forceinline__ void iteration(const Ctx& C) {
     TR();
     PHASE(P_REWIRE);
     int cid;
+    const bool crec = opt && conn_stage(C, B);
     if (take_spec(OV_NN)) {
       cid = uni(g_L.spec_nn);
+    } else if (crec) {
+      cid = uni(g_L.sr.cc.d < 10000.0 ? g_L.sr.cc.id : 0);
+      if (threadIdx.x == 0) { g_L.S.nn_nodes += g_L.S.n[B]; g_L.S.sc_nn++; }
     } else if (uni(!opt && g_L.sp_on && g_L.sp_stage >= SC_DONE && g_L.sr.cn.ok && g_L.sr.cn.t == B &&
                    g_L.sr.cn.X <= g_L.S.n[B] && same8(g_L.sr.cn.q, g_L.xn.q))) {
       // the scout's nearest node over the first X nodes; only the nodes appended since are scanned (one of them
@@ -2492,6 +2626,90 @@ __device__ bool sc_stale(const Ctx& C, unsigned tag) {
   return s != 0;
 }
 
+// Scout, after its record's rewire stage (two scouts, after the first solution): waits until the leader reports
+// tree_B of iteration `it` final (its size in the cgo granule) and computes connect's scans for x_new (g_L.xn):
+// nearest node, near set, and the segment-norm sums of the direct edge and of the near candidates (stage SC_CONN).
+// Publishes SC_CONN with cc.ok = 0 if the leader moved on first.
+__device__ void scout_connect(const Ctx& C, long long it, int t, int par, unsigned tag) {
+  ScoutRec& R = g_L.sr;
+  ScoutBoard* sb = C.Q.scb;
+  const int tb = 1 - t;
+  for (int k = 0;; k ^= 1) {
+    if (threadIdx.x == 0) {
+      const unsigned long long v = ld_agent(&sb->cgo);
+      int go = 0;
+      if ((unsigned)(v >> 32) == tag) { go = 1; g_L.cnt = (int)(unsigned)v; }
+      else if ((long long)ld_agent(&sb->cur) > it || ld_agent(&sb->stop)) go = -1;
+      g_L.sp_go[k] = go;
+    }
+    __syncthreads();
+    const int go = uni(g_L.sp_go[k]);
+    if (go < 0) return;  // stale: nobody waits for this record any more
+    if (go > 0) break;
+    __builtin_amdgcn_s_sleep(2);
+  }
+  // the tree's stores are the leader's (drained before cgo): drop stale cached copies
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  if (threadIdx.x == 0) g_L.S.n[tb] = g_L.cnt;
+  __syncthreads();
+  double d;
+  int cid = nearest_scan(C, tb, g_L.xn.q, 0, &d);
+  if (threadIdx.x == 0) {
+    if (!(d < 10000.0)) { cid = 0; d = 10000.0; }
+    R.cc.d = d; R.cc.id = cid;
+    load_node(C, tb, cid, &g_L.xc);
+  }
+  near_set<20>(C, tb, g_L.xn.q, g_L.xn.id);
+  if (threadIdx.x == 0) {
+    const int E = min(g_L.n_lo, g_L.S.max_near);
+    g_L.cnt = E;
+    for (int j = 0; j < NJ; ++j) { g_L.eg_start[0][j] = g_L.xc.q[j]; g_L.eg_target[0][j] = g_L.xn.q[j]; }
+    for (int k = 0; k < 3; ++k) g_L.eg_base[0][k] = 0.0;
+  }
+  __syncthreads();
+  const int E = uni(g_L.cnt);
+  if (threadIdx.x < E) {
+    const int e = threadIdx.x;
+    NodeRef nd;
+    load_node(C, tb, g_L.lo_i[e], &nd);
+    for (int j = 0; j < NJ; ++j) { g_L.eg_start[1 + e][j] = nd.q[j]; g_L.eg_target[1 + e][j] = g_L.xn.q[j]; }
+    for (int k = 0; k < 3; ++k) g_L.eg_base[1 + e][k] = 0.0;
+  }
+  __syncthreads();
+  edge_costs(C, 1 + E);
+  if (threadIdx.x < MAX_NEAR) {
+    R.cc.lo_i[threadIdx.x] = g_L.lo_i[threadIdx.x]; R.cc.lo_c[threadIdx.x] = g_L.lo_c[threadIdx.x];
+    R.cc.hi_i[threadIdx.x] = g_L.hi_i[threadIdx.x]; R.cc.hi_c[threadIdx.x] = g_L.hi_c[threadIdx.x];
+  }
+  if (threadIdx.x < E * 3) {
+    const int e = threadIdx.x / 3, k = threadIdx.x - e * 3;
+    R.cc.acc[e][k] = g_L.eg_acc[1 + e][k];
+  }
+  if (threadIdx.x == 0) {
+    for (int j = 0; j < NJ; ++j) R.cc.q[j] = g_L.xn.q[j];
+    for (int k = 0; k < 3; ++k) R.cc.acc0[k] = g_L.eg_acc[0][k];
+    R.cc.X = g_L.S.n[tb]; R.cc.t = tb; R.cc.excl = g_L.xn.id;
+    R.cc.nk = g_L.nk; R.cc.n_lo = g_L.n_lo; R.cc.n_hi = g_L.n_hi;
+    R.cc.ok = 1;
+  }
+  __syncthreads();
+  sc_copy_out(sb, par, &R.cc, sizeof(ScoutConn));
+  sc_publish(C, par, tag, SC_CONN);
+}
+
+// Scout: ends a record without connect's scans; a post-solution record of two scouts still reaches stage SC_CONN
+// (with cc.ok = 0), so the leader never waits for it.
+__device__ void sc_end(const Ctx& C, int par, unsigned tag, int opt) {
+  if (opt && uni(g_L.two_scouts)) {
+    if (threadIdx.x == 0) g_L.sr.cc.ok = 0;
+    __syncthreads();
+    sc_copy_out(C.Q.scb, par, &g_L.sr.cc, sizeof(ScoutConn));
+    sc_publish(C, par, tag, SC_CONN);
+  } else {
+    sc_publish(C, par, tag, SC_DONE);
+  }
+}
+
 // The scout's pass for iteration `it` of the leader, which expands tree t from a snapshot of its first X nodes:
 // the leader's steps up to its rewire collision job (iteration / choose_parent / rewire, same functions on the
 // scout's own LDS, job board, helpers and via-node scratch), recording the results the leader keys on; nothing is
@@ -2514,7 +2732,7 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
     S.n[t] = X;
     S.n[1 - t] = XB;
     R.cn.ok = 0;
-    R.nn.ok = 0; R.ex.ok = 0; R.nr.ok = 0; R.n_choose = 0; R.n_rewire = 0;
+    R.nn.ok = 0; R.ex.ok = 0; R.nr.ok = 0; R.n_choose = 0; R.n_rewire = 0; R.cc.ok = 0;
   }
   sc_publish(C, par, tag, SC_STARTED);
   // the sample: the sampler's ring slot for (it, ver), if it is there within ~20 us
@@ -2546,7 +2764,7 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
     sc_copy_out(sb, par, &R.nn, sizeof(ScoutNN));
     sc_copy_out(sb, par, &R.nr, sizeof(ScoutNear));
     sc_copy_out(sb, par, &R.n_choose, 4 * sizeof(int));
-    sc_publish(C, par, tag, SC_DONE);
+    sc_end(C, par, tag, opt);
     return;
   }
   // nearest + expand edge (iteration())
@@ -2581,6 +2799,7 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
   edge_validity(C, 1, false, P_XEXPAND, opt ? OV_NEAR_EXPAND : OV_NONE, t);
   if (threadIdx.x == 0) {
     for (int j = 0; j < NJ; ++j) { R.e[0].s[j] = g_L.eg_start[0][j]; R.e[0].g[j] = g_L.eg_target[0][j]; }
+    for (int k = 0; k < 3; ++k) R.e[0].acc[k] = g_L.eg_acc[0][k];
     R.e[0].first = g_L.eg_first[0];
     const int f = g_L.eg_first[0];
     g_L.ext_nn = f > S.n_pts;
@@ -2688,6 +2907,7 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
       const int e = threadIdx.x;
       ScoutEdge& w = R.e[SCOUT_CHOOSE0 + e];
       for (int j = 0; j < NJ; ++j) { w.s[j] = g_L.eg_start[e][j]; w.g[j] = g_L.eg_target[e][j]; }
+      for (int k = 0; k < 3; ++k) w.acc[k] = g_L.eg_acc[e][k];
       w.first = g_L.eg_need[e] ? g_L.eg_first[e] : -1;
     }
     if (threadIdx.x == 0) {
@@ -2724,7 +2944,7 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
   }
   SC_PHASE(5);
   TR();
-  if (!uni(g_L.ext_nn || g_L.ext_bp)) { sc_publish(C, par, tag, SC_DONE); return; }
+  if (!uni(g_L.ext_nn || g_L.ext_bp)) { sc_end(C, par, tag, opt); return; }
   // rewire's candidate edges (rewire())
   const TreeDev& T = C.Q.tr[t];
   rewire_count(T);
@@ -2751,6 +2971,7 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
       const int e = threadIdx.x;
       ScoutEdge& w = R.e[SCOUT_REWIRE0 + e];
       for (int j = 0; j < NJ; ++j) { w.s[j] = g_L.eg_start[e][j]; w.g[j] = g_L.eg_target[e][j]; }
+      for (int k = 0; k < 3; ++k) w.acc[k] = g_L.eg_acc[e][k];
       w.first = g_L.eg_need[e] ? g_L.eg_first[e] : -1;
     }
     if (threadIdx.x == 0) R.n_rewire = cnt;
@@ -2760,6 +2981,8 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
   sc_copy_out(sb, par, &R.e[SCOUT_REWIRE0], cnt * (int)sizeof(ScoutEdge));
   sc_publish(C, par, tag, SC_DONE);
   SC_PHASE(6);
+  TR();
+  if (uni(g_L.two_scouts)) scout_connect(C, it, t, par, tag);
   TR();
 }
 #undef SC_PHASE
@@ -2795,6 +3018,8 @@ __device__ __forceinline__ void scout_main(Ctx& C, int which) {
     g_L.spec = OV_NONE;
     g_L.sp_on = 0;
     st_agent(&C.Q.scb->xcc, xcc_id() + 1);
+    g_L.two_scouts = C.Q.scb2 != nullptr;
+    g_L.rec_grp = -1;
 #ifdef SMP_TRACE
     g_L.trole = which;
     g_L.tit = -1;
@@ -2876,7 +3101,9 @@ __global__ void __launch_bounds__(BLOCK) plan_kernel(const RobotDev* __restrict_
   if (threadIdx.x == 0) {
     g_L.sp_on = 0;
     g_L.sc_same[0] = g_L.sc_same[1] = -1;
-    for (int k = 0; k < 4; ++k) g_L.asked[k] = 0;
+    for (int k = 0; k < 4; ++k) { g_L.asked[k] = 0; g_L.asked_conn[k] = 0; }
+    g_L.conn_rec = 0;
+    g_L.rec_grp = -1;
     g_L.count_slot = 0;
     g_L.job_seq = 0;
     g_L.S = *C.Q.st;

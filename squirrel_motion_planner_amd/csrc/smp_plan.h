@@ -123,7 +123,7 @@ struct JobBoard {
 // drained before the record's stage granule, (tag << 32) | stage with tag = iteration + 1.
 constexpr int SCOUT_EDGES = 1 + 2 * MAX_NEAR;  // expand edge, choose-parent candidates, rewire candidates
 constexpr int SCOUT_CHOOSE0 = 1, SCOUT_REWIRE0 = 1 + MAX_NEAR;
-enum { SC_STARTED = 0, SC_NN = 1, SC_EXPAND = 2, SC_NEAR = 3, SC_CHOOSE = 4, SC_DONE = 5 };
+enum { SC_STARTED = 0, SC_NN = 1, SC_EXPAND = 2, SC_NEAR = 3, SC_CHOOSE = 4, SC_DONE = 5, SC_CONN = 6 };
 struct ScoutNN {               // stage SC_NN: nearest node of the sample in the snapshot
   double q[NJ];                // the sample scanned
   double d;                    // its distance (the running minimum of the reference scan, 10000 if none)
@@ -137,6 +137,7 @@ struct ScoutNear {             // stage SC_NEAR: near set of x_new in the snapsh
 };
 struct ScoutEdge {             // one candidate edge: interpolation start / target, first colliding point
   double s[NJ], g[NJ];
+  double acc[3];               // segment-norm sums (edge_costs' eg_acc; cost = start node's cost + acc)
   int first, pad;              // first: as eg_first (n_pts + 1 = free), -1 = not checked
 };
 struct ScoutExpand {           // stage SC_EXPAND: the expand edge's interpolation data (edge_costs of edge 0)
@@ -151,11 +152,27 @@ struct ScoutConnect {          // stage SC_DONE, before the first solution: conn
   int id, X, t, ok;            // that node, the snapshot size, the tree, 1 = valid
   ScoutEdge e;                 // the direct edge nearest -> x_new and its first colliding point
 };
+// Stage SC_CONN (two scouts, after the first solution): connect's scans of the iteration, computed once the leader
+// reports that the tree connect searches (tree_B of the iteration = tree_A of the one before) is final (its rewire
+// commits are done; nothing appends to it before connect): the nearest node of x_new, its near set (excluding the
+// id x_new has in its own tree, as find_near_vertices does) and the segment-norm sums of connect's edges.
+struct ScoutConn {
+  double q[NJ];                // x_new
+  double d;                    // distance of the nearest node (10000 if none)
+  int id, X, t, excl;          // nearest node, tree size scanned, tree, excluded id
+  int nk, n_lo, n_hi, ok;      // near count, list lengths, 1 = valid
+  int lo_i[MAX_NEAR], hi_i[MAX_NEAR];
+  double lo_c[MAX_NEAR], hi_c[MAX_NEAR];
+  double acc0[3];              // direct edge nearest -> x_new
+  double pad0;
+  double acc[MAX_NEAR][3];     // near candidate lo_i[e] -> x_new (e < min(n_lo, max_near))
+};
 struct ScoutRec {
   ScoutNN nn;
   ScoutExpand ex;
   ScoutConnect cn;
   ScoutNear nr;
+  ScoutConn cc;
   int n_choose, n_rewire, pad[2];
   ScoutEdge e[SCOUT_EDGES];    // [0] expand, [SCOUT_CHOOSE0 ..) choose-parent, [SCOUT_REWIRE0 ..) rewire
 };
@@ -169,7 +186,8 @@ struct ScoutBoard {
   unsigned long long cur;      // leader -> scout: the leader's current iteration (a record of an earlier one is stale)
   int pad2[30];
   unsigned long long stage[4]; // scout -> leader, by iteration mod 4 (a scout may work two iterations ahead)
-  int pad1[24];
+  unsigned long long cgo;      // leader -> scout: granule (iteration k + 1, n of tree_B(k)) once tree_B(k) is final
+  int pad1[22];
   unsigned long long prof[32]; // the scout's phase clocks of the launch (written when it leaves)
   ScoutRec rec[4];
 };
