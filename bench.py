@@ -182,13 +182,15 @@ def main():
         alg_bytes_rank0 = 64.0 * totals["nn"] + 72.0 * totals["near"] + BYTES_PER_CONFIG * totals["checked"]
         # per launch: algorithmic bytes of one launch / its average duration (HIP events on the planner stream)
         achieved = alg_bytes_rank0 / (plan_ms_rank0 * 1e-3) / 1e9 if plan_ms_rank0 > 0 else 0.0
-        traffic = None
-        # HBM bytes per launch from the latest committed rocprofv3 FETCH_SIZE/WRITE_SIZE pass of this bench
+        traffic, traffic_src = None, None
+        # HBM bytes per launch: not measurable inside this run (counter passes serialise dispatches and need
+        # rocprofv3); taken from the newest committed FETCH_SIZE + WRITE_SIZE passes of this bench, named below
         import glob
         pmcs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_plan_kernel.json")))
         if pmcs:
             try:
                 traffic = json.load(open(pmcs[-1])).get("hbm_bytes_per_launch")
+                traffic_src = "profiles/" + os.path.basename(pmcs[-1]) + " (rocprofv3 --pmc passes, --helpers -1)"
             except (OSError, ValueError):
                 traffic = None
         out = {
@@ -217,8 +219,11 @@ def main():
             "valid_configs_per_s": valid / elapsed,
             "iterations_per_s": iters / elapsed,
             "time_to_first_feasible_path_s": (sum(first_t) / len(first_t)) if first_t else None,
+            # priced against HBM (no dense contraction); the measured limiter is the dependent latency of
+            # one query's iteration chain, not bandwidth: trees and grid stay in L2 / Infinity Cache
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                         "limiter": "latency (sequential iteration chain of one query)",
                          "kernel": "smp::plan_kernel", "kernel_ms_rank0": plan_ms_rank0,
                          "avg_launch_ms": plan_ms_rank0 / max(totals["launches"], 1),
                          "launches_rank0": totals["launches"],

@@ -3,7 +3,9 @@
 // The ROS node (squirrel_8dof_planner) owns a BiRRTstarPlanner by value (squirrel_8dof_planner.h:131) and calls
 // the methods below (squirrel_8dof_planner.cpp:16, 482-810, 872-915, 1179-1248).  This class keeps those
 // signatures (birrt_star.h:27-110) and forwards every call to the C ABI in smp_gpu.h, so the node compiles
-// against it unchanged; the planning loop itself runs in the HIP kernels of libsmp_gpu.so.
+// against it unchanged except for its two calls outside the sampling / collision path, getCollisions
+// (squirrel_8dof_planner.cpp:839) and getFullPoseFromEEPose (squirrel_8dof_planner.cpp:1179), which this class does
+// not provide; the planning loop itself runs in the HIP kernels of libsmp_gpu.so.
 //
 // Build: include this header instead of <birrt_star_algorithm/birrt_star.h> and link -lsmp_gpu.
 // Configuration (environment, read by initialize()):

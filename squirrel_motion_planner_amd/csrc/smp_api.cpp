@@ -359,16 +359,18 @@ int smp_planner_create(int device, const smp_robot* robot, const smp_params* par
       }
     }
   }
-  HIPCHK(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
+  // every failure from here on releases what was created so far (smp_planner_destroy skips null handles)
   int prio_lo = 0, prio_hi = 0;
-  HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
-  HIPCHK(hipStreamCreateWithPriority(&p->hstream, hipStreamNonBlocking, prio_hi));
-  HIPCHK(hipEventCreateWithFlags(&p->ev_board, hipEventDisableTiming));
-  HIPCHK(hipMalloc(&p->d_rb, sizeof(RobotDev)));
-  HIPCHK(hipMalloc(&p->d_mc, sizeof(MapCfg)));
-  HIPCHK(hipMemcpy(p->d_rb, &p->robot.dev, sizeof(RobotDev), hipMemcpyHostToDevice));
-  HIPCHK(hipEventCreate(&p->ev0));
-  HIPCHK(hipEventCreate(&p->ev1));
+  if (hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess ||
+      hipStreamCreateWithPriority(&p->hstream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
+      hipEventCreateWithFlags(&p->ev_board, hipEventDisableTiming) != hipSuccess ||
+      hipMalloc(&p->d_rb, sizeof(RobotDev)) != hipSuccess || hipMalloc(&p->d_mc, sizeof(MapCfg)) != hipSuccess ||
+      hipMemcpy(p->d_rb, &p->robot.dev, sizeof(RobotDev), hipMemcpyHostToDevice) != hipSuccess ||
+      hipEventCreate(&p->ev0) != hipSuccess || hipEventCreate(&p->ev1) != hipSuccess) {
+    smp_planner_destroy(p);
+    return SMP_ERR_HIP;
+  }
   int khz = 0;
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) == hipSuccess && khz > 0)
     p->wall_rate_hz = khz * 1000.0;
@@ -377,7 +379,7 @@ int smp_planner_create(int device, const smp_robot* robot, const smp_params* par
     p->num_cus = cus;
   std::memset(&p->sc, 0, sizeof(p->sc));
   int st = update_mapcfg(p);
-  if (st) { delete p; return st; }
+  if (st) { smp_planner_destroy(p); return st; }
   *out = p;
   return SMP_OK;
 }
@@ -385,7 +387,8 @@ int smp_planner_create(int device, const smp_robot* robot, const smp_params* par
 void smp_planner_destroy(smp_planner* p) {
   if (!p) return;
   (void)hipSetDevice(p->device);
-  (void)hipStreamSynchronize(p->stream);
+  if (p->stream) (void)hipStreamSynchronize(p->stream);
+  if (p->hstream) (void)hipStreamSynchronize(p->hstream);
   for (auto& q : p->qb) q.release();
   p->d_qdev.release(); p->d_counts.release(); p->d_cq.release(); p->d_valid.release();
   p->d_bricks.release(); p->d_d2.release(); p->d_d2b.release();
@@ -637,10 +640,12 @@ static int upload_roots(smp_planner* p, QueryBuffers& b, const QueryDev& d, cons
   return SMP_OK;
 }
 
-extern "C" int smp_plan_batch(smp_planner* p, const smp_query* qs, int nq, smp_result* out) {
-  if (!p || !qs || nq <= 0 || !out) return SMP_ERR_ARG;
+// smp_plan_batch's body.  done[i] is set once out[i] holds query i's complete result; a call that fails on the way
+// (a HIP error, the no-progress guard) returns early, and smp_plan_batch then reports that status in every
+// result not yet complete.
+static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_result* out, std::vector<char>& done) {
+  const auto t_entry = std::chrono::steady_clock::now();
   HIPCHK(hipSetDevice(p->device));
-  for (int i = 0; i < nq; ++i) { std::memset(&out[i], 0, sizeof(smp_result)); }
   // init_planner validity of start and goal (birrt_star.cpp:350-362)
   std::vector<int> status(nq, SMP_OK);
   {
@@ -653,7 +658,9 @@ extern "C" int smp_plan_batch(smp_planner* p, const smp_query* qs, int nq, smp_r
       if (st) return st;
       if (!v[0]) status[i] = SMP_ERR_START_INVALID;
       else if (!v[1]) status[i] = SMP_ERR_GOAL_INVALID;
-      if (!(qs[i].budget >= 0)) status[i] = SMP_ERR_ARG;
+      const int bk = qs[i].budget_kind;
+      if (!(qs[i].budget >= 0) || (bk != SMP_BUDGET_ITERATIONS && bk != SMP_BUDGET_SECONDS && bk != SMP_BUDGET_SAMPLES))
+        status[i] = SMP_ERR_ARG;
     }
   }
   if ((int)p->qb.size() < nq) p->qb.resize(nq);
@@ -675,6 +682,14 @@ extern "C" int smp_plan_batch(smp_planner* p, const smp_query* qs, int nq, smp_r
     HIPCHK(alloc_query(p->qb[i], (size_t)cap, via_cap, rows_cap[i]));
     qdev[i] = make_qdev(p->qb[i], (size_t)cap, rows_cap[i]);
     init_qstate(p, q, cap, via_cap, &S[i]);
+    if (q.budget_kind == SMP_BUDGET_SECONDS) {
+      // the budget counts from smp_plan entry (start / goal checks and first-call allocation included); the kernel
+      // turns the rest into a deadline when it records the planning start
+      const double left = q.budget - std::chrono::duration<double>(std::chrono::steady_clock::now() - t_entry).count();
+      S[i].has_deadline = 1;
+      S[i].budget_ticks = (unsigned long long)(std::max(left, 0.0) * p->wall_rate_hz);
+      S[i].stop_margin = 2 * via_cap + 4;  // nodes one iteration can add at most (two via chains + x_new + connection)
+    }
     if (status[i] != SMP_OK) { S[i].status = status[i]; S[i].phase = 2; }
     if (by_iter && iters <= 0 && S[i].phase == 0) S[i].max_iter = 0;
     int st = upload_roots(p, p->qb[i], qdev[i], q, (size_t)cap);
@@ -736,7 +751,6 @@ extern "C" int smp_plan_batch(smp_planner* p, const smp_query* qs, int nq, smp_r
   for (auto& a : scout_prof) a.fill(0);
   float total_ms = 0;
   int64_t launches = 0;
-  bool deadline_set = false;
   long long max_iters = 0;
   for (int i = 0; i < nq; ++i)
     if (qs[i].budget_kind != SMP_BUDGET_SECONDS) max_iters = std::max(max_iters, (long long)qs[i].budget);
@@ -819,15 +833,6 @@ extern "C" int smp_plan_batch(smp_planner* p, const smp_query* qs, int nq, smp_r
     bool all_done = true;
     for (int i = 0; i < nq; ++i) all_done &= (S[i].phase == 2 || S[i].status != 0);
     if (all_done) break;
-    if (tmax > 0 && !deadline_set) {
-      // convert the wall-clock budget into a device-clock deadline per timed query
-      for (int i = 0; i < nq; ++i) {
-        if (qs[i].budget_kind != SMP_BUDGET_SECONDS || S[i].phase == 2) continue;
-        S[i].deadline = S[i].t0 + (unsigned long long)(qs[i].budget * p->wall_rate_hz);
-        HIPCHK(hipMemcpyAsync(&qdev[i].st->deadline, &S[i].deadline, sizeof(unsigned long long), hipMemcpyHostToDevice, p->stream));
-      }
-      deadline_set = true;
-    }
     if (chunk < 4096) chunk *= 2;
     double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_begin).count();
     (void)el;
@@ -885,7 +890,7 @@ extern "C" int smp_plan_batch(smp_planner* p, const smp_query* qs, int nq, smp_r
       HIPCHK(hipMemcpy(r.cost_rows, p->qb[i].rows.p, sizeof(double) * 5 * s.n_rows, hipMemcpyDeviceToHost));
       for (int64_t k = 0; k < s.n_rows; ++k) r.cost_rows[k * 5 + 1] /= p->wall_rate_hz;
     }
-    if (r.status != SMP_OK) continue;
+    if (r.status != SMP_OK) { done[i] = 1; continue; }
     int ns = counts[2 * i], ng = counts[2 * i + 1];
     std::vector<int> ids(ns + ng);
     if (ns) HIPCHK(hipMemcpy(ids.data(), qdev[i].path_nodes, ns * sizeof(int), hipMemcpyDeviceToHost));
@@ -920,8 +925,26 @@ extern "C" int smp_plan_batch(smp_planner* p, const smp_query* qs, int nq, smp_r
       r.waypoints = (double*)malloc(sizeof(double) * wp.size());
       std::memcpy(r.waypoints, wp.data(), sizeof(double) * wp.size());
     }
+    done[i] = 1;
   }
   for (int i = 0; i < nq; ++i) if (out[i].status != SMP_OK && rc == SMP_OK) rc = out[i].status;
+  return rc;
+}
+
+extern "C" int smp_plan_batch(smp_planner* p, const smp_query* qs, int nq, smp_result* out) {
+  if (!p || !qs || nq <= 0 || !out) return SMP_ERR_ARG;
+  for (int i = 0; i < nq; ++i) std::memset(&out[i], 0, sizeof(smp_result));
+  std::vector<char> done(nq, 0);
+  const int rc = plan_batch_impl(p, qs, nq, out, done);
+  // the runtime's last-error slot still holds a failed call's error (e.g. an allocation): clear it, so the next
+  // call's launch checks do not report it again
+  if (rc == SMP_ERR_HIP) (void)hipGetLastError();
+  // a call that stopped early leaves no result looking like a success
+  for (int i = 0; i < nq; ++i) {
+    if (done[i]) continue;
+    smp_result_free(&out[i]);
+    out[i].status = rc != SMP_OK ? rc : SMP_ERR_HIP;
+  }
   return rc;
 }
 

@@ -2597,7 +2597,13 @@ __device__ __forceinline__ void iteration(const Ctx& C) {
     if ((S.cbest[0] - S.h0[0]) < S.opt_thresh) S.phase = 2;  // birrt_star.cpp:1333-1338
     if (S.iter >= S.max_iter) S.phase = 2;
     if (S.max_checked && S.checked >= S.max_checked) S.phase = 2;
-    if (S.deadline && wall_clock64() >= S.deadline) S.phase = 2;
+    if (S.has_deadline && wall_clock64() >= S.deadline) S.phase = 2;
+    // a time budget sizes no tree: stop with the best path so far before a tree could overflow (a run without a
+    // path reports the capacity instead)
+    if (S.stop_margin && (S.n[0] + S.stop_margin > S.cap || S.n[1] + S.stop_margin > S.cap)) {
+      S.phase = 2;
+      if (!S.have_sol) S.status = -7;
+    }
   }
   __syncthreads();
 }
@@ -3107,7 +3113,11 @@ __global__ void __launch_bounds__(BLOCK) plan_kernel(const RobotDev* __restrict_
     g_L.count_slot = 0;
     g_L.job_seq = 0;
     g_L.S = *C.Q.st;
-    if (g_L.S.phase == 0 && g_L.S.t0 == 0) g_L.S.t0 = wall_clock64();
+    if (g_L.S.phase == 0 && g_L.S.t0 == 0) {
+      g_L.S.t0 = wall_clock64();
+      // run_planner reads the wall clock every iteration (birrt_star.cpp:1313-1320): the budget counts from here
+      if (g_L.S.has_deadline) g_L.S.deadline = g_L.S.t0 + g_L.S.budget_ticks;
+    }
     g_L.n_via = 0;
     g_L.near_blo = ~0ull;
     g_L.near_bhi = 0;

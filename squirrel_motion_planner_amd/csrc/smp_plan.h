@@ -47,6 +47,9 @@ struct QState {                // per query, persisted in global memory across l
   unsigned long long sc_wait;      // device-clock ticks the leader waited for the scout
   unsigned long long prof[32];     // device-clock ticks per planner phase (SMP_PROF_* in smp_kernels.hip)
   unsigned long long t0, t_first, t_end, deadline;  // device wall clock (0 deadline = none)
+  unsigned long long budget_ticks;  // seconds budget in device-clock ticks (has_deadline): deadline = t0 + this
+  int has_deadline;
+  int stop_margin;             // > 0 (seconds budgets): end the run once a tree is within this many nodes of cap
   double cbest[3], h0[3];
   NodeRef nB, nA;              // m_node_tree_B / m_node_tree_A
   double qs[NJ], qg[NJ];

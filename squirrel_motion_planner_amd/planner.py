@@ -214,12 +214,17 @@ class GpuPlanner:
         n = len(queries)
         qa = (L.Query * n)(*queries)
         ra = (L.Result * n)()
-        lib().smp_plan_batch(self.h, qa, n, ra)
+        rc = lib().smp_plan_batch(self.h, qa, n, ra)
         out = []
         for r in ra:
             d = _result_dict(r)
             lib().smp_result_free(ctypes.byref(r))
             out.append(d)
+        # per-query outcomes (a path, no path, invalid start / goal / budget, a full tree) come back in the results;
+        # a failure of the call itself (HIP error, no device, the no-progress guard) raises
+        failed = [d["status"] for d in out if d["status"] in _CALL_FAILURES]
+        if rc in _CALL_FAILURES or failed:
+            raise L.SmpError(rc if rc in _CALL_FAILURES else failed[0], "smp_plan_batch")
         return out
 
     def plan(self, query):
@@ -240,6 +245,9 @@ class GpuPlanner:
         if getattr(self, "h", None):
             lib().smp_planner_destroy(self.h)
             self.h = None
+
+
+_CALL_FAILURES = (L.SMP_ERR_HIP, L.SMP_ERR_NO_DEVICE, L.SMP_ERR_PARSE)
 
 
 def _result_dict(r):
