@@ -83,10 +83,10 @@ typedef struct smp_params {
   int helpers;             /* helper workgroups per query that share its collision tiles across CUs
                               (0: automatic, up to 127 with the scout / 63 without; -1: none, the query runs on
                               its own workgroup) */
-  int scout;               /* 1 (default): a scout workgroup per query computes the next iteration's scans and
-                              collision jobs ahead (needs >= 4 helpers), and with >= 16 helpers a second one takes
-                              every other iteration two ahead until the first solution; 0: off.  Results are
-                              identical either way */
+  int scout;               /* 1 (default): scout workgroups compute the coming iterations' scans and collision jobs
+                              ahead of the leader -- 2 when a query has 18 CUs or more (before the first solution
+                              they take the iterations in turn, after it they alternate, two ahead), 1 from 6 CUs;
+                              2..4: that many (with >= 4 helpers); 0: off.  Results are identical either way */
 } smp_params;
 
 typedef struct smp_query {
@@ -131,7 +131,7 @@ typedef struct smp_stats {
   double scout_phase_seconds[32]; /* the scout's time per stage (0 sample, 1 nearest, 2 expand, 3 near, 4 choose,
                                     5 via chain, 6 rewire, 28 idle, 29 publishing, 31 busy; 30 = iterations) */
   int32_t helpers;               /* helper workgroups per query used */
-  int32_t scout;                 /* 1 if the scout ran */
+  int32_t scout;                 /* scout workgroups per query used (0: none) */
 } smp_stats;
 
 typedef struct smp_result {

@@ -83,15 +83,16 @@ struct QueryBuffers {
   DBuf<double> q, cost, e_start, e_target, rows;
   DBuf<int> parent, first_child, next_sib, prev_sib, stack, path_nodes;
   DBuf<ViaNode> via;
-  DBuf<JobBoard> jb, sjb, sjb2;    // the leader's and the scouts' collision-job boards
-  DBuf<ScoutBoard> scb, scb2;
-  DBuf<ViaNode> svia, svia2;
+  DBuf<JobBoard> jb;               // the leader's collision-job board
+  DBuf<JobBoard> sjb[MAX_SCOUTS];  // the scouts' collision-job boards, record boards and via scratch
+  DBuf<ScoutBoard> scb[MAX_SCOUTS];
+  DBuf<ViaNode> svia[MAX_SCOUTS];
   size_t cap = 0;
   void release() {
     st.release(); q.release(); cost.release(); e_start.release(); e_target.release(); rows.release();
     parent.release(); first_child.release(); next_sib.release(); prev_sib.release(); stack.release();
-    path_nodes.release(); via.release(); jb.release(); sjb.release(); scb.release(); svia.release();
-    sjb2.release(); scb2.release(); svia2.release();
+    path_nodes.release(); via.release(); jb.release();
+    for (int s = 0; s < MAX_SCOUTS; ++s) { sjb[s].release(); scb[s].release(); svia[s].release(); }
     cap = 0;
   }
 };
@@ -310,7 +311,7 @@ int smp_scene_export(const smp_scene* s, uint64_t* bits, uint16_t* d2) {
 
 static bool params_ok(const smp_params& q) {
   return q.max_near_nodes >= 1 && q.max_near_nodes <= 20 && q.num_traj_segments >= 1 && q.num_traj_segments <= MAX_PTS &&
-         q.near_threshold > 0 && q.step_factor > 0 && q.node_capacity >= 0;
+         q.near_threshold > 0 && q.step_factor > 0 && q.node_capacity >= 0 && q.scout >= 0 && q.scout <= MAX_SCOUTS;
 }
 
 int smp_planner_set_params(smp_planner* p, const smp_params* params) {
@@ -575,12 +576,11 @@ static hipError_t alloc_query(QueryBuffers& b, size_t cap, int via_cap, long lon
   if ((e = b.via.reserve(via_cap))) return e;
   if ((e = b.rows.reserve(std::max<long long>(rows, 1) * 5))) return e;
   if ((e = b.jb.reserve(1))) return e;
-  if ((e = b.sjb.reserve(1))) return e;
-  if ((e = b.scb.reserve(1))) return e;
-  if ((e = b.svia.reserve(via_cap))) return e;
-  if ((e = b.sjb2.reserve(1))) return e;
-  if ((e = b.scb2.reserve(1))) return e;
-  if ((e = b.svia2.reserve(via_cap))) return e;
+  for (int s = 0; s < MAX_SCOUTS; ++s) {
+    if ((e = b.sjb[s].reserve(1))) return e;
+    if ((e = b.scb[s].reserve(1))) return e;
+    if ((e = b.svia[s].reserve(via_cap))) return e;
+  }
   b.cap = cap;
   return hipSuccess;
 }
@@ -605,15 +605,15 @@ static QueryDev make_qdev(QueryBuffers& b, size_t cap, long long rows) {
   d.rows_cap = rows;
   d.path_nodes = b.path_nodes.p;
   d.jb = nullptr;
-  d.sjb = nullptr;
   d.sampler_jb = nullptr;
+  d.nscouts = 0;
+  for (int s = 0; s < MAX_SCOUTS; ++s) {
+    d.scbs[s] = nullptr; d.sjbs[s] = nullptr; d.svias[s] = nullptr; d.sworkers_s[s] = 1;
+  }
   d.scb = nullptr;
+  d.sjb = nullptr;
   d.svia = nullptr;
   d.sworkers = 1;
-  d.sjb2 = nullptr;
-  d.scb2 = nullptr;
-  d.svia2 = nullptr;
-  d.sworkers2 = 1;
   d.nworkers = 1;
   d.sampler = 0;
   d.trace = nullptr;
@@ -697,35 +697,44 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
     HIPCHK(hipMemcpyAsync(qdev[i].st, &S[i], sizeof(QState), hipMemcpyHostToDevice, p->stream));
   }
   // helper workgroups per query (DESIGN.md "Helpers", "Scout"): one workgroup per CU, leaders (and scouts) first.
-  // With a scout the helpers are the leader's tile helpers, the scout's tile helpers and the run-ahead sampler.
+  // Workgroups per query (one per CU): the leader, its scouts and the helpers (DESIGN.md "Helpers", "Scouts").
+  // Scouts: smp_params.scout of them (1: automatic -- 2 from 18 CUs per query, 1 from 6; four scouts before the
+  // first solution were measured and gain nothing there, the leader's own work bounds those iterations).  Helpers:
+  // the leader's tile helpers, each scout's, and the run-ahead sampler (the last one).
   int nh = p->params.helpers;
   const bool want_scout = p->params.scout != 0;
-  if (nh == 0) nh = want_scout ? std::min(127, std::max(0, p->num_cus / nq - 2)) : std::min(63, std::max(0, p->num_cus / nq - 1));
+  const int cpq = std::max(1, p->num_cus / nq);
+  int ns = 0;
+  if (nh == 0) {
+    if (want_scout) ns = cpq >= 18 ? 2 : cpq >= 6 ? 1 : 0;
+    nh = want_scout ? std::min(127, std::max(0, cpq - 1 - ns)) : std::min(63, std::max(0, cpq - 1));
+  } else if (nh > 0 && want_scout) {
+    ns = nh >= 16 ? 2 : nh >= 4 ? 1 : 0;
+  }
+  if (want_scout && p->params.scout > 1) ns = std::min(p->params.scout, MAX_SCOUTS);  // explicit count
   if (nh < 0) nh = 0;
-  const bool scout = want_scout && nh >= 4;
-  // a second scout (iterations of the other parity, two ahead of the leader) with as many helpers as the first:
-  // after the first solution both check choose-parent / rewire candidate batches; the leader's own jobs (edges no
-  // record had) are rare, so it keeps a fifth
-  const bool scout2 = scout && nh >= 16;
-  const int h_lead = scout ? (scout2 ? (nh - 1) / 5 : (nh - 1) / 2) : 0;
-  const int h_s2 = scout2 ? (nh - 1 - h_lead) / 2 : 0;
-  const int h_scout = scout ? nh - 1 - h_s2 - h_lead : 0;
+  if (nh < 4) ns = 0;
+  // after the first solution scouts 0 and 1 check choose-parent / rewire candidate batches (many tiles); scouts 2
+  // and 3 only work before it, one edge per job (3 tiles); the leader's own jobs (edges no record had) are rare
+  int h_lead = 0, h_s[MAX_SCOUTS] = {0, 0, 0, 0};
+  if (ns > 0) {
+    const int avail = nh - 1;  // minus the sampler
+    h_lead = ns >= 2 ? avail / 5 : avail / 2;
+    int rest = avail - h_lead;
+    for (int s = 2; s < ns; ++s) { h_s[s] = std::min(3, rest); rest -= h_s[s]; }
+    if (ns >= 2) { h_s[0] = rest - rest / 2; h_s[1] = rest / 2; } else { h_s[0] = rest; }
+  }
   for (int i = 0; i < nq; ++i) {
     qdev[i].jb = nh > 0 ? p->qb[i].jb.p : nullptr;
     qdev[i].sampler = nh >= 2;              // with two or more helpers, the last one runs ahead sampling
-    qdev[i].nworkers = scout ? 1 + h_lead : (nh >= 2 ? nh : 1 + nh);
-    if (scout) {
-      qdev[i].sjb = p->qb[i].sjb.p;
-      qdev[i].scb = p->qb[i].scb.p;
-      qdev[i].svia = p->qb[i].svia.p;
-      qdev[i].sampler_jb = p->qb[i].jb.p;
-      qdev[i].sworkers = 1 + h_scout;
-      if (scout2) {
-        qdev[i].sjb2 = p->qb[i].sjb2.p;
-        qdev[i].scb2 = p->qb[i].scb2.p;
-        qdev[i].svia2 = p->qb[i].svia2.p;
-        qdev[i].sworkers2 = 1 + h_s2;
-      }
+    qdev[i].nworkers = ns > 0 ? 1 + h_lead : (nh >= 2 ? nh : 1 + nh);
+    qdev[i].nscouts = ns;
+    qdev[i].sampler_jb = p->qb[i].jb.p;
+    for (int s = 0; s < ns; ++s) {
+      qdev[i].sjbs[s] = p->qb[i].sjb[s].p;
+      qdev[i].scbs[s] = p->qb[i].scb[s].p;
+      qdev[i].svias[s] = p->qb[i].svia[s].p;
+      qdev[i].sworkers_s[s] = 1 + h_s[s];
     }
   }
   static int* trace_host = nullptr;
@@ -763,13 +772,9 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
       // for the reset and leave when the leader signals stop
       for (int i = 0; i < nq; ++i) {
         HIPCHK(hipMemsetAsync(qdev[i].jb, 0, sizeof(JobBoard), p->stream));
-        if (scout) {
-          HIPCHK(hipMemsetAsync(qdev[i].sjb, 0, sizeof(JobBoard), p->stream));
-          HIPCHK(hipMemsetAsync(qdev[i].scb, 0, sizeof(ScoutBoard), p->stream));
-        }
-        if (scout2) {
-          HIPCHK(hipMemsetAsync(qdev[i].sjb2, 0, sizeof(JobBoard), p->stream));
-          HIPCHK(hipMemsetAsync(qdev[i].scb2, 0, sizeof(ScoutBoard), p->stream));
+        for (int s = 0; s < ns; ++s) {
+          HIPCHK(hipMemsetAsync(qdev[i].sjbs[s], 0, sizeof(JobBoard), p->stream));
+          HIPCHK(hipMemsetAsync(qdev[i].scbs[s], 0, sizeof(ScoutBoard), p->stream));
         }
       }
       HIPCHK(hipEventRecord(p->ev_board, p->stream));
@@ -779,10 +784,11 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
       HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(p->ev0, p->stream));
-    // scouts at block scout_base + q, scout_base a multiple of 8: blocks b and b + 8 are dealt to the same XCD
-    const int scout_base = scout ? (nq + 7) / 8 * 8 : 0;
-    // second scouts at scout_base + round8(nq) + q (plan_kernel)
-    const int grid = scout2 ? scout_base + (nq + 7) / 8 * 8 + nq : (scout ? scout_base + nq : nq);
+    // scout s of query q at block scout_base + s * round8(nq) + q, scout_base a multiple of 8: blocks b and b + 8
+    // are dealt to the same XCD (plan_kernel)
+    const int r8 = (nq + 7) / 8 * 8;
+    const int scout_base = ns > 0 ? r8 : 0;
+    const int grid = ns > 0 ? scout_base + (ns - 1) * r8 + nq : nq;
     hipLaunchKernelGGL(plan_kernel, dim3(grid), dim3(BLOCK), 0, p->stream, p->d_rb, p->sc,
                        p->d_mc, p->d_qdev.p, nq, scout_base, chunk);
     HIPCHK(hipGetLastError());
@@ -803,13 +809,14 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
     }
     for (int i = 0; i < nq; ++i)
       HIPCHK(hipMemcpyAsync(&S[i], qdev[i].st, sizeof(QState), hipMemcpyDeviceToHost, p->stream));
-    if (scout) {
+    if (ns > 0) {  // every scout's phase clocks, summed (per-pass averages divide by the summed pass count)
       HIPCHK(hipStreamSynchronize(p->stream));
-      for (int i = 0; i < nq; ++i) {
-        unsigned long long sp[32];
-        HIPCHK(hipMemcpy(sp, qdev[i].scb->prof, sizeof(sp), hipMemcpyDeviceToHost));
-        for (int k = 0; k < 32; ++k) scout_prof[i][k] += sp[k];
-      }
+      for (int i = 0; i < nq; ++i)
+        for (int sc = 0; sc < ns; ++sc) {
+          unsigned long long sp[32];
+          HIPCHK(hipMemcpy(sp, qdev[i].scbs[sc]->prof, sizeof(sp), hipMemcpyDeviceToHost));
+          for (int k = 0; k < 32; ++k) scout_prof[i][k] += sp[k];
+        }
     }
     HIPCHK(hipStreamSynchronize(p->stream));
     if (nh > 0) HIPCHK(hipStreamSynchronize(p->hstream));
@@ -879,7 +886,7 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
       st.scout_phase_seconds[k] = count ? (double)scout_prof[i][k] : (double)scout_prof[i][k] / p->wall_rate_hz;
     }
     st.helpers = nh;
-    st.scout = scout2 ? 2 : (scout ? 1 : 0);
+    st.scout = ns;
     for (int k = 0; k < 32; ++k)
       st.phase_seconds[k] = (k == 8 || k == 11 || k >= 20) ? (double)s.prof[k] : (double)s.prof[k] / p->wall_rate_hz;
     if (i == 0) { p->last_n[0] = s.n[0]; p->last_n[1] = s.n[1]; }

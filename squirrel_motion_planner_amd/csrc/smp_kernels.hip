@@ -224,9 +224,9 @@ struct PlanLds {
   long long tit;                // iteration the records belong to
 #endif
   int sp_on, sp_stage, sp_go[2];
-  int sc_same[2];               // leader: scout 1 / 2 runs on this XCD (1), another (0), not yet known (-1)
-  int asked[4];                 // leader: scout (1, 2) asked for iteration k in slot k % 4, 0 = none
-  int asked_conn[4];            // leader: that record will carry connect's scans (stage SC_CONN)
+  int sc_same[MAX_SCOUTS];      // leader: scout s runs on this XCD (1), another (0), not yet known (-1)
+  int asked[SCOUT_SLOTS];       // leader: scout s + 1 asked for iteration k in slot k % SCOUT_SLOTS, 0 = none
+  int asked_conn[SCOUT_SLOTS];  // leader: that record will carry connect's scans (stage SC_CONN)
   int conn_rec;                 // leader: connect of this iteration takes its scans from the record (g_L.sr.cc)
   int two_scouts;               // scout: two scouts share the iterations (post-solution records get SC_CONN)
   int eg_hit[MAXE];
@@ -272,7 +272,14 @@ __device__ unsigned g_tlog_n[4];
 // Phase clocks (thread 0, s_memrealtime ticks): where an iteration spends its time.
 enum { P_SAMPLE, P_NN, P_EXPAND, P_NEAR, P_CHOOSE, P_REWIRE, P_CONNECT, P_TILES, P_NTILES, P_COSTS, P_VIA, P_NVIA,
        P_TFK, P_TCHAIN, P_TCENTRE, P_TTEST, P_XEXPAND, P_XCHOOSE, P_XREWIRE, P_XCONNECT };
-#define PROF_BEGIN() unsigned long long _pt = threadIdx.x == 0 ? wall_clock64() : 0
+// Phase clocks read the device wall clock (s_memrealtime, a scalar memory round trip each); SMP_NOCLK builds
+// compile them out of the phase / stage accounting (the timeouts and the planning clock keep theirs).
+#ifdef SMP_NOCLK
+__device__ __forceinline__ unsigned long long pclk() { return 0; }
+#else
+__device__ __forceinline__ unsigned long long pclk() { return wall_clock64(); }
+#endif
+#define PROF_BEGIN() unsigned long long _pt = threadIdx.x == 0 ? pclk() : 0
 #ifdef SMP_DETAIL_PROF  // thread-0 clocks of serial sections into prof[28..31] (perf_probe.py SMP_DETAIL_PROF=1)
 #define DETAIL_BEGIN(v) const unsigned long long v = threadIdx.x == 0 ? wall_clock64() : 0
 #define DETAIL_END(v, k) if (threadIdx.x == 0) g_L.S.prof[k] += wall_clock64() - v
@@ -280,7 +287,7 @@ enum { P_SAMPLE, P_NN, P_EXPAND, P_NEAR, P_CHOOSE, P_REWIRE, P_CONNECT, P_TILES,
 #define DETAIL_BEGIN(v)
 #define DETAIL_END(v, k)
 #endif
-#define PROF_END(k) if (threadIdx.x == 0) { g_L.S.prof[k] += wall_clock64() - _pt; }
+#define PROF_END(k) if (threadIdx.x == 0) { g_L.S.prof[k] += pclk() - _pt; }
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 // Block-uniform control value read from LDS, made provably wave-uniform (a scalar register): every loop
@@ -1186,7 +1193,7 @@ __device__ __forceinline__ void edge_validity_job(const Ctx& C, int E, int pslot
     __builtin_amdgcn_s_sleep(1);
   }
   TR();
-  if (threadIdx.x == 0) g_L.S.prof[P_TCENTRE] += wall_clock64() - tj1;  // waiting for helpers' tiles
+  if (threadIdx.x == 0) g_L.S.prof[P_TCENTRE] += pclk() - tj1;  // waiting for helpers' tiles
   // first collision per job edge from the tile masks
   for (int t = threadIdx.x; t < nt; t += BLOCK) {
     unsigned m = J.rmask[t];
@@ -1201,7 +1208,7 @@ __device__ __forceinline__ void edge_validity_job(const Ctx& C, int E, int pslot
   if (threadIdx.x < ne) g_L.eg_first[J.emap[threadIdx.x]] = J.first[threadIdx.x];
   PROF_END(P_TILES);
   if (threadIdx.x == 0) {
-    g_L.S.prof[pslot] += wall_clock64() - _pt;
+    g_L.S.prof[pslot] += pclk() - _pt;
     g_L.S.prof[P_NTILES] += nt;
     g_L.S.prof[pslot + 8] += J.nslots;
   }
@@ -1340,8 +1347,8 @@ __device__ bool spec_stage(const Ctx& C, int s, unsigned long long wait) {
   if (wait == 0) wait = SCOUT_WAIT;
   const int have = uni(g_L.sp_stage);
   if (have >= s) return true;
-  const ScoutBoard* sb = uni(g_L.asked[g_L.S.iter & 3]) == 2 ? C.Q.scb2 : C.Q.scb;
-  const int par = (int)(g_L.S.iter & 3);
+  const ScoutBoard* sb = C.Q.scbs[uni(g_L.asked[g_L.S.iter & (SCOUT_SLOTS - 1)]) - 1];
+  const int par = (int)(g_L.S.iter & (SCOUT_SLOTS - 1));
   const unsigned tag = (unsigned)(g_L.S.iter + 1);
   const unsigned long long t0 = threadIdx.x == 0 ? wall_clock64() : 0;
   TR();
@@ -1401,12 +1408,13 @@ __device__ void spec_copy(const ScoutBoard* sb, int par, int have, int st) {
 // requested tree stay as they are until the record is used (only appends before then), and their stores are
 // drained here, so the scout reads them as the leader will.  Iteration j looks a record up only if it was asked
 // for (asked[j % 4]); every scout also gets the leader's current iteration (its staleness test).
-// Thread 0: asks the scout for iteration k (expanding `tree`, whose first n[tree] nodes are final for it); with a
-// second scout the two alternate by parity (scout 2 takes the even iterations).
+// Thread 0: asks a scout for iteration k (expanding `tree`, whose first n[tree] nodes are final for it): before the
+// first solution scout k mod nscouts, after it scout k mod 2 (scouts 0 and 1).
 __device__ void scout_ask(const Ctx& C, long long k, int tree, bool pre, bool& fenced) {
   const QState& S = g_L.S;
-  const int which = C.Q.scb2 && !(k & 1) ? 2 : 1;
-  ScoutBoard* sb = which == 2 ? C.Q.scb2 : C.Q.scb;
+  const int ns = C.Q.nscouts;
+  const int which = 1 + (int)(pre ? k % ns : (ns >= 2 ? (k & 1) : 0));
+  ScoutBoard* sb = C.Q.scbs[which - 1];
   int& same = g_L.sc_same[which - 1];
   if (same < 0) {
     const int x = ld_agent(&sb->xcc);
@@ -1423,8 +1431,8 @@ __device__ void scout_ask(const Ctx& C, long long k, int tree, bool pre, bool& f
   st_agent(&sb->req[2], granule(tag, (unsigned)S.n[1 - tree]));
   st_agent(&sb->req[1], granule(tag, (unsigned)g_L.smp_ver));
   st_agent(&sb->req[0], granule(tag, w0));
-  g_L.asked[k & 3] = which;
-  g_L.asked_conn[k & 3] = !pre && C.Q.scb2 != nullptr;
+  g_L.asked[k & (SCOUT_SLOTS - 1)] = which;
+  g_L.asked_conn[k & (SCOUT_SLOTS - 1)] = !pre && ns >= 2;
 }
 
 __device__ void scout_request(const Ctx& C, int t) {
@@ -1434,18 +1442,19 @@ __device__ void scout_request(const Ctx& C, int t) {
     const QState& S = g_L.S;
     const long long j = S.iter;
     const bool pre = !(S.tree_opt && S.have_sol);
-    const bool two = pre && C.Q.scb2 != nullptr;
-    g_L.asked[(j + 3) & 3] = 0;  // iteration j - 1's slot
-    g_L.asked_conn[(j + 3) & 3] = 0;
-    st_agent(&C.Q.scb->cur, (unsigned long long)j);
-    if (C.Q.scb2) st_agent(&C.Q.scb2->cur, (unsigned long long)j);
+    const int ns = C.Q.nscouts;
+    g_L.asked[(j - 1) & (SCOUT_SLOTS - 1)] = 0;  // iteration j - 1's slot
+    g_L.asked_conn[(j - 1) & (SCOUT_SLOTS - 1)] = 0;
+    for (int s = 0; s < ns; ++s) st_agent(&C.Q.scbs[s]->cur, (unsigned long long)j);
     bool fenced = false;
-    for (int ahead = 1; ahead <= (two ? 2 : 1); ++ahead) {
+    // before the first solution every scout has a request out (the trees only grow: records stay exact up to the
+    // appended nodes); iteration j + a expands tree t for odd a, the other one for even a
+    for (int ahead = 1; ahead <= (pre ? ns : 1); ++ahead) {
       const long long k = j + ahead;
-      if (g_L.asked[k & 3]) continue;
-      scout_ask(C, k, ahead == 1 ? t : 1 - t, pre, fenced);
+      if (g_L.asked[k & (SCOUT_SLOTS - 1)]) continue;
+      scout_ask(C, k, (ahead & 1) ? t : 1 - t, pre, fenced);
     }
-    g_L.sp_on = g_L.asked[j & 3] != 0;
+    g_L.sp_on = g_L.asked[j & (SCOUT_SLOTS - 1)] != 0;
     g_L.sp_stage = -1;
   }
   __syncthreads();
@@ -1456,19 +1465,20 @@ __device__ void scout_request(const Ctx& C, int t) {
 // and iteration j + 1 only appends to (its connect step), so the record stays exact up to the appended nodes, which
 // the leader patches in as before; each scout gets two leader iterations for its pass.
 __device__ void scout_request_ahead2(const Ctx& C, int tA) {
-  if (!C.Q.scb2) return;
+  if (C.Q.nscouts < 2) return;
   drain();
   __syncthreads();
   if (threadIdx.x == 0) {
     const long long j = g_L.S.iter, k = j + 2;
     bool fenced = false;
-    if (!g_L.asked[k & 3]) scout_ask(C, k, tA, false, fenced);
+    if (!g_L.asked[k & (SCOUT_SLOTS - 1)]) scout_ask(C, k, tA, false, fenced);
     // tree_A of this iteration is tree_B of iteration j + 1 and final for its connect step (which comes before any
     // other write to it): the scout of record j + 1 may run connect's scans now
     const long long k1 = j + 1;
-    if (g_L.asked[k1 & 3] && g_L.asked_conn[k1 & 3]) {
-      ScoutBoard* sb = g_L.asked[k1 & 3] == 2 ? C.Q.scb2 : C.Q.scb;
-      if (!fenced && g_L.sc_same[g_L.asked[k1 & 3] - 1] != 1) {
+    const int w1 = g_L.asked[k1 & (SCOUT_SLOTS - 1)];
+    if (w1 && g_L.asked_conn[k1 & (SCOUT_SLOTS - 1)]) {
+      ScoutBoard* sb = C.Q.scbs[w1 - 1];
+      if (!fenced && g_L.sc_same[w1 - 1] != 1) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         drain();
       }
@@ -1618,7 +1628,7 @@ __device__ void edge_validity(const Ctx& C, int E, bool stop_first_valid, int ps
                      &g_L.S.prof[P_TFK]);
     PROF_END(P_TILES);
     if (threadIdx.x == 0) {
-      g_L.S.prof[pslot] += wall_clock64() - _pt;
+      g_L.S.prof[pslot] += pclk() - _pt;
       g_L.S.prof[P_NTILES]++;
       g_L.S.prof[pslot + 8] += nc;
     }
@@ -1977,8 +1987,9 @@ __device__ void sample_read(const Ctx& C) {
   QState& S = g_L.S;
   const uint32_t it = (uint32_t)S.iter;
   const bool pre = uni(g_L.sp_on && g_L.sp_stage < 0) != 0;
-  const ScoutBoard* sb = uni(g_L.asked[S.iter & 3]) == 2 ? C.Q.scb2 : C.Q.scb;
-  const int par = (int)(S.iter & 3);
+  const int sw = uni(g_L.asked[S.iter & (SCOUT_SLOTS - 1)]);
+  const ScoutBoard* sb = sw > 0 ? C.Q.scbs[sw - 1] : nullptr;
+  const int par = (int)(S.iter & (SCOUT_SLOTS - 1));
   if (threadIdx.x == 64) {
     int st = -1;
     if (pre) {
@@ -2444,7 +2455,7 @@ __device__ void connect_graphs(const Ctx& C, int t) {
 __device__ bool conn_stage(const Ctx& C, int B) {
   if (threadIdx.x == 0) g_L.conn_rec = 0;
   __syncthreads();
-  if (!uni(g_L.asked_conn[g_L.S.iter & 3])) return false;
+  if (!uni(g_L.asked_conn[g_L.S.iter & (SCOUT_SLOTS - 1)])) return false;
   if (!spec_stage(C, SC_CONN, 1000)) return false;
   const ScoutConn& R = g_L.sr.cc;
   const bool ok = uni(R.ok && R.t == B && R.X == g_L.S.n[B] && R.excl == g_L.xn.id && same8(R.q, g_L.xn.q));
@@ -2458,16 +2469,16 @@ __device__ bool conn_stage(const Ctx& C, int B) {
 // iterations (tools/experiments/README.md), builds that inline it run clean.
 __device__ __forceinline__ void iteration(const Ctx& C) {
   const int A = uni(g_L.S.A), B = 1 - A;
-  unsigned long long _t0 = threadIdx.x == 0 ? wall_clock64() : 0, _t1;
+  unsigned long long _t0 = threadIdx.x == 0 ? pclk() : 0, _t1;
 #ifdef SMP_TRACE
   if (threadIdx.x == 0) g_L.tit = g_L.S.iter;
 #endif
   if (threadIdx.x == 0) g_L.conn_rec = 0;
   TR();
-#define PHASE(k) if (threadIdx.x == 0) { _t1 = wall_clock64(); g_L.S.prof[k] += _t1 - _t0; _t0 = _t1; }
+#define PHASE(k) if (threadIdx.x == 0) { _t1 = pclk(); g_L.S.prof[k] += _t1 - _t0; _t0 = _t1; }
   sample_publish(C);
   TR();
-  if (C.Q.scb) scout_request(C, B);
+  if (C.Q.nscouts > 0) scout_request(C, B);
   TR();
   sample_read(C);
   TR();
@@ -2558,7 +2569,8 @@ __device__ __forceinline__ void iteration(const Ctx& C) {
     } else if (crec) {
       cid = uni(g_L.sr.cc.d < 10000.0 ? g_L.sr.cc.id : 0);
       if (threadIdx.x == 0) { g_L.S.nn_nodes += g_L.S.n[B]; g_L.S.sc_nn++; }
-    } else if (uni(!opt && g_L.sp_on && g_L.sp_stage >= SC_DONE && g_L.sr.cn.ok && g_L.sr.cn.t == B &&
+    } else if (uni(!opt && g_L.sp_on) && spec_stage(C, SC_DONE, 2500) &&
+               uni(g_L.sr.cn.ok && g_L.sr.cn.t == B &&
                    g_L.sr.cn.X <= g_L.S.n[B] && same8(g_L.sr.cn.q, g_L.xn.q))) {
       // the scout's nearest node over the first X nodes; only the nodes appended since are scanned (one of them
       // replaces it only with a strictly smaller distance: it has a larger index)
@@ -2612,16 +2624,16 @@ __device__ __forceinline__ void iteration(const Ctx& C) {
 // Scout: publishes `nbytes` of section p of its record, then (stage >= 0) the stage granule once every wave's
 // stores are drained.
 __device__ void sc_publish(const Ctx& C, int par, unsigned tag, int stage) {
-  const unsigned long long t0 = threadIdx.x == 0 ? wall_clock64() : 0;
+  const unsigned long long t0 = threadIdx.x == 0 ? pclk() : 0;
   drain();
   __syncthreads();
   if (threadIdx.x == 0) {
     st_agent(&C.Q.scb->stage[par], granule(tag, (unsigned)stage));
-    g_L.S.prof[29] += wall_clock64() - t0;
+    g_L.S.prof[29] += pclk() - t0;
   }
   __syncthreads();
 }
-#define SC_PHASE(k) if (threadIdx.x == 0) { const unsigned long long _t = wall_clock64(); g_L.S.prof[k] += _t - _ts; _ts = _t; }
+#define SC_PHASE(k) if (threadIdx.x == 0) { const unsigned long long _t = pclk(); g_L.S.prof[k] += _t - _ts; _ts = _t; }
 // True (block-uniform) once the leader has moved past the iteration with record tag `tag` (iteration tag - 1):
 // the rest of the record would not be used.
 __device__ bool sc_stale(const Ctx& C, unsigned tag) {
@@ -2725,10 +2737,10 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
   ScoutRec& R = g_L.sr;
   ScoutBoard* sb = C.Q.scb;
   JobBoard* jb = C.Q.jb;  // this Ctx's board is the scout's; the sampler ring lives on the leader's (sampler_jb)
-  const int par = (int)(it & 3);
+  const int par = (int)(it & (SCOUT_SLOTS - 1));
   const unsigned tag = (unsigned)(it + 1);
   (void)jb;
-  unsigned long long _ts = threadIdx.x == 0 ? wall_clock64() : 0;
+  unsigned long long _ts = threadIdx.x == 0 ? pclk() : 0;
 #ifdef SMP_TRACE
   if (threadIdx.x == 0) g_L.tit = it;
 #endif
@@ -2993,15 +3005,13 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
 }
 #undef SC_PHASE
 
-// Scout workgroup of a query (plan_kernel blocks nq .. 2nq-1): takes the leader's newest request, runs
-// scout_iteration on it, repeats; leaves on the stop flag (then stops its helpers) or after two idle seconds.
+// Scout workgroup `which` of a query (plan_kernel): takes the leader's newest request, runs scout_iteration on it,
+// repeats; leaves on the stop flag (then stops its helpers) or after two idle seconds.
 __device__ __forceinline__ void scout_main(Ctx& C, int which) {
-  if (which == 2) {  // the second scout: its own record board, job board, helpers and via scratch
-    C.Q.scb = C.Q.scb2;
-    C.Q.sjb = C.Q.sjb2;
-    C.Q.svia = C.Q.svia2;
-    C.Q.sworkers = C.Q.sworkers2;
-  }
+  C.Q.scb = C.Q.scbs[which];  // its own record board, job board, helpers and via scratch
+  C.Q.sjb = C.Q.sjbs[which];
+  C.Q.svia = C.Q.svias[which];
+  C.Q.sworkers = C.Q.sworkers_s[which];
   {
     const int* src = reinterpret_cast<const int*>(C.Q.st);
     int* dst = reinterpret_cast<int*>(&g_L.S);
@@ -3024,12 +3034,12 @@ __device__ __forceinline__ void scout_main(Ctx& C, int which) {
     g_L.spec = OV_NONE;
     g_L.sp_on = 0;
     st_agent(&C.Q.scb->xcc, xcc_id() + 1);
-    g_L.two_scouts = C.Q.scb2 != nullptr;
+    g_L.two_scouts = C.Q.nscouts >= 2;
     g_L.rec_grp = -1;
 #ifdef SMP_TRACE
-    g_L.trole = which;
+    g_L.trole = which + 1 < 3 ? which + 1 : 3;
     g_L.tit = -1;
-    g_L.tn = g_tlog_n[which];
+    g_L.tn = g_tlog_n[g_L.trole];
 #endif
   }
   __syncthreads();
@@ -3088,26 +3098,26 @@ __device__ __forceinline__ void scout_main(Ctx& C, int which) {
 __global__ void __launch_bounds__(BLOCK) plan_kernel(const RobotDev* __restrict__ rb, SceneDev sc,
                                                      const MapCfg* __restrict__ mc, QueryDev* qs, int nq, int scout_base,
                                                      int iters) {
-  // blocks [0, nq): leaders; [scout_base, scout_base + nq): their scouts (scout_base a multiple of 8, so that query
-  // q's two blocks are dealt to the same XCD); any other block has nothing to do
-  // second scouts at scout_base2 + q (again a multiple of 8 apart: same XCD as their leader)
+  // blocks [0, nq): leaders; scout s of query q at scout_base + s * r8 + q (scout_base and r8 = nq rounded up to 8
+  // are multiples of 8, and blocks are dealt to the 8 XCDs round-robin: a query's workgroups share an XCD); any
+  // other block has nothing to do
   const int b = (int)blockIdx.x;
-  const int scout_base2 = scout_base + (nq + 7) / 8 * 8;
-  const bool s1 = scout_base > 0 && b >= scout_base && b < scout_base + nq;
-  const bool s2 = scout_base > 0 && b >= scout_base2 && b < scout_base2 + nq;
-  if (b >= nq && !s1 && !s2) return;
+  const int r8 = (nq + 7) / 8 * 8;
+  const int so = b - scout_base, srole = scout_base > 0 && b >= scout_base ? so / r8 : -1;
+  const int sq = srole >= 0 ? so - srole * r8 : b;
+  if (b >= nq && (srole < 0 || sq >= nq)) return;
   stage_model(rb, mc, &g_rb, &g_mc);
   Ctx C;
   C.sc = sc;
-  C.Q = qs[b < nq ? b : (s1 ? b - scout_base : b - scout_base2)];
-  if (b >= nq) {
-    if ((s1 && C.Q.scb) || (s2 && C.Q.scb2)) scout_main(C, s2 ? 2 : 1);  // one call site: inlined
+  C.Q = qs[sq];
+  if (srole >= 0) {
+    if (srole < C.Q.nscouts) scout_main(C, srole);  // one call site: inlined
     return;
   }
   if (threadIdx.x == 0) {
     g_L.sp_on = 0;
-    g_L.sc_same[0] = g_L.sc_same[1] = -1;
-    for (int k = 0; k < 4; ++k) { g_L.asked[k] = 0; g_L.asked_conn[k] = 0; }
+    for (int k = 0; k < MAX_SCOUTS; ++k) g_L.sc_same[k] = -1;
+    for (int k = 0; k < SCOUT_SLOTS; ++k) { g_L.asked[k] = 0; g_L.asked_conn[k] = 0; }
     g_L.conn_rec = 0;
     g_L.rec_grp = -1;
     g_L.count_slot = 0;
@@ -3157,8 +3167,7 @@ __global__ void __launch_bounds__(BLOCK) plan_kernel(const RobotDev* __restrict_
 #endif
     *C.Q.st = g_L.S;
     if (C.Q.jb) st_agent(&C.Q.jb->stop, 1);
-    if (C.Q.scb) st_agent(&C.Q.scb->stop, 1);
-    if (C.Q.scb2) st_agent(&C.Q.scb2->stop, 1);
+    for (int s = 0; s < C.Q.nscouts; ++s) st_agent(&C.Q.scbs[s]->stop, 1);
   }
 }
 
@@ -3241,19 +3250,19 @@ __global__ void __launch_bounds__(BLOCK) helper_kernel(const RobotDev* __restric
   if (!C.Q.jb) return;
   if (C.Q.sampler && hidx == nh - 1) {
     sampler_main(C, SL);
-  } else if (hidx < C.Q.nworkers - 1) {
-    helper_main(C, hidx, J);                 // the leader's tile helpers
-  } else if (C.Q.sjb && hidx - (C.Q.nworkers - 1) < C.Q.sworkers - 1) {
-    const int h = hidx - (C.Q.nworkers - 1);  // the scout's tile helpers
-    C.Q.jb = C.Q.sjb;
-    C.Q.nworkers = C.Q.sworkers;
-    helper_main(C, h, J);
-  } else if (C.Q.sjb2 && hidx - (C.Q.nworkers - 1) - (C.Q.sworkers - 1) < C.Q.sworkers2 - 1) {
-    const int h = hidx - (C.Q.nworkers - 1) - (C.Q.sworkers - 1);  // the second scout's tile helpers
-    C.Q.jb = C.Q.sjb2;
-    C.Q.nworkers = C.Q.sworkers2;
-    helper_main(C, h, J);
+    return;
   }
+  // the leader's tile helpers first, then each scout's
+  int h = hidx;
+  if (h >= C.Q.nworkers - 1) {
+    h -= C.Q.nworkers - 1;
+    int s = 0;
+    for (; s < C.Q.nscouts && h >= C.Q.sworkers_s[s] - 1; ++s) h -= C.Q.sworkers_s[s] - 1;
+    if (s >= C.Q.nscouts) return;
+    C.Q.jb = C.Q.sjbs[s];
+    C.Q.nworkers = C.Q.sworkers_s[s];
+  }
+  helper_main(C, h, J);
 }
 
 __global__ void path_kernel(QueryDev* qs, int* counts) {

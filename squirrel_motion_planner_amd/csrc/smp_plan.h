@@ -179,6 +179,12 @@ struct ScoutRec {
   int n_choose, n_rewire, pad[2];
   ScoutEdge e[SCOUT_EDGES];    // [0] expand, [SCOUT_CHOOSE0 ..) choose-parent, [SCOUT_REWIRE0 ..) rewire
 };
+// Record slots of a scout board, by iteration mod SCOUT_SLOTS: a scout may be asked for iteration k + MAX_SCOUTS
+// while the leader still reads its record of k (before the first solution the scouts take the iterations in turn,
+// up to MAX_SCOUTS ahead).
+constexpr int MAX_SCOUTS = 4;
+constexpr int SCOUT_SLOTS = 8;
+static_assert(SCOUT_SLOTS > MAX_SCOUTS && (SCOUT_SLOTS & (SCOUT_SLOTS - 1)) == 0, "record slots");
 struct ScoutBoard {
   // leader -> scout: the request for iteration k carries tag k + 1; req[0] low word = X | t << 28 | opt << 29,
   // req[1] low word = the sampler parameter version, req[2] low word = XB (nodes of the other tree)
@@ -188,26 +194,30 @@ struct ScoutBoard {
   int pad0[8];
   unsigned long long cur;      // leader -> scout: the leader's current iteration (a record of an earlier one is stale)
   int pad2[30];
-  unsigned long long stage[4]; // scout -> leader, by iteration mod 4 (a scout may work two iterations ahead)
+  unsigned long long stage[SCOUT_SLOTS];  // scout -> leader, by iteration mod SCOUT_SLOTS
   unsigned long long cgo;      // leader -> scout: granule (iteration k + 1, n of tree_B(k)) once tree_B(k) is final
-  int pad1[22];
+  int pad1[14];
   unsigned long long prof[32]; // the scout's phase clocks of the launch (written when it leaves)
-  ScoutRec rec[4];
+  ScoutRec rec[SCOUT_SLOTS];
 };
 
 struct QueryDev {
   QState* st;
   JobBoard* jb;                // null: no helpers
-  JobBoard* sjb;               // the scout's collision-job board (null: no scout)
   JobBoard* sampler_jb;        // scout: the leader's board (run-ahead sampler ring)
+  // scouts (DESIGN.md "Scouts"): nscouts workgroups compute records of the leader's coming iterations -- before the
+  // first solution iteration k goes to scout k mod nscouts (up to nscouts ahead), after it to scout k mod 2 (two
+  // ahead); each has its record board, collision-job board, helpers and via-node scratch
+  int nscouts;
+  ScoutBoard* scbs[MAX_SCOUTS];
+  JobBoard* sjbs[MAX_SCOUTS];
+  ViaNode* svias[MAX_SCOUTS];
+  int sworkers_s[MAX_SCOUTS];  // scout + its tile helper workgroups
+  // a scout workgroup's own board, job board, via scratch and workers (set by scout_main)
   ScoutBoard* scb;
-  ViaNode* svia;               // the scout's via-node scratch [via_cap]
-  int sworkers;                // scout + its tile helper workgroups
-  // second scout (pre-solution iterations, two ahead of the leader; null: none) and its board / helpers
-  JobBoard* sjb2;
-  ScoutBoard* scb2;
-  ViaNode* svia2;
-  int sworkers2;
+  JobBoard* sjb;
+  ViaNode* svia;
+  int sworkers;
   int* trace;                  // debug only (SMP_DEBUG): host-mapped progress markers of the leader
   int nworkers;                // leader + tile helper workgroups (tile w, w + nworkers, ... is worker w's)
   int sampler;                 // 1: the last helper workgroup is the run-ahead sampler

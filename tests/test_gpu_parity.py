@@ -218,6 +218,20 @@ def test_planner_parity_helper_counts(orobot, robot, helpers):
     assert_same_run(gp2, r, o)
 
 
+@pytest.mark.parametrize("scouts", [2, 3, 4])
+def test_planner_parity_scout_counts(orobot, robot, scouts):
+    """Two, three and four scouts taking the iterations in turn before the first solution (records up to
+    four iterations ahead, patched by the leader), across the first solution and 2000 iterations after it."""
+    gp2 = GpuPlanner(robot, helpers=63, scout=scouts, path_optimality_threshold=-np.inf)
+    sc, gscene, osc = scene_pair("c2")
+    gp2.set_scene(gscene)
+    r = gp2.plan(GpuPlanner.make_query(sc.start, sc.goal, sc.env_x, sc.env_y, iterations=2000, seed=5))
+    o = O.Oracle(orobot, osc).plan(sc.start, sc.goal, env_x=sc.env_x, env_y=sc.env_y, max_iter=2000, seed=5,
+                                   opt_thresh=-np.inf)
+    assert r["scout"] == scouts
+    assert_same_run(gp2, r, o)
+
+
 def test_planner_parity_yaml_profile(orobot, robot):
     gp2 = GpuPlanner(robot, near_threshold=1.5, step_factor=0.6)
     sc, r, o = run_both(gp2, orobot, "c2", 5, 200, near_threshold=1.5, step_factor=0.6)
