@@ -716,7 +716,7 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
   if (nh < 4) ns = 0;
   // after the first solution scouts 0 and 1 check choose-parent / rewire candidate batches (many tiles); scouts 2
   // and 3 only work before it, one edge per job (3 tiles); the leader's own jobs (edges no record had) are rare
-  int h_lead = 0, h_s[MAX_SCOUTS] = {0, 0, 0, 0};
+  int h_lead = 0, h_s[MAX_SCOUTS] = {};
   if (ns > 0) {
     const int avail = nh - 1;  // minus the sampler
     h_lead = ns >= 2 ? avail / 5 : avail / 2;

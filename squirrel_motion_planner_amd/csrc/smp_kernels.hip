@@ -152,6 +152,7 @@ constexpr int NEAR_NBK = 16;     // near_set register path: 64-node batches per 
 #define SMP_PLAN_CT 32
 #endif
 constexpr int PLAN_CT = SMP_PLAN_CT;  // configurations per collision tile of the planner
+constexpr int PATCH_K = 32;           // leader: recently appended nodes kept in LDS per tree (power of two)
 struct PlanLds {
   QState S;
   union {
@@ -233,6 +234,11 @@ struct PlanLds {
   int eg_rec[MAXE];             // leader: record edge (index into sr.e) equal to batch edge e, -1 = none
   int rec_grp;                  // leader: the record stage eg_rec was matched against (-1 = not matched)
   int rec_all, ev_job;          // rec_match: every edge matched; edge_validity: a job is needed
+  int req_need;                 // scout_request: some coming iteration is not asked for yet
+  // leader: configurations of the last PATCH_K nodes appended to each tree, by node index mod PATCH_K (kept by
+  // insert_node / insert_via, loaded at launch start); before the first solution no node changes after its insert,
+  // so pre_commit's patch scans over the nodes appended since a record's snapshot read these
+  double pc_q[2][PATCH_K][NJ];
 };
 
 // The planner's LDS objects live at namespace scope so that every device function addresses them as LDS
@@ -357,6 +363,7 @@ __device__ void insert_node(const Ctx& C, int t, const double* e_start, const do
     st_tree(&T.q[(size_t)j * cap + i], x.q[j]);
     T.e_start[(size_t)j * cap + i] = e_start[j];
     T.e_target[(size_t)j * cap + i] = e_target[j];
+    g_L.pc_q[t][i & (PATCH_K - 1)][j] = x.q[j];
   }
   for (int k = 0; k < 3; ++k) st_tree(&T.cost[(size_t)k * cap + i], x.c[k]);
   st_tree(&T.parent[i], x.parent);
@@ -439,6 +446,37 @@ __device__ int nearest_scan(const Ctx& C, int t, const double* q, int i_begin, d
   *d_out = __longlong_as_double((long long)bk);
   TR();
   return bi;
+}
+
+// nearest_scan over the nodes [i0, n) of tree t, n - i0 <= PATCH_K, from the leader's LDS copy of the recently
+// appended nodes (valid before the first solution): wave 0, one node per lane, the same distance and the same
+// (distance, id) minimum.  All threads; returns the id, *d_out = its distance (10000 if none is below it).
+__device__ int patch_scan(int t, const double* q, int i0, int n, double* d_out) {
+  if (threadIdx.x < 64) {
+    const int i = i0 + (int)threadIdx.x;
+    double best = 10000.0;
+    int bid = 0x7fffffff;
+    if (i < n) {
+      const double* x = g_L.pc_q[t][i & (PATCH_K - 1)];
+      double s = 0.0;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const double d = q[j] - x[j];
+        s += d * d;
+      }
+      const double dist = sqrt(s);
+      if (dist < best) { best = dist; bid = i; }
+    }
+    const unsigned long long key = (unsigned long long)__double_as_longlong(best);
+    const unsigned long long wk = __ockl_wfred_min_u64(key);
+    const int wi = __ockl_wfred_min_i32(key == wk ? bid : 0x7fffffff);
+    if (threadIdx.x == 0) { g_L.wk[0] = wk; g_L.wi[0] = wi; }
+  }
+  __syncthreads();
+  *d_out = __longlong_as_double((long long)g_L.wk[0]);
+  const int id = g_L.wi[0];
+  __syncthreads();
+  return id;
 }
 
 // find_nearest_neighbour_interpolation (birrt_star.cpp:4076-4133).  With `spec`, the scout's scan of the same
@@ -1333,6 +1371,7 @@ __device__ __forceinline__ void sc_copy_in(const ScoutBoard* sb, int par, void* 
 static_assert(sizeof(ScoutNN) % 8 == 0 && sizeof(ScoutNear) % 8 == 0 && sizeof(ScoutEdge) % 8 == 0 &&
               sizeof(ScoutExpand) % 8 == 0 && offsetof(ScoutRec, ex) % 8 == 0 && offsetof(ScoutRec, nr) % 8 == 0 &&
               sizeof(ScoutConnect) % 8 == 0 && offsetof(ScoutRec, cn) % 8 == 0 && sizeof(ScoutConn) % 8 == 0 &&
+              sizeof(ScoutPre) % 8 == 0 && offsetof(ScoutRec, pre) % 8 == 0 && sizeof(ViaNode) % 8 == 0 &&
               offsetof(ScoutRec, cc) % 8 == 0 && offsetof(ScoutRec, n_choose) % 8 == 0 && offsetof(ScoutRec, e) % 8 == 0,
               "scout record sections are 8-byte words");
 
@@ -1393,7 +1432,10 @@ __device__ void spec_copy(const ScoutBoard* sb, int par, int have, int st) {
     sc_copy_in(sb, par, &R.n_choose, 4 * sizeof(int));
   if (opt_now && have < SC_CHOOSE && st >= SC_CHOOSE) sc_copy_in(sb, par, &R.e[SCOUT_CHOOSE0], MAX_NEAR * sizeof(ScoutEdge));
   if (opt_now && have < SC_DONE && st >= SC_DONE) sc_copy_in(sb, par, &R.e[SCOUT_REWIRE0], MAX_NEAR * sizeof(ScoutEdge));
-  if (!opt_now && have < SC_DONE && st >= SC_DONE) sc_copy_in(sb, par, &R.cn, sizeof(ScoutConnect));
+  if (!opt_now && have < SC_DONE && st >= SC_DONE) {
+    sc_copy_in(sb, par, &R.cn, sizeof(ScoutConnect));
+    sc_copy_in(sb, par, &R.pre, sizeof(ScoutPre));
+  }
   if (have < SC_CONN && st >= SC_CONN) sc_copy_in(sb, par, &R.cc, sizeof(ScoutConn));
   __syncthreads();
   if (threadIdx.x == 0) g_L.sp_stage = st;
@@ -1435,29 +1477,48 @@ __device__ void scout_ask(const Ctx& C, long long k, int tree, bool pre, bool& f
   g_L.asked_conn[k & (SCOUT_SLOTS - 1)] = !pre && ns >= 2;
 }
 
-__device__ void scout_request(const Ctx& C, int t) {
-  drain();
-  __syncthreads();
+// Leader, start of iteration j, before any store of the iteration: the requests for the coming iterations not yet
+// asked for.  Their snapshots include the nodes the last iteration appended, whose stores are drained first -- only
+// when something is asked (after the first solution the next iteration was usually asked for by
+// scout_request_ahead2), and before this iteration's own stores, so the drain finds the last iteration's long done.
+// Iteration j - 1's record slot is free again, j's record is looked up only if it was asked for, and every scout
+// gets the leader's iteration (its staleness test).
+// scout_prepare: the drain (all threads); scout_request (thread 0, after sample_publish, whose new parameter version
+// the requests carry): the asks; the caller's next barrier publishes the LDS bookkeeping.
+__device__ void scout_prepare(const Ctx& C) {
   if (threadIdx.x == 0) {
     const QState& S = g_L.S;
     const long long j = S.iter;
     const bool pre = !(S.tree_opt && S.have_sol);
-    const int ns = C.Q.nscouts;
-    g_L.asked[(j - 1) & (SCOUT_SLOTS - 1)] = 0;  // iteration j - 1's slot
+    int need = 0;
+    for (int ahead = 1; ahead <= (pre ? C.Q.nscouts : 1); ++ahead) need |= !g_L.asked[(j + ahead) & (SCOUT_SLOTS - 1)];
+    g_L.req_need = need;
+  }
+  __syncthreads();
+  if (uni(g_L.req_need)) {
+    drain();
+    __syncthreads();
+  }
+}
+__device__ void scout_request(const Ctx& C, int t) {
+  if (threadIdx.x == 0) {
+    const QState& S = g_L.S;
+    const long long j = S.iter;
+    const bool pre = !(S.tree_opt && S.have_sol);
+    g_L.asked[(j - 1) & (SCOUT_SLOTS - 1)] = 0;
     g_L.asked_conn[(j - 1) & (SCOUT_SLOTS - 1)] = 0;
-    for (int s = 0; s < ns; ++s) st_agent(&C.Q.scbs[s]->cur, (unsigned long long)j);
+    g_L.sp_on = g_L.asked[j & (SCOUT_SLOTS - 1)] != 0;
+    g_L.sp_stage = -1;
+    for (int s = 0; s < C.Q.nscouts; ++s) st_agent(&C.Q.scbs[s]->cur, (unsigned long long)j);
     bool fenced = false;
     // before the first solution every scout has a request out (the trees only grow: records stay exact up to the
     // appended nodes); iteration j + a expands tree t for odd a, the other one for even a
-    for (int ahead = 1; ahead <= (pre ? ns : 1); ++ahead) {
+    for (int ahead = 1; ahead <= (pre ? C.Q.nscouts : 1); ++ahead) {
       const long long k = j + ahead;
       if (g_L.asked[k & (SCOUT_SLOTS - 1)]) continue;
       scout_ask(C, k, (ahead & 1) ? t : 1 - t, pre, fenced);
     }
-    g_L.sp_on = g_L.asked[j & (SCOUT_SLOTS - 1)] != 0;
-    g_L.sp_stage = -1;
   }
-  __syncthreads();
 }
 
 // After the first solution, with two scouts: iteration j asks for iteration j + 2 once its own rewire commits are
@@ -1775,7 +1836,10 @@ __device__ void via_chain(const Ctx& C, const double* target) {
 // chain -- via k's parent is via k-1, the first one's an existing node p0 -- so the result of the sequential
 // inserts is known up front: node n0+k gets first child n0+k+1 (none for the last), and only p0's child list
 // changes among the existing nodes.  One thread per node; thread 0 also links the first node under p0.
-__device__ void insert_via(const Ctx& C, int t) {
+// rec (pre-solution commits): the nodes come from a scout record's via chain instead of C.Q.via, read
+// with agent-scope loads; their ids (and parents) at or above rec_x are the scout's, relative to its snapshot size
+// rec_x, and are rebased onto this tree's size.
+__device__ void insert_via(const Ctx& C, int t, const ViaNode* rec = nullptr, int rec_x = 0) {
   TR();
   DETAIL_BEGIN(_di);
   const int nv = uni(g_L.n_via);
@@ -1787,22 +1851,34 @@ __device__ void insert_via(const Ctx& C, int t) {
       if (threadIdx.x == 0) { S.status = -7; S.phase = 2; }
     } else {
       for (int k = threadIdx.x; k < nv; k += BLOCK) {
-        const ViaNode& w = C.Q.via[k];
-        const int i = n0 + k;
-        if (w.id != i || (k > 0 && w.parent != i - 1)) S.status = -7;  // not the chain insert_node expects
-        for (int j = 0; j < NJ; ++j) {
-          st_tree(&T.q[(size_t)j * cap + i], w.q[j]);
-          T.e_start[(size_t)j * cap + i] = w.e_start[j];
-          T.e_target[(size_t)j * cap + i] = w.e_target[j];
+        const ViaNode& w = rec ? rec[k] : C.Q.via[k];
+        // record words are read with agent-scope loads (the scout may run on another XCD)
+        auto ldd = [&](const double* p) {
+          return rec ? __longlong_as_double((long long)ld_agent(reinterpret_cast<const unsigned long long*>(p))) : *p;
+        };
+        int wid = rec ? ld_agent(&w.id) : w.id, wpar = rec ? ld_agent(&w.parent) : w.parent;
+        if (rec) {
+          const int off = n0 - rec_x;
+          if (wid >= rec_x) wid += off;
+          if (wpar >= rec_x) wpar += off;
         }
-        for (int c = 0; c < 3; ++c) st_tree(&T.cost[(size_t)c * cap + i], w.c[c]);
-        st_tree(&T.parent[i], w.parent);
+        const int i = n0 + k;
+        if (wid != i || (k > 0 && wpar != i - 1)) S.status = -7;  // not the chain insert_node expects
+        for (int j = 0; j < NJ; ++j) {
+          const double qj = ldd(&w.q[j]);
+          st_tree(&T.q[(size_t)j * cap + i], qj);
+          g_L.pc_q[t][i & (PATCH_K - 1)][j] = qj;
+          T.e_start[(size_t)j * cap + i] = ldd(&w.e_start[j]);
+          T.e_target[(size_t)j * cap + i] = ldd(&w.e_target[j]);
+        }
+        for (int c = 0; c < 3; ++c) st_tree(&T.cost[(size_t)c * cap + i], ldd(&w.c[c]));
+        st_tree(&T.parent[i], wpar);
         T.first_child[i] = k + 1 < nv ? i + 1 : -1;
         T.prev_sib[i] = -1;
         if (k > 0) {
           T.next_sib[i] = -1;
         } else {
-          const int p = w.parent, f = T.first_child[p];
+          const int p = wpar, f = T.first_child[p];
           T.next_sib[i] = f;
           if (f >= 0) T.prev_sib[f] = i;
           T.first_child[p] = i;
@@ -2260,6 +2336,7 @@ __device__ void rewire(const Ctx& C, int t) {
 
 // connectGraphsInterpolation, unconstrained branch + commit (birrt_star.cpp:2608-3046, 3219-3288).
 // t = tree_B; g_L.xc = its nearest node to x_new; g_L.xn = x_new (node of the other tree).
+__device__ void connect_tail(const Ctx& C, int t);
 __device__ void connect_graphs(const Ctx& C, int t) {
   if (threadIdx.x == 0) {
     g_L.tree_expand = 0;
@@ -2428,6 +2505,12 @@ __device__ void connect_graphs(const Ctx& C, int t) {
     }
   }
   insert_via(C, t);
+  connect_tail(C, t);
+}
+
+// connectGraphs' commit (birrt_star.cpp:3219-3288), after the via nodes are inserted: the connection node on a
+// cheaper solution (the first one sets the first-solution iteration and time), else the extension's last node.
+__device__ void connect_tail(const Ctx& C, int t) {
   if (threadIdx.x == 0) {
     QState& S = g_L.S;
     if (g_L.csp[0] < S.cbest[0]) {
@@ -2464,6 +2547,114 @@ __device__ bool conn_stage(const Ctx& C, int B) {
   return ok;
 }
 
+// Leader, an iteration before the first solution committed from its complete scout record (DESIGN.md "Pre-solution
+// commits").  Before the first solution nothing rewires, so a tree only grows and a record computed on the first X
+// nodes of a tree is exact up to the nodes appended since, which the leader scans here: one of them replaces the
+// record's nearest node only with a strictly smaller distance (it has a larger index, birrt_star.cpp:4122).  If none
+// does, the iteration is the record's -- expand edge (birrt_star.cpp:2224-2256), x_new, connect's nearest node,
+// direct edge and via chain (connectGraphs without a solution has no near loop, birrt_star.cpp:2608-2812) -- and the
+// leader only counts and inserts.  Returns false, having changed nothing, if the record does not hold (the caller
+// runs the iteration itself); a record whose connect part does not hold is completed by connect_graphs.
+// Outcome counters of pre_commit in prof[28..31] (committed / no usable record / a newer nearest node / connect
+// completed by connect_graphs); those slots belong to the profiling builds' own clocks otherwise.
+#if defined(SMP_DETAIL_PROF) || defined(SMP_JOB_PROF) || defined(SMP_NEAR_PROF) || defined(SMP_SAMPLE_PROF)
+#define PRE_COUNT(k)
+#else
+#define PRE_COUNT(k) if (threadIdx.x == 0) g_L.S.prof[28 + (k)]++
+#endif
+__device__ bool pre_commit(const Ctx& C, int A, int B) {
+  if (!uni(g_L.sp_on) || !spec_stage(C, SC_DONE)) { PRE_COUNT(1); return false; }
+  const ScoutRec& R = g_L.sr;
+  const int nA = uni(g_L.S.n[A]);
+  if (!uni(R.nn.ok && R.ex.ok && R.nn.t == A && R.nn.X <= nA && same8(R.nn.q, g_L.xr))) { PRE_COUNT(1); return false; }
+  if (uni(R.nn.X < nA)) {
+    double dp;
+    if (uni(nA - R.nn.X <= PATCH_K)) patch_scan(A, g_L.xr, R.nn.X, nA, &dp);
+    else nearest_scan(C, A, g_L.xr, R.nn.X, &dp);
+    if (uni(dp < R.nn.d)) { PRE_COUNT(2); return false; }
+  }
+  PRE_COUNT(0);
+  TR();
+  if (threadIdx.x == 0) {
+    QState& S = g_L.S;
+    S.nn_nodes += nA;
+    S.sc_nn++;
+    S.sc_edge_hit++;
+    const int nid = R.nn.d < 10000.0 ? R.nn.id : 0;
+    g_L.count_slot = P_XEXPAND + 4;
+    const int f = R.e[0].first;
+    count_edge(f);
+    g_L.ext_nn = f > S.n_pts;
+    g_L.ext_bp = 0;
+    if (g_L.ext_nn) {
+      for (int j = 0; j < NJ; ++j) { g_L.xn.q[j] = R.ex.end[j]; g_L.en_start[j] = R.e[0].s[j]; g_L.en_target[j] = R.ex.ext[j]; }
+      for (int k = 0; k < 3; ++k) g_L.xn.c[k] = R.nn.c[k] + R.ex.acc[k];
+      g_L.xn.id = S.n[A];
+      g_L.xn.parent = nid;
+      insert_node(C, A, g_L.en_start, g_L.en_target, g_L.xn);
+    }
+  }
+  __syncthreads();
+  if (!uni(g_L.ext_nn)) return true;
+  // connect (birrt_star.cpp:1256-1275): tree_B's nearest node of x_new
+  const ScoutConnect& K = R.cn;
+  const int nB = uni(g_L.S.n[B]);
+  bool rec = uni(K.ok && K.t == B && K.X <= nB && same8(K.q, g_L.xn.q)) != 0;
+  int cid;
+  if (rec) {
+    cid = K.d < 10000.0 ? K.id : 0;
+    if (uni(K.X < nB)) {
+      double dp;
+      const int ip = uni(nB - K.X <= PATCH_K) ? patch_scan(B, g_L.xn.q, K.X, nB, &dp)
+                                               : nearest_scan(C, B, g_L.xn.q, K.X, &dp);
+      if (uni(dp < K.d)) { cid = ip; rec = false; }
+    }
+    if (threadIdx.x == 0) { g_L.S.nn_nodes += nB; g_L.S.sc_nn++; }
+  } else {
+    cid = nearest(C, B, g_L.xn.q);
+  }
+  TR();
+  if (!rec || !uni(R.pre.ok)) {
+    PRE_COUNT(3);
+    if (threadIdx.x == 0) load_node(C, B, cid, &g_L.xc);
+    __syncthreads();
+    connect_graphs(C, B);  // takes the record's direct-edge result if it is the same edge
+    return true;
+  }
+  // the record's connect outcome: count the direct edge, insert its via chain and the last node
+  if (threadIdx.x == 0) {
+    QState& S = g_L.S;
+    const ScoutPre& P = R.pre;
+    const int off = S.n[B] - K.X;
+    g_L.tree_expand = 0;
+    g_L.best_nv = 10000.0;
+    for (int k = 0; k < 3; ++k) g_L.csp[k] = S.cbest[k];
+    if (P.need) {
+      g_L.count_slot = P_XCONNECT + 4;
+      count_edge(K.e.first);
+      S.sc_edge_hit++;
+      if (P.flag == 1) {
+        for (int k = 0; k < 3; ++k) g_L.csp[k] = P.sol[k];
+      } else if (P.flag == 2) {
+        g_L.tree_expand = 1;
+        g_L.best_nv = P.sol[0];
+      }
+    }
+    g_L.n_via = P.nv;
+    g_L.sel = P.sel;
+    if (g_L.sel.id >= K.X) g_L.sel.id += off;
+    if (g_L.sel.parent >= K.X) g_L.sel.parent += off;
+    for (int j = 0; j < NJ; ++j) { g_L.sel_start[j] = P.sel_start[j]; g_L.sel_target[j] = P.sel_target[j]; }
+  }
+  __syncthreads();
+  const int par = (int)(g_L.S.iter & (SCOUT_SLOTS - 1));
+  const ScoutBoard* sb = C.Q.scbs[uni(g_L.asked[par]) - 1];
+  insert_via(C, B, sb->pre_via[par], K.X);
+  connect_tail(C, B);
+  TR();
+  return true;
+}
+
 // One C-space iteration of run_planner (birrt_star.cpp:1163-1338).  Always inlined into plan_kernel: builds in
 // which the inliner outlined it (a larger scout) fault the GPU with a memory-aperture violation in the first
 // iterations (tools/experiments/README.md), builds that inline it run clean.
@@ -2476,13 +2667,18 @@ __device__ __forceinline__ void iteration(const Ctx& C) {
   if (threadIdx.x == 0) g_L.conn_rec = 0;
   TR();
 #define PHASE(k) if (threadIdx.x == 0) { _t1 = pclk(); g_L.S.prof[k] += _t1 - _t0; _t0 = _t1; }
+  if (C.Q.nscouts > 0) scout_prepare(C);
   sample_publish(C);
-  TR();
   if (C.Q.nscouts > 0) scout_request(C, B);
+  __syncthreads();
   TR();
   sample_read(C);
   TR();
   PHASE(P_SAMPLE);
+  const bool opt = uni(g_L.S.tree_opt && g_L.S.have_sol);
+  if (C.Q.nscouts > 0 && !uni(g_L.S.have_sol) && pre_commit(C, A, B)) {
+    PHASE(P_CONNECT);
+  } else {
   int nid = nearest(C, A, g_L.xr, true);
   TR();
   PHASE(P_NN);
@@ -2517,7 +2713,6 @@ __device__ __forceinline__ void iteration(const Ctx& C) {
   }
   __syncthreads();
   TR();
-  const bool opt = uni(g_L.S.tree_opt && g_L.S.have_sol);
   if (!uni(g_L.flag)) edge_costs(C, 1);
   edge_validity(C, 1, false, P_XEXPAND, opt ? OV_NEAR_EXPAND : OV_NONE, A, SC_EXPAND);
   TR();
@@ -2593,6 +2788,7 @@ __device__ __forceinline__ void iteration(const Ctx& C) {
   }
   else if (opt) {
     scout_request_ahead2(C, A);
+  }
   }
 #undef PHASE
   if (threadIdx.x == 0) {
@@ -2728,6 +2924,69 @@ __device__ void sc_end(const Ctx& C, int par, unsigned tag, int opt) {
   }
 }
 
+// Scout, before the first solution, once connect's direct edge is checked (g_L.xc = x_new's nearest node in tree tb,
+// g_L.xn = x_new, batch edge 0 = xc -> x_new with its costs and first collision): connectGraphs' outcome without a
+// solution (birrt_star.cpp:2608-2812; no near loop then) -> R.pre: the stepping flag and the via chain towards x_new
+// (connect) or the last valid point (extend), whose nodes go to the board's pre_via[par].  A chain longer than
+// PRE_VIA is not recorded (pre.ok = 0; the leader steps it itself).
+__device__ void scout_pre_connect(const Ctx& C, int par, int tb) {
+  ScoutRec& R = g_L.sr;
+  QState& S = g_L.S;
+  if (threadIdx.x == 0) {
+    ScoutPre& P = R.pre;
+    for (int k = 0; k < 3; ++k) P.sol[k] = g_L.eg_cost[0][k] + g_L.xn.c[k];
+    P.need = P.sol[0] < S.cbest[0];
+    int flag = 0;
+    if (P.need) {
+      const int f = g_L.eg_first[0];
+      if (f > S.n_pts) {
+        flag = 1;
+      } else {
+        const int lv = f == 0 ? 0 : f - 1;
+        if (lv != 0) {
+          for (int j = 0; j < NJ; ++j) g_L.ext[j] = g_L.eg_start[0][j] + lv * g_L.eg_step[0][j];
+          flag = 2;
+        }
+      }
+    }
+    P.flag = flag;
+    P.nv = 0;
+    P.ok = 1;
+    P.sel.id = -1;
+    P.sel.parent = -1;
+    g_L.flag = flag;
+    g_L.n_via = 0;
+    g_L.nn_t = S.n[tb];
+    g_L.cur = g_L.xc;
+  }
+  __syncthreads();
+  const int flag = uni(g_L.flag);
+  if (!flag) return;
+  const int vcap = S.via_cap, st0 = S.status, ph0 = S.phase;
+  __syncthreads();
+  if (threadIdx.x == 0) S.via_cap = PRE_VIA;  // a longer chain stops with status -7 (restored below)
+  __syncthreads();
+  via_chain(C, flag == 1 ? g_L.xn.q : g_L.ext);
+  if (threadIdx.x == 0) {
+    ScoutPre& P = R.pre;
+    P.ok = S.status == st0;
+    S.status = st0;
+    S.phase = ph0;
+    S.via_cap = vcap;
+    P.nv = g_L.n_via;
+    P.sel = g_L.sel;
+    for (int j = 0; j < NJ; ++j) { P.sel_start[j] = g_L.sel_start[j]; P.sel_target[j] = g_L.sel_target[j]; }
+    g_L.n_via = 0;
+  }
+  // the chain's nodes (plain stores of thread 0 into the scout's via scratch) -> the record slot, agent scope
+  drain();
+  __syncthreads();
+  const int nw = uni(R.pre.ok ? R.pre.nv : 0) * (int)(sizeof(ViaNode) / 8);
+  const unsigned long long* src = reinterpret_cast<const unsigned long long*>(C.Q.via);
+  unsigned long long* dst = reinterpret_cast<unsigned long long*>(&C.Q.scb->pre_via[par][0]);
+  for (int w = threadIdx.x; w < nw; w += BLOCK) st_agent(&dst[w], ld_agent(&src[w]));
+}
+
 // The scout's pass for iteration `it` of the leader, which expands tree t from a snapshot of its first X nodes:
 // the leader's steps up to its rewire collision job (iteration / choose_parent / rewire, same functions on the
 // scout's own LDS, job board, helpers and via-node scratch), recording the results the leader keys on; nothing is
@@ -2750,6 +3009,7 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
     S.n[t] = X;
     S.n[1 - t] = XB;
     R.cn.ok = 0;
+    R.pre.ok = 0;
     R.nn.ok = 0; R.ex.ok = 0; R.nr.ok = 0; R.n_choose = 0; R.n_rewire = 0; R.cc.ok = 0;
   }
   sc_publish(C, par, tag, SC_STARTED);
@@ -2781,6 +3041,8 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
   if (!uni(g_L.flag)) {
     sc_copy_out(sb, par, &R.nn, sizeof(ScoutNN));
     sc_copy_out(sb, par, &R.nr, sizeof(ScoutNear));
+    sc_copy_out(sb, par, &R.cn, sizeof(ScoutConnect));
+    sc_copy_out(sb, par, &R.pre, sizeof(ScoutPre));
     sc_copy_out(sb, par, &R.n_choose, 4 * sizeof(int));
     sc_end(C, par, tag, opt);
     return;
@@ -2794,6 +3056,7 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
     const double d = sqrt(s);
     for (int j = 0; j < NJ; ++j) R.nn.q[j] = g_L.xr[j];
     R.nn.d = d < 10000.0 ? d : 10000.0;
+    for (int k = 0; k < 3; ++k) R.nn.c[k] = g_L.nn.c[k];
     R.nn.id = nid; R.nn.X = X; R.nn.t = t; R.nn.ok = 1;
     for (int j = 0; j < NJ; ++j) g_L.ext[j] = g_L.xr[j];
     step_towards((&g_rb), g_L.nn.q, g_L.ext, S.step);
@@ -2860,13 +3123,16 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
     edge_validity(C, 1, false, P_XCONNECT);
     if (threadIdx.x == 0) {
       for (int j = 0; j < NJ; ++j) { R.cn.e.s[j] = g_L.eg_start[0][j]; R.cn.e.g[j] = g_L.eg_target[0][j]; }
+      for (int k = 0; k < 3; ++k) { R.cn.e.acc[k] = g_L.eg_acc[0][k]; R.cn.c[k] = g_L.xc.c[k]; }
       R.cn.e.first = g_L.eg_first[0];
       R.cn.ok = 1;
     }
     __syncthreads();
-    sc_copy_out(sb, par, &R.cn, sizeof(ScoutConnect));
+    scout_pre_connect(C, par, tb);
   }
   if (!opt || sc_stale(C, tag)) {
+    sc_copy_out(sb, par, &R.cn, sizeof(ScoutConnect));
+    sc_copy_out(sb, par, &R.pre, sizeof(ScoutPre));
     sc_copy_out(sb, par, &R.nr, sizeof(ScoutNear));
     sc_copy_out(sb, par, &R.n_choose, 4 * sizeof(int));
     sc_publish(C, par, tag, SC_DONE);
@@ -3137,6 +3403,13 @@ __global__ void __launch_bounds__(BLOCK) plan_kernel(const RobotDev* __restrict_
     g_L.tit = -1;
     g_L.tn = g_tlog_n[0];
 #endif
+  }
+  __syncthreads();
+  // the last PATCH_K nodes of each tree -> the LDS copy kept by insert_node / insert_via
+  for (int it = threadIdx.x; it < 2 * PATCH_K * NJ; it += BLOCK) {
+    const int t = it / (PATCH_K * NJ), r = it - t * (PATCH_K * NJ), k = r / NJ, j = r - k * NJ;
+    const int i = g_L.S.n[t] - PATCH_K + k;
+    if (i >= 0) g_L.pc_q[t][i & (PATCH_K - 1)][j] = C.Q.tr[t].q[(size_t)j * g_L.S.cap + i];
   }
   __syncthreads();
   if (uni(g_L.S.status == 0 && g_L.S.phase == 0)) {

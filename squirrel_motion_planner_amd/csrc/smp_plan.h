@@ -130,6 +130,7 @@ enum { SC_STARTED = 0, SC_NN = 1, SC_EXPAND = 2, SC_NEAR = 3, SC_CHOOSE = 4, SC_
 struct ScoutNN {               // stage SC_NN: nearest node of the sample in the snapshot
   double q[NJ];                // the sample scanned
   double d;                    // its distance (the running minimum of the reference scan, 10000 if none)
+  double c[3];                 // that node's cost (a node's cost never changes before the first solution)
   int id, X, t, ok;            // node id, snapshot size, tree, 1 = valid
 };
 struct ScoutNear {             // stage SC_NEAR: near set of x_new in the snapshot
@@ -152,8 +153,22 @@ struct ScoutExpand {           // stage SC_EXPAND: the expand edge's interpolati
 struct ScoutConnect {          // stage SC_DONE, before the first solution: connect's nearest node and direct edge
   double q[NJ];                // x_new (the expand edge's end)
   double d;                    // its nearest node's distance over the other tree's first X nodes (10000 if none)
+  double c[3];                 // that node's cost
   int id, X, t, ok;            // that node, the snapshot size, the tree, 1 = valid
-  ScoutEdge e;                 // the direct edge nearest -> x_new and its first colliding point
+  ScoutEdge e;                 // the direct edge nearest -> x_new (segment-norm sums, first colliding point)
+};
+// Stage SC_DONE, before the first solution, with cn.ok: connect's outcome on the snapshot (connectGraphs before a
+// solution has no near loop, so it is a function of x_new, its nearest node and the direct edge): the stepping flag
+// and the via chain (nodes in ScoutBoard::pre_via of the record's slot, ids from the snapshot size XB upward, which
+// the leader rebases onto its tree size).  The leader commits it when its own nearest node is the record's.
+constexpr int PRE_VIA = 16;
+struct ScoutPre {
+  int ok;                      // 1: recorded (0: chain longer than PRE_VIA, the leader steps it itself)
+  int flag;                    // 0 nothing, 1 connect (stepped to x_new), 2 extend (stepped to the last valid point)
+  int nv, need;                // via nodes; the direct edge was checked (its cost is below c_best)
+  double sol[3];               // direct edge cost + x_new's cost
+  NodeRef sel;                 // the last stepped edge's node (id / parent relative to XB as above)
+  double sel_start[NJ], sel_target[NJ];
 };
 // Stage SC_CONN (two scouts, after the first solution): connect's scans of the iteration, computed once the leader
 // reports that the tree connect searches (tree_B of the iteration = tree_A of the one before) is final (its rewire
@@ -174,6 +189,7 @@ struct ScoutRec {
   ScoutNN nn;
   ScoutExpand ex;
   ScoutConnect cn;
+  ScoutPre pre;
   ScoutNear nr;
   ScoutConn cc;
   int n_choose, n_rewire, pad[2];
@@ -182,8 +198,8 @@ struct ScoutRec {
 // Record slots of a scout board, by iteration mod SCOUT_SLOTS: a scout may be asked for iteration k + MAX_SCOUTS
 // while the leader still reads its record of k (before the first solution the scouts take the iterations in turn,
 // up to MAX_SCOUTS ahead).
-constexpr int MAX_SCOUTS = 4;
-constexpr int SCOUT_SLOTS = 8;
+constexpr int MAX_SCOUTS = 8;
+constexpr int SCOUT_SLOTS = 16;
 static_assert(SCOUT_SLOTS > MAX_SCOUTS && (SCOUT_SLOTS & (SCOUT_SLOTS - 1)) == 0, "record slots");
 struct ScoutBoard {
   // leader -> scout: the request for iteration k carries tag k + 1; req[0] low word = X | t << 28 | opt << 29,
@@ -199,6 +215,7 @@ struct ScoutBoard {
   int pad1[14];
   unsigned long long prof[32]; // the scout's phase clocks of the launch (written when it leaves)
   ScoutRec rec[SCOUT_SLOTS];
+  ViaNode pre_via[SCOUT_SLOTS][PRE_VIA];  // ScoutPre's via chains, by record slot
 };
 
 struct QueryDev {

@@ -218,7 +218,7 @@ def test_planner_parity_helper_counts(orobot, robot, helpers):
     assert_same_run(gp2, r, o)
 
 
-@pytest.mark.parametrize("scouts", [2, 3, 4])
+@pytest.mark.parametrize("scouts", [2, 3, 4, 6, 8])
 def test_planner_parity_scout_counts(orobot, robot, scouts):
     """Two, three and four scouts taking the iterations in turn before the first solution (records up to
     four iterations ahead, patched by the leader), across the first solution and 2000 iterations after it."""

@@ -22,7 +22,7 @@ lib = L.lib()
 lib.smp_debug_tlog.restype = ctypes.c_int
 lib.smp_debug_tlog.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int, ctypes.c_int]
 sc = scenes.box_room()
-gp = GpuPlanner(path_optimality_threshold=-math.inf)
+gp = GpuPlanner(path_optimality_threshold=-math.inf, scout=int(os.environ.get("SMP_SCOUTS", "1")))
 gp.set_scene(Scene.from_keys(sc.keys, sc.res))
 buf = (ctypes.c_uint64 * (1 << 18))()
 lib.smp_debug_tlog(buf, 1 << 18, 1)  # reset
