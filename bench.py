@@ -38,6 +38,8 @@ def parse():
     ap.add_argument("--helpers", type=int, default=0,
                     help="helper workgroups per query (0 automatic, -1 none: e.g. for counter passes, which "
                          "serialise dispatches)")
+    ap.add_argument("--scout", type=int, default=1,
+                    help="scout workgroups per query (1 automatic, 0 none, 2..8 that many)")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--workload", choices=("c2", "c3", "c5"), default="c2",
                     help="c2 (default, BASELINE configs[1]): the single C2 query; c3: random (start, goal) pairs on "
@@ -112,7 +114,7 @@ def main():
     s0 = Scene.from_keys(sc.keys, sc.res) if rank == 0 else None
     scene = D.broadcast_scene(s0, device="cuda") if world > 1 else s0
 
-    gp = GpuPlanner(device=local, path_optimality_threshold=-math.inf, helpers=a.helpers)
+    gp = GpuPlanner(device=local, path_optimality_threshold=-math.inf, helpers=a.helpers, scout=a.scout)
     gp.set_scene(scene)
 
     # (start, goal) of every query of the job: C2 repeats its own pair; C3/C5 draw world * queries_per_gpu

@@ -607,6 +607,8 @@ static QueryDev make_qdev(QueryBuffers& b, size_t cap, long long rows) {
   d.jb = nullptr;
   d.sampler_jb = nullptr;
   d.nscouts = 0;
+  d.pre_delay = 0;
+  d.pre_commit = 0;
   for (int s = 0; s < MAX_SCOUTS; ++s) {
     d.scbs[s] = nullptr; d.sjbs[s] = nullptr; d.svias[s] = nullptr; d.sworkers_s[s] = 1;
   }
@@ -724,11 +726,19 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
     for (int s = 2; s < ns; ++s) { h_s[s] = std::min(3, rest); rest -= h_s[s]; }
     if (ns >= 2) { h_s[0] = rest - rest / 2; h_s[1] = rest / 2; } else { h_s[0] = rest; }
   }
+  // before the first solution a scout starts record k when the leader reaches k - pre_delay (DESIGN.md "Pre-solution
+  // commits"); SMP_PRE_DELAY overrides it for experiments (0: at the request)
+  int pre_delay = 2;
+  if (const char* e = std::getenv("SMP_PRE_DELAY")) pre_delay = std::atoi(e);
+  int pre_commit = 1;  // SMP_PRE_COMMIT=0: every iteration runs the full path (experiments)
+  if (const char* e = std::getenv("SMP_PRE_COMMIT")) pre_commit = std::atoi(e);
   for (int i = 0; i < nq; ++i) {
     qdev[i].jb = nh > 0 ? p->qb[i].jb.p : nullptr;
     qdev[i].sampler = nh >= 2;              // with two or more helpers, the last one runs ahead sampling
     qdev[i].nworkers = ns > 0 ? 1 + h_lead : (nh >= 2 ? nh : 1 + nh);
     qdev[i].nscouts = ns;
+    qdev[i].pre_delay = pre_delay;
+    qdev[i].pre_commit = pre_commit;
     qdev[i].sampler_jb = p->qb[i].jb.p;
     for (int s = 0; s < ns; ++s) {
       qdev[i].sjbs[s] = p->qb[i].sjb[s].p;

@@ -189,6 +189,7 @@ struct PlanLds {
   int count_slot;  // profiling: phase the checked configurations are attributed to
   int job_seq;     // last job published by this leader (this launch)
   int smp_ver, smp_have_sol, smp_hit;  // run-ahead sampler: published parameter version / snapshot, slot hit
+  int smp_pub;                         // the version changed this iteration: publish the parameters
   int spec, spec_nn;                   // overlap_work: what was computed during the last collision job, its result
   long long spec_cnt;                  // ... and the nodes it scanned (counted only if the result is used)
   double smp_cbest[3];
@@ -219,6 +220,8 @@ struct PlanLds {
   // still worth asking; eg_hit[e] = first colliding point of batch edge e taken from the record, -2 = none.
   // Scout: the record it builds.
   ScoutRec sr;
+  PreRec prer;                  // pre-solution record: the leader's copy (pre_read) / the scout's, being written
+  int prer_ok;                  // leader: prer holds this iteration's complete record
 #ifdef SMP_TRACE
   int trole;                    // SMP_TRACE builds: 0 leader, 1 / 2 scout (trace records of this workgroup)
   unsigned tn;                  // records of this role so far
@@ -228,13 +231,13 @@ struct PlanLds {
   int sc_same[MAX_SCOUTS];      // leader: scout s runs on this XCD (1), another (0), not yet known (-1)
   int asked[SCOUT_SLOTS];       // leader: scout s + 1 asked for iteration k in slot k % SCOUT_SLOTS, 0 = none
   int asked_conn[SCOUT_SLOTS];  // leader: that record will carry connect's scans (stage SC_CONN)
+  int asked_pre[SCOUT_SLOTS];   // leader: asked before the first solution (a pre-solution record)
   int conn_rec;                 // leader: connect of this iteration takes its scans from the record (g_L.sr.cc)
   int two_scouts;               // scout: two scouts share the iterations (post-solution records get SC_CONN)
   int eg_hit[MAXE];
   int eg_rec[MAXE];             // leader: record edge (index into sr.e) equal to batch edge e, -1 = none
   int rec_grp;                  // leader: the record stage eg_rec was matched against (-1 = not matched)
   int rec_all, ev_job;          // rec_match: every edge matched; edge_validity: a job is needed
-  int req_need;                 // scout_request: some coming iteration is not asked for yet
   // leader: configurations of the last PATCH_K nodes appended to each tree, by node index mod PATCH_K (kept by
   // insert_node / insert_via, loaded at launch start); before the first solution no node changes after its insert,
   // so pre_commit's patch scans over the nodes appended since a record's snapshot read these
@@ -1253,6 +1256,9 @@ __device__ __forceinline__ void edge_validity_job(const Ctx& C, int E, int pslot
   __syncthreads();
 }
 
+#ifndef SMP_HELPER_SLEEP
+#define SMP_HELPER_SLEEP 2  // s_sleep units (64 clocks) between an idle helper's polls of its job board
+#endif
 // Helper workgroup w (1 .. W-1): wave 0 polls the first 64 payload granules of its query's board; a new job is
 // taken once every granule it needs carries the header's job number (jobs of one or two edges arrive within the
 // poll itself; longer payloads take one more read).  Then tiles w - 1, w - 1 + W, ... of the job, each result
@@ -1288,7 +1294,7 @@ __device__ __forceinline__ void helper_main(const Ctx& C, int hidx, JobLds& J) {
     const int go = uni(J.go[k]);
     if (go == -1) break;
     if (go == 0) {
-      __builtin_amdgcn_s_sleep(2);
+      __builtin_amdgcn_s_sleep(SMP_HELPER_SLEEP);
       continue;
     }
     const int seq = uni(J.seq);
@@ -1417,26 +1423,50 @@ __device__ bool spec_stage(const Ctx& C, int s, unsigned long long wait) {
   return true;
 }
 
-// Copies the sections of record stages (have, st] of record slot par into g_L.sr; all threads.
+// Copies the sections of record stages (have, st] of record slot par into g_L.sr; all threads.  The sections are
+// concatenated into one list of 8-byte words, each thread taking words tid, tid + BLOCK, ... with every load of a
+// thread issued before its LDS stores: one memory round trip for the whole copy (a loop per section would queue
+// one round trip per section behind the other).
 __device__ void spec_copy(const ScoutBoard* sb, int par, int have, int st) {
   ScoutRec& R = g_L.sr;
-  if (have < SC_NN && st >= SC_NN) sc_copy_in(sb, par, &R.nn, sizeof(ScoutNN));
-  if (have < SC_EXPAND && st >= SC_EXPAND) {
-    sc_copy_in(sb, par, &R.e[0], sizeof(ScoutEdge));
-    sc_copy_in(sb, par, &R.ex, sizeof(ScoutExpand));
-  }
   // choose-parent / rewire candidates only in iterations that have those steps (tree optimisation, a solution)
   const bool opt_now = uni(g_L.S.tree_opt && g_L.S.have_sol) != 0;
-  if (have < SC_NEAR && st >= SC_NEAR) sc_copy_in(sb, par, &R.nr, sizeof(ScoutNear));
-  if ((have < SC_CHOOSE && st >= SC_CHOOSE) || (have < SC_DONE && st >= SC_DONE))
-    sc_copy_in(sb, par, &R.n_choose, 4 * sizeof(int));
-  if (opt_now && have < SC_CHOOSE && st >= SC_CHOOSE) sc_copy_in(sb, par, &R.e[SCOUT_CHOOSE0], MAX_NEAR * sizeof(ScoutEdge));
-  if (opt_now && have < SC_DONE && st >= SC_DONE) sc_copy_in(sb, par, &R.e[SCOUT_REWIRE0], MAX_NEAR * sizeof(ScoutEdge));
-  if (!opt_now && have < SC_DONE && st >= SC_DONE) {
-    sc_copy_in(sb, par, &R.cn, sizeof(ScoutConnect));
-    sc_copy_in(sb, par, &R.pre, sizeof(ScoutPre));
+  int off[8], nw[8], ns = 0;
+  auto add = [&](const void* p, int nbytes) {
+    off[ns] = (int)((const char*)p - (const char*)&R) / 8;
+    nw[ns] = nbytes / 8;
+    ++ns;
+  };
+  if (have < SC_NN && st >= SC_NN) add(&R.nn, sizeof(ScoutNN));
+  if (have < SC_EXPAND && st >= SC_EXPAND) { add(&R.e[0], sizeof(ScoutEdge)); add(&R.ex, sizeof(ScoutExpand)); }
+  if (have < SC_NEAR && st >= SC_NEAR) add(&R.nr, sizeof(ScoutNear));
+  if ((have < SC_CHOOSE && st >= SC_CHOOSE) || (have < SC_DONE && st >= SC_DONE)) add(&R.n_choose, 4 * sizeof(int));
+  if (opt_now && have < SC_CHOOSE && st >= SC_CHOOSE) add(&R.e[SCOUT_CHOOSE0], MAX_NEAR * sizeof(ScoutEdge));
+  if (opt_now && have < SC_DONE && st >= SC_DONE) add(&R.e[SCOUT_REWIRE0], MAX_NEAR * sizeof(ScoutEdge));
+  if (!opt_now && have < SC_DONE && st >= SC_DONE) { add(&R.cn, sizeof(ScoutConnect)); add(&R.pre, sizeof(ScoutPre)); }
+  if (have < SC_CONN && st >= SC_CONN) add(&R.cc, sizeof(ScoutConn));
+  int total = 0;
+  for (int i = 0; i < ns; ++i) total += nw[i];
+  const unsigned long long* src = reinterpret_cast<const unsigned long long*>(&sb->rec[par]);
+  unsigned long long* dst = reinterpret_cast<unsigned long long*>(&R);
+  constexpr int U = 4;  // words per thread per round (a round holds 4 * BLOCK words: every section set fits)
+  static_assert(sizeof(ScoutRec) / 8 <= U * BLOCK, "one round per record copy");
+  int idx[U];
+  unsigned long long v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int w = (int)threadIdx.x + u * BLOCK;
+    idx[u] = -1;
+    if (w < total) {
+      int rem = w, i = 0;
+      while (rem >= nw[i]) { rem -= nw[i]; ++i; }
+      idx[u] = off[i] + rem;
+      v[u] = ld_agent(&src[idx[u]]);
+    }
   }
-  if (have < SC_CONN && st >= SC_CONN) sc_copy_in(sb, par, &R.cc, sizeof(ScoutConn));
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (idx[u] >= 0) dst[idx[u]] = v[u];
   __syncthreads();
   if (threadIdx.x == 0) g_L.sp_stage = st;
   __syncthreads();
@@ -1475,6 +1505,7 @@ __device__ void scout_ask(const Ctx& C, long long k, int tree, bool pre, bool& f
   st_agent(&sb->req[0], granule(tag, w0));
   g_L.asked[k & (SCOUT_SLOTS - 1)] = which;
   g_L.asked_conn[k & (SCOUT_SLOTS - 1)] = !pre && ns >= 2;
+  g_L.asked_pre[k & (SCOUT_SLOTS - 1)] = pre;
 }
 
 // Leader, start of iteration j, before any store of the iteration: the requests for the coming iterations not yet
@@ -1483,41 +1514,43 @@ __device__ void scout_ask(const Ctx& C, long long k, int tree, bool pre, bool& f
 // scout_request_ahead2), and before this iteration's own stores, so the drain finds the last iteration's long done.
 // Iteration j - 1's record slot is free again, j's record is looked up only if it was asked for, and every scout
 // gets the leader's iteration (its staleness test).
-// scout_prepare: the drain (all threads); scout_request (thread 0, after sample_publish, whose new parameter version
-// the requests carry): the asks; the caller's next barrier publishes the LDS bookkeeping.
-__device__ void scout_prepare(const Ctx& C) {
-  if (threadIdx.x == 0) {
-    const QState& S = g_L.S;
-    const long long j = S.iter;
-    const bool pre = !(S.tree_opt && S.have_sol);
-    int need = 0;
-    for (int ahead = 1; ahead <= (pre ? C.Q.nscouts : 1); ++ahead) need |= !g_L.asked[(j + ahead) & (SCOUT_SLOTS - 1)];
-    g_L.req_need = need;
-  }
-  __syncthreads();
-  if (uni(g_L.req_need)) {
-    drain();
-    __syncthreads();
-  }
+// scout_slots (thread 0, LDS only, before the iteration's first memory round): iteration j - 1's slot is free
+// again, and j's record is looked up only if it was asked for.  scout_asks (thread 0, after that round, whose drain
+// covers the last iteration's stores): the leader's iteration for every scout, before the first solution the tree
+// sizes for the scouts' late snapshots, and the requests for the coming iterations not yet asked for (their snapshots
+// include the nodes the last iteration appended).
+__device__ void scout_slots() {
+  const QState& S = g_L.S;
+  const long long j = S.iter;
+  g_L.asked[(j - 1) & (SCOUT_SLOTS - 1)] = 0;
+  g_L.asked_conn[(j - 1) & (SCOUT_SLOTS - 1)] = 0;
+  // a record asked for before the first solution (found in iteration f) is exact only while the tree it expands has
+  // not been rewired since its snapshot: f + 1 rewires tree_B(f), which f + 3 expands, and f + 2 rewires tree_A(f)
+  // after its own expand, so records of f + 1 and f + 2 hold and later ones are not looked up
+  g_L.sp_on = g_L.asked[j & (SCOUT_SLOTS - 1)] != 0 &&
+              !(g_L.asked_pre[j & (SCOUT_SLOTS - 1)] && S.have_sol && j >= S.first_iter + 3);
+  g_L.sp_stage = -1;
 }
-__device__ void scout_request(const Ctx& C, int t) {
-  if (threadIdx.x == 0) {
-    const QState& S = g_L.S;
-    const long long j = S.iter;
-    const bool pre = !(S.tree_opt && S.have_sol);
-    g_L.asked[(j - 1) & (SCOUT_SLOTS - 1)] = 0;
-    g_L.asked_conn[(j - 1) & (SCOUT_SLOTS - 1)] = 0;
-    g_L.sp_on = g_L.asked[j & (SCOUT_SLOTS - 1)] != 0;
-    g_L.sp_stage = -1;
-    for (int s = 0; s < C.Q.nscouts; ++s) st_agent(&C.Q.scbs[s]->cur, (unsigned long long)j);
-    bool fenced = false;
-    // before the first solution every scout has a request out (the trees only grow: records stay exact up to the
-    // appended nodes); iteration j + a expands tree t for odd a, the other one for even a
-    for (int ahead = 1; ahead <= (pre ? C.Q.nscouts : 1); ++ahead) {
-      const long long k = j + ahead;
-      if (g_L.asked[k & (SCOUT_SLOTS - 1)]) continue;
-      scout_ask(C, k, (ahead & 1) ? t : 1 - t, pre, fenced);
-    }
+__device__ void scout_asks(const Ctx& C, int t) {
+  const QState& S = g_L.S;
+  const long long j = S.iter;
+  const bool pre = !(S.tree_opt && S.have_sol);
+  const bool sz = pre && S.n[0] < (1 << 20) && S.n[1] < (1 << 20);
+  const unsigned long long csz = ((unsigned long long)(j & 0xffffff) << 40) | ((unsigned long long)S.n[0] << 20) |
+                                 (unsigned long long)S.n[1];
+  for (int s = 0; s < C.Q.nscouts; ++s) {
+    st_agent(&C.Q.scbs[s]->cur, (unsigned long long)j);
+    // only to a scout on this XCD: the sizes hand over nodes stored without an agent release (a scout on another XCD
+    // takes its request's sizes, whose nodes scout_ask released)
+    if (sz && g_L.sc_same[s] == 1) st_agent(&C.Q.scbs[s]->cur_sz, csz);
+  }
+  bool fenced = false;
+  // before the first solution every scout has a request out (the trees only grow: records stay exact up to the
+  // appended nodes); iteration j + a expands tree t for odd a, the other one for even a
+  for (int ahead = 1; ahead <= (pre ? C.Q.nscouts : 1); ++ahead) {
+    const long long k = j + ahead;
+    if (g_L.asked[k & (SCOUT_SLOTS - 1)]) continue;
+    scout_ask(C, k, (ahead & 1) ? t : 1 - t, pre, fenced);
   }
 }
 
@@ -2030,34 +2063,50 @@ __device__ __forceinline__ int sample_conf(const QState& S, uint32_t it, SmpLds&
   return sample_uniform(S, it, W, out);
 }
 
-// Leader: the sample of this iteration -> g_L.xr.  With a run-ahead sampler, first publish the iteration and,
-// when they changed, the informed-sampling parameters (versioned); then take the ring slot if its tag is this
-// iteration at the current version, else draw the sample here.
-// Leader, first part of its sample step: publishes its iteration and (on a change) the informed-sampling
-// parameters for the run-ahead sampler.
-__device__ void sample_publish(const Ctx& C) {
+// Leader, start of an iteration, thread 0, LDS only: a new informed-sampling parameter version when have_sol or
+// c_best changed (the ring is then read at the new version); sample_publish (thread 0, after the iteration's first
+// memory round) stores its iteration and, on a change, the parameters for the run-ahead sampler.
+__device__ void sample_version(const Ctx& C) {
   QState& S = g_L.S;
-  if (C.Q.sampler && threadIdx.x == 0) {
-    JobBoard* jb = C.Q.jb;
-    const bool changed = g_L.smp_ver == 0 || g_L.smp_have_sol != S.have_sol || g_L.smp_cbest[0] != S.cbest[0] ||
-                         g_L.smp_cbest[1] != S.cbest[1] || g_L.smp_cbest[2] != S.cbest[2];
-    if (changed) {
-      g_L.smp_have_sol = S.have_sol;
-      st_agent(&jb->s_have_sol, S.have_sol);
-      for (int k = 0; k < 3; ++k) {
-        g_L.smp_cbest[k] = S.cbest[k];
-        st_agent(&jb->s_cbest[k], (unsigned long long)__double_as_longlong(S.cbest[k]));
-      }
-      drain();
-      st_agent(&jb->s_ver, ++g_L.smp_ver);
-    }
-    st_agent(reinterpret_cast<unsigned long long*>(&jb->s_iter), (unsigned long long)S.iter);
+  g_L.smp_pub = 0;
+  if (!C.Q.sampler) return;
+  const bool changed = g_L.smp_ver == 0 || g_L.smp_have_sol != S.have_sol || g_L.smp_cbest[0] != S.cbest[0] ||
+                       g_L.smp_cbest[1] != S.cbest[1] || g_L.smp_cbest[2] != S.cbest[2];
+  if (changed) {
+    g_L.smp_have_sol = S.have_sol;
+    for (int k = 0; k < 3; ++k) g_L.smp_cbest[k] = S.cbest[k];
+    ++g_L.smp_ver;
+    g_L.smp_pub = 1;
   }
+}
+__device__ void sample_publish(const Ctx& C) {
+  if (!C.Q.sampler) return;
+  const QState& S = g_L.S;
+  JobBoard* jb = C.Q.jb;
+  if (g_L.smp_pub) {
+    st_agent(&jb->s_have_sol, g_L.smp_have_sol);
+    for (int k = 0; k < 3; ++k) st_agent(&jb->s_cbest[k], (unsigned long long)__double_as_longlong(g_L.smp_cbest[k]));
+    drain();  // payload before the version
+    st_agent(&jb->s_ver, g_L.smp_ver);
+  }
+  st_agent(reinterpret_cast<unsigned long long*>(&jb->s_iter), (unsigned long long)S.iter);
 }
 
 // Second part: the sample from the ring (one round of tagged granules, wave 0) -- and, in the same round (wave 1),
 // a look at the stage of this iteration's scout record, whose sections are then copied ahead of the steps that
 // use them -- else drawn here.
+// Leader, one round of the pre-solution record's granules (threads 64 .. 64 + PRE_GRANULES - 1, waves 1-3): each
+// thread's 32-bit half goes to g_L.prer; returns, in every thread, whether its own granule carried this iteration's
+// tag (the caller combines them at its barrier).  No ordering is needed: each granule says itself whether it is
+// current.
+__device__ __forceinline__ bool pre_read_round(const ScoutBoard* sb, int par, unsigned tag) {
+  const int g = (int)threadIdx.x - 64;
+  if (g < 0 || g >= PRE_GRANULES) return true;
+  const unsigned long long v = ld_agent(&sb->pre_g[par][g]);
+  reinterpret_cast<unsigned*>(&g_L.prer)[g] = (unsigned)v;
+  return (unsigned)(v >> 32) == tag;
+}
+
 __device__ void sample_read(const Ctx& C) {
   TR();
   QState& S = g_L.S;
@@ -2066,9 +2115,14 @@ __device__ void sample_read(const Ctx& C) {
   const int sw = uni(g_L.asked[S.iter & (SCOUT_SLOTS - 1)]);
   const ScoutBoard* sb = sw > 0 ? C.Q.scbs[sw - 1] : nullptr;
   const int par = (int)(S.iter & (SCOUT_SLOTS - 1));
+  // before the first solution the record is the data-tagged PreRec (read whole in this round); after it, a look at
+  // the stage of the staged record, whose sections are then copied ahead of the steps that use them
+  const bool prerec = pre && !uni(S.have_sol);
+  bool pre_ok = true;
+  if (prerec) pre_ok = pre_read_round(sb, par, (unsigned)(S.iter + 1));
   if (threadIdx.x == 64) {
     int st = -1;
-    if (pre) {
+    if (pre && !prerec) {
       const unsigned long long v = ld_agent(&sb->stage[par]);
       if ((unsigned)(v >> 32) == (unsigned)(S.iter + 1)) st = (int)(unsigned)v;
     }
@@ -2089,10 +2143,26 @@ __device__ void sample_read(const Ctx& C) {
   } else if (threadIdx.x == 0) {
     g_L.smp_hit = 0;
   }
-  __syncthreads();
+  // this round's loads and the last iteration's stores (tree inserts the requests below hand to the scouts) complete
+  // together; then thread 0's stores of the iteration
+  drain();
+  const bool stale_granule = __syncthreads_or(!pre_ok) != 0;  // also the round's barrier
+  const bool prer_ok = prerec && !stale_granule;
+  if (threadIdx.x == 0) {
+    g_L.prer_ok = prer_ok;
+    sample_publish(C);
+    if (C.Q.nscouts > 0) scout_asks(C, 1 - g_L.S.A);
+  }
   const int st = uni(g_L.sp_go[0]);
   __syncthreads();
-  if (pre && st >= 0) spec_copy(sb, par, -1, st);
+  if (pre && !prerec && st >= 0) spec_copy(sb, par, -1, st);
+  if (prer_ok && !uni(g_L.smp_hit) && uni(g_L.prer.t >= 0)) {
+    // a valid record holds this iteration's sample (the ring's, at the pre-solution parameter version; an empty
+    // record, t = -1, carries none)
+    if (threadIdx.x < NJ) g_L.xr[threadIdx.x] = g_L.prer.xr[threadIdx.x];
+    if (threadIdx.x == 0) g_L.smp_hit = 1;
+    __syncthreads();
+  }
   if (!uni(g_L.smp_hit)) {
     if (sample_conf(S, it, g_L.u.smp, g_L.xr) < 0 && threadIdx.x == 0) { S.status = -1; S.phase = 2; }
     __syncthreads();
@@ -2562,33 +2632,175 @@ __device__ bool conn_stage(const Ctx& C, int B) {
 #else
 #define PRE_COUNT(k) if (threadIdx.x == 0) g_L.S.prof[28 + (k)]++
 #endif
+// Leader: the pre-solution record of this iteration, complete in g_L.prer -- from sample_read's round, else polled
+// (every granule tagged) until it is or SCOUT_WAIT passes or the scout has left.  All threads.
+__device__ bool pre_wait(const Ctx& C) {
+  if (uni(g_L.prer_ok)) return true;
+  const int par = (int)(g_L.S.iter & (SCOUT_SLOTS - 1));
+  const ScoutBoard* sb = C.Q.scbs[uni(g_L.asked[par]) - 1];
+  const unsigned tag = (unsigned)(g_L.S.iter + 1);
+  const unsigned long long t0 = threadIdx.x == 0 ? wall_clock64() : 0;
+  for (int k = 0;; k ^= 1) {
+    __builtin_amdgcn_s_sleep(1);
+    const bool ok = pre_read_round(sb, par, tag);
+    if (threadIdx.x == 0) g_L.sp_go[k] = wall_clock64() - t0 > SCOUT_WAIT || ld_agent(&sb->stop);
+    const bool bad = __syncthreads_or(!ok) != 0;
+    if (!bad) break;
+    if (uni(g_L.sp_go[k])) {
+      if (threadIdx.x == 0) g_L.S.sc_wait += wall_clock64() - t0;
+      __syncthreads();  // every wave has read sp_go[k] before the next poll loop writes it again
+      return false;
+    }
+  }
+  if (threadIdx.x == 0) { g_L.S.sc_wait += wall_clock64() - t0; g_L.prer_ok = 1; }
+  __syncthreads();
+  return true;
+}
+
+#ifdef SMP_PRE_VERIFY
+// Debugging build: every record-committed decision is recomputed the full way and compared; g_pv[0] counts checks,
+// g_pv[1] holds the first mismatch: iteration | kind << 40 (1 nearest, 2 expand edge, 3 connect nearest, 4 connect
+// edge, 5 x_new / edge costs) | block << 48; read by smp_debug_preverify.
+__device__ unsigned long long g_pv[4];
+__device__ void pv_fail(int kind) {
+  if (threadIdx.x == 0)
+    atomicCAS(&g_pv[1], 0ull, (unsigned long long)g_L.S.iter | ((unsigned long long)kind << 40) |
+                                  ((unsigned long long)blockIdx.x << 48));
+}
+__device__ void pre_verify_expand(const Ctx& C, int A) {
+  const PreRec& P = g_L.prer;
+  double d;
+  int full = nearest_scan(C, A, g_L.xr, 0, &d);
+  full = d < 10000.0 ? full : 0;
+  if (threadIdx.x == 0) atomicAdd(&g_pv[0], 1ull);
+  if (uni(full != (P.nn_d < 10000.0 ? P.nn_id : 0))) pv_fail(1);
+  if (threadIdx.x == 0) {
+    NodeRef nn;
+    load_node(C, A, full, &nn);
+    for (int j = 0; j < NJ; ++j) { g_L.ext[j] = g_L.xr[j]; }
+    step_towards((&g_rb), nn.q, g_L.ext, g_L.S.step);
+    for (int j = 0; j < NJ; ++j) { g_L.eg_start[0][j] = nn.q[j]; g_L.eg_target[0][j] = g_L.ext[j]; }
+    for (int k = 0; k < 3; ++k) g_L.eg_base[0][k] = nn.c[k];
+    g_L.eg_need[0] = 1;
+    g_L.rec_grp = -1;
+  }
+  for (int e = 1 + threadIdx.x; e < MAXE; e += BLOCK) g_L.eg_need[e] = 0;
+  __syncthreads();
+  edge_costs(C, 1);
+  edge_validity(C, 1, false, P_XEXPAND);
+  bool bad_costs = false;
+  for (int j = 0; j < NJ; ++j) bad_costs |= g_L.eg_end[0][j] != P.end[j] || g_L.eg_start[0][j] != P.nn_q[j];
+  for (int k = 0; k < 3; ++k) bad_costs |= g_L.eg_cost[0][k] != P.nn_c[k] + P.acc[k];
+  if (uni(g_L.eg_first[0] != P.first)) pv_fail(2);
+  if (uni(bad_costs)) pv_fail(5);
+  __syncthreads();
+}
+__device__ void pre_verify_connect(const Ctx& C, int B, int cid) {
+  const PreRec& P = g_L.prer;
+  double d;
+  int full = nearest_scan(C, B, g_L.xn.q, 0, &d);
+  full = d < 10000.0 ? full : 0;
+  if (uni(full != cid)) pv_fail(3);
+  if (threadIdx.x == 0) {
+    NodeRef xc;
+    load_node(C, B, full, &xc);
+    for (int j = 0; j < NJ; ++j) { g_L.eg_start[0][j] = xc.q[j]; g_L.eg_target[0][j] = g_L.xn.q[j]; }
+    for (int k = 0; k < 3; ++k) g_L.eg_base[0][k] = xc.c[k];
+    g_L.eg_need[0] = 1;
+    g_L.rec_grp = -1;
+  }
+  for (int e = 1 + threadIdx.x; e < MAXE; e += BLOCK) g_L.eg_need[e] = 0;
+  __syncthreads();
+  edge_costs(C, 1);
+  edge_validity(C, 1, false, P_XCONNECT);
+  if (uni(P.pre_ok && P.need && g_L.eg_first[0] != P.cn_first)) pv_fail(4);
+  __syncthreads();
+  if (!uni(P.pre_ok)) return;
+  // the connect outcome the full path would take (connect_graphs without a solution): flag, via chain, last node
+  if (threadIdx.x == 0) {
+    QState& S = g_L.S;
+    double sol[3];
+    for (int k = 0; k < 3; ++k) sol[k] = g_L.eg_cost[0][k] + g_L.xn.c[k];
+    const int need = sol[0] < S.cbest[0];
+    int flag = 0;
+    if (need) {
+      const int f = g_L.eg_first[0];
+      if (f > S.n_pts) flag = 1;
+      else {
+        const int lv = f == 0 ? 0 : f - 1;
+        if (lv != 0) { for (int j = 0; j < NJ; ++j) g_L.ext[j] = g_L.eg_start[0][j] + lv * g_L.eg_step[0][j]; flag = 2; }
+      }
+    }
+    bool bad = need != P.need || flag != P.flag;
+    for (int k = 0; k < 3; ++k) bad |= sol[k] != P.sol[k];
+    if (bad) pv_fail(8);
+    g_L.flag = flag;
+    g_L.n_via = 0;
+    g_L.nn_t = S.n[B];
+    load_node(C, B, cid, &g_L.cur);
+  }
+  __syncthreads();
+  const int flag = uni(g_L.flag);
+  if (!flag) return;
+  via_chain(C, flag == 1 ? g_L.xn.q : g_L.ext);
+  if (threadIdx.x == 0) {
+    const int par = (int)(g_L.S.iter & (SCOUT_SLOTS - 1));
+    const ScoutBoard* sb = C.Q.scbs[g_L.asked[par] - 1];
+    const int off = g_L.S.n[B] - P.XB;
+    bool bad = g_L.n_via != P.nv;
+    for (int k = 0; k < g_L.n_via && k < P.nv && !bad; ++k) {
+      const ViaNode& a = C.Q.via[k];
+      const ViaNode& b = sb->pre_via[par][k];
+      for (int j = 0; j < NJ; ++j)
+        bad |= a.q[j] != __longlong_as_double((long long)ld_agent((const unsigned long long*)&b.q[j])) ||
+               a.e_start[j] != __longlong_as_double((long long)ld_agent((const unsigned long long*)&b.e_start[j])) ||
+               a.e_target[j] != __longlong_as_double((long long)ld_agent((const unsigned long long*)&b.e_target[j]));
+      for (int c = 0; c < 3; ++c) bad |= a.c[c] != __longlong_as_double((long long)ld_agent((const unsigned long long*)&b.c[c]));
+      const int bid = ld_agent(&b.id), bpar = ld_agent(&b.parent);
+      bad |= a.id != (bid >= P.XB ? bid + off : bid) || a.parent != (bpar >= P.XB ? bpar + off : bpar);
+    }
+    if (bad) pv_fail(6);
+    bool bs = false;
+    for (int j = 0; j < NJ; ++j) bs |= g_L.sel.q[j] != P.sel_q[j] || g_L.sel_start[j] != P.sel_start[j] || g_L.sel_target[j] != P.sel_target[j];
+    for (int k = 0; k < 3; ++k) bs |= g_L.sel.c[k] != P.sel_c[k];
+    bs |= g_L.sel.id != (P.sel_id >= P.XB ? P.sel_id + off : P.sel_id);
+    bs |= g_L.sel.parent != (P.sel_parent >= P.XB ? P.sel_parent + off : P.sel_parent);
+    if (bs) pv_fail(7);
+    g_L.n_via = 0;
+  }
+  __syncthreads();
+}
+#endif
+
 __device__ bool pre_commit(const Ctx& C, int A, int B) {
-  if (!uni(g_L.sp_on) || !spec_stage(C, SC_DONE)) { PRE_COUNT(1); return false; }
-  const ScoutRec& R = g_L.sr;
+  if (!uni(g_L.sp_on) || !pre_wait(C)) { PRE_COUNT(1); return false; }
+  const PreRec& P = g_L.prer;
   const int nA = uni(g_L.S.n[A]);
-  if (!uni(R.nn.ok && R.ex.ok && R.nn.t == A && R.nn.X <= nA && same8(R.nn.q, g_L.xr))) { PRE_COUNT(1); return false; }
-  if (uni(R.nn.X < nA)) {
+  if (!uni(P.t == A && P.X <= nA && same8(P.xr, g_L.xr))) { PRE_COUNT(1); return false; }
+  if (uni(P.X < nA)) {
     double dp;
-    if (uni(nA - R.nn.X <= PATCH_K)) patch_scan(A, g_L.xr, R.nn.X, nA, &dp);
-    else nearest_scan(C, A, g_L.xr, R.nn.X, &dp);
-    if (uni(dp < R.nn.d)) { PRE_COUNT(2); return false; }
+    if (uni(nA - P.X <= PATCH_K)) patch_scan(A, g_L.xr, P.X, nA, &dp);
+    else nearest_scan(C, A, g_L.xr, P.X, &dp);
+    if (uni(dp < P.nn_d)) { PRE_COUNT(2); return false; }
   }
   PRE_COUNT(0);
   TR();
+#ifdef SMP_PRE_VERIFY
+  pre_verify_expand(C, A);
+#endif
   if (threadIdx.x == 0) {
     QState& S = g_L.S;
     S.nn_nodes += nA;
     S.sc_nn++;
     S.sc_edge_hit++;
-    const int nid = R.nn.d < 10000.0 ? R.nn.id : 0;
+    const int nid = P.nn_d < 10000.0 ? P.nn_id : 0;
     g_L.count_slot = P_XEXPAND + 4;
-    const int f = R.e[0].first;
-    count_edge(f);
-    g_L.ext_nn = f > S.n_pts;
+    count_edge(P.first);
+    g_L.ext_nn = P.first > S.n_pts;
     g_L.ext_bp = 0;
     if (g_L.ext_nn) {
-      for (int j = 0; j < NJ; ++j) { g_L.xn.q[j] = R.ex.end[j]; g_L.en_start[j] = R.e[0].s[j]; g_L.en_target[j] = R.ex.ext[j]; }
-      for (int k = 0; k < 3; ++k) g_L.xn.c[k] = R.nn.c[k] + R.ex.acc[k];
+      for (int j = 0; j < NJ; ++j) { g_L.xn.q[j] = P.end[j]; g_L.en_start[j] = P.nn_q[j]; g_L.en_target[j] = P.ext[j]; }
+      for (int k = 0; k < 3; ++k) g_L.xn.c[k] = P.nn_c[k] + P.acc[k];
       g_L.xn.id = S.n[A];
       g_L.xn.parent = nid;
       insert_node(C, A, g_L.en_start, g_L.en_target, g_L.xn);
@@ -2596,42 +2808,43 @@ __device__ bool pre_commit(const Ctx& C, int A, int B) {
   }
   __syncthreads();
   if (!uni(g_L.ext_nn)) return true;
-  // connect (birrt_star.cpp:1256-1275): tree_B's nearest node of x_new
-  const ScoutConnect& K = R.cn;
+  // connect (birrt_star.cpp:1256-1275): tree_B's nearest node of x_new (the record's x_new is P.end)
   const int nB = uni(g_L.S.n[B]);
-  bool rec = uni(K.ok && K.t == B && K.X <= nB && same8(K.q, g_L.xn.q)) != 0;
+  bool rec = uni(P.cn_ok && P.XB <= nB) != 0;
   int cid;
   if (rec) {
-    cid = K.d < 10000.0 ? K.id : 0;
-    if (uni(K.X < nB)) {
+    cid = P.cn_d < 10000.0 ? P.cn_id : 0;
+    if (uni(P.XB < nB)) {
       double dp;
-      const int ip = uni(nB - K.X <= PATCH_K) ? patch_scan(B, g_L.xn.q, K.X, nB, &dp)
-                                               : nearest_scan(C, B, g_L.xn.q, K.X, &dp);
-      if (uni(dp < K.d)) { cid = ip; rec = false; }
+      const int ip = uni(nB - P.XB <= PATCH_K) ? patch_scan(B, g_L.xn.q, P.XB, nB, &dp)
+                                                : nearest_scan(C, B, g_L.xn.q, P.XB, &dp);
+      if (uni(dp < P.cn_d)) { cid = ip; rec = false; }
     }
     if (threadIdx.x == 0) { g_L.S.nn_nodes += nB; g_L.S.sc_nn++; }
   } else {
     cid = nearest(C, B, g_L.xn.q);
   }
   TR();
-  if (!rec || !uni(R.pre.ok)) {
+#ifdef SMP_PRE_VERIFY
+  if (rec) pre_verify_connect(C, B, cid);
+#endif
+  if (!rec || !uni(P.pre_ok) || C.Q.pre_commit == 2) {
     PRE_COUNT(3);
     if (threadIdx.x == 0) load_node(C, B, cid, &g_L.xc);
     __syncthreads();
-    connect_graphs(C, B);  // takes the record's direct-edge result if it is the same edge
+    connect_graphs(C, B);
     return true;
   }
   // the record's connect outcome: count the direct edge, insert its via chain and the last node
   if (threadIdx.x == 0) {
     QState& S = g_L.S;
-    const ScoutPre& P = R.pre;
-    const int off = S.n[B] - K.X;
+    const int off = S.n[B] - P.XB;
     g_L.tree_expand = 0;
     g_L.best_nv = 10000.0;
     for (int k = 0; k < 3; ++k) g_L.csp[k] = S.cbest[k];
     if (P.need) {
       g_L.count_slot = P_XCONNECT + 4;
-      count_edge(K.e.first);
+      count_edge(P.cn_first);
       S.sc_edge_hit++;
       if (P.flag == 1) {
         for (int k = 0; k < 3; ++k) g_L.csp[k] = P.sol[k];
@@ -2641,15 +2854,19 @@ __device__ bool pre_commit(const Ctx& C, int A, int B) {
       }
     }
     g_L.n_via = P.nv;
-    g_L.sel = P.sel;
-    if (g_L.sel.id >= K.X) g_L.sel.id += off;
-    if (g_L.sel.parent >= K.X) g_L.sel.parent += off;
-    for (int j = 0; j < NJ; ++j) { g_L.sel_start[j] = P.sel_start[j]; g_L.sel_target[j] = P.sel_target[j]; }
+    for (int j = 0; j < NJ; ++j) {
+      g_L.sel.q[j] = P.sel_q[j];
+      g_L.sel_start[j] = P.sel_start[j];
+      g_L.sel_target[j] = P.sel_target[j];
+    }
+    for (int k = 0; k < 3; ++k) g_L.sel.c[k] = P.sel_c[k];
+    g_L.sel.id = P.sel_id >= P.XB ? P.sel_id + off : P.sel_id;
+    g_L.sel.parent = P.sel_parent >= P.XB ? P.sel_parent + off : P.sel_parent;
   }
   __syncthreads();
   const int par = (int)(g_L.S.iter & (SCOUT_SLOTS - 1));
   const ScoutBoard* sb = C.Q.scbs[uni(g_L.asked[par]) - 1];
-  insert_via(C, B, sb->pre_via[par], K.X);
+  insert_via(C, B, sb->pre_via[par], P.XB);
   connect_tail(C, B);
   TR();
   return true;
@@ -2667,16 +2884,17 @@ __device__ __forceinline__ void iteration(const Ctx& C) {
   if (threadIdx.x == 0) g_L.conn_rec = 0;
   TR();
 #define PHASE(k) if (threadIdx.x == 0) { _t1 = pclk(); g_L.S.prof[k] += _t1 - _t0; _t0 = _t1; }
-  if (C.Q.nscouts > 0) scout_prepare(C);
-  sample_publish(C);
-  if (C.Q.nscouts > 0) scout_request(C, B);
+  if (threadIdx.x == 0) {
+    sample_version(C);
+    if (C.Q.nscouts > 0) scout_slots();
+  }
   __syncthreads();
   TR();
   sample_read(C);
   TR();
   PHASE(P_SAMPLE);
   const bool opt = uni(g_L.S.tree_opt && g_L.S.have_sol);
-  if (C.Q.nscouts > 0 && !uni(g_L.S.have_sol) && pre_commit(C, A, B)) {
+  if (C.Q.pre_commit && C.Q.nscouts > 0 && !uni(g_L.S.have_sol) && pre_commit(C, A, B)) {
     PHASE(P_CONNECT);
   } else {
   int nid = nearest(C, A, g_L.xr, true);
@@ -2858,7 +3076,10 @@ __device__ void scout_connect(const Ctx& C, long long it, int t, int par, unsign
     }
     __syncthreads();
     const int go = uni(g_L.sp_go[k]);
-    if (go < 0) return;  // stale: nobody waits for this record any more
+    if (go < 0) {  // stale: nobody waits for this record any more
+      __syncthreads();  // every wave has read sp_go[k] before scout_main's poll writes it again
+      return;
+    }
     if (go > 0) break;
     __builtin_amdgcn_s_sleep(2);
   }
@@ -2987,6 +3208,49 @@ __device__ void scout_pre_connect(const Ctx& C, int par, int tb) {
   for (int w = threadIdx.x; w < nw; w += BLOCK) st_agent(&dst[w], ld_agent(&src[w]));
 }
 
+// Scout, end of a pre-solution pass: the record as PreRec granules (DESIGN.md "Pre-solution commits"); `valid` = 0
+// publishes an empty one (t = -1: the leader stops waiting for it).  A via chain's node copies (scout_pre_connect)
+// are drained first, so a leader that has the whole record finds them.
+__device__ void scout_pre_publish(const Ctx& C, int par, unsigned tag, bool valid) {
+  const ScoutRec& R = g_L.sr;
+  PreRec& P = g_L.prer;
+  if (threadIdx.x == 0) {
+    P.t = valid ? R.nn.t : -1;  // (an empty record's other fields are stale and never read)
+    P.X = R.nn.X;
+    P.nn_id = R.nn.id;
+    P.nn_d = R.nn.d;
+    P.first = R.e[0].first;
+    for (int j = 0; j < NJ; ++j) {
+      P.xr[j] = R.nn.q[j]; P.nn_q[j] = R.e[0].s[j]; P.ext[j] = R.ex.ext[j]; P.end[j] = R.ex.end[j];
+      P.sel_q[j] = R.pre.sel.q[j]; P.sel_start[j] = R.pre.sel_start[j]; P.sel_target[j] = R.pre.sel_target[j];
+    }
+    for (int k = 0; k < 3; ++k) {
+      P.nn_c[k] = R.nn.c[k]; P.acc[k] = R.ex.acc[k]; P.cn_c[k] = R.cn.c[k]; P.sol[k] = R.pre.sol[k];
+      P.sel_c[k] = R.pre.sel.c[k];
+    }
+    P.cn_ok = R.cn.ok;
+    P.cn_d = R.cn.d;
+    P.cn_id = R.cn.id;
+    P.XB = R.cn.X;
+    P.cn_first = R.cn.e.first;
+    P.pre_ok = R.cn.ok && R.pre.ok;
+    P.flag = R.pre.flag;
+    P.nv = R.pre.nv;
+    P.need = R.pre.need;
+    P.sel_id = R.pre.sel.id;
+    P.sel_parent = R.pre.sel.parent;
+    P.pad[0] = P.pad[1] = 0;
+  }
+  __syncthreads();
+  if (uni(P.pre_ok && P.nv > 0)) {
+    drain();
+    __syncthreads();
+  }
+  for (int g = threadIdx.x; g < PRE_GRANULES; g += BLOCK)
+    st_agent(&C.Q.scb->pre_g[par][g], granule((int)tag, reinterpret_cast<const unsigned*>(&P)[g]));
+  __syncthreads();
+}
+
 // The scout's pass for iteration `it` of the leader, which expands tree t from a snapshot of its first X nodes:
 // the leader's steps up to its rewire collision job (iteration / choose_parent / rewire, same functions on the
 // scout's own LDS, job board, helpers and via-node scratch), recording the results the leader keys on; nothing is
@@ -3012,7 +3276,7 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
     R.pre.ok = 0;
     R.nn.ok = 0; R.ex.ok = 0; R.nr.ok = 0; R.n_choose = 0; R.n_rewire = 0; R.cc.ok = 0;
   }
-  sc_publish(C, par, tag, SC_STARTED);
+  if (opt) sc_publish(C, par, tag, SC_STARTED);  // (a pre-solution pass publishes its record once, at its end)
   // the sample: the sampler's ring slot for (it, ver), if it is there within ~20 us
   if (threadIdx.x < 64) {  // wave 0 polls the slot's 16 granules (one round each time)
     const JobBoard* lb = C.Q.sampler_jb;
@@ -3038,6 +3302,10 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
   __syncthreads();
   SC_PHASE(0);
   TR();
+  if (!uni(g_L.flag) && !opt) {
+    scout_pre_publish(C, par, tag, false);
+    return;
+  }
   if (!uni(g_L.flag)) {
     sc_copy_out(sb, par, &R.nn, sizeof(ScoutNN));
     sc_copy_out(sb, par, &R.nr, sizeof(ScoutNear));
@@ -3065,8 +3333,10 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
     g_L.eg_need[0] = 1;
   }
   __syncthreads();
-  sc_copy_out(sb, par, &R.nn, sizeof(ScoutNN));
-  sc_publish(C, par, tag, SC_NN);
+  if (opt) {
+    sc_copy_out(sb, par, &R.nn, sizeof(ScoutNN));
+    sc_publish(C, par, tag, SC_NN);
+  }
   SC_PHASE(1);
   TR();
   edge_costs(C, 1);
@@ -3096,13 +3366,14 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
     g_L.ext_bp = 0;
   }
   __syncthreads();
-  sc_copy_out(sb, par, &R.e[0], sizeof(ScoutEdge));
-  sc_copy_out(sb, par, &R.ex, sizeof(ScoutExpand));
+  if (opt) {
+    sc_copy_out(sb, par, &R.e[0], sizeof(ScoutEdge));
+    sc_copy_out(sb, par, &R.ex, sizeof(ScoutExpand));
+  }
   if (!opt && uni(g_L.ext_nn) && !sc_stale(C, tag)) {
     // before the first solution the iteration goes on with connect (connectGraphs): x_new is the expand edge's
     // end; its nearest node in the other tree over that tree's first XB nodes (the tree only grows until then)
     // and the direct edge to it, whose check always runs while there is no solution (c_best = inf)
-    sc_publish(C, par, tag, SC_EXPAND);
     const int tb = 1 - t;
     const int cid = nearest(C, tb, g_L.xn.q);
     if (threadIdx.x == 0) {
@@ -3130,9 +3401,11 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
     __syncthreads();
     scout_pre_connect(C, par, tb);
   }
-  if (!opt || sc_stale(C, tag)) {
-    sc_copy_out(sb, par, &R.cn, sizeof(ScoutConnect));
-    sc_copy_out(sb, par, &R.pre, sizeof(ScoutPre));
+  if (!opt) {
+    scout_pre_publish(C, par, tag, true);
+    return;
+  }
+  if (sc_stale(C, tag)) {
     sc_copy_out(sb, par, &R.nr, sizeof(ScoutNear));
     sc_copy_out(sb, par, &R.n_choose, 4 * sizeof(int));
     sc_publish(C, par, tag, SC_DONE);
@@ -3340,14 +3613,43 @@ __device__ __forceinline__ void scout_main(Ctx& C, int which) {
       continue;
     }
     const unsigned w0 = (unsigned)uni(g_L.cnt), ver = (unsigned)uni(g_L.nn_t), tag = (unsigned)uni(g_L.tree_expand);
-    const int XB = uni(g_L.found);
+    int XB = uni(g_L.found);
+    int X = (int)(w0 & ((1u << 28) - 1));
+    const int t = (int)(w0 >> 28) & 1, opt = (int)(w0 >> 29) & 1;
     __syncthreads();
-    // tree words stored by the leader since this CU / XCD last cached them: drop stale copies
+    if (!opt && C.Q.pre_delay > 0) {
+      // before the first solution: start once the leader is pre_delay iterations from this one, on the tree sizes
+      // it published after its latest drain (trees only grow until the first solution, so they are at least the
+      // request's): fewer nodes appended between the snapshot and the record's use, fewer records a newer node beats
+      const long long k = (long long)tag - 1;
+      for (int r = 0;; r ^= 1) {
+        if (threadIdx.x == 0) {
+          const long long cur = (long long)ld_agent(&C.Q.scb->cur);
+          const int go = cur >= k - C.Q.pre_delay || ld_agent(&C.Q.scb->stop);
+          if (go) {
+            const unsigned long long sz = ld_agent(&C.Q.scb->cur_sz);
+            const int n0 = (int)((sz >> 20) & 0xfffff), n1 = (int)(sz & 0xfffff);
+            g_L.cnt = max(X, t == 0 ? n0 : n1);
+            g_L.found = max(XB, t == 0 ? n1 : n0);
+          }
+          g_L.sp_go[r] = go;
+        }
+        __syncthreads();
+        if (uni(g_L.sp_go[r])) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+      X = uni(g_L.cnt);
+      XB = uni(g_L.found);
+      __syncthreads();
+    }
+    // tree words stored by the leader since this CU / XCD last cached them: drop stale copies (the invalidate completes
+    // asynchronously: every wave waits for it before its first plain load, MI355X_MICROARCH.md consumer form)
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    drain();
+    __syncthreads();
     const unsigned long long tb = wall_clock64();
     if (threadIdx.x == 0) g_L.S.prof[28] += tb - t_last;  // idle: waiting for a request
-    scout_iteration(C, (long long)tag - 1, (int)(w0 >> 28) & 1, (int)(w0 & ((1u << 28) - 1)), (int)(w0 >> 29) & 1, ver,
-                    XB);
+    scout_iteration(C, (long long)tag - 1, t, X, opt, ver, XB);
     last = tag;
     t_last = wall_clock64();
     if (threadIdx.x == 0) g_L.S.prof[31] += t_last - tb;
@@ -3383,7 +3685,7 @@ __global__ void __launch_bounds__(BLOCK) plan_kernel(const RobotDev* __restrict_
   if (threadIdx.x == 0) {
     g_L.sp_on = 0;
     for (int k = 0; k < MAX_SCOUTS; ++k) g_L.sc_same[k] = -1;
-    for (int k = 0; k < SCOUT_SLOTS; ++k) { g_L.asked[k] = 0; g_L.asked_conn[k] = 0; }
+    for (int k = 0; k < SCOUT_SLOTS; ++k) { g_L.asked[k] = 0; g_L.asked_conn[k] = 0; g_L.asked_pre[k] = 0; }
     g_L.conn_rec = 0;
     g_L.rec_grp = -1;
     g_L.count_slot = 0;
@@ -3623,6 +3925,20 @@ extern "C" int smp_debug_tlog(unsigned long long* out, int cap, int reset) {
 }
 #else
 extern "C" int smp_debug_tlog(unsigned long long*, int, int) { return -1; }
+#endif
+
+#ifdef SMP_PRE_VERIFY
+extern "C" int smp_debug_preverify(unsigned long long* out, int reset) {
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(smp::g_pv), 4 * sizeof(unsigned long long)) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[4] = {0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(smp::g_pv), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#else
+extern "C" int smp_debug_preverify(unsigned long long*, int) { return -1; }
 #endif
 
 #ifdef SMP_BOUNDS

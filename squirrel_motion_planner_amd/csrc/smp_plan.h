@@ -185,6 +185,28 @@ struct ScoutConn {
   double pad0;
   double acc[MAX_NEAR][3];     // near candidate lo_i[e] -> x_new (e < min(n_lo, max_near))
 };
+// Pre-solution record (DESIGN.md "Pre-solution commits"): everything pre_commit needs, written by the scout at the
+// end of its pass as data-tagged granules (tag = iteration + 1 in the high 32 bits, one 32-bit half of the struct
+// in the low 32), so the leader reads it whole in one round and knows it complete when every tag matches.
+struct PreRec {
+  double xr[NJ];               // the sample
+  double nn_q[NJ];             // its nearest node's configuration over the snapshot (the expand edge's start)
+  double nn_c[3];              // that node's cost
+  double nn_d;                 // its distance (10000 if none)
+  double ext[NJ], end[NJ];     // the expand edge's step target and end point (x_new)
+  double acc[3];               // the expand edge's segment-norm sums
+  double cn_d, cn_c[3];        // connect: x_new's nearest node in the other tree (distance, cost)
+  double sol[3];               // connect: direct edge cost + x_new's cost
+  double sel_q[NJ], sel_c[3];  // connect: the last stepped edge's node
+  double sel_start[NJ], sel_target[NJ];
+  int nn_id, X, t, first;      // nearest node, snapshot size, tree, expand edge's first collision
+  int cn_id, XB, cn_ok, cn_first;  // connect's nearest node, other tree's snapshot size, 1 = computed, first collision
+  int pre_ok, flag, nv, need;  // as ScoutPre
+  int sel_id, sel_parent, pad[2];
+};
+constexpr int PRE_GRANULES = (int)(sizeof(PreRec) / 4);
+static_assert(sizeof(PreRec) % 8 == 0 && PRE_GRANULES <= 4 * 64, "pre-solution record: one granule per lane of 4 waves");
+
 struct ScoutRec {
   ScoutNN nn;
   ScoutExpand ex;
@@ -209,13 +231,17 @@ struct ScoutBoard {
   int xcc;                     // the scout's XCD (XCC_ID) + 1, 0 = not yet known
   int pad0[8];
   unsigned long long cur;      // leader -> scout: the leader's current iteration (a record of an earlier one is stale)
-  int pad2[30];
+  // leader -> scout, before the first solution: (iteration & 0xffffff) << 40 | n[0] << 20 | n[1], stored after the
+  // iteration's drain, so both trees' first n nodes are visible (a scout binds its snapshot to it late)
+  unsigned long long cur_sz;
+  int pad2[28];
   unsigned long long stage[SCOUT_SLOTS];  // scout -> leader, by iteration mod SCOUT_SLOTS
   unsigned long long cgo;      // leader -> scout: granule (iteration k + 1, n of tree_B(k)) once tree_B(k) is final
   int pad1[14];
   unsigned long long prof[32]; // the scout's phase clocks of the launch (written when it leaves)
   ScoutRec rec[SCOUT_SLOTS];
   ViaNode pre_via[SCOUT_SLOTS][PRE_VIA];  // ScoutPre's via chains, by record slot
+  unsigned long long pre_g[SCOUT_SLOTS][PRE_GRANULES];  // PreRec granules, by record slot
 };
 
 struct QueryDev {
@@ -226,6 +252,8 @@ struct QueryDev {
   // first solution iteration k goes to scout k mod nscouts (up to nscouts ahead), after it to scout k mod 2 (two
   // ahead); each has its record board, collision-job board, helpers and via-node scratch
   int nscouts;
+  int pre_delay;               // before the first solution a scout starts record k once the leader is at k - pre_delay
+  int pre_commit;              // 1: pre-solution iterations are committed from complete scout records
   ScoutBoard* scbs[MAX_SCOUTS];
   JobBoard* sjbs[MAX_SCOUTS];
   ViaNode* svias[MAX_SCOUTS];

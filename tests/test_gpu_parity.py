@@ -282,6 +282,19 @@ def test_batch_equals_single(gp):
         assert np.array_equal(b["path"], s["path"])
 
 
+def test_batch_repeated_is_deterministic(gp):
+    """Race detector: the 4-query batch (every CU busy: leaders, scouts, helpers) repeated 30 times gives the same
+    runs each time.  Caught a stale sample taken from empty pre-solution records and a barrier desync after a
+    record time-out, both timing-dependent."""
+    sc, gscene, _ = scene_pair("c2")
+    gp.set_scene(gscene)
+    qs = [GpuPlanner.make_query(sc.start, sc.goal, sc.env_x, sc.env_y, iterations=150, seed=s, query_id=s)
+          for s in range(4)]
+    ref = [gp.plan(q)["configs_checked"] for q in qs]
+    for _ in range(30):
+        assert [r["configs_checked"] for r in gp.plan_batch(qs)] == ref
+
+
 def _same_query_result(r, o):
     assert r["status"] == {0: 0, 1: L.SMP_ERR_NO_SOLUTION}[o["status"]]
     for k_r, k_o in (("iterations", "iterations"), ("first_solution_iter", "first_iter"), ("configs_checked", "checked"),

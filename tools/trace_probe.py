@@ -26,7 +26,12 @@ gp = GpuPlanner(path_optimality_threshold=-math.inf, scout=int(os.environ.get("S
 gp.set_scene(Scene.from_keys(sc.keys, sc.res))
 buf = (ctypes.c_uint64 * (1 << 18))()
 lib.smp_debug_tlog(buf, 1 << 18, 1)  # reset
-r = gp.plan(GpuPlanner.make_query(sc.start, sc.goal, sc.env_x, sc.env_y, iterations=iters, seed=1))
+start, goal = sc.start, sc.goal
+if os.environ.get("SMP_TRACE_C3Q"):  # one of C3's random queries (bench.py --workload c3) instead of C2's pair
+    pairs = scenes.random_queries(sc, 8, seed=7, check=lambda q: bool(gp.check_configs([q])[0]))
+    start, goal = pairs[int(os.environ["SMP_TRACE_C3Q"])]
+r = gp.plan(GpuPlanner.make_query(start, goal, sc.env_x, sc.env_y, iterations=iters, seed=1,
+                                  query_id=int(os.environ.get("SMP_TRACE_C3Q", "0"))))
 n = lib.smp_debug_tlog(buf, 1 << 18, 1)
 print("iterations %d, checked %d, first solution iter %d, %d trace records" % (
     r["iterations"], r["configs_checked"], r["first_solution_iter"], n))
