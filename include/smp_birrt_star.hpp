@@ -3,9 +3,9 @@
 // The ROS node (squirrel_8dof_planner) owns a BiRRTstarPlanner by value (squirrel_8dof_planner.h:131) and calls
 // the methods below (squirrel_8dof_planner.cpp:16, 482-810, 872-915, 1179-1248).  This class keeps those
 // signatures (birrt_star.h:27-110) and forwards every call to the C ABI in smp_gpu.h, so the node compiles
-// against it unchanged except for its two calls outside the sampling / collision path, getCollisions
-// (squirrel_8dof_planner.cpp:839) and getFullPoseFromEEPose (squirrel_8dof_planner.cpp:1179), which this class does
-// not provide; the planning loop itself runs in the HIP kernels of libsmp_gpu.so.
+// against it unchanged except for getCollisions (squirrel_8dof_planner.cpp:839, a visualisation helper outside the
+// sampling / collision path), which this class does not provide; the planning loop and the goal
+// search's IK controller run in the HIP kernels of libsmp_gpu.so.
 //
 // Build: include this header instead of <birrt_star_algorithm/birrt_star.h> and link -lsmp_gpu.
 // Configuration (environment, read by initialize()):
@@ -221,6 +221,45 @@ class BiRRTstarPlanner {
     int v = 0;
     check(smp_is_config_valid(planner_, config.data(), check_self_collision, check_map_collision, &v), "isConfigValid");
     return v != 0;
+  }
+
+  // birrt_star.cpp:1627-1686: the VDLS controller (control_laws.cpp:3283-3712) from poseInit towards
+  // endEffectorPose = (x, y, z, roll, pitch, yaw); true and poseSolution on REACHED.
+  bool getFullPoseFromEEPose(const vector<double>& endEffectorPose, const vector<pair<double, double> >& endEffectorDeviations,
+                             const vector<double>& poseInit, vector<double>& poseSolution) {
+    need();
+    if (endEffectorPose.size() < 6 || endEffectorDeviations.size() < 6 || poseInit.size() < 8) return false;
+    smp_ik_request r;
+    std::memset(&r, 0, sizeof(r));
+    for (int k = 0; k < 6; ++k) {
+      r.ee_pose[k] = endEffectorPose[k];
+      r.deviation[k][0] = endEffectorDeviations[k].first;
+      r.deviation[k][1] = endEffectorDeviations[k].second;
+    }
+    for (int j = 0; j < 8; ++j) r.q_init[j] = poseInit[j];
+    r.max_iter = 1000;
+    smp_ik_result o;
+    check(smp_ik_solve(planner_, &r, 1, &o), "getFullPoseFromEEPose");
+    if (!o.reached) return false;
+    poseSolution.assign(o.q, o.q + 8);
+    return true;
+  }
+
+  // Planner::findGoalPose (squirrel_8dof_planner.cpp:1129-1201) in one call: every candidate base angle's
+  // controller run at once, one batched validity check, the first valid pose in the reference's order.  Returns
+  // the reference's codes: 0 (poseGoal set), 1 (reached poses all collide), 2 (no pose reached; poseGoal cleared).
+  int findGoalPose(const vector<double>& poseEndEffector, const vector<double>& poseCurrent,
+                   double goalPoseSearchDiscretizationDeg, bool checkSelfCollision, bool checkMapCollision,
+                   vector<double>& poseGoal) {
+    need();
+    if (poseEndEffector.size() < 6 || poseCurrent.size() < 8) throw std::runtime_error("smp: findGoalPose: dimension");
+    double goal[8];
+    int res = 2;
+    check(smp_find_goal_pose(planner_, poseEndEffector.data(), poseCurrent.data(), goalPoseSearchDiscretizationDeg,
+                             checkSelfCollision, checkMapCollision, goal, &res, nullptr), "findGoalPose");
+    if (res == 0) poseGoal.assign(goal, goal + 8);
+    else poseGoal.clear();
+    return res;
   }
 
   // Planner statistics of the last run (birrt_star.cpp:6300-6355 writes the same quantities to files).

@@ -27,6 +27,11 @@
  *   smp_check_sequence         the node's keyframe loops over isConfigValid (fold / unfold arm,
  *                              squirrel_8dof_planner.cpp:759-784, 814-823): first invalid pose, one kernel launch
  *   smp_normalize_trajectory   Planner::normalizeTrajectory (squirrel_8dof_planner.cpp:1557-1637), host only
+ *   smp_ik_solve               BiRRTstarPlanner::getFullPoseFromEEPose (birrt_star.cpp:1627-1686) ->
+ *                              RobotController::run_VDLS_Control_Connector (control_laws.cpp:3283-3712):
+ *                              n independent controller runs, one wavefront each
+ *   smp_find_goal_pose         Planner::findGoalPose (squirrel_8dof_planner.cpp:1129-1201): every candidate base
+ *                              angle's controller run at once, then one batch validity check, first valid in order
  *   smp_result_free            releases library-owned result buffers
  *   smp_strerror               text of a status code
  *
@@ -197,6 +202,41 @@ int smp_check_sequence(smp_planner* p, const double* q_rows, int64_t n, int chec
  * untouched: *n_out = 0.  Host only (no GPU needed). */
 int smp_normalize_trajectory(const double* raw, int64_t n, int dim, const double* normalized_pose, double* out,
                              int64_t out_cap, int64_t* n_out);
+
+/* End-effector goal -> 8-DoF pose (IK of the node's goal search). */
+typedef struct smp_ik_request {
+  double ee_pose[6];        /* x, y, z, roll, pitch, yaw: getFullPoseFromEEPose's endEffectorPose (birrt_star.cpp:1627) */
+  double deviation[6][2];   /* (lower, upper) permitted error per task coordinate: endEffectorDeviations
+                               (setVariableConstraints, control_laws.cpp:1740-1761) */
+  double q_init[8];         /* poseInit (setStartConf, control_laws.cpp:1464-1495) */
+  int max_iter;             /* controller iterations, >= 1 (the reference passes 1000, birrt_star.cpp:1670) */
+} smp_ik_request;
+
+typedef struct smp_ik_result {
+  int reached;              /* 1: REACHED -- getFullPoseFromEEPose returns true; 0: ADVANCED (control_laws.cpp:3691-3710) */
+  int iterations;           /* controller iterations run */
+  int fallback_iterations;  /* iterations whose manipulability needed the Jacobi eigenvalue path (near-singular J) */
+  double q[8];              /* poseSolution = joint_trajectory.back() (birrt_star.cpp:1675) */
+  double error[6];          /* last task-space error (zero inside the deviation band) */
+  double manipulability;    /* last manipulability measure (control_laws.cpp:6050-6089) */
+} smp_ik_result;
+
+int smp_ik_solve(smp_planner* p, const smp_ik_request* reqs, int n, smp_ik_result* out);
+
+typedef struct smp_goal_search {
+  int n_candidates;         /* base angles of the search (2 * ceil(180 / discretization) - 1 or so) */
+  int n_reached;            /* candidates whose controller run REACHED the pose */
+  int chosen;               /* candidate index of pose_goal, -1 if none */
+  int downward;             /* 1 if the hand points downward (squirrel_8dof_planner.cpp:1140) */
+  double kernel_ms;         /* IK + validity kernels, HIP events */
+} smp_goal_search;
+
+/* findGoalPose for end-effector pose ee_pose (x, y, z, roll, pitch, yaw in the planning frame) from the robot's
+ * current pose, candidate spacing in degrees (goal_pose_search_discretization, default 20; values < 1 count as 1).
+ * *result: 0 = pose found (pose_goal written), 1 = every pose the controller reached collides (COLLISION_GOAL_POSE),
+ * 2 = the controller reached no pose (INVALID_END_EFFECTOR_POSE) -- the reference's return codes.  info may be NULL. */
+int smp_find_goal_pose(smp_planner* p, const double ee_pose[6], const double pose_current[8], double discretization_deg,
+                       int check_self, int check_map, double pose_goal[8], int* result, smp_goal_search* info);
 
 /* Kernel timing of the last smp_check_configs / smp_plan call: milliseconds on the launch stream. */
 int smp_last_kernel_ms(const smp_planner* p, double* check_ms, double* plan_ms, int64_t* plan_launches);

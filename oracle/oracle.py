@@ -86,6 +86,14 @@ def lib():
         L.orc_get_tree.restype = _i
         L.orc_get_cost_rows.argtypes = [ctypes.c_void_p, _pd]
         L.orc_get_cost_rows.restype = _i
+        L.orc_ik_solve.argtypes = [ctypes.c_void_p, _pd, _i, _i, _pd, _pi]
+        L.orc_ik_goal.argtypes = [_pd, _pd]
+        L.orc_ik_fk_jac.argtypes = [ctypes.c_void_p, _pd, _i, _pd, _pd]
+        L.orc_goal_candidates.argtypes = [_pd, _pd, _d, _pd, _pi]
+        L.orc_goal_candidates.restype = _i
+        L.orc_find_goal_pose.argtypes = [ctypes.c_void_p, _pd, _pd, _d, _i, _i, _pd,
+                                         ctypes.POINTER(ctypes.c_longlong)]
+        L.orc_find_goal_pose.restype = _i
         _lib = L
     return _lib
 
@@ -284,6 +292,35 @@ class Oracle:
         lib().orc_body_fk(self.h, _p(q, _d), len(q), _p(fr, _d))
         return fr
 
+    def ik_solve(self, tasks, max_iter=1000):
+        """run_VDLS_Control_Connector for rows of ik_tasks() -> dict of q (n x 8), err (n x 6), manip, reached,
+        iters, fallback."""
+        tasks = np.ascontiguousarray(tasks, np.float64).reshape(-1, 27)
+        n = len(tasks)
+        out = np.zeros((n, 15))
+        st = np.zeros((n, 3), np.int32)
+        lib().orc_ik_solve(self.h, _p(tasks, _d), n, int(max_iter), _p(out, _d), _p(st, _i))
+        return dict(q=out[:, :8], err=out[:, 8:14], manip=out[:, 14], reached=st[:, 0], iters=st[:, 1],
+                    fallback=st[:, 2])
+
+    def ik_fk_jac(self, q):
+        """compute_FK poses (n, 7: x y z qx qy qz qw) and float-cast KDL Jacobians (n, 6, 8)."""
+        q = np.ascontiguousarray(q, np.float64).reshape(-1, 8)
+        ee = np.zeros((len(q), 7))
+        J = np.zeros((len(q), 6, 8))
+        lib().orc_ik_fk_jac(self.h, _p(q, _d), len(q), _p(ee, _d), _p(J, _d))
+        return ee, J
+
+    def find_goal_pose(self, ee, cur, disc_deg=20.0, self_=True, map_=True):
+        """Planner::findGoalPose -> (result 0/1/2, pose_goal or None, tried, chosen, summed IK iterations)."""
+        ee = np.ascontiguousarray(ee, np.float64)
+        cur = np.ascontiguousarray(cur, np.float64)
+        pose = np.zeros(8)
+        info = (ctypes.c_longlong * 3)()
+        r = lib().orc_find_goal_pose(self.h, _p(ee, _d), _p(cur, _d), float(disc_deg), int(self_), int(map_),
+                                     _p(pose, _d), info)
+        return r, (pose if r == 0 else None), info[0], info[1], info[2]
+
     def plan(self, start, goal, **kw):
         p = dict(DEFAULT_PARAMS)
         p.update(kw)
@@ -318,6 +355,44 @@ class Oracle:
                 lib().orc_get_cost_rows(self.h, _p(rows, _d))
             out["cost_rows"] = rows
         return out
+
+
+def ik_goal(ee):
+    """[x, y, z, qx, qy, qz, qw] of an end-effector pose [x, y, z, roll, pitch, yaw] (BS:1630-1645)."""
+    ee = np.ascontiguousarray(ee, np.float64)
+    g = np.zeros(7)
+    lib().orc_ik_goal(_p(ee, _d), _p(g, _d))
+    return g
+
+
+IK_DEV = np.array([[-0.005, 0.005]] * 3 + [[-0.025, 0.025]] * 3)  # findGoalPose's endEffectorDeviations (SP:1131-1137)
+
+
+def ik_tasks(ee, q_init, dev=IK_DEV):
+    """Rows of 27 doubles (goal quaternion pose, deviation lo[6], hi[6], q_init[8]) for Oracle.ik_solve."""
+    q_init = np.asarray(q_init, np.float64).reshape(-1, 8)
+    ee = np.asarray(ee, np.float64).reshape(-1, 6)
+    if len(ee) == 1:
+        ee = np.repeat(ee, len(q_init), 0)
+    dev = np.asarray(dev, np.float64).reshape(6, 2)
+    t = np.zeros((len(q_init), 27))
+    for i in range(len(q_init)):
+        t[i, :7] = ik_goal(ee[i])
+        t[i, 7:13] = dev[:, 0]
+        t[i, 13:19] = dev[:, 1]
+        t[i, 19:27] = q_init[i]
+    return t
+
+
+def goal_candidates(ee, cur, disc_deg=20.0):
+    """findGoalPose's candidate tasks (rows as ik_tasks) and the downward flag."""
+    ee = np.ascontiguousarray(ee, np.float64)
+    cur = np.ascontiguousarray(cur, np.float64)
+    n = lib().orc_goal_candidates(_p(ee, _d), _p(cur, _d), float(disc_deg), None, None)
+    t = np.zeros((n, 27))
+    down = ctypes.c_int(0)
+    lib().orc_goal_candidates(_p(ee, _d), _p(cur, _d), float(disc_deg), _p(t, _d), ctypes.byref(down))
+    return t, bool(down.value)
 
 
 def sincos(x):

@@ -950,6 +950,367 @@ struct Planner {
   }
 };
 
+// ------------------------------------------------------------------------------------------ IK goal search
+// Planner::findGoalPose (SP = squirrel_8dof_planner/src/squirrel_8dof_planner.cpp:1129-1201) ->
+// BiRRTstarPlanner::getFullPoseFromEEPose (BS:1627-1686) -> RobotController::run_VDLS_Control_Connector
+// (CL:3283-3712).  Unpinned choices (DESIGN.md "IK goal search"): portable sin/cos; KDL's Jacobian and
+// GetQuaternion as published (orocos_kdl chainjnttojacsolver.cpp, frames.cpp); the damped pseudo-inverse
+// sum_i s_i/(s_i^2+d^2) v_i u_i^T (CL:5591-5596) evaluated as J^T (J J^T + d^2 I)^-1 by Cholesky; the
+// manipulability product of the singular values > 1e-5 (CL:6061-6084) as prod(diag chol(J J^T)) when
+// chol(J J^T - 1e-10 I) has positive pivots (every singular value > 1e-5), else by cyclic Jacobi eigenvalues.
+
+static const int MAX_IK_SEG = 16;
+
+struct IkTask {
+  double goal[7];      // x, y, z, qx, qy, qz, qw (BS:1639-1645)
+  double lo[6], hi[6]; // endEffectorDeviations (setVariableConstraints, CL:1740-1761)
+  double q[8];         // poseInit (setStartConf, CL:1464-1495)
+  int max_iter;        // 1000 (BS:1670)
+};
+
+struct IkOut {
+  double q[8];
+  double err[6];
+  double manip;
+  int reached;  // REACHED (1) / ADVANCED (0), CL:3691-3710
+  int iters;
+  int fallback; // iterations that needed the Jacobi eigenvalue path
+};
+
+static const double IK_DT = 0.1;                      // delta_t_ (CL:3325)
+static const double IK_GAIN = 1.0;                    // error_gain_ (CL:306)
+static const double IK_MANIP_THR = (double)0.03f;     // min_manip_treshold_ (CL:3299), a float parameter (CL:5505)
+static const double IK_DAMP_MAX = (double)0.07f;      // max_damping_factor_ (CL:320), float parameter
+static const double IK_SV_EPS = 0.00001;              // CL:6073
+static const double IK_BOUND = 0.0001;                // is_error_within_bounds (CL:6925)
+
+// Goal quaternion of getFullPoseFromEEPose (BS:1630-1645).
+static void ik_goal_quat(const double* ee, double* g) {
+  double sx, cx, sy, cy, sz, cz;
+  psincos(ee[3] / 2, &sx, &cx);
+  psincos(ee[4] / 2, &sy, &cy);
+  psincos(ee[5] / 2, &sz, &cz);
+  g[0] = ee[0]; g[1] = ee[1]; g[2] = ee[2];
+  g[3] = sx * cy * cz - cx * sy * sz;
+  g[4] = cx * sy * cz + sx * cy * sz;
+  g[5] = cx * cy * sz - sx * sy * cz;
+  g[6] = cx * cy * cz + sx * sy * sz;
+}
+
+// KDL Rotation::GetQuaternion (frames.cpp), used by compute_FK (KM:302).
+static void get_quaternion(const double* R, double* x, double* y, double* z, double* w) {
+  double trace = R[0] + R[4] + R[8];
+  if (trace > 1e-12) {
+    double s = 0.5 / std::sqrt(trace + 1.0);
+    *w = 0.25 / s;
+    *x = (R[7] - R[5]) * s;
+    *y = (R[2] - R[6]) * s;
+    *z = (R[3] - R[1]) * s;
+  } else if (R[0] > R[4] && R[0] > R[8]) {
+    double s = 2.0 * std::sqrt(1.0 + R[0] - R[4] - R[8]);
+    *w = (R[7] - R[5]) / s;
+    *x = 0.25 * s;
+    *y = (R[1] + R[3]) / s;
+    *z = (R[2] + R[6]) / s;
+  } else if (R[4] > R[8]) {
+    double s = 2.0 * std::sqrt(1.0 + R[4] - R[0] - R[8]);
+    *w = (R[2] - R[6]) / s;
+    *x = (R[1] + R[3]) / s;
+    *y = 0.25 * s;
+    *z = (R[5] + R[7]) / s;
+  } else {
+    double s = 2.0 * std::sqrt(1.0 + R[8] - R[0] - R[4]);
+    *w = (R[3] - R[1]) / s;
+    *x = (R[2] + R[6]) / s;
+    *y = (R[5] + R[7]) / s;
+    *z = 0.25 * s;
+  }
+}
+
+// Segment frames of the 12-segment chain (KDL ChainFkSolverPos_recursive, KM:278-305; the same products as
+// ChainJntToJacSolver's T_tmp * segment.pose(q)): T[0] = I, T[s+1] = T[s] * (joint(q) * f_tip).
+static void chain_frames(const Robot& rb, const double* q, Frame* T) {
+  std::memset(&T[0], 0, sizeof(Frame));
+  T[0].R[0] = T[0].R[4] = T[0].R[8] = 1.0;
+  for (int s = 0; s < rb.n_seg; ++s) {
+    Frame J;
+    std::memset(&J, 0, sizeof(J));
+    if (rb.seg_type[s] == 1) {
+      rot2(&rb.seg_axis[s * 3], q[rb.seg_joint[s]], J.R);
+      for (int d = 0; d < 3; ++d) J.p[d] = rb.seg_origin[s * 3 + d];
+    } else if (rb.seg_type[s] == 2) {
+      J.R[0] = J.R[4] = J.R[8] = 1.0;
+      double qq = q[rb.seg_joint[s]];
+      for (int d = 0; d < 3; ++d) J.p[d] = rb.seg_origin[s * 3 + d] + rb.seg_axis[s * 3 + d] * qq;
+    } else {
+      J.R[0] = J.R[4] = J.R[8] = 1.0;
+    }
+    Frame F;
+    std::memcpy(F.R, &rb.seg_R[s * 9], 9 * sizeof(double));
+    std::memcpy(F.p, &rb.seg_p[s * 3], 3 * sizeof(double));
+    T[s + 1] = fmul(T[s], fmul(J, F));
+  }
+}
+
+// compute_FK (KM:278-305): [x, y, z, qx, qy, qz, qw] of the chain tip.
+static void ee_pose(const Robot& rb, const Frame* T, double* ee) {
+  const Frame& E = T[rb.n_seg];
+  ee[0] = E.p[0]; ee[1] = E.p[1]; ee[2] = E.p[2];
+  get_quaternion(E.R, &ee[3], &ee[4], &ee[5], &ee[6]);
+}
+
+// Cartesian error (set_EE_goal_pose CL:1690-1720 without, update_error_vec CL:2203-2239 with the deviation
+// clamp): position des - cur, orientation eta_c eps_d - eta_d eps_c - S(eps_d) eps_c.
+static void ik_error(const double* cur, const IkTask& t, bool clamp, double* e) {
+  const double* d = t.goal;
+  const double S[3][3] = {{0.0, -d[5], d[4]}, {d[5], 0.0, -d[3]}, {-d[4], d[3], 0.0}};
+  for (int i = 0; i < 6; ++i) {
+    if (i < 3) e[i] = d[i] - cur[i];
+    else e[i] = cur[6] * d[i] - d[6] * cur[i] - (S[i - 3][0] * cur[3] + S[i - 3][1] * cur[4] + S[i - 3][2] * cur[5]);
+  }
+  if (clamp)
+    for (int i = 0; i < 6; ++i) e[i] = (e[i] < t.lo[i] || e[i] > t.hi[i]) ? e[i] : 0.0;
+}
+
+// KDL ChainJntToJacSolver::JntToJac for the frames T of q: column k of the k-th movable segment s is
+// T[s].M * (joint twist referred to the segment tip), then moved to every later tip by
+// Twist::RefPoint(total.p - T_tmp.p).  Rows 0-2 linear, 3-5 angular; cast to float (getJacobian, CL:5273-5301).
+static void jacobian(const Robot& rb, const double* q, const Frame* T, double J[6][8]) {
+  int k = 0;
+  for (int s = 0; s < rb.n_seg; ++s) {
+    if (rb.seg_type[s] == 0) continue;
+    const double* ax = &rb.seg_axis[s * 3];
+    double M[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    if (rb.seg_type[s] == 1) rot2(ax, q[rb.seg_joint[s]], M);
+    const double* fp = &rb.seg_p[s * 3];
+    double v[3], rl[3], vl[3];
+    for (int r = 0; r < 3; ++r) v[r] = M[r * 3 + 0] * fp[0] + M[r * 3 + 1] * fp[1] + M[r * 3 + 2] * fp[2];
+    for (int d = 0; d < 3; ++d) {
+      rl[d] = rb.seg_type[s] == 1 ? ax[d] * 1.0 : 0.0;
+      vl[d] = rb.seg_type[s] == 2 ? ax[d] * 1.0 : 0.0;
+    }
+    double c0 = rl[1] * v[2] - rl[2] * v[1], c1 = rl[2] * v[0] - rl[0] * v[2], c2 = rl[0] * v[1] - rl[1] * v[0];
+    vl[0] = vl[0] + c0; vl[1] = vl[1] + c1; vl[2] = vl[2] + c2;
+    const double* B = T[s].R;
+    double vel[3], rot[3];
+    for (int r = 0; r < 3; ++r) {
+      vel[r] = B[r * 3 + 0] * vl[0] + B[r * 3 + 1] * vl[1] + B[r * 3 + 2] * vl[2];
+      rot[r] = B[r * 3 + 0] * rl[0] + B[r * 3 + 1] * rl[1] + B[r * 3 + 2] * rl[2];
+    }
+    for (int i = s + 1; i < rb.n_seg; ++i) {
+      double dl[3];
+      for (int d = 0; d < 3; ++d) dl[d] = T[i + 1].p[d] - T[i].p[d];
+      double x0 = rot[1] * dl[2] - rot[2] * dl[1], x1 = rot[2] * dl[0] - rot[0] * dl[2], x2 = rot[0] * dl[1] - rot[1] * dl[0];
+      vel[0] = vel[0] + x0; vel[1] = vel[1] + x1; vel[2] = vel[2] + x2;
+    }
+    for (int d = 0; d < 3; ++d) {
+      J[d][k] = (double)(float)vel[d];
+      J[3 + d][k] = (double)(float)rot[d];
+    }
+    ++k;
+  }
+}
+
+// Cholesky of M + shift*I (column by column, sums in ascending k).  Returns false if a pivot is <= 0.
+static bool cholesky6(const double A[6][6], double shift, double L[6][6]) {
+  bool pd = true;
+  for (int j = 0; j < 6; ++j) {
+    for (int i = j; i < 6; ++i) {
+      double s = i == j ? A[i][j] + shift : A[i][j];
+      for (int k = 0; k < j; ++k) s = s - L[i][k] * L[j][k];
+      if (i == j) {
+        if (!(s > 0.0)) pd = false;
+        L[j][j] = std::sqrt(s);
+      } else {
+        L[i][j] = s / L[j][j];
+      }
+    }
+  }
+  return pd;
+}
+
+// Cyclic Jacobi eigen-decomposition of a symmetric 6x6: eigenvalues on the diagonal of a, eigenvectors in the
+// columns of V (rows p < q in order, at most 30 sweeps).
+static void jacobi_eigen6(const double A[6][6], double a[6][6], double V[6][6]) {
+  std::memcpy(a, A, sizeof(double) * 36);
+  for (int i = 0; i < 6; ++i)
+    for (int k = 0; k < 6; ++k) V[i][k] = i == k ? 1.0 : 0.0;
+  for (int sweep = 0; sweep < 30; ++sweep) {
+    double off = 0.0;
+    for (int p = 0; p < 5; ++p)
+      for (int q = p + 1; q < 6; ++q) off = off + a[p][q] * a[p][q];
+    if (off == 0.0) break;
+    for (int p = 0; p < 5; ++p)
+      for (int q = p + 1; q < 6; ++q) {
+        double apq = a[p][q];
+        if (apq == 0.0) continue;
+        double theta = (a[q][q] - a[p][p]) / (2.0 * apq);
+        double t = (theta >= 0.0 ? 1.0 : -1.0) / (std::fabs(theta) + std::sqrt(theta * theta + 1.0));
+        double c = 1.0 / std::sqrt(t * t + 1.0), s = t * c;
+        for (int k = 0; k < 6; ++k) {
+          double vkp = V[k][p], vkq = V[k][q];
+          V[k][p] = c * vkp - s * vkq;
+          V[k][q] = s * vkp + c * vkq;
+          if (k == p || k == q) continue;
+          double akp = a[k][p], akq = a[k][q];
+          double np = c * akp - s * akq, nq = s * akp + c * akq;
+          a[k][p] = np; a[p][k] = np; a[k][q] = nq; a[q][k] = nq;
+        }
+        double app = a[p][p] - t * apq, aqq = a[q][q] + t * apq;
+        a[p][p] = app; a[q][q] = aqq; a[p][q] = 0.0; a[q][p] = 0.0;
+      }
+  }
+}
+
+// run_VDLS_Control_Connector (CL:3283-3712) for one start configuration and one goal pose.
+static void ik_solve(const Robot& rb, const IkTask& t, IkOut* o) {
+  double q[8];
+  for (int j = 0; j < 8; ++j) q[j] = t.q[j];
+  Frame T[MAX_IK_SEG + 1];
+  double ee[7], err[6];
+  chain_frames(rb, q, T);
+  ee_pose(rb, T, ee);
+  ik_error(ee, t, false, err);  // set_EE_goal_pose (CL:1689-1720)
+  bool within = false;          // CL:3328
+  int iter = 0, fallback = 0;
+  double manip = 0.0;
+  const double tau = IK_SV_EPS * IK_SV_EPS;
+  while (!within) {
+    double J[6][8], A[6][6], L[6][6], Lt[6][6], E[6][6], V[6][6];
+    jacobian(rb, q, T, J);
+    for (int i = 0; i < 6; ++i)
+      for (int k = 0; k < 6; ++k) {
+        double s = J[i][0] * J[k][0];
+        for (int c = 1; c < 8; ++c) s = s + J[i][c] * J[k][c];
+        A[i][k] = s;
+      }
+    // computeManipulabilityMeasure (CL:6050-6089)
+    cholesky6(A, 0.0, L);
+    const bool normal = cholesky6(A, -tau, Lt);
+    if (normal) {
+      manip = 1.0;
+      for (int j = 0; j < 6; ++j) manip = manip * L[j][j];
+    } else {
+      jacobi_eigen6(A, E, V);
+      manip = 1.0;
+      for (int j = 0; j < 6; ++j) {
+        double sv = std::sqrt(E[j][j] > 0.0 ? E[j][j] : 0.0);
+        if (std::fabs(sv) > IK_SV_EPS) manip = manip * std::fabs(sv);
+      }
+      ++fallback;
+    }
+    if (manip == 1.0 || manip < 0.00001) manip = 0.0001;
+    // compute_J_vdls (CL:5505-5614)
+    double damp = 0.0;
+    if (manip < IK_MANIP_THR)
+      damp = IK_DAMP_MAX * ((1 - (manip / IK_MANIP_THR)) * (1 - (manip / IK_MANIP_THR)));
+    if (normal && damp != 0.0) cholesky6(A, damp * damp, L);
+    // q_dot (CL:3455-3497): J_vdls row c = column c of (A + d^2 I)^-1 J -- by the Cholesky factor, or (a singular
+    // value <= 1e-5) by the eigenvectors u_i of A: sum_i (J^T u_i)_c u_i / (max(lambda_i, 0) + d^2)
+    double coef[6];
+    if (!normal)
+      for (int i = 0; i < 6; ++i) coef[i] = 1.0 / ((E[i][i] > 0.0 ? E[i][i] : 0.0) + damp * damp);
+    double qd[8];
+    for (int c = 0; c < 8; ++c) {
+      double y[6], x[6];
+      if (!normal) {
+        for (int j = 0; j < 6; ++j) x[j] = 0.0;
+        for (int i = 0; i < 6; ++i) {
+          double w = J[0][c] * V[0][i];
+          for (int k = 1; k < 6; ++k) w = w + J[k][c] * V[k][i];
+          const double cw = coef[i] * w;
+          for (int j = 0; j < 6; ++j) x[j] = x[j] + cw * V[j][i];
+        }
+      } else {
+        for (int i = 0; i < 6; ++i) {
+          double s = J[i][c];
+          for (int k = 0; k < i; ++k) s = s - L[i][k] * y[k];
+          y[i] = s / L[i][i];
+        }
+        for (int i = 5; i >= 0; --i) {
+          double s = y[i];
+          for (int k = i + 1; k < 6; ++k) s = s - L[k][i] * x[k];
+          x[i] = s / L[i][i];
+        }
+      }
+      double v = 0.0;
+      for (int j = 0; j < 6; ++j) v = v + x[j] * (0.0 + IK_GAIN * err[j]);
+      qd[c] = v;
+    }
+    // joint update with the joint-limit check (CL:3504-3550, KM:680-703)
+    int c = 0;
+    for (int s = 0; s < rb.n_seg; ++s) {
+      if (rb.seg_type[s] == 0) continue;
+      int j = rb.seg_joint[s];
+      double nv = q[j] + qd[c] * IK_DT;
+      if (!(nv < rb.q_min[j] || nv > rb.q_max[j])) q[j] = nv;
+      ++c;
+    }
+    chain_frames(rb, q, T);
+    ee_pose(rb, T, ee);
+    ik_error(ee, t, true, err);
+    within = true;
+    for (int i = 0; i < 6; ++i)
+      if (std::fabs(err[i]) > IK_BOUND) within = false;
+    ++iter;
+    if (iter == t.max_iter) break;
+  }
+  for (int j = 0; j < 8; ++j) o->q[j] = q[j];
+  for (int i = 0; i < 6; ++i) o->err[i] = err[i];
+  o->manip = manip;
+  o->reached = iter == t.max_iter ? 0 : 1;
+  o->iters = iter;
+  o->fallback = fallback;
+}
+
+// Base-angle candidates and start configurations of Planner::findGoalPose (SP:1129-1194), in the order the
+// reference tries them.  getEndEffectorDirection (SP:1639-1661): the y axis of tf setRPY(roll, pitch, yaw).
+static bool ee_downward(const double* ee) {
+  double sr, cr, sp, cp, sy, cy;
+  psincos(ee[3] * 0.5, &sr, &cr);
+  psincos(ee[4] * 0.5, &sp, &cp);
+  psincos(ee[5] * 0.5, &sy, &cy);
+  double x = sr * cp * cy - cr * sp * sy, y = cr * sp * cy + sr * cp * sy;
+  double z = cr * cp * sy - sr * sp * cy, w = cr * cp * cy + sr * sp * sy;
+  double d = x * x + y * y + z * z + w * w, s = 2.0 / d;
+  double xs = x * s, ys = y * s, zs = z * s;
+  double wx = w * xs, yy = y * ys, yz = y * zs, xx = x * xs;
+  double az = (x * zs - w * ys) * 0.0 + (yz + wx) * 1.0 + (1.0 - (xx + yy)) * 0.0;
+  return !(std::fabs(az) < 0.9);
+}
+
+static int goal_candidates(const double* ee, const double* cur, double disc_deg, std::vector<IkTask>& tasks) {
+  if (disc_deg < 1) disc_deg = 1.0;  // SP:80-83
+  const double disc = disc_deg * (M_PI / 180.0);
+  const bool down = ee_downward(ee);
+  const double dist = down ? 0.44 : 0.47;
+  const double arm_down[5] = {-0.8, 0.8, 0.0, -1.5, 0.0}, arm_side[5] = {-1.2, 1.1, 0.0, 0.7, -1.5};
+  const double gx = ee[0] - cur[0], gy = ee[1] - cur[1];
+  const double start = gy > 0 ? std::acos(gx / std::sqrt(std::pow(gx, 2) + std::pow(gy, 2)))
+                              : -std::acos(gx / std::sqrt(std::pow(gx, 2) + std::pow(gy, 2)));
+  IkTask t;
+  double g[7];
+  ik_goal_quat(ee, g);
+  for (int i = 0; i < 7; ++i) t.goal[i] = g[i];
+  for (int i = 0; i < 3; ++i) { t.lo[i] = -0.005; t.hi[i] = 0.005; t.lo[i + 3] = -0.025; t.hi[i + 3] = 0.025; }
+  t.max_iter = 1000;
+  double diff = 0.0;
+  while (std::fabs(diff) < M_PI) {
+    const double a = start + diff;
+    double sa, ca;
+    psincos(a, &sa, &ca);
+    t.q[0] = ee[0] - dist * ca;
+    t.q[1] = ee[1] - dist * sa;
+    t.q[2] = a + 0.99;
+    for (int j = 0; j < 5; ++j) t.q[3 + j] = down ? arm_down[j] : arm_side[j];
+    tasks.push_back(t);
+    diff *= -1;
+    diff += 0.0;
+    if (diff >= 0.0) diff += disc;
+  }
+  return down ? 1 : 0;
+}
+
 }  // namespace orc
 
 // ============================================================================================ C ABI
@@ -1195,6 +1556,88 @@ int orc_get_tree(void* hp, int which, int* parent, double* conf, double* cost) {
     if (cost) { cost[3 * i] = t.nodes[i].cost.total; cost[3 * i + 1] = t.nodes[i].cost.rev; cost[3 * i + 2] = t.nodes[i].cost.prism; }
   }
   return (int)t.nodes.size();
+}
+
+// IK (getFullPoseFromEEPose -> run_VDLS_Control_Connector) for n tasks: tasks[i] = goal[7], lo[6], hi[6], q[8]
+// (27 doubles), max_iter shared; out[i] = q[8], err[6], manip (15 doubles); st[i] = reached, iters, fallback.
+void orc_ik_solve(void* hp, const double* tasks, int n, int max_iter, double* out, int* st) {
+  orc_handle* h = (orc_handle*)hp;
+  for (int i = 0; i < n; ++i) {
+    orc::IkTask t;
+    const double* a = tasks + (size_t)27 * i;
+    std::memcpy(t.goal, a, 7 * sizeof(double));
+    std::memcpy(t.lo, a + 7, 6 * sizeof(double));
+    std::memcpy(t.hi, a + 13, 6 * sizeof(double));
+    std::memcpy(t.q, a + 19, 8 * sizeof(double));
+    t.max_iter = max_iter;
+    orc::IkOut o;
+    orc::ik_solve(*h->rb, t, &o);
+    std::memcpy(out + (size_t)15 * i, o.q, 8 * sizeof(double));
+    std::memcpy(out + (size_t)15 * i + 8, o.err, 6 * sizeof(double));
+    out[(size_t)15 * i + 14] = o.manip;
+    st[3 * i] = o.reached; st[3 * i + 1] = o.iters; st[3 * i + 2] = o.fallback;
+  }
+}
+
+// compute_FK pose (7) and the float-cast KDL Jacobian (6 x 8, row-major) of n configurations (checker input).
+void orc_ik_fk_jac(void* hp, const double* q, int n, double* ee, double* J) {
+  orc_handle* h = (orc_handle*)hp;
+  orc::Frame T[orc::MAX_IK_SEG + 1];
+  for (int i = 0; i < n; ++i) {
+    orc::chain_frames(*h->rb, q + 8 * i, T);
+    if (ee) orc::ee_pose(*h->rb, T, ee + 7 * i);
+    if (J) {
+      double Jm[6][8];
+      orc::jacobian(*h->rb, q + 8 * i, T, Jm);
+      std::memcpy(J + 48 * i, Jm, sizeof(Jm));
+    }
+  }
+}
+
+// Goal quaternion of an end-effector pose [x, y, z, roll, pitch, yaw] (BS:1630-1645).
+void orc_ik_goal(const double* ee, double* g) { orc::ik_goal_quat(ee, g); }
+
+// Candidate tasks of findGoalPose (27 doubles each as orc_ik_solve); returns their number (tasks may be NULL).
+int orc_goal_candidates(const double* ee, const double* cur, double disc_deg, double* tasks, int* downward) {
+  std::vector<orc::IkTask> ts;
+  int d = orc::goal_candidates(ee, cur, disc_deg, ts);
+  if (downward) *downward = d;
+  if (tasks)
+    for (size_t i = 0; i < ts.size(); ++i) {
+      double* a = tasks + 27 * i;
+      std::memcpy(a, ts[i].goal, 7 * sizeof(double));
+      std::memcpy(a + 7, ts[i].lo, 6 * sizeof(double));
+      std::memcpy(a + 13, ts[i].hi, 6 * sizeof(double));
+      std::memcpy(a + 19, ts[i].q, 8 * sizeof(double));
+    }
+  return (int)ts.size();
+}
+
+// Planner::findGoalPose (SP:1129-1201): candidates in order, IK then isConfigValid, first valid wins.
+// Returns 0 (pose_goal set), 1 (an IK solution exists but collides) or 2 (no IK solution); info = {candidates
+// tried, candidate chosen or -1, IK iterations summed over the tried candidates}.
+int orc_find_goal_pose(void* hp, const double* ee, const double* cur, double disc_deg, int self, int map,
+                       double* pose_goal, long long* info) {
+  orc_handle* h = (orc_handle*)hp;
+  std::vector<orc::IkTask> ts;
+  orc::goal_candidates(ee, cur, disc_deg, ts);
+  bool found = false;
+  long long iters = 0;
+  for (size_t i = 0; i < ts.size(); ++i) {
+    orc::IkOut o;
+    orc::ik_solve(*h->rb, ts[i], &o);
+    iters += o.iters;
+    if (o.reached) {
+      found = true;
+      if (!h->ck.in_collision(o.q, self, map)) {
+        std::memcpy(pose_goal, o.q, 8 * sizeof(double));
+        if (info) { info[0] = (long long)i + 1; info[1] = (long long)i; info[2] = iters; }
+        return 0;
+      }
+    }
+  }
+  if (info) { info[0] = (long long)ts.size(); info[1] = -1; info[2] = iters; }
+  return found ? 1 : 2;
 }
 
 int orc_get_cost_rows(void* hp, double* rows) {

@@ -67,6 +67,19 @@ class Result(ctypes.Structure):
                 ("cost_rows", _pd)]
 
 
+class IkRequest(ctypes.Structure):
+    _fields_ = [("ee_pose", _d * 6), ("deviation", (_d * 2) * 6), ("q_init", _d * 8), ("max_iter", _i)]
+
+
+class IkResult(ctypes.Structure):
+    _fields_ = [("reached", _i), ("iterations", _i), ("fallback_iterations", _i), ("q", _d * 8), ("error", _d * 6),
+                ("manipulability", _d)]
+
+
+class GoalSearch(ctypes.Structure):
+    _fields_ = [("n_candidates", _i), ("n_reached", _i), ("chosen", _i), ("downward", _i), ("kernel_ms", _d)]
+
+
 # (name, restype, argtypes) of every symbol declared in include/smp_gpu.h
 EXPORTS = [
     ("smp_params_default", None, [ctypes.POINTER(Params)]),
@@ -99,6 +112,8 @@ EXPORTS = [
     ("smp_is_config_valid", _i, [_p, _pd, _i, _i, ctypes.POINTER(_i)]),
     ("smp_check_sequence", _i, [_p, _pd, _i64, _i, _i, ctypes.POINTER(_i64)]),
     ("smp_normalize_trajectory", _i, [_pd, _i64, _i, _pd, _pd, _i64, ctypes.POINTER(_i64)]),
+    ("smp_ik_solve", _i, [_p, ctypes.POINTER(IkRequest), _i, ctypes.POINTER(IkResult)]),
+    ("smp_find_goal_pose", _i, [_p, _pd, _pd, _d, _i, _i, _pd, ctypes.POINTER(_i), ctypes.POINTER(GoalSearch)]),
     ("smp_last_kernel_ms", _i, [_p, _pd, _pd, ctypes.POINTER(_i64)]),
     ("smp_strerror", ctypes.c_char_p, [_i]),
 ]

@@ -16,6 +16,7 @@
 
 #include "../../include/smp_gpu.h"
 #include "smp_host.h"
+#include "smp_ik.h"
 #include "smp_math.h"
 #include "smp_plan.h"
 #include "smp_types.h"
@@ -28,6 +29,9 @@ __global__ void plan_kernel(const RobotDev* rb, SceneDev sc, const MapCfg* mc, Q
 __global__ void helper_kernel(const RobotDev* rb, SceneDev sc, const MapCfg* mc, QueryDev* qs, int nq);
 __global__ void path_kernel(QueryDev* qs, int* counts);
 size_t check_kernels_private_bytes();
+size_t ik_kernels_private_bytes();
+__global__ void ik_kernel(const RobotDev* rb, const IkTaskDev* tasks, int n, IkOutDev* out);
+__global__ void ik_gather_kernel(const IkOutDev* out, int n, double* q_soa);
 __global__ void sincos_kernel(const double* x, int n, double* s, double* c);
 __global__ void u01_kernel(unsigned long long seed, unsigned query, const uint32_t* ctr, int n, double* out);
 __global__ void fk_kernel(const RobotDev* rb, const double* q, int n, double* frames, double* eez);
@@ -121,6 +125,8 @@ struct smp_planner {
   DBuf<int> d_counts;
   DBuf<double> d_cq;
   DBuf<uint8_t> d_valid;
+  DBuf<IkTaskDev> d_ik_tasks;
+  DBuf<IkOutDev> d_ik_out;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   double last_check_ms = 0, last_plan_ms = 0;
   int64_t last_plan_launches = 0;
@@ -351,6 +357,7 @@ int smp_planner_create(int device, const smp_robot* robot, const smp_params* par
     for (const void* k : ks)
       if (hipFuncGetAttributes(&fa, k) == hipSuccess) need = std::max(need, (size_t)fa.localSizeBytes);
     need = std::max(need, check_kernels_private_bytes());
+    need = std::max(need, ik_kernels_private_bytes());
     size_t cur = 0;
     if (hipDeviceGetLimit(&cur, hipLimitStackSize) == hipSuccess && cur < need) {
       need = (need + 255) / 256 * 256;
@@ -486,6 +493,109 @@ int smp_is_config_valid(smp_planner* p, const double q[8], int check_self, int c
   int st = smp_check_configs(p, soa, 1, check_self, check_map, &v);
   *valid = v;
   return st;
+}
+
+// IK controller runs (getFullPoseFromEEPose, birrt_star.cpp:1627-1686): one wavefront per task.  Launches
+// ik_kernel on p->stream and, with check != 0, gathers the final configurations and checks them (isConfigValid,
+// birrt_star.cpp:6897-6908) in the same stream; one host synchronisation.
+static int ik_run(smp_planner* p, const std::vector<IkTaskDev>& tasks, std::vector<IkOutDev>& outs, int check,
+                  int check_self, int check_map, std::vector<uint8_t>* valid, double* ms) {
+  const int n = (int)tasks.size();
+  outs.assign(n, IkOutDev{});
+  if (n == 0) return SMP_OK;
+  HIPCHK(hipSetDevice(p->device));
+  HIPCHK(p->d_ik_tasks.reserve(n));
+  HIPCHK(p->d_ik_out.reserve(n));
+  HIPCHK(hipMemcpyAsync(p->d_ik_tasks.p, tasks.data(), n * sizeof(IkTaskDev), hipMemcpyHostToDevice, p->stream));
+  HIPCHK(hipEventRecord(p->ev0, p->stream));
+  hipLaunchKernelGGL(ik_kernel, dim3(n), dim3(IK_THREADS), 0, p->stream, p->d_rb, p->d_ik_tasks.p, n, p->d_ik_out.p);
+  HIPCHK(hipGetLastError());
+  if (check) {
+    HIPCHK(p->d_cq.reserve((size_t)n * NJ));
+    HIPCHK(p->d_valid.reserve((size_t)n));
+    hipLaunchKernelGGL(ik_gather_kernel, dim3((n * NJ + 255) / 256), dim3(256), 0, p->stream, p->d_ik_out.p, n,
+                       p->d_cq.p);
+    HIPCHK(hipGetLastError());
+    const long long tiles = (n + 7) / 8;
+    launch_check(8, (int)std::min<long long>(tiles, 256 * 8), p->stream, p->d_rb, p->sc, p->d_mc, p->d_cq.p,
+                 (long long)n, check_self, check_map && p->have_scene, p->d_valid.p, nullptr);
+    HIPCHK(hipGetLastError());
+  }
+  HIPCHK(hipEventRecord(p->ev1, p->stream));
+  HIPCHK(hipMemcpyAsync(outs.data(), p->d_ik_out.p, n * sizeof(IkOutDev), hipMemcpyDeviceToHost, p->stream));
+  if (check) {
+    valid->assign(n, 0);
+    HIPCHK(hipMemcpyAsync(valid->data(), p->d_valid.p, n, hipMemcpyDeviceToHost, p->stream));
+  }
+  HIPCHK(hipStreamSynchronize(p->stream));
+  float f = 0;
+  HIPCHK(hipEventElapsedTime(&f, p->ev0, p->ev1));
+  if (ms) *ms = f;
+  return SMP_OK;
+}
+
+int smp_ik_solve(smp_planner* p, const smp_ik_request* reqs, int n, smp_ik_result* out) {
+  if (!p || n < 0 || (n > 0 && (!reqs || !out))) return SMP_ERR_ARG;
+  if (n == 0) return SMP_OK;
+  std::vector<IkTaskDev> tasks(n);
+  for (int i = 0; i < n; ++i) {
+    const smp_ik_request& r = reqs[i];
+    if (r.max_iter < 1) return SMP_ERR_ARG;
+    IkTaskDev& t = tasks[i];
+    std::memset(&t, 0, sizeof(t));
+    ik_goal_quat(r.ee_pose, t.goal);
+    for (int k = 0; k < 6; ++k) { t.lo[k] = r.deviation[k][0]; t.hi[k] = r.deviation[k][1]; }
+    for (int j = 0; j < NJ; ++j) t.q[j] = r.q_init[j];
+    t.max_iter = r.max_iter;
+  }
+  std::vector<IkOutDev> outs;
+  double ms = 0;
+  const int st = ik_run(p, tasks, outs, 0, 0, 0, nullptr, &ms);
+  if (st != SMP_OK) return st;
+  p->last_check_ms = ms;
+  for (int i = 0; i < n; ++i) {
+    smp_ik_result& o = out[i];
+    o.reached = outs[i].reached;
+    o.iterations = outs[i].iters;
+    o.fallback_iterations = outs[i].fallback;
+    for (int j = 0; j < NJ; ++j) o.q[j] = outs[i].q[j];
+    for (int k = 0; k < 6; ++k) o.error[k] = outs[i].err[k];
+    o.manipulability = outs[i].manip;
+  }
+  return SMP_OK;
+}
+
+int smp_find_goal_pose(smp_planner* p, const double ee_pose[6], const double pose_current[8], double discretization_deg,
+                       int check_self, int check_map, double pose_goal[8], int* result, smp_goal_search* info) {
+  if (!p || !ee_pose || !pose_current || !pose_goal || !result || !(discretization_deg == discretization_deg))
+    return SMP_ERR_ARG;
+  int n = 0;
+  ik_goal_candidates(ee_pose, pose_current, discretization_deg, nullptr, 0, &n);
+  std::vector<IkTaskDev> tasks(n);
+  const int down = ik_goal_candidates(ee_pose, pose_current, discretization_deg, tasks.data(), n, &n);
+  std::vector<IkOutDev> outs;
+  std::vector<uint8_t> valid;
+  double ms = 0;
+  const int st = ik_run(p, tasks, outs, 1, check_self, check_map, &valid, &ms);
+  if (st != SMP_OK) return st;
+  p->last_check_ms = ms;
+  int chosen = -1, reached = 0;
+  for (int i = 0; i < n; ++i) {
+    if (!outs[i].reached) continue;
+    ++reached;
+    if (chosen < 0 && valid[i]) chosen = i;
+  }
+  *result = chosen >= 0 ? 0 : (reached ? 1 : 2);
+  if (chosen >= 0)
+    for (int j = 0; j < NJ; ++j) pose_goal[j] = outs[chosen].q[j];
+  if (info) {
+    info->n_candidates = n;
+    info->n_reached = reached;
+    info->chosen = chosen;
+    info->downward = down;
+    info->kernel_ms = ms;
+  }
+  return SMP_OK;
 }
 
 int smp_last_kernel_ms(const smp_planner* p, double* check_ms, double* plan_ms, int64_t* plan_launches) {

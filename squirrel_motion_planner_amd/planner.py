@@ -182,6 +182,48 @@ class GpuPlanner:
                                        ctypes.byref(first)), "smp_check_sequence")
         return first.value
 
+    def ik_solve(self, ee_poses, q_inits, deviation=None, max_iter=1000):
+        """getFullPoseFromEEPose's controller (run_VDLS_Control_Connector) for n (end-effector pose, start
+        configuration) pairs, one wavefront each.  ee_poses: (n, 6) or one (6,) pose for every start; deviation: (6, 2)
+        error bands (default: findGoalPose's).  Returns dict of arrays q (n, 8), reached, iterations, error, manip."""
+        q_inits = np.asarray(q_inits, np.float64).reshape(-1, 8)
+        ee = np.asarray(ee_poses, np.float64).reshape(-1, 6)
+        if len(ee) == 1:
+            ee = np.repeat(ee, len(q_inits), 0)
+        dev = np.asarray(IK_DEVIATION if deviation is None else deviation, np.float64).reshape(6, 2)
+        n = len(q_inits)
+        reqs = (L.IkRequest * max(n, 1))()
+        for i in range(n):
+            r = reqs[i]
+            for k in range(6):
+                r.ee_pose[k] = float(ee[i, k])
+                r.deviation[k][0], r.deviation[k][1] = float(dev[k, 0]), float(dev[k, 1])
+            for j in range(8):
+                r.q_init[j] = float(q_inits[i, j])
+            r.max_iter = int(max_iter)
+        res = (L.IkResult * max(n, 1))()
+        check(lib().smp_ik_solve(self.h, reqs, n, res), "smp_ik_solve")
+        return dict(q=np.array([list(r.q) for r in res[:n]]).reshape(n, 8),
+                    reached=np.array([r.reached for r in res[:n]], np.int32),
+                    iterations=np.array([r.iterations for r in res[:n]], np.int32),
+                    fallback=np.array([r.fallback_iterations for r in res[:n]], np.int32),
+                    error=np.array([list(r.error) for r in res[:n]]).reshape(n, 6),
+                    manip=np.array([r.manipulability for r in res[:n]]))
+
+    def find_goal_pose(self, ee_pose, pose_current, discretization_deg=20.0, check_self=True, check_map=True):
+        """Planner::findGoalPose -> (result 0 found / 1 collision / 2 no IK solution, pose_goal or None, info dict)."""
+        ee = np.ascontiguousarray(ee_pose, np.float64).reshape(6)
+        cur = np.ascontiguousarray(pose_current, np.float64).reshape(8)
+        goal = np.zeros(8)
+        res = ctypes.c_int()
+        info = L.GoalSearch()
+        check(lib().smp_find_goal_pose(self.h, ee.ctypes.data_as(_pd), cur.ctypes.data_as(_pd),
+                                       float(discretization_deg), int(check_self), int(check_map),
+                                       goal.ctypes.data_as(_pd), ctypes.byref(res), ctypes.byref(info)),
+              "smp_find_goal_pose")
+        d = {f: getattr(info, f) for f, _ in L.GoalSearch._fields_}
+        return res.value, (goal if res.value == 0 else None), d
+
     def last_kernel_ms(self):
         a, b = ctypes.c_double(), ctypes.c_double()
         n = ctypes.c_int64()
@@ -246,6 +288,9 @@ class GpuPlanner:
             lib().smp_planner_destroy(self.h)
             self.h = None
 
+
+# findGoalPose's endEffectorDeviations (squirrel_8dof_planner.cpp:1131-1137)
+IK_DEVIATION = [(-0.005, 0.005)] * 3 + [(-0.025, 0.025)] * 3
 
 _CALL_FAILURES = (L.SMP_ERR_HIP, L.SMP_ERR_NO_DEVICE, L.SMP_ERR_PARSE)
 
@@ -349,6 +394,15 @@ class BiRRTstarPlanner:
 
     def getJointTrajectoryRef(self):
         return self._traj
+
+    def getFullPoseFromEEPose(self, endEffectorPose, endEffectorDeviations, poseInit, poseSolution):
+        """birrt_star.cpp:1627-1686: the VDLS controller from poseInit towards endEffectorPose (x, y, z, roll, pitch,
+        yaw); on REACHED fills the list poseSolution with the final configuration and returns True."""
+        r = self._gpu.ik_solve([endEffectorPose], [poseInit], deviation=endEffectorDeviations)
+        if not r["reached"][0]:
+            return False
+        poseSolution[:] = [float(v) for v in r["q"][0]]
+        return True
 
 
 def normalize_trajectory(raw, normalized_pose):

@@ -63,5 +63,18 @@ int main(int argc, char** argv) {
   std::vector<double> short_conf(start.begin(), start.begin() + 7);
   std::printf("dim_mismatch_rejected %d\n", planner.init_planner(short_conf, goal, 1, true, true) ? 0 : 1);
   std::printf("start_valid %d\n", planner.isConfigValid(start, true, true) ? 1 : 0);
+  // goal search of find_plan_end_effector (SP:578, 1129-1201) and one getFullPoseFromEEPose call (SP:1179)
+  std::vector<double> ee = {start[0] + 0.6, start[1] + 0.2, 0.5, 1.57, 0.0, 0.3}, pose_goal;
+  int res = planner.findGoalPose(ee, start, 20.0, true, true, pose_goal);
+  std::printf("goal_search %d", res);
+  for (double v : pose_goal) std::printf(" %.17g", v);
+  std::printf("\n");
+  std::vector<std::pair<double, double> > dev(3, std::make_pair(-0.005, 0.005));
+  dev.resize(6, std::make_pair(-0.025, 0.025));
+  std::vector<double> init = {ee[0] - 0.47, ee[1], 0.99, -1.2, 1.1, 0.0, 0.7, -1.5}, sol;
+  bool ik = planner.getFullPoseFromEEPose(ee, dev, init, sol);
+  std::printf("ee_ik %d", ik ? 1 : 0);
+  for (double v : sol) std::printf(" %.17g", v);
+  std::printf("\n");
   return 0;
 }

@@ -66,8 +66,21 @@ def test_shim_node_sequence_matches_oracle(tmp_path):
     assert lines[2 + n] == "dim_mismatch_rejected 1"
     assert lines[3 + n] == "start_valid 1"
     res, keys = octomap_bt.read_bt(open(bt, "rb").read())
-    o = O.Oracle(O.OracleRobot(MODEL), O.OracleScene(keys, res)).plan(
-        sc.start, sc.goal, env_x=sc.env_x, env_y=sc.env_y, max_iter=iters, seed=seed)
+    orc = O.Oracle(O.OracleRobot(MODEL), O.OracleScene(keys, res))
+    # findGoalPose / getFullPoseFromEEPose through the shim
+    ee = [sc.start[0] + 0.6, sc.start[1] + 0.2, 0.5, 1.57, 0.0, 0.3]
+    gs = lines[4 + n].split()
+    ores, opose, _, _, _ = orc.find_goal_pose(ee, sc.start, 20.0, True, True)
+    assert gs[0] == "goal_search" and int(gs[1]) == ores
+    if ores == 0:
+        assert np.array_equal(np.array([float(v) for v in gs[2:]]), opose)
+    ik = lines[5 + n].split()
+    init = [ee[0] - 0.47, ee[1], 0.99, -1.2, 1.1, 0.0, 0.7, -1.5]
+    oi = orc.ik_solve(O.ik_tasks(ee, [init]))
+    assert ik[0] == "ee_ik" and int(ik[1]) == oi["reached"][0]
+    if oi["reached"][0]:
+        assert np.array_equal(np.array([float(v) for v in ik[2:]]), oi["q"][0])
+    o = orc.plan(sc.start, sc.goal, env_x=sc.env_x, env_y=sc.env_y, max_iter=iters, seed=seed)
     assert lines[0] == "status %d" % o["status"]
     assert checked == o["checked"]
     assert path.shape == o["path"].reshape(-1, 8).shape
