@@ -31,7 +31,8 @@
  *                              RobotController::run_VDLS_Control_Connector (control_laws.cpp:3283-3712):
  *                              n independent controller runs, one wavefront each
  *   smp_find_goal_pose         Planner::findGoalPose (squirrel_8dof_planner.cpp:1129-1201): every candidate base
- *                              angle's controller run at once, then one batch validity check, first valid in order
+ *                              angle's controller run at once, each REACHED pose checked in the same kernel, the
+ *                              first valid one in the reference's order (later candidates stop once it is known)
  *   smp_result_free            releases library-owned result buffers
  *   smp_strerror               text of a status code
  *
@@ -224,8 +225,9 @@ typedef struct smp_ik_result {
 int smp_ik_solve(smp_planner* p, const smp_ik_request* reqs, int n, smp_ik_result* out);
 
 typedef struct smp_goal_search {
-  int n_candidates;         /* base angles of the search (2 * ceil(180 / discretization) - 1 or so) */
-  int n_reached;            /* candidates whose controller run REACHED the pose */
+  int n_candidates;         /* base angles of the search (17 at the default 20 degrees) */
+  int n_reached;            /* candidates whose controller run REACHED the pose; candidates after the chosen one may
+                               have stopped early (they can no longer be chosen), so this counts the ones that ran */
   int chosen;               /* candidate index of pose_goal, -1 if none */
   int downward;             /* 1 if the hand points downward (squirrel_8dof_planner.cpp:1140) */
   double kernel_ms;         /* IK + validity kernels, HIP events */

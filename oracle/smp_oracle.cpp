@@ -1111,19 +1111,31 @@ static void jacobian(const Robot& rb, const double* q, const Frame* T, double J[
   }
 }
 
-// Cholesky of M + shift*I (column by column, sums in ascending k).  Returns false if a pivot is <= 0.
-static bool cholesky6(const double A[6][6], double shift, double L[6][6]) {
+// Gauss-Jordan elimination of the augmented [B | rhs] (6 x 7, no pivoting: B is symmetric positive definite on
+// this path): step k divides every other row's column-k entry by the pivot and subtracts that multiple of row k
+// from the row's columns > k.  The pivots are those of B's LDL^T; the solution is z_i = M[i][6] / M[i][i].
+static void gauss_jordan6(double M[6][7], double* z) {
+  for (int k = 0; k < 6; ++k)
+    for (int i = 0; i < 6; ++i) {
+      if (i == k) continue;
+      const double f = M[i][k] / M[k][k];
+      for (int j = k + 1; j < 7; ++j) M[i][j] = M[i][j] - f * M[k][j];
+    }
+  for (int i = 0; i < 6; ++i) z[i] = M[i][6] / M[i][i];
+}
+
+// Positive definiteness of A - tau I by symmetric elimination of the upper triangle (the LDL^T pivots): every
+// singular value of J exceeds sqrt(tau) iff every pivot is > 0.
+static bool shifted_pd6(const double A[6][6], double tau) {
+  double P[6][6];
+  for (int i = 0; i < 6; ++i)
+    for (int j = i; j < 6; ++j) P[i][j] = i == j ? A[i][i] + (-tau) : A[i][j];
   bool pd = true;
-  for (int j = 0; j < 6; ++j) {
-    for (int i = j; i < 6; ++i) {
-      double s = i == j ? A[i][j] + shift : A[i][j];
-      for (int k = 0; k < j; ++k) s = s - L[i][k] * L[j][k];
-      if (i == j) {
-        if (!(s > 0.0)) pd = false;
-        L[j][j] = std::sqrt(s);
-      } else {
-        L[i][j] = s / L[j][j];
-      }
+  for (int k = 0; k < 6; ++k) {
+    if (!(P[k][k] > 0.0)) pd = false;
+    for (int i = k + 1; i < 6; ++i) {
+      const double f = P[k][i] / P[k][k];
+      for (int j = i; j < 6; ++j) P[i][j] = P[i][j] - f * P[k][j];
     }
   }
   return pd;
@@ -1176,7 +1188,7 @@ static void ik_solve(const Robot& rb, const IkTask& t, IkOut* o) {
   double manip = 0.0;
   const double tau = IK_SV_EPS * IK_SV_EPS;
   while (!within) {
-    double J[6][8], A[6][6], L[6][6], Lt[6][6], E[6][6], V[6][6];
+    double J[6][8], A[6][6], M[6][7], E[6][6], V[6][6], z[6], ep[6];
     jacobian(rb, q, T, J);
     for (int i = 0; i < 6; ++i)
       for (int k = 0; k < 6; ++k) {
@@ -1184,12 +1196,18 @@ static void ik_solve(const Robot& rb, const IkTask& t, IkOut* o) {
         for (int c = 1; c < 8; ++c) s = s + J[i][c] * J[k][c];
         A[i][k] = s;
       }
-    // computeManipulabilityMeasure (CL:6050-6089)
-    cholesky6(A, 0.0, L);
-    const bool normal = cholesky6(A, -tau, Lt);
+    for (int i = 0; i < 6; ++i) ep[i] = 0.0 + IK_GAIN * err[i];  // current_goal_ee_vel_ + error_gain_ * error_
+    for (int i = 0; i < 6; ++i) {
+      for (int k = 0; k < 6; ++k) M[i][k] = A[i][k];
+      M[i][6] = ep[i];
+    }
+    // computeManipulabilityMeasure (CL:6050-6089): product of the singular values > 1e-5
+    const bool normal = shifted_pd6(A, tau);
     if (normal) {
-      manip = 1.0;
-      for (int j = 0; j < 6; ++j) manip = manip * L[j][j];
+      gauss_jordan6(M, z);
+      double pr = 1.0;
+      for (int k = 0; k < 6; ++k) pr = pr * M[k][k];
+      manip = std::sqrt(pr);
     } else {
       jacobi_eigen6(A, E, V);
       manip = 1.0;
@@ -1200,41 +1218,36 @@ static void ik_solve(const Robot& rb, const IkTask& t, IkOut* o) {
       ++fallback;
     }
     if (manip == 1.0 || manip < 0.00001) manip = 0.0001;
-    // compute_J_vdls (CL:5505-5614)
+    // compute_J_vdls (CL:5505-5614) applied to the error (CL:3455-3497): q_dot = J_vdls e = J^T (J J^T + d^2 I)^-1 e,
+    // the inverse applied by Gauss-Jordan, or (a singular value <= 1e-5) through the eigenvectors u_i of J J^T:
+    // sum_i u_i (u_i^T e) / (max(lambda_i, 0) + d^2)
     double damp = 0.0;
     if (manip < IK_MANIP_THR)
       damp = IK_DAMP_MAX * ((1 - (manip / IK_MANIP_THR)) * (1 - (manip / IK_MANIP_THR)));
-    if (normal && damp != 0.0) cholesky6(A, damp * damp, L);
-    // q_dot (CL:3455-3497): J_vdls row c = column c of (A + d^2 I)^-1 J -- by the Cholesky factor, or (a singular
-    // value <= 1e-5) by the eigenvectors u_i of A: sum_i (J^T u_i)_c u_i / (max(lambda_i, 0) + d^2)
-    double coef[6];
-    if (!normal)
-      for (int i = 0; i < 6; ++i) coef[i] = 1.0 / ((E[i][i] > 0.0 ? E[i][i] : 0.0) + damp * damp);
+    if (normal && damp != 0.0) {
+      for (int i = 0; i < 6; ++i) {
+        for (int k = 0; k < 6; ++k) M[i][k] = i == k ? A[i][i] + damp * damp : A[i][k];
+        M[i][6] = ep[i];
+      }
+      gauss_jordan6(M, z);
+    }
+    if (!normal) {
+      double g[6];
+      for (int i = 0; i < 6; ++i) {
+        double t = V[0][i] * ep[0];
+        for (int j = 1; j < 6; ++j) t = t + V[j][i] * ep[j];
+        g[i] = (1.0 / ((E[i][i] > 0.0 ? E[i][i] : 0.0) + damp * damp)) * t;
+      }
+      for (int k = 0; k < 6; ++k) {
+        double y = g[0] * V[k][0];
+        for (int i = 1; i < 6; ++i) y = y + g[i] * V[k][i];
+        z[k] = y;
+      }
+    }
     double qd[8];
     for (int c = 0; c < 8; ++c) {
-      double y[6], x[6];
-      if (!normal) {
-        for (int j = 0; j < 6; ++j) x[j] = 0.0;
-        for (int i = 0; i < 6; ++i) {
-          double w = J[0][c] * V[0][i];
-          for (int k = 1; k < 6; ++k) w = w + J[k][c] * V[k][i];
-          const double cw = coef[i] * w;
-          for (int j = 0; j < 6; ++j) x[j] = x[j] + cw * V[j][i];
-        }
-      } else {
-        for (int i = 0; i < 6; ++i) {
-          double s = J[i][c];
-          for (int k = 0; k < i; ++k) s = s - L[i][k] * y[k];
-          y[i] = s / L[i][i];
-        }
-        for (int i = 5; i >= 0; --i) {
-          double s = y[i];
-          for (int k = i + 1; k < 6; ++k) s = s - L[k][i] * x[k];
-          x[i] = s / L[i][i];
-        }
-      }
-      double v = 0.0;
-      for (int j = 0; j < 6; ++j) v = v + x[j] * (0.0 + IK_GAIN * err[j]);
+      double v = J[0][c] * z[0];
+      for (int i = 1; i < 6; ++i) v = v + J[i][c] * z[i];
       qd[c] = v;
     }
     // joint update with the joint-limit check (CL:3504-3550, KM:680-703)

@@ -30,8 +30,8 @@ __global__ void helper_kernel(const RobotDev* rb, SceneDev sc, const MapCfg* mc,
 __global__ void path_kernel(QueryDev* qs, int* counts);
 size_t check_kernels_private_bytes();
 size_t ik_kernels_private_bytes();
-__global__ void ik_kernel(const RobotDev* rb, const IkTaskDev* tasks, int n, IkOutDev* out);
-__global__ void ik_gather_kernel(const IkOutDev* out, int n, double* q_soa);
+void launch_ik(bool search, int n, hipStream_t st, const RobotDev* rb, const IkTaskDev* tasks, IkOutDev* out,
+               SceneDev sc, const MapCfg* mc, int self, int map, int* best);
 __global__ void sincos_kernel(const double* x, int n, double* s, double* c);
 __global__ void u01_kernel(unsigned long long seed, unsigned query, const uint32_t* ctr, int n, double* out);
 __global__ void fk_kernel(const RobotDev* rb, const double* q, int n, double* frames, double* eez);
@@ -127,6 +127,7 @@ struct smp_planner {
   DBuf<uint8_t> d_valid;
   DBuf<IkTaskDev> d_ik_tasks;
   DBuf<IkOutDev> d_ik_out;
+  DBuf<int> d_ik_best;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   double last_check_ms = 0, last_plan_ms = 0;
   int64_t last_plan_launches = 0;
@@ -495,38 +496,26 @@ int smp_is_config_valid(smp_planner* p, const double q[8], int check_self, int c
   return st;
 }
 
-// IK controller runs (getFullPoseFromEEPose, birrt_star.cpp:1627-1686): one wavefront per task.  Launches
-// ik_kernel on p->stream and, with check != 0, gathers the final configurations and checks them (isConfigValid,
-// birrt_star.cpp:6897-6908) in the same stream; one host synchronisation.
-static int ik_run(smp_planner* p, const std::vector<IkTaskDev>& tasks, std::vector<IkOutDev>& outs, int check,
-                  int check_self, int check_map, std::vector<uint8_t>* valid, double* ms) {
+// IK controller runs (getFullPoseFromEEPose, birrt_star.cpp:1627-1686): one wavefront per task, on p->stream.
+// search != 0: the candidates of one findGoalPose -- a run that REACHED checks its pose (isConfigValid,
+// birrt_star.cpp:6897-6908) in the same kernel and runs that can no longer be chosen stop early.
+static int ik_run(smp_planner* p, const std::vector<IkTaskDev>& tasks, std::vector<IkOutDev>& outs, int search,
+                  int check_self, int check_map, double* ms) {
   const int n = (int)tasks.size();
   outs.assign(n, IkOutDev{});
   if (n == 0) return SMP_OK;
   HIPCHK(hipSetDevice(p->device));
   HIPCHK(p->d_ik_tasks.reserve(n));
   HIPCHK(p->d_ik_out.reserve(n));
+  HIPCHK(p->d_ik_best.reserve(1));
   HIPCHK(hipMemcpyAsync(p->d_ik_tasks.p, tasks.data(), n * sizeof(IkTaskDev), hipMemcpyHostToDevice, p->stream));
+  HIPCHK(hipMemsetAsync(p->d_ik_best.p, 0x7f, sizeof(int), p->stream));
   HIPCHK(hipEventRecord(p->ev0, p->stream));
-  hipLaunchKernelGGL(ik_kernel, dim3(n), dim3(IK_THREADS), 0, p->stream, p->d_rb, p->d_ik_tasks.p, n, p->d_ik_out.p);
+  launch_ik(search != 0, n, p->stream, p->d_rb, p->d_ik_tasks.p, p->d_ik_out.p, p->sc, p->d_mc, check_self,
+            check_map && p->have_scene, p->d_ik_best.p);
   HIPCHK(hipGetLastError());
-  if (check) {
-    HIPCHK(p->d_cq.reserve((size_t)n * NJ));
-    HIPCHK(p->d_valid.reserve((size_t)n));
-    hipLaunchKernelGGL(ik_gather_kernel, dim3((n * NJ + 255) / 256), dim3(256), 0, p->stream, p->d_ik_out.p, n,
-                       p->d_cq.p);
-    HIPCHK(hipGetLastError());
-    const long long tiles = (n + 7) / 8;
-    launch_check(8, (int)std::min<long long>(tiles, 256 * 8), p->stream, p->d_rb, p->sc, p->d_mc, p->d_cq.p,
-                 (long long)n, check_self, check_map && p->have_scene, p->d_valid.p, nullptr);
-    HIPCHK(hipGetLastError());
-  }
   HIPCHK(hipEventRecord(p->ev1, p->stream));
   HIPCHK(hipMemcpyAsync(outs.data(), p->d_ik_out.p, n * sizeof(IkOutDev), hipMemcpyDeviceToHost, p->stream));
-  if (check) {
-    valid->assign(n, 0);
-    HIPCHK(hipMemcpyAsync(valid->data(), p->d_valid.p, n, hipMemcpyDeviceToHost, p->stream));
-  }
   HIPCHK(hipStreamSynchronize(p->stream));
   float f = 0;
   HIPCHK(hipEventElapsedTime(&f, p->ev0, p->ev1));
@@ -550,7 +539,7 @@ int smp_ik_solve(smp_planner* p, const smp_ik_request* reqs, int n, smp_ik_resul
   }
   std::vector<IkOutDev> outs;
   double ms = 0;
-  const int st = ik_run(p, tasks, outs, 0, 0, 0, nullptr, &ms);
+  const int st = ik_run(p, tasks, outs, 0, 0, 0, &ms);
   if (st != SMP_OK) return st;
   p->last_check_ms = ms;
   for (int i = 0; i < n; ++i) {
@@ -574,16 +563,16 @@ int smp_find_goal_pose(smp_planner* p, const double ee_pose[6], const double pos
   std::vector<IkTaskDev> tasks(n);
   const int down = ik_goal_candidates(ee_pose, pose_current, discretization_deg, tasks.data(), n, &n);
   std::vector<IkOutDev> outs;
-  std::vector<uint8_t> valid;
   double ms = 0;
-  const int st = ik_run(p, tasks, outs, 1, check_self, check_map, &valid, &ms);
+  const int st = ik_run(p, tasks, outs, 1, check_self, check_map, &ms);
   if (st != SMP_OK) return st;
   p->last_check_ms = ms;
+  // candidates below the chosen one always run to the end; those above it may have stopped early (IK_ABANDONED)
   int chosen = -1, reached = 0;
   for (int i = 0; i < n; ++i) {
     if (!outs[i].reached) continue;
     ++reached;
-    if (chosen < 0 && valid[i]) chosen = i;
+    if (chosen < 0 && (outs[i].flags & IK_VALID)) chosen = i;
   }
   *result = chosen >= 0 ? 0 : (reached ? 1 : 2);
   if (chosen >= 0)

@@ -29,8 +29,10 @@ struct IkOutDev {
   int32_t reached;      // REACHED 1 / ADVANCED 0 (control_laws.cpp:3691-3710)
   int32_t iters;
   int32_t fallback;     // iterations whose manipulability needed the Jacobi eigenvalue path
-  int32_t pad;
+  int32_t flags;        // goal search: IK_CHECKED | IK_VALID | IK_ABANDONED (0 for plain controller runs)
 };
+
+enum { IK_CHECKED = 1, IK_VALID = 2, IK_ABANDONED = 4 };
 
 // Host side (smp_ik_host.cpp): goal quaternion of [x, y, z, roll, pitch, yaw] (birrt_star.cpp:1630-1645) and the
 // candidate controller runs of findGoalPose in the reference's order; returns 1 if the hand points downward.

@@ -5,14 +5,27 @@
 // control_laws.cpp:5273-5301), the manipulability measure (control_laws.cpp:6050-6089), the variable damping
 // (control_laws.cpp:5557-5569), the damped pseudo-inverse applied to the error (control_laws.cpp:3455-3497), the
 // joint update with the joint-limit check (control_laws.cpp:3504-3550), forward kinematics and the clamped error
-// (control_laws.cpp:2167-2245).  The work of an iteration is a dependent chain of small steps (a 12-frame product,
-// 6x6 Cholesky columns, triangular solves), so a run stays on one wavefront and spreads each step over its lanes:
-// local frames per segment, frame rows per lane, Jacobian columns per lane, J J^T entries per lane, Cholesky rows
-// per lane (the plain and the shifted factorization side by side), solve columns per lane.  Every value is
-// computed with the same operations in the same order as oracle/smp_oracle.cpp (ik_solve), so the two agree bit
-// for bit (-ffp-contract=off, IEEE sqrt and division).
+// (control_laws.cpp:2167-2245).  An iteration is a dependent chain of small steps, and gfx950 fp64 has ~40 cycles
+// of dependent latency, so a run stays on one wavefront and each step is laid out to be short and wide:
+//   J    lanes 0-7: Jacobian column c (the joint rotations come from the previous FK); lanes 8-13: the
+//        quaternion and error component of the previous FK, so the error leaves the critical path;
+//   A    lanes 0-35: J J^T; lanes 36-41: the error column of the augmented system;
+//   GJ   6 Gauss-Jordan steps on [J J^T | e] (lanes 0-41, one entry each) and, beside them, the symmetric
+//        elimination of J J^T - 1e-10 I (lanes 42-62) whose pivot signs decide the manipulability path;
+//   q    lanes 0-7: q_dot_c = (J^T z)_c, joint update with the limit check;
+//   FK   lanes 0-11: local frame of every segment; lanes 0-2: one frame row each through the chain.
+// Robot constants live in registers (each lane always owns the same segment / column), the iteration touches
+// only LDS, and phases are separated by wavefront syncs (one wave per workgroup: no s_barrier).  Every value is
+// computed with the same operations in the same order as oracle/smp_oracle.cpp (ik_solve): -ffp-contract=off,
+// IEEE sqrt and division, so the two agree bit for bit.
+//
+// Goal search (findGoalPose, squirrel_8dof_planner.cpp:1129-1201): the candidates of one search run as one grid;
+// a run that REACHED checks its pose for collision itself (collide_tile, the batch checker's tile) and, if free,
+// lowers the search's `best` candidate index; a run whose index is above `best` can no longer be chosen and stops.
+// Runs below `best` always finish, so the first valid candidate in the reference's order is found exactly.
 #include <hip/hip_runtime.h>
 
+#include "smp_collide.h"
 #include "smp_ik.h"
 #include "smp_math.h"
 #include "smp_types.h"
@@ -31,19 +44,20 @@ constexpr double IK_BOUND = 0.0001;                 // is_error_within_bounds (c
 struct IkLds {
   double q[NJ];
   double L[MAX_SEG][12];      // local frame joint(q) * f_tip of every segment (R row-major, p)
+  double JR[MAX_SEG][9];      // joint rotation of every revolute segment (the Jacobian's joint.pose(q).M)
   double T[MAX_SEG + 1][12];  // T[0] = I, T[s+1] = T[s] * L[s]
-  double dl[MAX_SEG][3];      // T[s+1].p - T[s].p (Twist::RefPoint offsets)
   double J[6][NJ];
   double A[6][6];             // J J^T
-  double C[2][6][6];          // Cholesky factors: [0] of A (+ d^2 I), [1] of A - 1e-10 I
-  double piv_ok[2][6];
-  double ee[7];
+  double M[6][7];             // [J J^T (+ d^2 I) | e], Gauss-Jordan in place
+  double P[6][6];             // upper triangle of J J^T - 1e-10 I, eliminated in place
+  double E[6][6], V[6][6];    // Jacobi fallback: eigenvalues on the diagonal, eigenvectors in the columns
+  double z[6];                // (J J^T + d^2 I)^-1 e of the fallback path
   double err[6];
   double manip, damp;
-  int mov[NJ];                // segment of Jacobian column c
+  double ql[8][NJ];           // goal search: the pose to check (collide_tile input)
 };
 
-// KDL Rotation::GetQuaternion (frames.cpp), as compute_FK uses it (kdl_kuka_model.cpp:302).
+// KDL Rotation::GetQuaternion (frames.cpp), as compute_FK uses it (kdl_kuka_model.cpp:302): q = x, y, z, w.
 __device__ __forceinline__ void get_quaternion(const double* R, double* q) {
   double trace = R[0] + R[4] + R[8];
   if (trace > 1e-12) {
@@ -73,101 +87,113 @@ __device__ __forceinline__ void get_quaternion(const double* R, double* q) {
   }
 }
 
-// Segment frames of q (ChainFkSolverPos_recursive, kdl_kuka_model.cpp:278-305, and the T_tmp chain of
-// ChainJntToJacSolver) and the end-effector pose [x, y, z, qx, qy, qz, qw].
-__device__ __forceinline__ void chain_fk(const RobotDev* __restrict__ rb, IkLds& S, int lane) {
+// Constants of the segment a lane owns in the FK (lane s < n_seg) and of the Jacobian column it owns (lane c < 8).
+struct LaneConst {
+  int f_ty, f_jn;
+  double f_ax[3], f_org[3], f_R[9], f_p[3];
+  int j_s, j_ty, j_jn;
+  double j_ax[3], j_fp[3], j_lo, j_hi;
+};
+
+__device__ __forceinline__ void load_const(const RobotDev* __restrict__ rb, int lane, LaneConst& k) {
   const int ns = rb->n_seg;
+  k.f_ty = 0; k.f_jn = 0;
+  for (int d = 0; d < 3; ++d) { k.f_ax[d] = 0.0; k.f_org[d] = 0.0; k.f_p[d] = 0.0; k.j_ax[d] = 0.0; k.j_fp[d] = 0.0; }
+  for (int i = 0; i < 9; ++i) k.f_R[i] = 0.0;
   if (lane < ns) {
-    const int s = lane;
-    Frame J;
-    for (int i = 0; i < 9; ++i) J.R[i] = (i % 4 == 0) ? 1.0 : 0.0;
-    J.p[0] = J.p[1] = J.p[2] = 0.0;
-    const int ty = rb->seg_type[s];
-    if (ty == 1) {
-      rot2(&rb->seg_axis[s * 3], S.q[rb->seg_joint[s]], J.R);
-      for (int d = 0; d < 3; ++d) J.p[d] = rb->seg_origin[s * 3 + d];
-    } else if (ty == 2) {
-      const double qq = S.q[rb->seg_joint[s]];
-      for (int d = 0; d < 3; ++d) J.p[d] = rb->seg_origin[s * 3 + d] + rb->seg_axis[s * 3 + d] * qq;
+    k.f_ty = rb->seg_type[lane];
+    k.f_jn = rb->seg_joint[lane] < 0 ? 0 : rb->seg_joint[lane];
+    for (int d = 0; d < 3; ++d) {
+      k.f_ax[d] = rb->seg_axis[lane * 3 + d];
+      k.f_org[d] = rb->seg_origin[lane * 3 + d];
+      k.f_p[d] = rb->seg_p[lane * 3 + d];
+    }
+    for (int i = 0; i < 9; ++i) k.f_R[i] = rb->seg_R[lane * 9 + i];
+  }
+  // the lane-th movable segment
+  k.j_s = 0; k.j_ty = 0; k.j_jn = 0; k.j_lo = 0.0; k.j_hi = 0.0;
+  int c = 0;
+  for (int s = 0; s < ns; ++s) {
+    if (rb->seg_type[s] == 0) continue;
+    if (c == lane) k.j_s = s;
+    ++c;
+  }
+  if (lane < NJ) {
+    const int s = k.j_s;
+    k.j_ty = rb->seg_type[s];
+    k.j_jn = rb->seg_joint[s];
+    for (int d = 0; d < 3; ++d) { k.j_ax[d] = rb->seg_axis[s * 3 + d]; k.j_fp[d] = rb->seg_p[s * 3 + d]; }
+    k.j_lo = rb->q_min[k.j_jn];
+    k.j_hi = rb->q_max[k.j_jn];
+  }
+}
+
+// Segment frames of S.q (ChainFkSolverPos_recursive, kdl_kuka_model.cpp:278-305 -- the same products as the T_tmp
+// chain of ChainJntToJacSolver): T[0] = I, T[s+1] = T[s] * (joint(q) * f_tip).
+__device__ __forceinline__ void chain_fk(int ns, IkLds& S, int lane, const LaneConst& k) {
+  if (lane < ns) {
+    Frame Jf;
+    frame_identity(&Jf);
+    if (k.f_ty == 1) {
+      rot2(k.f_ax, S.q[k.f_jn], Jf.R);
+      for (int d = 0; d < 3; ++d) Jf.p[d] = k.f_org[d];
+      for (int i = 0; i < 9; ++i) S.JR[lane][i] = Jf.R[i];
+    } else if (k.f_ty == 2) {
+      const double qq = S.q[k.f_jn];
+      for (int d = 0; d < 3; ++d) Jf.p[d] = k.f_org[d] + k.f_ax[d] * qq;
     }
     Frame F, Lf;
-    for (int i = 0; i < 9; ++i) F.R[i] = rb->seg_R[s * 9 + i];
-    for (int d = 0; d < 3; ++d) F.p[d] = rb->seg_p[s * 3 + d];
-    fmul(J, F, &Lf);
-    for (int i = 0; i < 9; ++i) S.L[s][i] = Lf.R[i];
-    for (int d = 0; d < 3; ++d) S.L[s][9 + d] = Lf.p[d];
+    for (int i = 0; i < 9; ++i) F.R[i] = k.f_R[i];
+    for (int d = 0; d < 3; ++d) F.p[d] = k.f_p[d];
+    fmul(Jf, F, &Lf);
+    for (int i = 0; i < 9; ++i) S.L[lane][i] = Lf.R[i];
+    for (int d = 0; d < 3; ++d) S.L[lane][9 + d] = Lf.p[d];
   }
-  __syncthreads();
+  wave_sync();
   if (lane < 3) {  // row r of every T[s]: the three-term sums of KDL Frame*Frame (smp_math.h fmul)
     const int r = lane;
     double t0 = r == 0 ? 1.0 : 0.0, t1 = r == 1 ? 1.0 : 0.0, t2 = r == 2 ? 1.0 : 0.0, tp = 0.0;
     S.T[0][r * 3 + 0] = t0; S.T[0][r * 3 + 1] = t1; S.T[0][r * 3 + 2] = t2; S.T[0][9 + r] = tp;
+    double l[12];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) l[i] = S.L[0][i];
     for (int s = 0; s < ns; ++s) {
-      const double* Lr = S.L[s];
-      double n0 = t0 * Lr[0] + t1 * Lr[3] + t2 * Lr[6];
-      double n1 = t0 * Lr[1] + t1 * Lr[4] + t2 * Lr[7];
-      double n2 = t0 * Lr[2] + t1 * Lr[5] + t2 * Lr[8];
-      double m = t0 * Lr[9] + t1 * Lr[10] + t2 * Lr[11];
+      double ln[12];  // next local frame loaded ahead of this step's products
+      const int sn = s + 1 < ns ? s + 1 : s;
+#pragma unroll
+      for (int i = 0; i < 12; ++i) ln[i] = S.L[sn][i];
+      const double n0 = t0 * l[0] + t1 * l[3] + t2 * l[6];
+      const double n1 = t0 * l[1] + t1 * l[4] + t2 * l[7];
+      const double n2 = t0 * l[2] + t1 * l[5] + t2 * l[8];
+      const double m = t0 * l[9] + t1 * l[10] + t2 * l[11];
       tp = m + tp;
       t0 = n0; t1 = n1; t2 = n2;
       S.T[s + 1][r * 3 + 0] = t0; S.T[s + 1][r * 3 + 1] = t1; S.T[s + 1][r * 3 + 2] = t2; S.T[s + 1][9 + r] = tp;
+#pragma unroll
+      for (int i = 0; i < 12; ++i) l[i] = ln[i];
     }
   }
-  __syncthreads();
-  if (lane == 0) {
-    const double* E = S.T[ns];
-    S.ee[0] = E[9]; S.ee[1] = E[10]; S.ee[2] = E[11];
-    get_quaternion(E, &S.ee[3]);
-  }
-  __syncthreads();
+  wave_sync();
 }
 
-// Cartesian error (set_EE_goal_pose control_laws.cpp:1689-1720 unclamped; update_error_vec
-// control_laws.cpp:2203-2239 clamped to zero inside the deviation band).  Returns 1 if every component is within
-// 1e-4 (is_error_within_bounds).  Uniform across the wavefront.
-__device__ __forceinline__ int ik_error(const IkTaskDev& t, IkLds& S, int lane, bool clamp) {
-  double e = 0.0;
-  if (lane < 6) {
-    const double* d = t.goal;
-    const double* c = S.ee;
-    if (lane < 3) {
-      e = d[lane] - c[lane];
-    } else {
-      const int i = lane - 3;
-      const double s0 = i == 0 ? 0.0 : (i == 1 ? d[5] : -d[4]);
-      const double s1 = i == 0 ? -d[5] : (i == 1 ? 0.0 : d[3]);
-      const double s2 = i == 0 ? d[4] : (i == 1 ? -d[3] : 0.0);
-      e = c[6] * d[lane] - d[6] * c[lane] - (s0 * c[3] + s1 * c[4] + s2 * c[5]);
-    }
-    if (clamp) e = (e < t.lo[lane] || e > t.hi[lane]) ? e : 0.0;
-    S.err[lane] = e;
-  }
-  const unsigned long long out = __ballot(lane < 6 && fabs(e) > IK_BOUND);
-  __syncthreads();
-  return out == 0ull;
-}
-
-// KDL ChainJntToJacSolver::JntToJac: column c (lane c) = T[s].M * (joint twist referred to the tip of segment s),
-// then Twist::RefPoint(T[i+1].p - T[i].p) for every later segment i; cast to float (getJacobian).
-__device__ __forceinline__ void jacobian(const RobotDev* __restrict__ rb, IkLds& S, int lane) {
-  const int ns = rb->n_seg;
-  if (lane < 3 * ns) {
-    const int s = lane / 3, d = lane - 3 * s;
-    S.dl[s][d] = S.T[s + 1][9 + d] - S.T[s][9 + d];
-  }
-  __syncthreads();
+// Lanes 0-7: KDL ChainJntToJacSolver::JntToJac column of movable segment s = T[s].M * (joint twist referred to
+// the tip of s), then Twist::RefPoint(T[i+1].p - T[i].p) for every later segment i; cast to float (getJacobian).
+// Lanes 8-13: error component lane-8 of the end-effector pose T[ns] (set_EE_goal_pose unclamped, update_error_vec
+// clamped).  Returns the ballot of components outside the 1e-4 bound (is_error_within_bounds).
+__device__ __forceinline__ unsigned long long jacobian_and_error(int ns, const IkTaskDev& t, IkLds& S, int lane,
+                                                                 const LaneConst& k, bool clamp) {
+  bool out = false;
   if (lane < NJ) {
-    const int s = S.mov[lane];
-    const int ty = rb->seg_type[s];
-    const double* ax = &rb->seg_axis[s * 3];
+    const int s = k.j_s;
     double M[9] = {1.0, 0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 1.0};
-    if (ty == 1) rot2(ax, S.q[rb->seg_joint[s]], M);
-    const double* fp = &rb->seg_p[s * 3];
+    if (k.j_ty == 1)
+#pragma unroll
+      for (int i = 0; i < 9; ++i) M[i] = S.JR[s][i];
     double v[3], rl[3], vl[3];
-    for (int r = 0; r < 3; ++r) v[r] = M[r * 3 + 0] * fp[0] + M[r * 3 + 1] * fp[1] + M[r * 3 + 2] * fp[2];
+    for (int r = 0; r < 3; ++r) v[r] = M[r * 3 + 0] * k.j_fp[0] + M[r * 3 + 1] * k.j_fp[1] + M[r * 3 + 2] * k.j_fp[2];
     for (int d = 0; d < 3; ++d) {
-      rl[d] = ty == 1 ? ax[d] * 1.0 : 0.0;
-      vl[d] = ty == 2 ? ax[d] * 1.0 : 0.0;
+      rl[d] = k.j_ty == 1 ? k.j_ax[d] * 1.0 : 0.0;
+      vl[d] = k.j_ty == 2 ? k.j_ax[d] * 1.0 : 0.0;
     }
     const double c0 = rl[1] * v[2] - rl[2] * v[1], c1 = rl[2] * v[0] - rl[0] * v[2], c2 = rl[0] * v[1] - rl[1] * v[0];
     vl[0] = vl[0] + c0; vl[1] = vl[1] + c1; vl[2] = vl[2] + c2;
@@ -177,44 +203,45 @@ __device__ __forceinline__ void jacobian(const RobotDev* __restrict__ rb, IkLds&
       vel[r] = B[r * 3 + 0] * vl[0] + B[r * 3 + 1] * vl[1] + B[r * 3 + 2] * vl[2];
       rot[r] = B[r * 3 + 0] * rl[0] + B[r * 3 + 1] * rl[1] + B[r * 3 + 2] * rl[2];
     }
+    double p0 = S.T[s + 1][9], p1 = S.T[s + 1][10], p2 = S.T[s + 1][11];
     for (int i = s + 1; i < ns; ++i) {
-      const double d0 = S.dl[i][0], d1 = S.dl[i][1], d2 = S.dl[i][2];
+      const double n0 = S.T[i + 1][9], n1 = S.T[i + 1][10], n2 = S.T[i + 1][11];
+      const double d0 = n0 - p0, d1 = n1 - p1, d2 = n2 - p2;
       const double x0 = rot[1] * d2 - rot[2] * d1, x1 = rot[2] * d0 - rot[0] * d2, x2 = rot[0] * d1 - rot[1] * d0;
       vel[0] = vel[0] + x0; vel[1] = vel[1] + x1; vel[2] = vel[2] + x2;
+      p0 = n0; p1 = n1; p2 = n2;
     }
     for (int d = 0; d < 3; ++d) {
       S.J[d][lane] = (double)(float)vel[d];
       S.J[3 + d][lane] = (double)(float)rot[d];
     }
-  }
-  __syncthreads();
-}
-
-// Cholesky of A + shift I, column by column: lanes g*8 + i (i < 6) own row i of factor g (g < ng).
-// Pivot flags piv_ok[g][j] = (pivot > 0).
-__device__ __forceinline__ void cholesky(IkLds& S, int lane, int ng, double shift0, double shift1) {
-  const int g = lane >> 3, i = lane & 7;
-  const bool act = g < ng && i < 6;
-  const double shift = g == 0 ? shift0 : shift1;
-  double(*L)[6] = S.C[g < 2 ? g : 0];
-  for (int j = 0; j < 6; ++j) {
-    double s = 0.0;
-    if (act && i >= j) {
-      s = i == j ? S.A[i][j] + shift : S.A[i][j];
-      for (int k = 0; k < j; ++k) s = s - L[i][k] * L[j][k];
-      if (i == j) {
-        S.piv_ok[g][j] = (s > 0.0) ? 1.0 : 0.0;
-        L[j][j] = sqrt(s);
-      }
+  } else if (lane >= 8 && lane < 14) {
+    const int i = lane - 8;
+    const double* E = S.T[ns];
+    double c[7] = {E[9], E[10], E[11], 0.0, 0.0, 0.0, 0.0};
+    get_quaternion(E, &c[3]);
+    const double* d = t.goal;
+    double e;
+    if (i < 3) {
+      e = d[i] - c[i];
+    } else {
+      const int r = i - 3;
+      const double s0 = r == 0 ? 0.0 : (r == 1 ? d[5] : -d[4]);
+      const double s1 = r == 0 ? -d[5] : (r == 1 ? 0.0 : d[3]);
+      const double s2 = r == 0 ? d[4] : (r == 1 ? -d[3] : 0.0);
+      e = c[6] * d[i] - d[6] * c[i] - (s0 * c[3] + s1 * c[4] + s2 * c[5]);
     }
-    __syncthreads();
-    if (act && i > j) L[i][j] = s / L[j][j];
-    __syncthreads();
+    if (clamp) e = (e < t.lo[i] || e > t.hi[i]) ? e : 0.0;
+    S.err[i] = e;
+    out = fabs(e) > IK_BOUND;
   }
+  const unsigned long long b = __ballot(out);
+  wave_sync();
+  return b;
 }
 
 // Cyclic Jacobi eigen-decomposition of the symmetric 6x6 A (rows p < q in order, at most 30 sweeps): eigenvalues
-// on the diagonal of the LDS scratch a, eigenvectors in the columns of V; one lane.
+// on the diagonal of a, eigenvectors in the columns of V; one lane.
 __device__ void jacobi_eigen6(const double (*A)[6], double (*a)[6], double (*V)[6]) {
   for (int i = 0; i < 6; ++i)
     for (int k = 0; k < 6; ++k) {
@@ -248,51 +275,93 @@ __device__ void jacobi_eigen6(const double (*A)[6], double (*a)[6], double (*V)[
   }
 }
 
+// Upper-triangle entry (i, j), i <= j, of shifted-elimination lane 42 + u (u < 21).
+__device__ __forceinline__ void upper_pair(int u, int* i, int* j) {
+  int r = 0, base = 0;
+  while (u >= base + (6 - r)) { base += 6 - r; ++r; }
+  *i = r;
+  *j = r + (u - base);
+}
+
 }  // namespace
 
-__global__ void __launch_bounds__(IK_THREADS) ik_kernel(const RobotDev* __restrict__ rb,
-                                                        const IkTaskDev* __restrict__ tasks, int n,
-                                                        IkOutDev* __restrict__ out) {
+// One controller run per wavefront (block = 64 threads).  SEARCH: goal-search mode (collision check of a REACHED
+// pose, `best` candidate index shared by the grid, runs that can no longer be chosen stop).
+template <bool SEARCH>
+__global__ void __launch_bounds__(IK_THREADS) ik_kernel_t(const RobotDev* __restrict__ rb,
+                                                          const IkTaskDev* __restrict__ tasks, int n,
+                                                          IkOutDev* __restrict__ out, SceneDev sc,
+                                                          const MapCfg* __restrict__ mc, int self, int map, int* best) {
   __shared__ IkLds S;
-  __shared__ double Eg[6][6], Ev[6][6], coef[6];  // Jacobi fallback: eigenvalues (diagonal), eigenvectors, 1/(s^2+d^2)
+  __shared__ TileLds<8> TL;
   const int lane = threadIdx.x;
   const int b = blockIdx.x;
   if (b >= n) return;
   const IkTaskDev& t = tasks[b];
   const int ns = rb->n_seg;
-  if (lane < NJ) S.q[lane] = t.q[lane];
-  if (lane == 0) {
-    int c = 0;
-    for (int s = 0; s < ns && c < NJ; ++s)
-      if (rb->seg_type[s] != 0) S.mov[c++] = s;
-  }
-  __syncthreads();
-  chain_fk(rb, S, lane);
-  int within = 0;
-  ik_error(t, S, lane, false);  // set_EE_goal_pose: error_within_bounds stays false (control_laws.cpp:3328)
-  int iter = 0, fallback = 0;
+  LaneConst k;
+  load_const(rb, lane, k);
+  const int max_iter = t.max_iter;
   const double tau = IK_SV_EPS * IK_SV_EPS;
-  while (!within) {
-    jacobian(rb, S, lane);
-    if (lane < 36) {
-      const int i = lane / 6, k = lane - 6 * (lane / 6);
-      double s = S.J[i][0] * S.J[k][0];
-      for (int c = 1; c < NJ; ++c) s = s + S.J[i][c] * S.J[k][c];
-      S.A[i][k] = s;
+  // main Gauss-Jordan lane (gi, gj) of the 6 x 7 system, or shifted-elimination lane (si, sj) of the upper triangle
+  const int gi = lane / 7, gj = lane - 7 * (lane / 7);
+  int si = 0, sj = 0;
+  const bool sh = lane >= 42 && lane < 63;
+  if (sh) upper_pair(lane - 42, &si, &sj);
+  if (lane < NJ) S.q[lane] = t.q[lane];
+  wave_sync();
+  chain_fk(ns, S, lane, k);
+  int iter = 0, fallback = 0, abandoned = 0;
+  while (true) {
+    const unsigned long long outb = jacobian_and_error(ns, t, S, lane, k, iter > 0);
+    if (iter > 0) {
+      if (iter == max_iter) break;
+      if (outb == 0ull) break;
     }
-    __syncthreads();
-    cholesky(S, lane, 2, 0.0, -tau);
-    // computeManipulabilityMeasure (control_laws.cpp:6050-6089)
+    // goal search: read the best candidate now, act on it after this iteration (the load overlaps the iteration)
+    int bst = 0x7fffffff;
+    if (SEARCH) bst = __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // J J^T, the augmented error column, the shifted upper triangle
+    if (lane < 36) {
+      const int i = lane / 6, c = lane - 6 * (lane / 6);
+      double s = S.J[i][0] * S.J[c][0];
+#pragma unroll
+      for (int x = 1; x < NJ; ++x) s = s + S.J[i][x] * S.J[c][x];
+      S.A[i][c] = s;
+      S.M[i][c] = s;
+      if (i <= c) S.P[i][c] = i == c ? s + (-tau) : s;
+    } else if (lane < 42) {
+      S.M[lane - 36][6] = 0.0 + IK_GAIN * S.err[lane - 36];
+    }
+    wave_sync();
+    // Gauss-Jordan on [A | e] and the symmetric elimination of A - tau I, side by side; lane 0 multiplies the pivots
+    double pr = 1.0;
+    for (int s = 0; s < 6; ++s) {
+      if (lane == 0) pr = pr * S.M[s][s];
+      if (lane < 42) {
+        if (gi != s && gj > s) {
+          const double f = S.M[gi][s] / S.M[s][s];
+          S.M[gi][gj] = S.M[gi][gj] - f * S.M[s][gj];
+        }
+      } else if (sh && si > s) {
+        const double f = S.P[s][si] / S.P[s][s];
+        S.P[si][sj] = S.P[si][sj] - f * S.P[s][sj];
+      }
+      wave_sync();
+    }
+    // computeManipulabilityMeasure (control_laws.cpp:6050-6089) and the damping (control_laws.cpp:5557-5569)
     bool normal = true;
-    for (int j = 0; j < 6; ++j) normal = normal && S.piv_ok[1][j] != 0.0;
+#pragma unroll
+    for (int s = 0; s < 6; ++s) normal = normal && S.P[s][s] > 0.0;
     if (lane == 0) {
-      double m = 1.0;
+      double m;
       if (normal) {
-        for (int j = 0; j < 6; ++j) m = m * S.C[0][j][j];
+        m = sqrt(pr);
       } else {
-        jacobi_eigen6(S.A, Eg, Ev);
+        jacobi_eigen6(S.A, S.E, S.V);
+        m = 1.0;
         for (int j = 0; j < 6; ++j) {
-          const double lam = Eg[j][j];
+          const double lam = S.E[j][j];
           const double sv = sqrt(lam > 0.0 ? lam : 0.0);
           if (fabs(sv) > IK_SV_EPS) m = m * fabs(sv);
         }
@@ -300,91 +369,97 @@ __global__ void __launch_bounds__(IK_THREADS) ik_kernel(const RobotDev* __restri
       if (m == 1.0 || m < 0.00001) m = 0.0001;
       double d = 0.0;
       if (m < IK_MANIP_THR) d = IK_DAMP_MAX * ((1 - (m / IK_MANIP_THR)) * (1 - (m / IK_MANIP_THR)));
-      S.manip = m;
-      S.damp = d;
-      if (!normal)
-        for (int i = 0; i < 6; ++i) coef[i] = 1.0 / ((Eg[i][i] > 0.0 ? Eg[i][i] : 0.0) + d * d);
-    }
-    fallback += normal ? 0 : 1;
-    __syncthreads();
-    const double damp = S.damp;
-    if (normal && damp != 0.0) cholesky(S, lane, 1, damp * damp, 0.0);
-    // damped pseudo-inverse times the error (control_laws.cpp:3455-3497), then the joint update with the limit
-    // check (control_laws.cpp:3504-3550): lane c owns column c of (A + d^2 I)^-1 J, i.e. row c of J_vdls -- by the
-    // Cholesky factor, or (a singular value <= 1e-5) sum_i (J^T u_i)_c u_i / (max(lambda_i, 0) + d^2)
-    if (lane < NJ) {
-      double x[6];
-      if (normal) {
-        const double(*L)[6] = S.C[0];
-        double y[6];
-#pragma unroll
+      if (!normal) {
+        double ep[6], g[6];
+        for (int i = 0; i < 6; ++i) ep[i] = 0.0 + IK_GAIN * S.err[i];
         for (int i = 0; i < 6; ++i) {
-          double s = S.J[i][lane];
-#pragma unroll
-          for (int k = 0; k < i; ++k) s = s - L[i][k] * y[k];
-          y[i] = s / L[i][i];
+          double tt = S.V[0][i] * ep[0];
+          for (int j = 1; j < 6; ++j) tt = tt + S.V[j][i] * ep[j];
+          g[i] = (1.0 / ((S.E[i][i] > 0.0 ? S.E[i][i] : 0.0) + d * d)) * tt;
         }
-#pragma unroll
-        for (int i = 5; i >= 0; --i) {
-          double s = y[i];
-#pragma unroll
-          for (int k = i + 1; k < 6; ++k) s = s - L[k][i] * x[k];
-          x[i] = s / L[i][i];
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < 6; ++j) x[j] = 0.0;
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-          double w = S.J[0][lane] * Ev[0][i];
-#pragma unroll
-          for (int k = 1; k < 6; ++k) w = w + S.J[k][lane] * Ev[k][i];
-          const double cw = coef[i] * w;
-#pragma unroll
-          for (int j = 0; j < 6; ++j) x[j] = x[j] + cw * Ev[j][i];
+        for (int r = 0; r < 6; ++r) {
+          double y = g[0] * S.V[r][0];
+          for (int i = 1; i < 6; ++i) y = y + g[i] * S.V[r][i];
+          S.z[r] = y;
         }
       }
-      double v = 0.0;
-#pragma unroll
-      for (int j = 0; j < 6; ++j) v = v + x[j] * (0.0 + IK_GAIN * S.err[j]);
-      const int s = S.mov[lane];
-      const int jn = rb->seg_joint[s];
-      const double nv = S.q[jn] + v * IK_DT;
-      if (!(nv < rb->q_min[jn] || nv > rb->q_max[jn])) S.q[jn] = nv;
+      S.manip = m;
+      S.damp = d;
     }
-    __syncthreads();
-    chain_fk(rb, S, lane);
-    within = ik_error(t, S, lane, true);
+    fallback += normal ? 0 : 1;
+    wave_sync();
+    const double damp = S.damp;
+    if (normal && damp != 0.0) {  // damped system (A + d^2 I) z = e
+      if (lane < 36) {
+        const int i = lane / 6, c = lane - 6 * (lane / 6);
+        S.M[i][c] = i == c ? S.A[i][i] + damp * damp : S.A[i][c];
+      } else if (lane < 42) {
+        S.M[lane - 36][6] = 0.0 + IK_GAIN * S.err[lane - 36];
+      }
+      wave_sync();
+      for (int s = 0; s < 6; ++s) {
+        if (lane < 42 && gi != s && gj > s) {
+          const double f = S.M[gi][s] / S.M[s][s];
+          S.M[gi][gj] = S.M[gi][gj] - f * S.M[s][gj];
+        }
+        wave_sync();
+      }
+    }
+    // q_dot = J_vdls e = J^T z (control_laws.cpp:3455-3497), joint update with the limit check (:3504-3550)
+    if (lane < NJ) {
+      double z[6];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) z[i] = normal ? S.M[i][6] / S.M[i][i] : S.z[i];
+      double v = S.J[0][lane] * z[0];
+#pragma unroll
+      for (int i = 1; i < 6; ++i) v = v + S.J[i][lane] * z[i];
+      const double nv = S.q[k.j_jn] + v * IK_DT;
+      if (!(nv < k.j_lo || nv > k.j_hi)) S.q[k.j_jn] = nv;
+    }
+    wave_sync();
+    chain_fk(ns, S, lane, k);
     ++iter;
-    if (iter == t.max_iter) break;
+    if (SEARCH && bst < b) {  // a lower candidate is REACHED and valid: this run can no longer be chosen
+      abandoned = 1;
+      break;
+    }
+  }
+  const int reached = (abandoned || iter == max_iter) ? 0 : 1;
+  int flags = abandoned ? IK_ABANDONED : 0;
+  if (SEARCH && reached) {
+    if (lane < NJ) S.ql[0][lane] = S.q[lane];
+    __syncthreads();
+    collide_tile<8>(rb, sc, mc, 1, S.ql, self, map, TL);
+    flags |= IK_CHECKED | (TL.coll[0] ? 0 : IK_VALID);
+    if (lane == 0 && !TL.coll[0]) __hip_atomic_fetch_min(best, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   IkOutDev& o = out[b];
   if (lane < NJ) o.q[lane] = S.q[lane];
   if (lane < 6) o.err[lane] = S.err[lane];
   if (lane == 0) {
     o.manip = S.manip;
-    o.reached = iter == t.max_iter ? 0 : 1;
+    o.reached = reached;
     o.iters = iter;
     o.fallback = fallback;
-    o.pad = 0;
+    o.flags = flags;
   }
 }
 
-// Gathers the final configurations of n runs into the structure-of-arrays layout of the batch check kernel.
-__global__ void ik_gather_kernel(const IkOutDev* __restrict__ out, int n, double* __restrict__ q_soa) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n * NJ) {
-    const int c = i / NJ, j = i - c * NJ;
-    q_soa[(size_t)j * n + c] = out[c].q[j];
-  }
+void launch_ik(bool search, int n, hipStream_t st, const RobotDev* rb, const IkTaskDev* tasks, IkOutDev* out,
+               SceneDev sc, const MapCfg* mc, int self, int map, int* best) {
+  if (search)
+    hipLaunchKernelGGL(ik_kernel_t<true>, dim3(n), dim3(IK_THREADS), 0, st, rb, tasks, n, out, sc, mc, self, map, best);
+  else
+    hipLaunchKernelGGL(ik_kernel_t<false>, dim3(n), dim3(IK_THREADS), 0, st, rb, tasks, n, out, sc, mc, self, map,
+                       best);
 }
 
 size_t ik_kernels_private_bytes() {
   size_t need = 0;
   hipFuncAttributes fa;
-  const void* ks[] = {reinterpret_cast<const void*>(&ik_kernel), reinterpret_cast<const void*>(&ik_gather_kernel)};
-  for (const void* k : ks)
-    if (hipFuncGetAttributes(&fa, k) == hipSuccess && (size_t)fa.localSizeBytes > need) need = fa.localSizeBytes;
+  const void* ks[] = {reinterpret_cast<const void*>(&ik_kernel_t<false>), reinterpret_cast<const void*>(&ik_kernel_t<true>)};
+  for (const void* kk : ks)
+    if (hipFuncGetAttributes(&fa, kk) == hipSuccess && (size_t)fa.localSizeBytes > need) need = fa.localSizeBytes;
   return need;
 }
 
