@@ -87,12 +87,13 @@ typedef struct smp_params {
   int informed_sampling;   /* m_informed_sampling_active (default 1) */
   int64_t node_capacity;   /* per-tree node capacity on the device (0: derived from the budget) */
   int helpers;             /* helper workgroups per query that share its collision tiles across CUs
-                              (0: automatic, up to 127 with the scout / 63 without; -1: none, the query runs on
+                              (0: automatic, up to 200 with scouts / 63 without; -1: none, the query runs on
                               its own workgroup) */
   int scout;               /* 1 (default): scout workgroups compute the coming iterations' scans and collision jobs
-                              ahead of the leader -- 2 when a query has 18 CUs or more (before the first solution
-                              they take the iterations in turn, after it they alternate, two ahead), 1 from 6 CUs;
-                              2..4: that many (with >= 4 helpers); 0: off.  Results are identical either way */
+                              ahead of the leader -- 4 when a query has 64 CUs or more, 2 from 18 CUs, 1 from 6
+                              (before the first solution they take the iterations in turn; after it scouts 0 and 1
+                              alternate, two ahead, and the others retire); 2..8: that many (with >= 4 helpers);
+                              0: off.  Results are identical either way */
 } smp_params;
 
 typedef struct smp_query {

@@ -1027,6 +1027,15 @@ static void get_quaternion(const double* R, double* x, double* y, double* z, dou
   }
 }
 
+// A segment whose joint does not rotate (prismatic or fixed) and whose f_tip rotation is the identity has the
+// identity as local rotation.
+static bool ik_rot_identity(const Robot& rb, int s) {
+  if (rb.seg_type[s] == 1) return false;
+  for (int i = 0; i < 9; ++i)
+    if (rb.seg_R[s * 9 + i] != ((i % 4 == 0) ? 1.0 : 0.0)) return false;
+  return true;
+}
+
 // Segment frames of the 12-segment chain (KDL ChainFkSolverPos_recursive, KM:278-305; the same products as
 // ChainJntToJacSolver's T_tmp * segment.pose(q)): T[0] = I, T[s+1] = T[s] * (joint(q) * f_tip).
 static void chain_frames(const Robot& rb, const double* q, Frame* T) {
@@ -1048,7 +1057,17 @@ static void chain_frames(const Robot& rb, const double* q, Frame* T) {
     Frame F;
     std::memcpy(F.R, &rb.seg_R[s * 9], 9 * sizeof(double));
     std::memcpy(F.p, &rb.seg_p[s * 3], 3 * sizeof(double));
-    T[s + 1] = fmul(T[s], fmul(J, F));
+    const Frame L = fmul(J, F);
+    if (ik_rot_identity(rb, s)) {
+      // the local rotation is exactly I: T.R * I == T.R up to the sign of a zero, so only the translation is applied
+      T[s + 1] = T[s];
+      for (int r = 0; r < 3; ++r) {
+        const double m = T[s].R[r * 3 + 0] * L.p[0] + T[s].R[r * 3 + 1] * L.p[1] + T[s].R[r * 3 + 2] * L.p[2];
+        T[s + 1].p[r] = m + T[s].p[r];
+      }
+    } else {
+      T[s + 1] = fmul(T[s], L);
+    }
   }
 }
 
@@ -1191,10 +1210,10 @@ static void ik_solve(const Robot& rb, const IkTask& t, IkOut* o) {
     double J[6][8], A[6][6], M[6][7], E[6][6], V[6][6], z[6], ep[6];
     jacobian(rb, q, T, J);
     for (int i = 0; i < 6; ++i)
-      for (int k = 0; k < 6; ++k) {
-        double s = J[i][0] * J[k][0];
-        for (int c = 1; c < 8; ++c) s = s + J[i][c] * J[k][c];
-        A[i][k] = s;
+      for (int k = 0; k < 6; ++k) {  // pairwise sums (a short dependent chain on the GPU)
+        double p[8];
+        for (int c = 0; c < 8; ++c) p[c] = J[i][c] * J[k][c];
+        A[i][k] = ((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7]));
       }
     for (int i = 0; i < 6; ++i) ep[i] = 0.0 + IK_GAIN * err[i];  // current_goal_ee_vel_ + error_gain_ * error_
     for (int i = 0; i < 6; ++i) {
@@ -1246,9 +1265,9 @@ static void ik_solve(const Robot& rb, const IkTask& t, IkOut* o) {
     }
     double qd[8];
     for (int c = 0; c < 8; ++c) {
-      double v = J[0][c] * z[0];
-      for (int i = 1; i < 6; ++i) v = v + J[i][c] * z[i];
-      qd[c] = v;
+      double p[6];
+      for (int i = 0; i < 6; ++i) p[i] = J[i][c] * z[i];
+      qd[c] = ((p[0] + p[1]) + (p[2] + p[3])) + (p[4] + p[5]);
     }
     // joint update with the joint-limit check (CL:3504-3550, KM:680-703)
     int c = 0;

@@ -797,18 +797,21 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
     if (st) return st;
     HIPCHK(hipMemcpyAsync(qdev[i].st, &S[i], sizeof(QState), hipMemcpyHostToDevice, p->stream));
   }
-  // helper workgroups per query (DESIGN.md "Helpers", "Scout"): one workgroup per CU, leaders (and scouts) first.
   // Workgroups per query (one per CU): the leader, its scouts and the helpers (DESIGN.md "Helpers", "Scouts").
-  // Scouts: smp_params.scout of them (1: automatic -- 2 from 18 CUs per query, 1 from 6; four scouts before the
-  // first solution were measured and gain nothing there, the leader's own work bounds those iterations).  Helpers:
-  // the leader's tile helpers, each scout's, and the run-ahead sampler (the last one).
+  // Scouts: smp_params.scout of them (1: automatic -- 4 from 64 CUs per query (scouts 2 and 3 take every other
+  // iteration before the first solution and retire after it: time to first path 2.1 -> 1.7 ms on C2), 2 from 18,
+  // 1 from 6).  Helpers: the leader's tile helpers, each scout's, and the run-ahead sampler (the last one); up to 200
+  // with scouts (C2: 127 -> 200 helpers 3.65 -> 3.75 M configs/s with four scouts; 250 no longer all fit and stall).
   int nh = p->params.helpers;
   const bool want_scout = p->params.scout != 0;
   const int cpq = std::max(1, p->num_cus / nq);
   int ns = 0;
+  int cap_s = 200;  // SMP_HELPER_CAP: experiments with other helper caps
+  if (const char* e = std::getenv("SMP_HELPER_CAP")) cap_s = std::max(1, std::atoi(e));
   if (nh == 0) {
-    if (want_scout) ns = cpq >= 18 ? 2 : cpq >= 6 ? 1 : 0;
-    nh = want_scout ? std::min(127, std::max(0, cpq - 1 - ns)) : std::min(63, std::max(0, cpq - 1));
+    if (want_scout) ns = cpq >= 64 ? 4 : cpq >= 18 ? 2 : cpq >= 6 ? 1 : 0;
+    if (want_scout && p->params.scout > 1) ns = std::min(p->params.scout, MAX_SCOUTS);
+    nh = want_scout ? std::min(cap_s, std::max(0, cpq - 1 - ns)) : std::min(63, std::max(0, cpq - 1));
   } else if (nh > 0 && want_scout) {
     ns = nh >= 16 ? 2 : nh >= 4 ? 1 : 0;
   }
@@ -827,7 +830,7 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
   }
   // before the first solution a scout starts record k when the leader reaches k - pre_delay (DESIGN.md "Pre-solution
   // commits"); SMP_PRE_DELAY overrides it for experiments (0: at the request)
-  int pre_delay = 2;
+  int pre_delay = 3;
   if (const char* e = std::getenv("SMP_PRE_DELAY")) pre_delay = std::atoi(e);
   int pre_commit = 1;  // SMP_PRE_COMMIT=0: every iteration runs the full path (experiments)
   if (const char* e = std::getenv("SMP_PRE_COMMIT")) pre_commit = std::atoi(e);

@@ -130,7 +130,7 @@ __device__ __forceinline__ void load_const(const RobotDev* __restrict__ rb, int 
 
 // Segment frames of S.q (ChainFkSolverPos_recursive, kdl_kuka_model.cpp:278-305 -- the same products as the T_tmp
 // chain of ChainJntToJacSolver): T[0] = I, T[s+1] = T[s] * (joint(q) * f_tip).
-__device__ __forceinline__ void chain_fk(int ns, IkLds& S, int lane, const LaneConst& k) {
+__device__ __forceinline__ void chain_fk(int ns, unsigned rid, IkLds& S, int lane, const LaneConst& k) {
   if (lane < ns) {
     Frame Jf;
     frame_identity(&Jf);
@@ -162,12 +162,14 @@ __device__ __forceinline__ void chain_fk(int ns, IkLds& S, int lane, const LaneC
       const int sn = s + 1 < ns ? s + 1 : s;
 #pragma unroll
       for (int i = 0; i < 12; ++i) ln[i] = S.L[sn][i];
-      const double n0 = t0 * l[0] + t1 * l[3] + t2 * l[6];
-      const double n1 = t0 * l[1] + t1 * l[4] + t2 * l[7];
-      const double n2 = t0 * l[2] + t1 * l[5] + t2 * l[8];
       const double m = t0 * l[9] + t1 * l[10] + t2 * l[11];
       tp = m + tp;
-      t0 = n0; t1 = n1; t2 = n2;
+      if (!((rid >> s) & 1u)) {  // else the local rotation is exactly I: the row stays (oracle chain_frames)
+        const double n0 = t0 * l[0] + t1 * l[3] + t2 * l[6];
+        const double n1 = t0 * l[1] + t1 * l[4] + t2 * l[7];
+        const double n2 = t0 * l[2] + t1 * l[5] + t2 * l[8];
+        t0 = n0; t1 = n1; t2 = n2;
+      }
       S.T[s + 1][r * 3 + 0] = t0; S.T[s + 1][r * 3 + 1] = t1; S.T[s + 1][r * 3 + 2] = t2; S.T[s + 1][9 + r] = tp;
 #pragma unroll
       for (int i = 0; i < 12; ++i) l[i] = ln[i];
@@ -203,12 +205,18 @@ __device__ __forceinline__ unsigned long long jacobian_and_error(int ns, const I
       vel[r] = B[r * 3 + 0] * vl[0] + B[r * 3 + 1] * vl[1] + B[r * 3 + 2] * vl[2];
       rot[r] = B[r * 3 + 0] * rl[0] + B[r * 3 + 1] * rl[1] + B[r * 3 + 2] * rl[2];
     }
-    double p0 = S.T[s + 1][9], p1 = S.T[s + 1][10], p2 = S.T[s + 1][11];
-    for (int i = s + 1; i < ns; ++i) {
+    // RefPoint shifts of the later segments i = s+1 .. ns-1 in order; every step's offset and cross product are
+    // computed for all i (no dependence on vel), only the additions of the lane's own steps are kept
+    double p0 = S.T[1][9], p1 = S.T[1][10], p2 = S.T[1][11];
+#pragma unroll
+    for (int i = 1; i < MAX_SEG; ++i) {
       const double n0 = S.T[i + 1][9], n1 = S.T[i + 1][10], n2 = S.T[i + 1][11];
       const double d0 = n0 - p0, d1 = n1 - p1, d2 = n2 - p2;
       const double x0 = rot[1] * d2 - rot[2] * d1, x1 = rot[2] * d0 - rot[0] * d2, x2 = rot[0] * d1 - rot[1] * d0;
-      vel[0] = vel[0] + x0; vel[1] = vel[1] + x1; vel[2] = vel[2] + x2;
+      const bool on = i > s && i < ns;
+      vel[0] = on ? vel[0] + x0 : vel[0];
+      vel[1] = on ? vel[1] + x1 : vel[1];
+      vel[2] = on ? vel[2] + x2 : vel[2];
       p0 = n0; p1 = n1; p2 = n2;
     }
     for (int d = 0; d < 3; ++d) {
@@ -308,9 +316,16 @@ __global__ void __launch_bounds__(IK_THREADS) ik_kernel_t(const RobotDev* __rest
   int si = 0, sj = 0;
   const bool sh = lane >= 42 && lane < 63;
   if (sh) upper_pair(lane - 42, &si, &sj);
+  // segments whose local rotation is exactly I (no revolute joint, identity f_tip rotation)
+  unsigned rid = 0;
+  for (int s = 0; s < ns; ++s) {
+    bool id = rb->seg_type[s] != 1;
+    for (int i = 0; i < 9; ++i) id = id && rb->seg_R[s * 9 + i] == ((i % 4 == 0) ? 1.0 : 0.0);
+    rid |= id ? 1u << s : 0u;
+  }
   if (lane < NJ) S.q[lane] = t.q[lane];
   wave_sync();
-  chain_fk(ns, S, lane, k);
+  chain_fk(ns, rid, S, lane, k);
   int iter = 0, fallback = 0, abandoned = 0;
   while (true) {
     const unsigned long long outb = jacobian_and_error(ns, t, S, lane, k, iter > 0);
@@ -324,9 +339,10 @@ __global__ void __launch_bounds__(IK_THREADS) ik_kernel_t(const RobotDev* __rest
     // J J^T, the augmented error column, the shifted upper triangle
     if (lane < 36) {
       const int i = lane / 6, c = lane - 6 * (lane / 6);
-      double s = S.J[i][0] * S.J[c][0];
+      double pp[NJ];
 #pragma unroll
-      for (int x = 1; x < NJ; ++x) s = s + S.J[i][x] * S.J[c][x];
+      for (int x = 0; x < NJ; ++x) pp[x] = S.J[i][x] * S.J[c][x];
+      const double s = ((pp[0] + pp[1]) + (pp[2] + pp[3])) + ((pp[4] + pp[5]) + (pp[6] + pp[7]));
       S.A[i][c] = s;
       S.M[i][c] = s;
       if (i <= c) S.P[i][c] = i == c ? s + (-tau) : s;
@@ -337,7 +353,7 @@ __global__ void __launch_bounds__(IK_THREADS) ik_kernel_t(const RobotDev* __rest
     // Gauss-Jordan on [A | e] and the symmetric elimination of A - tau I, side by side; lane 0 multiplies the pivots
     double pr = 1.0;
     for (int s = 0; s < 6; ++s) {
-      if (lane == 0) pr = pr * S.M[s][s];
+      pr = pr * S.M[s][s];
       if (lane < 42) {
         if (gi != s && gj > s) {
           const double f = S.M[gi][s] / S.M[s][s];
@@ -353,11 +369,12 @@ __global__ void __launch_bounds__(IK_THREADS) ik_kernel_t(const RobotDev* __rest
     bool normal = true;
 #pragma unroll
     for (int s = 0; s < 6; ++s) normal = normal && S.P[s][s] > 0.0;
-    if (lane == 0) {
+    double m_all = sqrt(pr), d_all = 0.0;  // the normal path's manipulability and damping, in every lane
+    if (m_all == 1.0 || m_all < 0.00001) m_all = 0.0001;
+    if (m_all < IK_MANIP_THR) d_all = IK_DAMP_MAX * ((1 - (m_all / IK_MANIP_THR)) * (1 - (m_all / IK_MANIP_THR)));
+    if (!normal && lane == 0) {
       double m;
-      if (normal) {
-        m = sqrt(pr);
-      } else {
+      {
         jacobi_eigen6(S.A, S.E, S.V);
         m = 1.0;
         for (int j = 0; j < 6; ++j) {
@@ -387,8 +404,9 @@ __global__ void __launch_bounds__(IK_THREADS) ik_kernel_t(const RobotDev* __rest
       S.damp = d;
     }
     fallback += normal ? 0 : 1;
-    wave_sync();
-    const double damp = S.damp;
+    if (!normal) wave_sync();
+    const double damp = normal ? d_all : S.damp;
+    if (normal && lane == 0) S.manip = m_all;
     if (normal && damp != 0.0) {  // damped system (A + d^2 I) z = e
       if (lane < 36) {
         const int i = lane / 6, c = lane - 6 * (lane / 6);
@@ -410,14 +428,15 @@ __global__ void __launch_bounds__(IK_THREADS) ik_kernel_t(const RobotDev* __rest
       double z[6];
 #pragma unroll
       for (int i = 0; i < 6; ++i) z[i] = normal ? S.M[i][6] / S.M[i][i] : S.z[i];
-      double v = S.J[0][lane] * z[0];
+      double pz[6];
 #pragma unroll
-      for (int i = 1; i < 6; ++i) v = v + S.J[i][lane] * z[i];
+      for (int i = 0; i < 6; ++i) pz[i] = S.J[i][lane] * z[i];
+      const double v = ((pz[0] + pz[1]) + (pz[2] + pz[3])) + (pz[4] + pz[5]);
       const double nv = S.q[k.j_jn] + v * IK_DT;
       if (!(nv < k.j_lo || nv > k.j_hi)) S.q[k.j_jn] = nv;
     }
     wave_sync();
-    chain_fk(ns, S, lane, k);
+    chain_fk(ns, rid, S, lane, k);
     ++iter;
     if (SEARCH && bst < b) {  // a lower candidate is REACHED and valid: this run can no longer be chosen
       abandoned = 1;

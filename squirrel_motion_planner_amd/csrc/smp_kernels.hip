@@ -1538,7 +1538,12 @@ __device__ void scout_asks(const Ctx& C, int t) {
   const bool sz = pre && S.n[0] < (1 << 20) && S.n[1] < (1 << 20);
   const unsigned long long csz = ((unsigned long long)(j & 0xffffff) << 40) | ((unsigned long long)S.n[0] << 20) |
                                  (unsigned long long)S.n[1];
-  for (int s = 0; s < C.Q.nscouts; ++s) {
+  const int nsc = pre ? C.Q.nscouts : min(C.Q.nscouts, 2);  // scouts 2 and up retire after the first solution
+  // from first_iter + 3 on no record asked before the first solution is looked up (scout_slots): scouts 2 and up
+  // stop (with their helpers) instead of polling beside the leader for the rest of the launch
+  if (!pre && j == S.first_iter + 3)
+    for (int s = 2; s < C.Q.nscouts; ++s) st_agent(&C.Q.scbs[s]->stop, 1);
+  for (int s = 0; s < nsc; ++s) {
     st_agent(&C.Q.scbs[s]->cur, (unsigned long long)j);
     // only to a scout on this XCD: the sizes hand over nodes stored without an agent release (a scout on another XCD
     // takes its request's sizes, whose nodes scout_ask released)
@@ -3584,7 +3589,10 @@ __device__ __forceinline__ void scout_main(Ctx& C, int which) {
   __syncthreads();
   unsigned last = 0;
   unsigned long long t_last = wall_clock64();
-  for (int k = 0;; k ^= 1) {
+  // scouts 2 and up only serve iterations before the first solution (scout_ask): in a launch that starts after it
+  // they retire at once, with their helpers, instead of polling beside the leader for the whole launch
+  const bool retired = which >= 2 && uni(g_L.S.tree_opt && g_L.S.have_sol);
+  for (int k = 0; !retired; k ^= 1) {
     if (threadIdx.x == 0) {
       int go = 0;
       if (ld_agent(&C.Q.scb->stop)) {
