@@ -1092,8 +1092,9 @@ static void ik_error(const double* cur, const IkTask& t, bool clamp, double* e) 
 }
 
 // KDL ChainJntToJacSolver::JntToJac for the frames T of q: column k of the k-th movable segment s is
-// T[s].M * (joint twist referred to the segment tip), then moved to every later tip by
-// Twist::RefPoint(total.p - T_tmp.p).  Rows 0-2 linear, 3-5 angular; cast to float (getJacobian, CL:5273-5301).
+// T[s].M * (joint twist referred to the segment tip), then referred to the chain tip (KDL: Twist::RefPoint to every
+// later tip in turn; the sum of those offsets telescopes to one).  Rows 0-2 linear, 3-5 angular; cast to float
+// (getJacobian, CL:5273-5301).
 static void jacobian(const Robot& rb, const double* q, const Frame* T, double J[6][8]) {
   int k = 0;
   for (int s = 0; s < rb.n_seg; ++s) {
@@ -1116,9 +1117,11 @@ static void jacobian(const Robot& rb, const double* q, const Frame* T, double J[
       vel[r] = B[r * 3 + 0] * vl[0] + B[r * 3 + 1] * vl[1] + B[r * 3 + 2] * vl[2];
       rot[r] = B[r * 3 + 0] * rl[0] + B[r * 3 + 1] * rl[1] + B[r * 3 + 2] * rl[2];
     }
-    for (int i = s + 1; i < rb.n_seg; ++i) {
+    // KDL moves the column to every later tip in turn (Twist::RefPoint(T[i+1].p - T[i].p), i > s); the offsets
+    // telescope, so the column is moved once, to the chain tip
+    {
       double dl[3];
-      for (int d = 0; d < 3; ++d) dl[d] = T[i + 1].p[d] - T[i].p[d];
+      for (int d = 0; d < 3; ++d) dl[d] = T[rb.n_seg].p[d] - T[s + 1].p[d];
       double x0 = rot[1] * dl[2] - rot[2] * dl[1], x1 = rot[2] * dl[0] - rot[0] * dl[2], x2 = rot[0] * dl[1] - rot[1] * dl[0];
       vel[0] = vel[0] + x0; vel[1] = vel[1] + x1; vel[2] = vel[2] + x2;
     }
@@ -1220,12 +1223,16 @@ static void ik_solve(const Robot& rb, const IkTask& t, IkOut* o) {
       for (int k = 0; k < 6; ++k) M[i][k] = A[i][k];
       M[i][6] = ep[i];
     }
-    // computeManipulabilityMeasure (CL:6050-6089): product of the singular values > 1e-5
-    const bool normal = shifted_pd6(A, tau);
+    // computeManipulabilityMeasure (CL:6050-6089): product of the singular values > 1e-5.  Every singular value
+    // exceeds 1e-5 (every eigenvalue of A exceeds tau) if det A > tau * tr(A)^5 (lambda_min >= det / lambda_max^5),
+    // else exactly when A - tau I is positive definite.
+    gauss_jordan6(M, z);
+    double pr = 1.0;
+    for (int k = 0; k < 6; ++k) pr = pr * M[k][k];
+    const double tr = ((((A[0][0] + A[1][1]) + A[2][2]) + A[3][3]) + A[4][4]) + A[5][5];
+    const double tr5 = (((tr * tr) * tr) * tr) * tr;
+    const bool normal = pr > tau * tr5 || shifted_pd6(A, tau);
     if (normal) {
-      gauss_jordan6(M, z);
-      double pr = 1.0;
-      for (int k = 0; k < 6; ++k) pr = pr * M[k][k];
       manip = std::sqrt(pr);
     } else {
       jacobi_eigen6(A, E, V);

@@ -8,10 +8,10 @@
 // (control_laws.cpp:2167-2245).  An iteration is a dependent chain of small steps, and gfx950 fp64 has ~40 cycles
 // of dependent latency, so a run stays on one wavefront and each step is laid out to be short and wide:
 //   J    lanes 0-7: Jacobian column c (the joint rotations come from the previous FK); lanes 8-13: the
-//        quaternion and error component of the previous FK, so the error leaves the critical path;
+//        quaternion and error component of the previous FK (divergent lanes of one wave run one after the other);
 //   A    lanes 0-35: J J^T; lanes 36-41: the error column of the augmented system;
-//   GJ   6 Gauss-Jordan steps on [J J^T | e] (lanes 0-41, one entry each) and, beside them, the symmetric
-//        elimination of J J^T - 1e-10 I (lanes 42-62) whose pivot signs decide the manipulability path;
+//   GJ   6 Gauss-Jordan steps on [J J^T | e] (lanes 0-41, one entry each); when det < 1e-10 tr^5 also the
+//        symmetric elimination of J J^T - 1e-10 I, whose pivot signs decide the manipulability path;
 //   q    lanes 0-7: q_dot_c = (J^T z)_c, joint update with the limit check;
 //   FK   lanes 0-11: local frame of every segment; lanes 0-2: one frame row each through the chain.
 // Robot constants live in registers (each lane always owns the same segment / column), the iteration touches
@@ -179,7 +179,8 @@ __device__ __forceinline__ void chain_fk(int ns, unsigned rid, IkLds& S, int lan
 }
 
 // Lanes 0-7: KDL ChainJntToJacSolver::JntToJac column of movable segment s = T[s].M * (joint twist referred to
-// the tip of s), then Twist::RefPoint(T[i+1].p - T[i].p) for every later segment i; cast to float (getJacobian).
+// the tip of s), referred to the chain tip (KDL's Twist::RefPoint(T[i+1].p - T[i].p) for every later segment i,
+// telescoped); cast to float (getJacobian).
 // Lanes 8-13: error component lane-8 of the end-effector pose T[ns] (set_EE_goal_pose unclamped, update_error_vec
 // clamped).  Returns the ballot of components outside the 1e-4 bound (is_error_within_bounds).
 __device__ __forceinline__ unsigned long long jacobian_and_error(int ns, const IkTaskDev& t, IkLds& S, int lane,
@@ -205,19 +206,11 @@ __device__ __forceinline__ unsigned long long jacobian_and_error(int ns, const I
       vel[r] = B[r * 3 + 0] * vl[0] + B[r * 3 + 1] * vl[1] + B[r * 3 + 2] * vl[2];
       rot[r] = B[r * 3 + 0] * rl[0] + B[r * 3 + 1] * rl[1] + B[r * 3 + 2] * rl[2];
     }
-    // RefPoint shifts of the later segments i = s+1 .. ns-1 in order; every step's offset and cross product are
-    // computed for all i (no dependence on vel), only the additions of the lane's own steps are kept
-    double p0 = S.T[1][9], p1 = S.T[1][10], p2 = S.T[1][11];
-#pragma unroll
-    for (int i = 1; i < MAX_SEG; ++i) {
-      const double n0 = S.T[i + 1][9], n1 = S.T[i + 1][10], n2 = S.T[i + 1][11];
-      const double d0 = n0 - p0, d1 = n1 - p1, d2 = n2 - p2;
+    // referred to the chain tip: KDL's RefPoint offsets to every later tip telescope to T[ns].p - T[s+1].p
+    {
+      const double d0 = S.T[ns][9] - S.T[s + 1][9], d1 = S.T[ns][10] - S.T[s + 1][10], d2 = S.T[ns][11] - S.T[s + 1][11];
       const double x0 = rot[1] * d2 - rot[2] * d1, x1 = rot[2] * d0 - rot[0] * d2, x2 = rot[0] * d1 - rot[1] * d0;
-      const bool on = i > s && i < ns;
-      vel[0] = on ? vel[0] + x0 : vel[0];
-      vel[1] = on ? vel[1] + x1 : vel[1];
-      vel[2] = on ? vel[2] + x2 : vel[2];
-      p0 = n0; p1 = n1; p2 = n2;
+      vel[0] = vel[0] + x0; vel[1] = vel[1] + x1; vel[2] = vel[2] + x2;
     }
     for (int d = 0; d < 3; ++d) {
       S.J[d][lane] = (double)(float)vel[d];
@@ -283,7 +276,7 @@ __device__ void jacobi_eigen6(const double (*A)[6], double (*a)[6], double (*V)[
   }
 }
 
-// Upper-triangle entry (i, j), i <= j, of shifted-elimination lane 42 + u (u < 21).
+// Upper-triangle entry (i, j), i <= j, of shifted-elimination lane u (u < 21).
 __device__ __forceinline__ void upper_pair(int u, int* i, int* j) {
   int r = 0, base = 0;
   while (u >= base + (6 - r)) { base += 6 - r; ++r; }
@@ -292,6 +285,19 @@ __device__ __forceinline__ void upper_pair(int u, int* i, int* j) {
 }
 
 }  // namespace
+
+#ifdef SMP_IK_PROF
+// Phase clocks (s_memtime) of block 0's iterations: tools/ik_phase_probe.py (profiling build only).
+__device__ unsigned long long g_ik_prof[8];
+#define IKP(k)                                                                \
+  if (lane == 0 && b == 0) {                                                  \
+    const unsigned long long _t = __builtin_amdgcn_s_memtime();               \
+    _pf[k] += _t - _tp;                                                       \
+    _tp = _t;                                                                 \
+  }
+#else
+#define IKP(k)
+#endif
 
 // One controller run per wavefront (block = 64 threads).  SEARCH: goal-search mode (collision check of a REACHED
 // pose, `best` candidate index shared by the grid, runs that can no longer be chosen stop).
@@ -314,8 +320,8 @@ __global__ void __launch_bounds__(IK_THREADS) ik_kernel_t(const RobotDev* __rest
   // main Gauss-Jordan lane (gi, gj) of the 6 x 7 system, or shifted-elimination lane (si, sj) of the upper triangle
   const int gi = lane / 7, gj = lane - 7 * (lane / 7);
   int si = 0, sj = 0;
-  const bool sh = lane >= 42 && lane < 63;
-  if (sh) upper_pair(lane - 42, &si, &sj);
+  const bool sh = lane < 21;
+  if (sh) upper_pair(lane, &si, &sj);
   // segments whose local rotation is exactly I (no revolute joint, identity f_tip rotation)
   unsigned rid = 0;
   for (int s = 0; s < ns; ++s) {
@@ -327,8 +333,12 @@ __global__ void __launch_bounds__(IK_THREADS) ik_kernel_t(const RobotDev* __rest
   wave_sync();
   chain_fk(ns, rid, S, lane, k);
   int iter = 0, fallback = 0, abandoned = 0;
+#ifdef SMP_IK_PROF
+  unsigned long long _pf[8] = {0, 0, 0, 0, 0, 0, 0, 0}, _tp = __builtin_amdgcn_s_memtime();
+#endif
   while (true) {
     const unsigned long long outb = jacobian_and_error(ns, t, S, lane, k, iter > 0);
+    IKP(0);
     if (iter > 0) {
       if (iter == max_iter) break;
       if (outb == 0ull) break;
@@ -350,25 +360,36 @@ __global__ void __launch_bounds__(IK_THREADS) ik_kernel_t(const RobotDev* __rest
       S.M[lane - 36][6] = 0.0 + IK_GAIN * S.err[lane - 36];
     }
     wave_sync();
-    // Gauss-Jordan on [A | e] and the symmetric elimination of A - tau I, side by side; lane 0 multiplies the pivots
+    IKP(1);
+    // Gauss-Jordan on [A | e]; every lane multiplies the pivots
     double pr = 1.0;
     for (int s = 0; s < 6; ++s) {
       pr = pr * S.M[s][s];
-      if (lane < 42) {
-        if (gi != s && gj > s) {
-          const double f = S.M[gi][s] / S.M[s][s];
-          S.M[gi][gj] = S.M[gi][gj] - f * S.M[s][gj];
-        }
-      } else if (sh && si > s) {
-        const double f = S.P[s][si] / S.P[s][s];
-        S.P[si][sj] = S.P[si][sj] - f * S.P[s][sj];
+      if (lane < 42 && gi != s && gj > s) {
+        const double f = S.M[gi][s] / S.M[s][s];
+        S.M[gi][gj] = S.M[gi][gj] - f * S.M[s][gj];
       }
       wave_sync();
     }
-    // computeManipulabilityMeasure (control_laws.cpp:6050-6089) and the damping (control_laws.cpp:5557-5569)
-    bool normal = true;
+    IKP(2);
+    // computeManipulabilityMeasure (control_laws.cpp:6050-6089) and the damping (control_laws.cpp:5557-5569): every
+    // singular value exceeds 1e-5 if det A > tau tr(A)^5, else exactly when A - tau I is positive definite (the
+    // symmetric elimination of its upper triangle, lanes 0-20; rare)
+    const double tr = ((((S.A[0][0] + S.A[1][1]) + S.A[2][2]) + S.A[3][3]) + S.A[4][4]) + S.A[5][5];
+    const double tr5 = (((tr * tr) * tr) * tr) * tr;
+    bool normal = pr > tau * tr5;
+    if (!normal) {
+      for (int s = 0; s < 6; ++s) {
+        if (sh && si > s) {
+          const double f = S.P[s][si] / S.P[s][s];
+          S.P[si][sj] = S.P[si][sj] - f * S.P[s][sj];
+        }
+        wave_sync();
+      }
+      normal = true;
 #pragma unroll
-    for (int s = 0; s < 6; ++s) normal = normal && S.P[s][s] > 0.0;
+      for (int s = 0; s < 6; ++s) normal = normal && S.P[s][s] > 0.0;
+    }
     double m_all = sqrt(pr), d_all = 0.0;  // the normal path's manipulability and damping, in every lane
     if (m_all == 1.0 || m_all < 0.00001) m_all = 0.0001;
     if (m_all < IK_MANIP_THR) d_all = IK_DAMP_MAX * ((1 - (m_all / IK_MANIP_THR)) * (1 - (m_all / IK_MANIP_THR)));
@@ -407,6 +428,7 @@ __global__ void __launch_bounds__(IK_THREADS) ik_kernel_t(const RobotDev* __rest
     if (!normal) wave_sync();
     const double damp = normal ? d_all : S.damp;
     if (normal && lane == 0) S.manip = m_all;
+    IKP(3);
     if (normal && damp != 0.0) {  // damped system (A + d^2 I) z = e
       if (lane < 36) {
         const int i = lane / 6, c = lane - 6 * (lane / 6);
@@ -436,7 +458,9 @@ __global__ void __launch_bounds__(IK_THREADS) ik_kernel_t(const RobotDev* __rest
       if (!(nv < k.j_lo || nv > k.j_hi)) S.q[k.j_jn] = nv;
     }
     wave_sync();
+    IKP(4);
     chain_fk(ns, rid, S, lane, k);
+    IKP(5);
     ++iter;
     if (SEARCH && bst < b) {  // a lower candidate is REACHED and valid: this run can no longer be chosen
       abandoned = 1;
@@ -452,6 +476,12 @@ __global__ void __launch_bounds__(IK_THREADS) ik_kernel_t(const RobotDev* __rest
     flags |= IK_CHECKED | (TL.coll[0] ? 0 : IK_VALID);
     if (lane == 0 && !TL.coll[0]) __hip_atomic_fetch_min(best, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+#ifdef SMP_IK_PROF
+  if (lane == 0 && b == 0) {
+    for (int i = 0; i < 6; ++i) g_ik_prof[i] += _pf[i];
+    g_ik_prof[6] += iter;
+  }
+#endif
   IkOutDev& o = out[b];
   if (lane < NJ) o.q[lane] = S.q[lane];
   if (lane < 6) o.err[lane] = S.err[lane];
@@ -472,6 +502,14 @@ void launch_ik(bool search, int n, hipStream_t st, const RobotDev* rb, const IkT
     hipLaunchKernelGGL(ik_kernel_t<false>, dim3(n), dim3(IK_THREADS), 0, st, rb, tasks, n, out, sc, mc, self, map,
                        best);
 }
+
+#ifdef SMP_IK_PROF
+extern "C" int smp_probe_ik_prof(unsigned long long* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ik_prof), sizeof(g_ik_prof)) != hipSuccess) return -5;
+  static const unsigned long long zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_ik_prof), zero, sizeof(zero)) == hipSuccess ? 0 : -5;
+}
+#endif
 
 size_t ik_kernels_private_bytes() {
   size_t need = 0;
