@@ -930,6 +930,13 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
           unsigned long long sp[32];
           HIPCHK(hipMemcpy(sp, qdev[i].scbs[sc]->prof, sizeof(sp), hipMemcpyDeviceToHost));
           for (int k = 0; k < 32; ++k) scout_prof[i][k] += sp[k];
+          if (i == 0 && std::getenv("SMP_DEBUG_SCOUTS")) {  // per-scout passes and XCD (experiments)
+            int xcc = 0;
+            HIPCHK(hipMemcpy(&xcc, &qdev[i].scbs[sc]->xcc, sizeof(int), hipMemcpyDeviceToHost));
+            std::fprintf(stderr, "[smp] launch %lld scout %d: passes %llu busy %.1f us idle %.1f us xcc %d\n",
+                         (long long)launches, sc, sp[30], sp[31] / (p->wall_rate_hz * 1e-6), sp[28] / (p->wall_rate_hz * 1e-6),
+                         xcc - 1);
+          }
         }
     }
     HIPCHK(hipStreamSynchronize(p->stream));

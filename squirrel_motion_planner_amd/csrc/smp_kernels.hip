@@ -229,6 +229,7 @@ struct PlanLds {
 #endif
   int sp_on, sp_stage, sp_go[2];
   int sc_same[MAX_SCOUTS];      // leader: scout s runs on this XCD (1), another (0), not yet known (-1)
+  unsigned sc_seen, sc_dead;    // leader: scouts that delivered a pre-solution record / that never did and timed out
   int asked[SCOUT_SLOTS];       // leader: scout s + 1 asked for iteration k in slot k % SCOUT_SLOTS, 0 = none
   int asked_conn[SCOUT_SLOTS];  // leader: that record will carry connect's scans (stage SC_CONN)
   int asked_pre[SCOUT_SLOTS];   // leader: asked before the first solution (a pre-solution record)
@@ -1485,7 +1486,17 @@ __device__ void spec_copy(const ScoutBoard* sb, int par, int have, int st) {
 __device__ void scout_ask(const Ctx& C, long long k, int tree, bool pre, bool& fenced) {
   const QState& S = g_L.S;
   const int ns = C.Q.nscouts;
-  const int which = 1 + (int)(pre ? k % ns : (ns >= 2 ? (k & 1) : 0));
+  int which = 1 + (int)(pre ? k % ns : (ns >= 2 ? (k & 1) : 0));
+  if ((g_L.sc_dead >> (which - 1)) & 1u) {  // a scout that never delivered: the next live one before the first
+    if (!pre) return;                         // solution, none after it (the iteration takes the full path)
+    int w = -1;
+    for (int d = 1; d < ns && w < 0; ++d) {
+      const int c = (int)((k + d) % ns);
+      if (!((g_L.sc_dead >> c) & 1u)) w = c;
+    }
+    if (w < 0) return;
+    which = 1 + w;
+  }
   ScoutBoard* sb = C.Q.scbs[which - 1];
   int& same = g_L.sc_same[which - 1];
   if (same < 0) {
@@ -2155,6 +2166,7 @@ __device__ void sample_read(const Ctx& C) {
   const bool prer_ok = prerec && !stale_granule;
   if (threadIdx.x == 0) {
     g_L.prer_ok = prer_ok;
+    if (prer_ok) g_L.sc_seen |= 1u << (sw - 1);
     sample_publish(C);
     if (C.Q.nscouts > 0) scout_asks(C, 1 - g_L.S.A);
   }
@@ -2652,12 +2664,27 @@ __device__ bool pre_wait(const Ctx& C) {
     const bool bad = __syncthreads_or(!ok) != 0;
     if (!bad) break;
     if (uni(g_L.sp_go[k])) {
-      if (threadIdx.x == 0) g_L.S.sc_wait += wall_clock64() - t0;
+      if (threadIdx.x == 0) {
+        g_L.S.sc_wait += wall_clock64() - t0;
+        // a scout that timed out without ever having delivered a record is taken as not running (its workgroup
+        // may start late): it is asked no more in this launch, and its outstanding iterations are asked again of
+        // the others instead of each waiting out SCOUT_WAIT
+        const int w = g_L.asked[par];
+        if (!((g_L.sc_seen >> (w - 1)) & 1u) && !ld_agent(&sb->stop)) {
+          g_L.sc_dead |= 1u << (w - 1);
+          for (int x = 0; x < SCOUT_SLOTS; ++x)
+            if (x != par && g_L.asked[x] == w) g_L.asked[x] = 0;
+        }
+      }
       __syncthreads();  // every wave has read sp_go[k] before the next poll loop writes it again
       return false;
     }
   }
-  if (threadIdx.x == 0) { g_L.S.sc_wait += wall_clock64() - t0; g_L.prer_ok = 1; }
+  if (threadIdx.x == 0) {
+    g_L.S.sc_wait += wall_clock64() - t0;
+    g_L.prer_ok = 1;
+    g_L.sc_seen |= 1u << (g_L.asked[par] - 1);
+  }
   __syncthreads();
   return true;
 }
@@ -3591,7 +3618,11 @@ __device__ __forceinline__ void scout_main(Ctx& C, int which) {
   unsigned long long t_last = wall_clock64();
   // scouts 2 and up only serve iterations before the first solution (scout_ask): in a launch that starts after it
   // they retire at once, with their helpers, instead of polling beside the leader for the whole launch
+#ifdef SMP_NO_RETIRE
+  const bool retired = false;
+#else
   const bool retired = which >= 2 && uni(g_L.S.tree_opt && g_L.S.have_sol);
+#endif
   for (int k = 0; !retired; k ^= 1) {
     if (threadIdx.x == 0) {
       int go = 0;
@@ -3693,6 +3724,8 @@ __global__ void __launch_bounds__(BLOCK) plan_kernel(const RobotDev* __restrict_
   if (threadIdx.x == 0) {
     g_L.sp_on = 0;
     for (int k = 0; k < MAX_SCOUTS; ++k) g_L.sc_same[k] = -1;
+    g_L.sc_seen = 0;
+    g_L.sc_dead = 0;
     for (int k = 0; k < SCOUT_SLOTS; ++k) { g_L.asked[k] = 0; g_L.asked_conn[k] = 0; g_L.asked_pre[k] = 0; }
     g_L.conn_rec = 0;
     g_L.rec_grp = -1;
