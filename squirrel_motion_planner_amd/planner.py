@@ -190,6 +190,8 @@ class GpuPlanner:
         ee = np.asarray(ee_poses, np.float64).reshape(-1, 6)
         if len(ee) == 1:
             ee = np.repeat(ee, len(q_inits), 0)
+        if len(ee) != len(q_inits):
+            raise ValueError("ik_solve: %d end-effector poses for %d start configurations" % (len(ee), len(q_inits)))
         dev = np.asarray(IK_DEVIATION if deviation is None else deviation, np.float64).reshape(6, 2)
         n = len(q_inits)
         reqs = (L.IkRequest * max(n, 1))()
