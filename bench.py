@@ -63,7 +63,7 @@ def workload_name(a, sc):
             "queries per GPU, path_optimality_threshold=-inf" % a.queries_per_gpu)
 
 
-def cpu_baseline(sc, pair, a, step0_seed):
+def cpu_baseline(sc, pair, a, step0_seed, step_seeds=()):
     """The oracle (sequential C++ restatement of the reference loop, 1 thread) on query 0 of GPU step 0.
 
     Same scene, (start, goal), seed, query id and budget, so the CPU run plans the identical trees; the bench
@@ -88,7 +88,17 @@ def cpu_baseline(sc, pair, a, step0_seed):
                                                            r["checked"], r["t_total"], cpu),
             "valid_configs_per_s": r["valid"] / r["t_total"],
             "iterations": r["iterations"], "checked": r["checked"], "time_first_solution_s": r["t_first"],
-            "iters_per_s": r["iterations"] / r["t_total"], "cost_best": r["cost"][0]}
+            "iters_per_s": r["iterations"] / r["t_total"], "cost_best": r["cost"][0],
+            # the oracle's time to the first feasible path for every timed step's seed (short runs, same query),
+            # beside the GPU's per-step list: the first-solution iteration differs from seed to seed
+            "time_first_solution_steps_s": [first_solution(orc, sc, pair, sd) for sd in step_seeds] or None}
+
+
+def first_solution(orc, sc, pair, seed, max_iter=600):
+    """Oracle time to the first feasible path of query 0 with this seed (None if not within max_iter)."""
+    r = orc.plan(pair[0], pair[1], env_x=sc.env_x, env_y=sc.env_y, seed=seed, query=0, opt_thresh=-math.inf,
+                 max_iter=max_iter)
+    return r["t_first"] if r["t_first"] >= 0 else None
 
 
 def main():
@@ -221,6 +231,7 @@ def main():
             "valid_configs_per_s": valid / elapsed,
             "iterations_per_s": iters / elapsed,
             "time_to_first_feasible_path_s": (sum(first_t) / len(first_t)) if first_t else None,
+            "time_to_first_feasible_path_steps_s": first_t if a.queries_per_gpu == 1 else None,
             # priced against HBM (no dense contraction); the measured limiter is the dependent latency of
             # one query's iteration chain, not bandwidth: trees and grid stay in L2 / Infinity Cache
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -232,7 +243,9 @@ def main():
                          "algorithmic_bytes_rank0": alg_bytes_rank0},
         }
         if not a.no_cpu and world == 1:
-            cb = cpu_baseline(sc, pairs[0], a, step0_seed=a.seed)
+            cb = cpu_baseline(sc, pairs[0], a, step0_seed=a.seed, step_seeds=[a.seed + 1000 * step for step in
+                                                                             range(a.steps)]
+                              if a.queries_per_gpu == 1 else ())
             cb["same_result_as_gpu_step0"] = bool(cb["checked"] == step0["configs_checked"] and
                                                   cb["iterations"] == step0["iterations"] and
                                                   cb["cost_best"] == step0["cost_best"][0])

@@ -827,7 +827,9 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
     if (const char* e = std::getenv("SMP_LEAD_DIV")) lead_div = std::max(1, std::atoi(e));
     h_lead = ns >= 2 ? avail / lead_div : avail / 2;
     int rest = avail - h_lead;
-    for (int s = 2; s < ns; ++s) { h_s[s] = std::min(3, rest); rest -= h_s[s]; }
+    int pre_h = 6;  // SMP_PRE_HELPERS: helpers of each pre-solution-only scout (its jobs: expand + connect edge, 6 tiles)
+    if (const char* e = std::getenv("SMP_PRE_HELPERS")) pre_h = std::max(0, std::atoi(e));
+    for (int s = 2; s < ns; ++s) { h_s[s] = std::min(pre_h, rest); rest -= h_s[s]; }
     if (ns >= 2) { h_s[0] = rest - rest / 2; h_s[1] = rest / 2; } else { h_s[0] = rest; }
   }
   // before the first solution a scout starts record k when the leader reaches k - pre_delay (DESIGN.md "Pre-solution
@@ -892,14 +894,11 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
         }
       }
       HIPCHK(hipEventRecord(p->ev_board, p->stream));
-      HIPCHK(hipStreamWaitEvent(p->hstream, p->ev_board, 0));
-      hipLaunchKernelGGL(helper_kernel, dim3(nq * nh), dim3(BLOCK), 0, p->hstream, p->d_rb, p->sc, p->d_mc,
-                         p->d_qdev.p, nq);
-      HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(p->ev0, p->stream));
     // scout s of query q at block scout_base + s * round8(nq) + q, scout_base a multiple of 8: blocks b and b + 8
-    // are dealt to the same XCD (plan_kernel)
+    // are dealt to the same XCD (plan_kernel).  The leaders and scouts are queued before the helpers, so their
+    // workgroups find CUs first (a scout queued behind 200 helpers was seen to start only when they left).
     const int r8 = (nq + 7) / 8 * 8;
     const int scout_base = ns > 0 ? r8 : 0;
     const int grid = ns > 0 ? scout_base + (ns - 1) * r8 + nq : nq;
@@ -907,6 +906,12 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
                        p->d_mc, p->d_qdev.p, nq, scout_base, chunk);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(p->ev1, p->stream));
+    if (nh > 0) {  // the helpers on their own (high-priority, separate hardware queue) stream, after the board reset
+      HIPCHK(hipStreamWaitEvent(p->hstream, p->ev_board, 0));
+      hipLaunchKernelGGL(helper_kernel, dim3(nq * nh), dim3(BLOCK), 0, p->hstream, p->d_rb, p->sc, p->d_mc,
+                         p->d_qdev.p, nq);
+      HIPCHK(hipGetLastError());
+    }
     launches++;
     if (debug) {  // bounded wait: print the leader's progress markers if the launch does not finish
       auto tw = std::chrono::steady_clock::now();

@@ -2652,7 +2652,9 @@ __device__ bool conn_stage(const Ctx& C, int B) {
 // Leader: the pre-solution record of this iteration, complete in g_L.prer -- from sample_read's round, else polled
 // (every granule tagged) until it is or SCOUT_WAIT passes or the scout has left.  All threads.
 __device__ bool pre_wait(const Ctx& C) {
+  TR();
   if (uni(g_L.prer_ok)) return true;
+  TR();
   const int par = (int)(g_L.S.iter & (SCOUT_SLOTS - 1));
   const ScoutBoard* sb = C.Q.scbs[uni(g_L.asked[par]) - 1];
   const unsigned tag = (unsigned)(g_L.S.iter + 1);
@@ -2685,6 +2687,7 @@ __device__ bool pre_wait(const Ctx& C) {
     g_L.prer_ok = 1;
     g_L.sc_seen |= 1u << (g_L.asked[par] - 1);
   }
+  TR();
   __syncthreads();
   return true;
 }
@@ -3377,9 +3380,29 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
     for (int k = 0; k < 3; ++k) R.ex.acc[k] = g_L.eg_acc[0][k];
     R.ex.ok = 1;
   }
-  // the near set of the edge's end (x_new if the edge is valid) is scanned while the helpers check the edge
+  // the near set of the edge's end (x_new if the edge is valid) is scanned while the helpers check the edge.
+  // Before the first solution connect's direct edge goes into the same job: x_new is the expand edge's end if that
+  // edge is valid, so its nearest node in the other tree (over that tree's first XB nodes; it only grows until then)
+  // and the edge from it are known now; the connect half is dropped when the expand edge collides.
   if (threadIdx.x == 0) g_L.spec = OV_NONE;
-  edge_validity(C, 1, false, P_XEXPAND, opt ? OV_NEAR_EXPAND : OV_NONE, t);
+  const bool spec_conn = !opt && !sc_stale(C, tag);
+  int cid_s = 0;
+  if (spec_conn) {
+    const int tb = 1 - t;
+    cid_s = nearest(C, tb, g_L.eg_end[0]);
+    if (threadIdx.x == 0) {
+      load_node(C, tb, cid_s, &g_L.xc);
+      for (int j = 0; j < NJ; ++j) { g_L.eg_start[1][j] = g_L.xc.q[j]; g_L.eg_target[1][j] = g_L.eg_end[0][j]; }
+      for (int k = 0; k < 3; ++k) g_L.eg_base[1][k] = g_L.xc.c[k];
+      g_L.eg_need[1] = 1;
+    }
+    for (int e = 2 + threadIdx.x; e < MAXE; e += BLOCK) g_L.eg_need[e] = 0;
+    __syncthreads();
+    edge_costs(C, 2);
+    edge_validity(C, 2, false, P_XEXPAND, OV_NONE, t);
+  } else {
+    edge_validity(C, 1, false, P_XEXPAND, opt ? OV_NEAR_EXPAND : OV_NONE, t);
+  }
   if (threadIdx.x == 0) {
     for (int j = 0; j < NJ; ++j) { R.e[0].s[j] = g_L.eg_start[0][j]; R.e[0].g[j] = g_L.eg_target[0][j]; }
     for (int k = 0; k < 3; ++k) R.e[0].acc[k] = g_L.eg_acc[0][k];
@@ -3402,28 +3425,31 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
     sc_copy_out(sb, par, &R.e[0], sizeof(ScoutEdge));
     sc_copy_out(sb, par, &R.ex, sizeof(ScoutExpand));
   }
-  if (!opt && uni(g_L.ext_nn) && !sc_stale(C, tag)) {
+  if (spec_conn && uni(g_L.ext_nn)) {
     // before the first solution the iteration goes on with connect (connectGraphs): x_new is the expand edge's
-    // end; its nearest node in the other tree over that tree's first XB nodes (the tree only grows until then)
-    // and the direct edge to it, whose check always runs while there is no solution (c_best = inf)
+    // end, and its direct edge from the nearest node of the other tree (whose check always runs while there is
+    // no solution, c_best = inf) was checked in the expand job; its data move to edge slot 0
     const int tb = 1 - t;
-    const int cid = nearest(C, tb, g_L.xn.q);
+    const int cid = cid_s;
+    if (threadIdx.x < NJ) {
+      const int j = threadIdx.x;
+      g_L.eg_start[0][j] = g_L.eg_start[1][j]; g_L.eg_target[0][j] = g_L.eg_target[1][j];
+      g_L.eg_step[0][j] = g_L.eg_step[1][j]; g_L.eg_end[0][j] = g_L.eg_end[1][j];
+    }
+    if (threadIdx.x < 3) {
+      const int k = threadIdx.x;
+      g_L.eg_base[0][k] = g_L.eg_base[1][k]; g_L.eg_acc[0][k] = g_L.eg_acc[1][k]; g_L.eg_cost[0][k] = g_L.eg_cost[1][k];
+    }
     if (threadIdx.x == 0) {
-      load_node(C, tb, cid, &g_L.xc);
+      g_L.eg_first[0] = g_L.eg_first[1];
       double s = 0.0;
       for (int j = 0; j < NJ; ++j) { double d = g_L.xn.q[j] - g_L.xc.q[j]; s += d * d; }
       const double d = sqrt(s);
       for (int j = 0; j < NJ; ++j) R.cn.q[j] = g_L.xn.q[j];
       R.cn.d = d < 10000.0 ? d : 10000.0;
       R.cn.id = cid; R.cn.X = XB; R.cn.t = tb;
-      for (int j = 0; j < NJ; ++j) { g_L.eg_start[0][j] = g_L.xc.q[j]; g_L.eg_target[0][j] = g_L.xn.q[j]; }
-      for (int k = 0; k < 3; ++k) g_L.eg_base[0][k] = g_L.xc.c[k];
-      g_L.eg_need[0] = 1;
     }
-    for (int e = 1 + threadIdx.x; e < MAXE; e += BLOCK) g_L.eg_need[e] = 0;
     __syncthreads();
-    edge_costs(C, 1);
-    edge_validity(C, 1, false, P_XCONNECT);
     if (threadIdx.x == 0) {
       for (int j = 0; j < NJ; ++j) { R.cn.e.s[j] = g_L.eg_start[0][j]; R.cn.e.g[j] = g_L.eg_target[0][j]; }
       for (int k = 0; k < 3; ++k) { R.cn.e.acc[k] = g_L.eg_acc[0][k]; R.cn.c[k] = g_L.xc.c[k]; }
