@@ -170,6 +170,16 @@ __device__ __forceinline__ void chain_local(const RobotDev* __restrict__ rb, int
 
 __device__ __forceinline__ uint32_t shfl_u32(uint32_t v, int src) { return (uint32_t)__shfl((int)v, src); }
 
+// Value of lane I of this lane's quad (DPP quad_perm broadcast, both 32-bit halves).  The whole quad must be active.
+template <int I>
+__device__ __forceinline__ double quad_bcast(double v) {
+  constexpr int ctrl = I | (I << 2) | (I << 4) | (I << 6);
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, ctrl, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), ctrl, 0xF, 0xF, false);
+  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+
 // Cooperative exact map test of sphere centre cc, radius r by one wavefront.  The brick words covering the
 // reach (<= 64) are loaded once, one per lane, and handed to the lanes testing their cells by shuffles; then
 // lanes sweep the cells in reach (exact box test, ballot early exit).  Larger reaches load per cell.
@@ -287,52 +297,54 @@ __device__ __forceinline__ void collide_tile(const RobotDev* __restrict__ rb, co
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   unsigned long long t0 = (prof && tid == 0) ? wall_clock64() : 0;
   const int nch = rb->n_chain;
-  // A
-  for (int it = tid; it < nc * nch; it += BLOCK) {
-    const int c = it / nch, k = it - c * nch;
-    double st = 0.0, ct = 1.0;
-    if (rb->ch_type[k] == 1) psincos(q_lds[c][rb->ch_joint[k]], &st, &ct);
-    Frame F;
-    chain_local(rb, k, q_lds[c], st, ct, &F);
-    double* o = L.u.lf[c][k];
-    for (int i = 0; i < 9; ++i) o[i] = F.R[i];
-    o[9] = F.p[0]; o[10] = F.p[1]; o[11] = F.p[2];
+  static_assert(CT <= 4 * NWAVE, "stages A/B: four configurations per wavefront");
+  // A: wavefront w builds the local frames of its configurations 4w .. 4w+3 (sin/cos included), one
+  // (configuration, chain step) per lane, so that B (same wavefront) needs no block barrier.
+  {
+    const int cb = wave * 4;
+    for (int it = lane; it < 4 * nch; it += 64) {
+      const int c = cb + it / nch, k = it - (it / nch) * nch;
+      if (c >= nc) break;
+      double st = 0.0, ct = 1.0;
+      if (rb->ch_type[k] == 1) psincos(q_lds[c][rb->ch_joint[k]], &st, &ct);
+      Frame F;
+      chain_local(rb, k, q_lds[c], st, ct, &F);
+      double* o = L.u.lf[c][k];
+      for (int i = 0; i < 9; ++i) o[i] = F.R[i];
+      o[9] = F.p[0]; o[10] = F.p[1]; o[11] = F.p[2];
+    }
+    for (int it = tid; it < CT * SW; it += BLOCK) (&L.cand[0][0])[it] = 0u;
+    if (tid < nc) L.coll[tid] = 0;
+    wave_sync();
   }
-  for (int it = tid; it < CT * SW; it += BLOCK) (&L.cand[0][0])[it] = 0u;
-  if (tid < nc) L.coll[tid] = 0;
-  __syncthreads();
   unsigned long long ta = (prof && tid == 0) ? wall_clock64() : 0;
-  // B: 3 lanes per configuration, one row each.  Row r of T * L needs only row r of T (and all of the local
-  // frame L), so each lane carries its row through the whole chain in registers, no exchange between lanes;
-  // fmul's evaluation order.  The next step's local frame is loaded before this step's products (software
-  // pipelining: the LDS latency hides behind the dependent fp64 chain instead of adding to it).
-  if (tid < nc * 3) {
-    const int c = tid / 3, r = tid - c * 3;
-    double t0 = r == 0 ? 1.0 : 0.0, t1 = r == 1 ? 1.0 : 0.0, t2 = r == 2 ? 1.0 : 0.0;
-    double tp = r == 2 ? rb->root_z : 0.0;
-    double l[12];
-    int bd = rb->ch_body[0];
-#pragma unroll
-    for (int i = 0; i < 12; ++i) l[i] = L.u.lf[c][0][i];
-    for (int k = 0; k < nch; ++k) {
-      const int kn = k + 1 < nch ? k + 1 : k;
-      double ln[12];
-#pragma unroll
-      for (int i = 0; i < 12; ++i) ln[i] = L.u.lf[c][kn][i];
-      const int bdn = rb->ch_body[kn];
-      const double n0 = t0 * l[0] + t1 * l[3] + t2 * l[6];
-      const double n1 = t0 * l[1] + t1 * l[4] + t2 * l[7];
-      const double n2 = t0 * l[2] + t1 * l[5] + t2 * l[8];
-      const double m = t0 * l[9] + t1 * l[10] + t2 * l[11];
-      tp = m + tp;
-      t0 = n0; t1 = n1; t2 = n2;
-      if (bd >= 0) {
-        double* o = L.fr[c][bd];
-        o[r * 3 + 0] = t0; o[r * 3 + 1] = t1; o[r * 3 + 2] = t2; o[9 + r] = tp;
+  // B: one lane per element of the chain product, 16 lanes per configuration (rows r = 0..2 of four lanes:
+  // columns 0..2 of R, then p; the fourth row of lanes idles).  Element (r, col) of T * L is row r of T times
+  // column col of L -- fmul's three-term sum in its order, p adding T.p[r] last -- and row r of T is read from
+  // the lane's own quad by DPP broadcasts, so a chain step costs one dependent mul/add/add plus the broadcast
+  // and each lane issues five fp64 operations per step instead of twenty (stage B is issue-bound in one wave).
+  {
+    const int c = wave * 4 + (lane >> 4), r = (lane >> 2) & 3, col = lane & 3;
+    if (c < nc && r < 3) {
+      const int lo = col < 3 ? col : 9, ls = col < 3 ? 3 : 1;  // column col of L: lf[lo + i * ls], i = 0..2
+      double v = col < 3 ? (r == col ? 1.0 : 0.0) : (r == 2 ? rb->root_z : 0.0);
+      const double* lf = L.u.lf[c][0];
+      double l0 = lf[lo], l1 = lf[lo + ls], l2 = lf[lo + 2 * ls];
+      int bd = rb->ch_body[0];
+      const int oidx = col < 3 ? r * 3 + col : 9 + r;
+      for (int k = 0; k < nch; ++k) {
+        const int kn = k + 1 < nch ? k + 1 : k;
+        const double* ln = L.u.lf[c][kn];
+        const double n0 = ln[lo], n1 = ln[lo + ls], n2 = ln[lo + 2 * ls];
+        const int bdn = rb->ch_body[kn];
+        const double t0 = quad_bcast<0>(v), t1 = quad_bcast<1>(v), t2 = quad_bcast<2>(v);
+        const double s = t0 * l0 + t1 * l1 + t2 * l2;
+        const double sp = s + v;
+        v = col < 3 ? s : sp;
+        if (bd >= 0) L.fr[c][bd][oidx] = v;
+        l0 = n0; l1 = n1; l2 = n2;
+        bd = bdn;
       }
-#pragma unroll
-      for (int i = 0; i < 12; ++i) l[i] = ln[i];
-      bd = bdn;
     }
   }
   __syncthreads();
