@@ -3,9 +3,8 @@
 // The ROS node (squirrel_8dof_planner) owns a BiRRTstarPlanner by value (squirrel_8dof_planner.h:131) and calls
 // the methods below (squirrel_8dof_planner.cpp:16, 482-810, 872-915, 1179-1248).  This class keeps those
 // signatures (birrt_star.h:27-110) and forwards every call to the C ABI in smp_gpu.h, so the node compiles
-// against it unchanged except for getCollisions (squirrel_8dof_planner.cpp:839, a visualisation helper outside the
-// sampling / collision path), which this class does not provide; the planning loop and the goal
-// search's IK controller run in the HIP kernels of libsmp_gpu.so.
+// against it unchanged; the planning loop, the collision listing of getCollisions (squirrel_8dof_planner.cpp:839) and
+// the goal search's IK controller run in the HIP kernels of libsmp_gpu.so.
 //
 // Build: include this header instead of <birrt_star_algorithm/birrt_star.h> and link -lsmp_gpu.
 // Configuration (environment, read by initialize()):
@@ -221,6 +220,23 @@ class BiRRTstarPlanner {
     int v = 0;
     check(smp_is_config_valid(planner_, config.data(), check_self_collision, check_map_collision, &v), "isConfigValid");
     return v != 0;
+  }
+
+  // birrt_star.cpp:6910-6914 (collision_checker.hpp:123-132, 594-630): appends the colliding self pairs (pair order)
+  // and the map-colliding links (name order, disabled links included) of one configuration.
+  void getCollisions(const std::vector<double>& jointPositions, std::vector<std::pair<std::string, std::string> >& selfCollisions,
+                     std::vector<std::string>& mapCollisions) {
+    need();
+    if (jointPositions.size() != 8) throw std::runtime_error("getCollisions: 8 joint positions expected");
+    const int nl = smp_robot_num_links(robot_);
+    std::vector<int32_t> sp(2 * 256), ml(nl > 0 ? nl : 1);
+    int ns = 0, nm = 0;
+    check(smp_get_collisions(planner_, jointPositions.data(), sp.data(), 256, &ns, ml.data(), nl, &nm), "getCollisions");
+    if (ns > 256 || nm > nl) throw std::runtime_error("getCollisions: more results than links");
+    for (int k = 0; k < ns; ++k)
+      selfCollisions.push_back(std::make_pair(std::string(smp_robot_link_name(robot_, sp[2 * k])),
+                                              std::string(smp_robot_link_name(robot_, sp[2 * k + 1]))));
+    for (int k = 0; k < nm; ++k) mapCollisions.push_back(smp_robot_link_name(robot_, ml[k]));
   }
 
   // birrt_star.cpp:1627-1686: the VDLS controller (control_laws.cpp:3283-3712) from poseInit towards

@@ -24,6 +24,8 @@
  *   smp_plan_batch             independent queries against one scene (one workgroup each)
  *   smp_check_configs          batched isConfigValid (birrt_star.cpp:6897-6908) -> valid flags
  *   smp_is_config_valid        BiRRTstarPlanner::isConfigValid for one configuration
+ *   smp_get_collisions         BiRRTstarPlanner::getCollisions (birrt_star.cpp:6910-6914 -> collision_checker.hpp:
+ *                              123-132, 594-630): colliding self pairs and map-colliding links of one configuration
  *   smp_check_sequence         the node's keyframe loops over isConfigValid (fold / unfold arm,
  *                              squirrel_8dof_planner.cpp:759-784, 814-823): first invalid pose, one kernel launch
  *   smp_normalize_trajectory   Planner::normalizeTrajectory (squirrel_8dof_planner.cpp:1557-1637), host only
@@ -196,6 +198,12 @@ int64_t smp_get_tree(smp_planner* p, int which, int32_t* parent, double* conf, d
 
 int smp_check_configs(smp_planner* p, const double* q_soa, int64_t n, int check_self, int check_map, uint8_t* valid);
 int smp_is_config_valid(smp_planner* p, const double q[8], int check_self, int check_map, int* valid);
+/* Every self pair that collides (2 link indices each, smp_robot_link_name, in the model's pair order -- the SRDF-enabled
+ * link pairs i < j in link order, CC:378-388) and every collision link that touches the map (link indices in name
+ * order, as the reference's std::map; disabled links included, CC:610-630).  Writes at most max_self pairs /
+ * max_map links; *n_self / *n_map receive the full counts (the caller compares them with its capacity). */
+int smp_get_collisions(smp_planner* p, const double q[8], int32_t* self_pairs, int max_self, int* n_self,
+                       int32_t* map_links, int max_map, int* n_map);
 /* n poses, row-major n x 8: *first_invalid = index of the first pose in collision, -1 if all are valid. */
 int smp_check_sequence(smp_planner* p, const double* q_rows, int64_t n, int check_self, int check_map,
                        int64_t* first_invalid);

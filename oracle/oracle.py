@@ -75,6 +75,7 @@ def lib():
         L.orc_create.argtypes = [ctypes.POINTER(RobotDesc), ctypes.POINTER(SceneDesc), ctypes.c_void_p]
         L.orc_destroy.argtypes = [ctypes.c_void_p]
         L.orc_check_configs.argtypes = [ctypes.c_void_p, _pd, _i, _i, _i, ctypes.c_void_p]
+        L.orc_collisions.argtypes = [ctypes.c_void_p, _pd, ctypes.c_void_p, ctypes.c_void_p]
         L.orc_fk.argtypes = [ctypes.c_void_p, _pd, _i, _pd, _pd]
         L.orc_sincos.argtypes = [_pd, _i, _pd, _pd]
         L.orc_body_fk.argtypes = [ctypes.c_void_p, _pd, _i, _pd]
@@ -278,6 +279,18 @@ class Oracle:
         out = np.zeros(len(q), np.uint8)
         lib().orc_check_configs(self.h, _p(q, _d), len(q), int(self_), int(map_), out.ctypes.data_as(ctypes.c_void_p))
         return out
+
+    def collisions(self, q):
+        """getCollisions restated (smp_oracle.cpp orc_collisions): ([(link a, link b)] of the overlapping model pairs in
+        pair order, [links touching the map] in name order), as link names."""
+        q = np.ascontiguousarray(q, np.float64).reshape(8)
+        rb = self.robot
+        lm = np.zeros(rb.n_links, np.uint8)
+        ps = np.zeros(max(rb.n_pairs, 1), np.uint8)
+        lib().orc_collisions(self.h, _p(q, _d), lm.ctypes.data_as(ctypes.c_void_p), ps.ctypes.data_as(ctypes.c_void_p))
+        names = [e["name"] for e in rb.model["links"]]
+        pairs = [(names[rb.pair_a[k]], names[rb.pair_b[k]]) for k in range(rb.n_pairs) if ps[k]]
+        return pairs, sorted(names[l] for l in range(rb.n_links) if lm[l])
 
     def fk(self, q):
         q = np.ascontiguousarray(q, np.float64).reshape(-1, 8)

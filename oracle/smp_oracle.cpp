@@ -1502,6 +1502,33 @@ void orc_check_configs(void* hp, const double* q, int n, int self, int map, uint
   for (int i = 0; i < n; ++i) valid[i] = h->ck.in_collision(q + 8 * i, self, map) ? 0 : 1;
 }
 
+// getCollisions (birrt_star.cpp:6910-6914 -> collision_checker.hpp:123-132): link_map[link] = 1 if a sphere of the
+// link touches the map (getMapCollisions, CC:610-630: disabled links included), pair_self[p] = 1 if model pair p
+// overlaps (getSelfCollisions, CC:594-608: every pair, no early exit).
+void orc_collisions(void* hp, const double* q, uint8_t* link_map, uint8_t* pair_self) {
+  orc_handle* h = (orc_handle*)hp;
+  orc::Checker& ck = h->ck;
+  const orc::Robot& rb = *ck.rb;
+  orc::body_frames(rb, q, ck.frames.data());
+  for (int i = 0; i < rb.n_sph; ++i) orc::xform(ck.frames[rb.sph_body[i]], &rb.sph_cb[i * 3], &ck.wc[i * 3]);
+  for (int l = 0; l < rb.n_links; ++l) link_map[l] = 0;
+  if (ck.sc)
+    for (int i = 0; i < rb.n_sph; ++i)
+      if (orc::sphere_hits_map(*ck.sc, &ck.wc[i * 3], rb.sph_r[i], ck.T[i])) link_map[rb.sph_link[i]] = 1;
+  for (int pi = 0; pi < rb.n_pairs; ++pi) {
+    bool hit = false;
+    for (int sa : rb.link_sph[rb.pair_a[pi]])
+      for (int sb : rb.link_sph[rb.pair_b[pi]]) {
+        const double* a = &ck.wc[sa * 3];
+        const double* b = &ck.wc[sb * 3];
+        double ex = a[0] - b[0], ey = a[1] - b[1], ez = a[2] - b[2];
+        double r2 = rb.sph_r[sa] + rb.sph_r[sb];
+        if (ex * ex + ey * ey + ez * ez <= r2 * r2) hit = true;
+      }
+    pair_self[pi] = hit ? 1 : 0;
+  }
+}
+
 // Link world frames (n_links x 12: R row-major then p) and the chain end-effector z.
 void orc_fk(void* hp, const double* q, int n, double* frames, double* eez) {
   orc_handle* h = (orc_handle*)hp;

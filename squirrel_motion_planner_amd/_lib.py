@@ -111,6 +111,8 @@ EXPORTS = [
     ("smp_check_configs", _i, [_p, _pd, _i64, _i, _i, _p]),
     ("smp_is_config_valid", _i, [_p, _pd, _i, _i, ctypes.POINTER(_i)]),
     ("smp_check_sequence", _i, [_p, _pd, _i64, _i, _i, ctypes.POINTER(_i64)]),
+    ("smp_get_collisions", _i, [_p, _pd, ctypes.POINTER(ctypes.c_int32), _i, ctypes.POINTER(_i),
+                                ctypes.POINTER(ctypes.c_int32), _i, ctypes.POINTER(_i)]),
     ("smp_normalize_trajectory", _i, [_pd, _i64, _i, _pd, _pd, _i64, ctypes.POINTER(_i64)]),
     ("smp_ik_solve", _i, [_p, ctypes.POINTER(IkRequest), _i, ctypes.POINTER(IkResult)]),
     ("smp_find_goal_pose", _i, [_p, _pd, _pd, _d, _i, _i, _pd, ctypes.POINTER(_i), ctypes.POINTER(GoalSearch)]),

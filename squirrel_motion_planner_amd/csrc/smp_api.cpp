@@ -30,6 +30,8 @@ __global__ void helper_kernel(const RobotDev* rb, SceneDev sc, const MapCfg* mc,
 __global__ void path_kernel(QueryDev* qs, int* counts);
 size_t check_kernels_private_bytes();
 size_t ik_kernels_private_bytes();
+void launch_collisions(hipStream_t st, const RobotDev* rb, SceneDev sc, const MapCfg* mc, const double* q, int map,
+                       uint8_t* link_map, uint8_t* pair_self);
 void launch_ik(bool search, int n, hipStream_t st, const RobotDev* rb, const IkTaskDev* tasks, IkOutDev* out,
                SceneDev sc, const MapCfg* mc, int self, int map, int* best);
 __global__ void sincos_kernel(const double* x, int n, double* s, double* c);
@@ -467,6 +469,44 @@ int smp_check_configs(smp_planner* p, const double* q_soa, int64_t n, int check_
   float ms = 0;
   HIPCHK(hipEventElapsedTime(&ms, p->ev0, p->ev1));
   p->last_check_ms = ms;
+  return SMP_OK;
+}
+
+// getCollisions (birrt_star.cpp:6910-6914 -> collision_checker.hpp:123-132, 594-630): one configuration's
+// colliding self pairs (pair order, CC:378-388) and map-colliding links (std::map name order, CC:189, 615).
+int smp_get_collisions(smp_planner* p, const double q[8], int32_t* self_pairs, int max_self, int* n_self,
+                       int32_t* map_links, int max_map, int* n_map) {
+  if (!p || !q || !n_self || !n_map || max_self < 0 || max_map < 0 || (max_self > 0 && !self_pairs) ||
+      (max_map > 0 && !map_links))
+    return SMP_ERR_ARG;
+  const RobotDev& d = p->robot.dev;
+  HIPCHK(hipSetDevice(p->device));
+  HIPCHK(p->d_cq.reserve(NJ));
+  HIPCHK(p->d_valid.reserve(MAX_CLINK + MAX_PAIRS));
+  HIPCHK(hipMemcpyAsync(p->d_cq.p, q, NJ * sizeof(double), hipMemcpyHostToDevice, p->stream));
+  launch_collisions(p->stream, p->d_rb, p->sc, p->d_mc, p->d_cq.p, p->have_scene ? 1 : 0, p->d_valid.p,
+                    p->d_valid.p + MAX_CLINK);
+  HIPCHK(hipGetLastError());
+  uint8_t flags[MAX_CLINK + MAX_PAIRS];
+  HIPCHK(hipMemcpyAsync(flags, p->d_valid.p, sizeof(flags), hipMemcpyDeviceToHost, p->stream));
+  HIPCHK(hipStreamSynchronize(p->stream));
+  int ns = 0;
+  for (int k = 0; k < d.n_pairs; ++k) {
+    if (!flags[MAX_CLINK + k]) continue;
+    if (ns < max_self) {
+      self_pairs[2 * ns] = d.cl_link[d.pair_a[k]];
+      self_pairs[2 * ns + 1] = d.cl_link[d.pair_b[k]];
+    }
+    ++ns;
+  }
+  std::vector<int> links;
+  for (int c = 0; c < d.n_clink; ++c)
+    if (flags[c]) links.push_back(d.cl_link[c]);
+  const std::vector<std::string>& names = p->robot.link_names;
+  std::sort(links.begin(), links.end(), [&](int a, int b) { return names[a] < names[b]; });
+  for (int k = 0; k < (int)links.size() && k < max_map; ++k) map_links[k] = links[k];
+  *n_self = ns;
+  *n_map = (int)links.size();
   return SMP_OK;
 }
 

@@ -93,6 +93,74 @@ void launch_check(int ct, int grid, hipStream_t st, const RobotDev* rb, SceneDev
   }
 }
 
+// ============================================================================================ collision listing
+// getCollisions (birrt_star.cpp:6910-6914 -> collision_checker.hpp:123-132): for one configuration, which collision
+// links touch the map (getMapCollisions, CC:610-630: every link with geometry, the disabled ones included) and which
+// self pairs overlap (getSelfCollisions, CC:594-608: every pair, no early exit).  One wavefront; the map test of a
+// sphere is the planner's (box-gap prefilter, then the exact sweep), the self test the planner's sphere-pair test.
+__global__ void __launch_bounds__(64) collisions_kernel(const RobotDev* __restrict__ rb, SceneDev sc,
+                                                        const MapCfg* __restrict__ mc, const double* __restrict__ q,
+                                                        int map, uint8_t* __restrict__ link_map,
+                                                        uint8_t* __restrict__ pair_self) {
+  __shared__ Frame B[MAX_BODY];
+  __shared__ double wc[MAX_SPH][3];
+  __shared__ uint32_t cand[(MAX_SPH + 31) / 32];
+  __shared__ int lm[MAX_CLINK];
+  const int lane = threadIdx.x;
+  if (lane == 0) {
+    double qq[NJ];
+    for (int j = 0; j < NJ; ++j) qq[j] = q[j];
+    Frame F[MAX_BODY];
+    body_frames(rb, qq, F);
+    for (int b = 0; b < rb->n_body; ++b) B[b] = F[b];
+  }
+  if (lane < (MAX_SPH + 31) / 32) cand[lane] = 0u;
+  if (lane < MAX_CLINK) lm[lane] = 0;
+  __syncthreads();
+  const int nsph = rb->n_sph;
+  for (int s = lane; s < nsph; s += 64) {
+    double w[3];
+    xform(B[rb->sph_body[s]], &rb->sph_cb[s * 3], w);
+    wc[s][0] = w[0]; wc[s][1] = w[1]; wc[s][2] = w[2];
+    if (map) {
+      const long long cell = centre_cell(sc, w);
+      const uint32_t dv = cell < 0 ? 0xffffffffu : (sc.d2b ? (uint32_t)sc.d2b[cell] : (uint32_t)sc.d2[cell]);
+      if (dv <= mc->T[s]) atomicOr(&cand[s >> 5], 1u << (s & 31));
+    }
+  }
+  __syncthreads();
+  for (int wd = 0; wd < (nsph + 31) / 32; ++wd) {
+    uint32_t m = cand[wd];
+    while (m) {
+      const int s = wd * 32 + __builtin_ctz(m);
+      m &= m - 1;
+      const int c = rb->sph_clink[s];
+      if (lm[c]) continue;  // the link is listed already
+      const bool hit = wave_sphere_map(sc, wc[s], rb->sph_r[s], lane);
+      __syncthreads();
+      if (hit && lane == 0) lm[c] = 1;
+      __syncthreads();
+    }
+  }
+  for (int c = lane; c < rb->n_clink; c += 64) link_map[c] = (uint8_t)lm[c];
+  for (int p = lane; p < rb->n_pairs; p += 64) {
+    const int a = rb->pair_a[p], b = rb->pair_b[p];
+    bool hit = false;
+    for (int sa = rb->cl_sph0[a]; sa < rb->cl_sph0[a] + rb->cl_nsph[a] && !hit; ++sa)
+      for (int sb = rb->cl_sph0[b]; sb < rb->cl_sph0[b] + rb->cl_nsph[b]; ++sb) {
+        const double rs = rb->sph_r[sa] + rb->sph_r[sb];
+        const double ex = wc[sa][0] - wc[sb][0], ey = wc[sa][1] - wc[sb][1], ez = wc[sa][2] - wc[sb][2];
+        if (ex * ex + ey * ey + ez * ez <= rs * rs) { hit = true; break; }
+      }
+    pair_self[p] = hit ? 1 : 0;
+  }
+}
+
+void launch_collisions(hipStream_t st, const RobotDev* rb, SceneDev sc, const MapCfg* mc, const double* q, int map,
+                       uint8_t* link_map, uint8_t* pair_self) {
+  hipLaunchKernelGGL(collisions_kernel, dim3(1), dim3(64), 0, st, rb, sc, mc, q, map, link_map, pair_self);
+}
+
 // ============================================================================================ parity kernels
 __global__ void sincos_kernel(const double* x, int n, double* s, double* c) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;

@@ -182,6 +182,22 @@ class GpuPlanner:
                                        ctypes.byref(first)), "smp_check_sequence")
         return first.value
 
+    def get_collisions(self, q):
+        """getCollisions (birrt_star.cpp:6910-6914): (self pairs [(link a, link b)] in pair order, map-colliding links
+        in name order) of one configuration, as link names; disabled links are listed too, as in the reference."""
+        qa = np.ascontiguousarray(np.asarray(q, np.float64).reshape(8))
+        names = self.robot.link_names
+        cap_s, cap_m = 256, len(names)
+        sp = (ctypes.c_int32 * (2 * cap_s))()
+        ml = (ctypes.c_int32 * max(cap_m, 1))()
+        ns, nm = ctypes.c_int(), ctypes.c_int()
+        check(lib().smp_get_collisions(self.h, qa.ctypes.data_as(_pd), sp, cap_s, ctypes.byref(ns), ml, cap_m,
+                                       ctypes.byref(nm)), "smp_get_collisions")
+        if ns.value > cap_s or nm.value > cap_m:
+            raise L.SmpError(L.SMP_ERR_ARG, "smp_get_collisions: more results than capacity")
+        return ([(names[sp[2 * k]], names[sp[2 * k + 1]]) for k in range(ns.value)],
+                [names[ml[k]] for k in range(nm.value)])
+
     def ik_solve(self, ee_poses, q_inits, deviation=None, max_iter=1000):
         """getFullPoseFromEEPose's controller (run_VDLS_Control_Connector) for n (end-effector pose, start
         configuration) pairs, one wavefront each.  ee_poses: (n, 6) or one (6,) pose for every start; deviation: (6, 2)
@@ -369,6 +385,12 @@ class BiRRTstarPlanner:
 
     def isConfigValid(self, config, check_self_collision=True, check_map_collision=True):
         return bool(self._gpu.check_configs([config], check_self_collision, check_map_collision)[0])
+
+    def getCollisions(self, joint_positions, self_collisions, map_collisions):
+        """birrt_star.cpp:6910-6914: appends to the two lists, as the reference does."""
+        s, m = self._gpu.get_collisions(joint_positions)
+        self_collisions.extend(s)
+        map_collisions.extend(m)
 
     def init_planner(self, start_conf, goal_conf, search_space=1, check_self_collision=True, check_map_collision=True):
         if len(start_conf) != 8 or len(goal_conf) != 8 or search_space != 1:

@@ -76,5 +76,21 @@ int main(int argc, char** argv) {
   std::printf("ee_ik %d", ik ? 1 : 0);
   for (double v : sol) std::printf(" %.17g", v);
   std::printf("\n");
+  // the print-and-show-collisions service (SP:833-860): getCollisions of the start, of the start's arm at its
+  // joint limits and of the start's arm at the corner of the map
+  std::vector<std::vector<double> > probes(3, start);
+  const double hi[5] = {1.5, 2.6, 1.8, 2.4, 2.9};
+  for (int j = 0; j < 5; ++j) probes[1][3 + j] = hi[j];
+  probes[2][0] = ex[1];
+  probes[2][1] = ey[1];
+  for (const std::vector<double>& q : probes) {
+    std::vector<std::pair<std::string, std::string> > self;
+    std::vector<std::string> map;
+    planner.getCollisions(q, self, map);
+    std::printf("collisions %zu %zu", self.size(), map.size());
+    for (const auto& pr : self) std::printf(" %s %s", pr.first.c_str(), pr.second.c_str());
+    for (const auto& m : map) std::printf(" %s", m.c_str());
+    std::printf("\n");
+  }
   return 0;
 }

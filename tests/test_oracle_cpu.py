@@ -178,3 +178,27 @@ def test_oracle_tree_invariants(orobot):
     if r["status"] == 0:
         p = r["path"]
         assert np.array_equal(p[0], np.array(sc.start))
+
+
+def test_collision_listing_agrees_with_validity():
+    """orc_collisions (getCollisions, CC:123-132, 594-630) lists something exactly when isInCollision is true (no
+    disabled links), self pairs in model pair order, map links sorted by name."""
+    model = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "squirrel_motion_planner_amd",
+                         "data", "robotino_model.json")
+    sc = scenes.box_room()
+    orc = O.Oracle(O.OracleRobot(model), O.OracleScene(sc.keys, sc.res))
+    rng = np.random.default_rng(3)
+    n = 300
+    q = np.column_stack([rng.uniform(-5, 5, n), rng.uniform(-5, 5, n), rng.uniform(-math.pi, math.pi, n)] +
+                        [rng.uniform(lo, hi, n) for lo, hi in zip([-1.2, -1.7, -1.8, -2.4, -2.9], [1.5, 2.6, 1.8, 2.4, 2.9])])
+    valid = orc.check_configs(q)
+    pair_order = {(a, b): k for k, (a, b) in enumerate(
+        (orc.robot.model["links"][a]["name"], orc.robot.model["links"][b]["name"])
+        for a, b in zip(orc.robot.pair_a, orc.robot.pair_b))}
+    listed = 0
+    for qi, v in zip(q, valid):
+        s, m = orc.collisions(qi)
+        assert (not s and not m) == bool(v)
+        assert m == sorted(m) and [pair_order[p] for p in s] == sorted(pair_order[p] for p in s)
+        listed += bool(s) + bool(m)
+    assert listed > 50

@@ -80,6 +80,18 @@ def test_shim_node_sequence_matches_oracle(tmp_path):
     assert ik[0] == "ee_ik" and int(ik[1]) == oi["reached"][0]
     if oi["reached"][0]:
         assert np.array_equal(np.array([float(v) for v in ik[2:]]), oi["q"][0])
+    # getCollisions (SP:839) of three probes: the start, its arm at the upper joint limits, the map's corner
+    probes = [list(sc.start) for _ in range(3)]
+    probes[1][3:8] = [1.5, 2.6, 1.8, 2.4, 2.9]
+    probes[2][0], probes[2][1] = sc.env_x[1], sc.env_y[1]
+    for k, q in enumerate(probes):
+        f = lines[6 + n + k].split()
+        assert f[0] == "collisions"
+        ns, nm = int(f[1]), int(f[2])
+        got_self = [(f[3 + 2 * i], f[4 + 2 * i]) for i in range(ns)]
+        got_map = f[3 + 2 * ns:3 + 2 * ns + nm]
+        want_self, want_map = orc.collisions(q)
+        assert got_self == want_self and got_map == want_map, (k, got_self, got_map, want_self, want_map)
     o = orc.plan(sc.start, sc.goal, env_x=sc.env_x, env_y=sc.env_y, max_iter=iters, seed=seed)
     assert lines[0] == "status %d" % o["status"]
     assert checked == o["checked"]
