@@ -170,6 +170,32 @@ __device__ __forceinline__ void chain_local(const RobotDev* __restrict__ rb, int
 
 __device__ __forceinline__ uint32_t shfl_u32(uint32_t v, int src) { return (uint32_t)__shfl((int)v, src); }
 
+// The scene's scalars in scalar registers.  A caller's SceneDev may live in private (scratch) memory -- the planner
+// keeps its context there -- and every use of a field would then be a scratch load, several of them dependent per
+// sphere centre (centre_cell) and per exact sweep (sphere_reach); read once here, they are wave-uniform SGPRs.
+__device__ __forceinline__ double rfl_f64(double v) {
+  const long long b = __double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)b);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(b >> 32));
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+template <class T>
+__device__ __forceinline__ T* rfl_ptr(T* p) {
+  const unsigned long long b = (unsigned long long)(uintptr_t)p;
+  const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)b);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(b >> 32));
+  return (T*)(uintptr_t)(((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ SceneDev uniform_scene(const SceneDev& s) {
+  SceneDev o;
+  o.nx = __builtin_amdgcn_readfirstlane(s.nx); o.ny = __builtin_amdgcn_readfirstlane(s.ny);
+  o.nz = __builtin_amdgcn_readfirstlane(s.nz); o.bnx = __builtin_amdgcn_readfirstlane(s.bnx);
+  o.bny = __builtin_amdgcn_readfirstlane(s.bny);
+  o.ox = rfl_f64(s.ox); o.oy = rfl_f64(s.oy); o.oz = rfl_f64(s.oz); o.res = rfl_f64(s.res); o.inv_res = rfl_f64(s.inv_res);
+  o.bricks = rfl_ptr(s.bricks); o.d2 = rfl_ptr(s.d2); o.d2b = rfl_ptr(s.d2b);
+  return o;
+}
+
 // Value of lane I of this lane's quad (DPP quad_perm broadcast, both 32-bit halves).  The whole quad must be active.
 template <int I>
 __device__ __forceinline__ double quad_bcast(double v) {
@@ -288,11 +314,12 @@ struct TileOrder {
 // gfx950 fp64 has ~40 cycles of dependent latency (tools/micro/fp64_latency.hip), so every stage is laid
 // out as many short independent chains per lane rather than one long chain.
 template <int CT>
-__device__ __forceinline__ void collide_tile(const RobotDev* __restrict__ rb, const SceneDev& sc,
+__device__ __forceinline__ void collide_tile(const RobotDev* __restrict__ rb, const SceneDev& sc_in,
                                              const MapCfg* __restrict__ mc, int nc, const double (*q_lds)[NJ],
                                              int self, int map, TileLds<CT>& L, const TileOrder* ord = nullptr,
                                              unsigned long long* prof = nullptr, unsigned long long* prof2 = nullptr) {
   static_assert(CT % NWAVE == 0, "tile size");
+  const SceneDev sc = uniform_scene(sc_in);
   constexpr int CPW = TileLds<CT>::CPW, SW = TileLds<CT>::SW;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   unsigned long long t0 = (prof && tid == 0) ? wall_clock64() : 0;

@@ -3672,11 +3672,22 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
 
 // Scout workgroup `which` of a query (plan_kernel): takes the leader's newest request, runs scout_iteration on it,
 // repeats; leaves on the stop flag (then stops its helpers) or after two idle seconds.
-__device__ __forceinline__ void scout_main(Ctx& C, int which) {
-  C.Q.scb = C.Q.scbs[which];  // its own record board, job board, helpers and via scratch
+// A scout's context: its own record board, job board, helpers and via scratch; collision jobs go to its own board and
+// helpers, the run-ahead sampler's ring stays the leader's.
+__device__ __forceinline__ void scout_ctx(Ctx& C, int which) {
+  C.Q.scb = C.Q.scbs[which];
   C.Q.sjb = C.Q.sjbs[which];
   C.Q.svia = C.Q.svias[which];
   C.Q.sworkers = C.Q.sworkers_s[which];
+  C.Q.sampler_jb = C.Q.jb;
+  C.Q.jb = C.Q.sjb;
+  C.Q.nworkers = C.Q.sworkers;
+  C.Q.via = C.Q.svia;
+  C.Q.rows = nullptr;
+  C.Q.trace = nullptr;
+}
+
+__device__ __forceinline__ void scout_main(Ctx& C, int which) {
   {
     const int* src = reinterpret_cast<const int*>(C.Q.st);
     int* dst = reinterpret_cast<int*>(&g_L.S);
@@ -3684,12 +3695,6 @@ __device__ __forceinline__ void scout_main(Ctx& C, int which) {
   }
   __syncthreads();
   if (threadIdx.x < 32) g_L.S.prof[threadIdx.x] = 0;
-  C.Q.sampler_jb = C.Q.jb;  // the run-ahead sampler's ring
-  C.Q.jb = C.Q.sjb;         // collision jobs go to the scout's own board and helpers
-  C.Q.nworkers = C.Q.sworkers;
-  C.Q.via = C.Q.svia;
-  C.Q.rows = nullptr;
-  C.Q.trace = nullptr;
   if (threadIdx.x == 0) {
     g_L.count_slot = 0;
     g_L.job_seq = 0;
@@ -3807,10 +3812,18 @@ __global__ void __launch_bounds__(BLOCK) plan_kernel(const RobotDev* __restrict_
   const int so = b - scout_base, srole = scout_base > 0 && b >= scout_base ? so / r8 : -1;
   const int sq = srole >= 0 ? so - srole * r8 : b;
   if (b >= nq && (srole < 0 || sq >= nq)) return;
-  stage_model(rb, mc, &g_rb, &g_mc);
-  Ctx C;
-  C.sc = sc;
-  C.Q = qs[sq];
+  // the block's context in LDS: every function takes it by reference, and a private copy would live in scratch (each
+  // field read a scratch load, invalidated with the L1 by every acquire)
+  __shared__ Ctx g_ctx;
+  if (threadIdx.x == 0) {
+    Ctx c;
+    c.sc = sc;
+    c.Q = qs[sq];
+    if (srole >= 0 && srole < c.Q.nscouts) scout_ctx(c, srole);
+    g_ctx = c;
+  }
+  stage_model(rb, mc, &g_rb, &g_mc);  // (ends with a barrier)
+  Ctx& C = g_ctx;
   if (srole >= 0) {
     if (srole < C.Q.nscouts) scout_main(C, srole);  // one call site: inlined
     return;
@@ -3952,27 +3965,41 @@ __global__ void __launch_bounds__(BLOCK) helper_kernel(const RobotDev* __restric
                                                        const MapCfg* __restrict__ mc, QueryDev* qs, int nq) {
   __shared__ JobLds J;
   __shared__ SamplerLds SL;
-  stage_model(rb, mc, &g_rb, &g_mc);
-  Ctx C;
-  C.sc = sc;
-  C.Q = qs[blockIdx.x % nq];
-  const int hidx = (int)blockIdx.x / nq, nh = (int)gridDim.x / nq;
-  if (!C.Q.jb) return;
-  if (C.Q.sampler && hidx == nh - 1) {
-    sampler_main(C, SL);
+  // the block's context and role in LDS (see plan_kernel): -1 nothing to do, -2 run-ahead sampler, else tile helper h
+  __shared__ Ctx g_ctx;
+  __shared__ int g_role;
+  if (threadIdx.x == 0) {
+    Ctx c;
+    c.sc = sc;
+    c.Q = qs[blockIdx.x % nq];
+    const int hidx = (int)blockIdx.x / nq, nh = (int)gridDim.x / nq;
+    int role = hidx;
+    if (!c.Q.jb) {
+      role = -1;
+    } else if (c.Q.sampler && hidx == nh - 1) {
+      role = -2;
+    } else if (role >= c.Q.nworkers - 1) {  // the leader's tile helpers first, then each scout's
+      role -= c.Q.nworkers - 1;
+      int s = 0;
+      for (; s < c.Q.nscouts && role >= c.Q.sworkers_s[s] - 1; ++s) role -= c.Q.sworkers_s[s] - 1;
+      if (s >= c.Q.nscouts) {
+        role = -1;
+      } else {
+        c.Q.jb = c.Q.sjbs[s];
+        c.Q.nworkers = c.Q.sworkers_s[s];
+      }
+    }
+    g_ctx = c;
+    g_role = role;
+  }
+  stage_model(rb, mc, &g_rb, &g_mc);  // (ends with a barrier)
+  const int role = uni(g_role);
+  if (role == -1) return;
+  if (role == -2) {
+    sampler_main(g_ctx, SL);
     return;
   }
-  // the leader's tile helpers first, then each scout's
-  int h = hidx;
-  if (h >= C.Q.nworkers - 1) {
-    h -= C.Q.nworkers - 1;
-    int s = 0;
-    for (; s < C.Q.nscouts && h >= C.Q.sworkers_s[s] - 1; ++s) h -= C.Q.sworkers_s[s] - 1;
-    if (s >= C.Q.nscouts) return;
-    C.Q.jb = C.Q.sjbs[s];
-    C.Q.nworkers = C.Q.sworkers_s[s];
-  }
-  helper_main(C, h, J);
+  helper_main(g_ctx, role, J);
 }
 
 __global__ void path_kernel(QueryDev* qs, int* counts) {
