@@ -63,17 +63,9 @@ def workload_name(a, sc):
             "queries per GPU, path_optimality_threshold=-inf" % a.queries_per_gpu)
 
 
-def cpu_baseline(sc, pair, a, step0_seed, step_seeds=()):
-    """The oracle (sequential C++ restatement of the reference loop, 1 thread) on query 0 of GPU step 0.
-
-    Same scene, (start, goal), seed, query id and budget, so the CPU run plans the identical trees; the bench
-    records whether its counters match the GPU's (a parity check of the measured run itself)."""
-    from oracle import oracle as O
-    rob = O.OracleRobot(os.path.join(ROOT, "squirrel_motion_planner_amd", "data", "robotino_model.json"))
-    orc = O.Oracle(rob, O.OracleScene(sc.keys, sc.res))
-    budget = dict(max_iter=a.iterations) if a.iterations else dict(max_checked=a.samples, max_iter=0)
-    r = orc.plan(pair[0], pair[1], env_x=sc.env_x, env_y=sc.env_y, seed=step0_seed, query=0,
-                 opt_thresh=-math.inf, **budget)
+def host_cpu():
+    """CPU model and the core count this process may use (the GPU box gives each GPU a share of its cores:
+    OMP_NUM_THREADS; nproc / os.cpu_count() report the whole machine there)."""
     cpu = "unknown"
     try:
         for line in open("/proc/cpuinfo"):
@@ -82,16 +74,53 @@ def cpu_baseline(sc, pair, a, step0_seed, step_seeds=()):
                 break
     except OSError:
         pass
+    share = int(os.environ.get("OMP_NUM_THREADS") or 0) or len(os.sched_getaffinity(0))
+    return cpu, max(1, min(share, len(os.sched_getaffinity(0))))
+
+
+def cpu_baseline(sc, pair, a, step0_seed, step_seeds=()):
+    """The oracle (C++ restatement of the reference loop) on query 0 of GPU step 0: one thread (the north_star's
+    single-thread reference) and all of this process's cores (OpenMP on the two scans, as the reference's
+    BS:4092 / BS:4283).
+
+    Same scene, (start, goal), seed, query id and budget, so the CPU runs plan the identical trees; the bench
+    records whether the counters match the GPU's (a parity check of the measured run itself)."""
+    from oracle import oracle as O
+    rob = O.OracleRobot(os.path.join(ROOT, "squirrel_motion_planner_amd", "data", "robotino_model.json"))
+    orc = O.Oracle(rob, O.OracleScene(sc.keys, sc.res))
+    budget = dict(max_iter=a.iterations) if a.iterations else dict(max_checked=a.samples, max_iter=0)
+    cpu, cores = host_cpu()
+    r = orc.plan(pair[0], pair[1], env_x=sc.env_x, env_y=sc.env_y, seed=step0_seed, query=0,
+                 opt_thresh=-math.inf, threads=1, **budget)
+    rm = orc.plan(pair[0], pair[1], env_x=sc.env_x, env_y=sc.env_y, seed=step0_seed, query=0,
+                  opt_thresh=-math.inf, threads=cores, **budget) if cores > 1 else r
+    ttff = [first_solution(orc, sc, pair, sd) for sd in step_seeds]
     return {"value": r["checked"] / r["t_total"], "unit": "configs/s", "cores": 1, "kind": "port",
             "sample": "%s query 0 (seed %d), oracle/smp_oracle.cpp single thread, same budget: %d iterations, "
                       "%d configs checked in %.2f s on %s" % (a.workload.upper(), step0_seed, r["iterations"],
                                                            r["checked"], r["t_total"], cpu),
+            "cpu_model": cpu,
             "valid_configs_per_s": r["valid"] / r["t_total"],
             "iterations": r["iterations"], "checked": r["checked"], "time_first_solution_s": r["t_first"],
             "iters_per_s": r["iterations"] / r["t_total"], "cost_best": r["cost"][0],
-            # the oracle's time to the first feasible path for every timed step's seed (short runs, same query),
-            # beside the GPU's per-step list: the first-solution iteration differs from seed to seed
-            "time_first_solution_steps_s": [first_solution(orc, sc, pair, sd) for sd in step_seeds] or None}
+            "all_cores": {"value": rm["checked"] / rm["t_total"], "unit": "configs/s", "cores": cores,
+                          "valid_configs_per_s": rm["valid"] / rm["t_total"], "t_total_s": rm["t_total"],
+                          "same_trees_as_1_thread": bool(rm["checked"] == r["checked"] and
+                                                         rm["iterations"] == r["iterations"]),
+                          "how": "oracle with the nearest / near scans as OpenMP loops on %d threads "
+                                 "(BS:4092, BS:4283)" % cores},
+            # the oracle's time to the first feasible path for every timed step's seed (short runs, same query,
+            # timed from run() entry), beside the GPU's per-step lists
+            "time_first_solution_steps_s": ttff or None,
+            "time_first_solution_stats_s": stats3(ttff)}
+
+
+def stats3(v):
+    v = sorted(x for x in v if x is not None)
+    if not v:
+        return None
+    return {"min": v[0], "median": v[len(v) // 2] if len(v) % 2 else 0.5 * (v[len(v) // 2 - 1] + v[len(v) // 2]),
+            "max": v[-1], "n": len(v)}
 
 
 def first_solution(orc, sc, pair, seed, max_iter=600):
@@ -151,7 +180,7 @@ def main():
         gp.plan_batch(queries(-1 - w, a.warmup_samples or a.samples))
 
     totals = dict(checked=0, valid=0, iters=0, nn=0, near=0, plan_ms=0.0, launches=0)
-    first_t = []
+    first_t, first_host = [], []
     step0 = None
     if world > 1:
         dist.barrier()
@@ -171,6 +200,7 @@ def main():
             totals["near"] += r["near_nodes_scanned"]
             if r["time_first_solution"] >= 0:
                 first_t.append(r["time_first_solution"])
+                first_host.append(r["time_first_solution_host"])
         _, pms, nl = gp.last_kernel_ms()
         totals["plan_ms"] += pms
         totals["launches"] += nl
@@ -230,8 +260,14 @@ def main():
                        "tiles; queries sharded over ranks, scene broadcast once"},
             "valid_configs_per_s": valid / elapsed,
             "iterations_per_s": iters / elapsed,
-            "time_to_first_feasible_path_s": (sum(first_t) / len(first_t)) if first_t else None,
-            "time_to_first_feasible_path_steps_s": first_t if a.queries_per_gpu == 1 else None,
+            # time to the first feasible path on the host's clock from smp_plan entry (start / goal checks, uploads,
+            # launch and the kernel's iterations; SURVEY 8d counts from run_planner entry) and, beside it, the
+            # kernel's own device-clock value (from its planning start)
+            "time_to_first_feasible_path_s": (sum(first_host) / len(first_host)) if first_host else None,
+            "time_to_first_feasible_path_host_steps_s": first_host if a.queries_per_gpu == 1 else None,
+            "time_to_first_feasible_path_host_stats_s": stats3(first_host),
+            "time_to_first_feasible_path_device_steps_s": first_t if a.queries_per_gpu == 1 else None,
+            "time_to_first_feasible_path_device_stats_s": stats3(first_t),
             # priced against HBM (no dense contraction); the measured limiter is the dependent latency of
             # one query's iteration chain, not bandwidth: trees and grid stay in L2 / Infinity Cache
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

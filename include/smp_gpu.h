@@ -118,7 +118,8 @@ typedef struct smp_stats {
   int64_t last_solution_iter;
   int64_t configs_checked;       /* isInCollision calls of the reference semantics */
   int64_t configs_valid;         /* ... of which collision free */
-  double time_first_solution;    /* seconds from planning start (device clock) */
+  double time_first_solution;    /* seconds from the kernel's planning start (device clock; see also
+                                    time_first_solution_host) */
   double time_total;             /* seconds of the planning loop (device clock) */
   double cost_best[3];           /* total, revolute, prismatic */
   double cost_theoretical[3];
@@ -141,6 +142,9 @@ typedef struct smp_stats {
                                     5 via chain, 6 rewire, 28 idle, 29 publishing, 31 busy; 30 = iterations) */
   int32_t helpers;               /* helper workgroups per query used */
   int32_t scout;                 /* scout workgroups per query used (0: none) */
+  double time_first_solution_host; /* seconds from smp_plan entry until the host saw the first feasible path (host
+                                    clock: start / goal checks, allocation, uploads and launch included; SURVEY 8d
+                                    counts from run_planner entry, birrt_star.cpp:1075-1081); -1 if none */
 } smp_stats;
 
 typedef struct smp_result {

@@ -34,19 +34,22 @@ class RobotDesc(ctypes.Structure):
                 ("q_min", _pd), ("q_max", _pd), ("rev", _pi), ("root_z", _d),
                 ("n_chain", _i), ("ch_type", _pi), ("ch_joint", _pi), ("ch_body", _pi),
                 ("ch_axis", _pd), ("ch_origin", _pd), ("ch_R", _pd), ("ch_p", _pd),
-                ("n_body", _i), ("sph_body", _pi), ("lb_body", _pi), ("sph_cb", _pd), ("lb_cb", _pd)]
+                ("n_body", _i), ("sph_body", _pi), ("lb_body", _pi), ("sph_cb", _pd), ("lb_cb", _pd),
+                ("n_prim", _i), ("prim_type", _pi), ("prim_body", _pi), ("prim_link", _pi),
+                ("prim_cb", _pd), ("prim_ab", _pd), ("prim_h", _pd), ("prim_rxy", _pd)]
 
 
 class SceneDesc(ctypes.Structure):
     _fields_ = [("nx", _i), ("ny", _i), ("nz", _i), ("ox", _d), ("oy", _d), ("oz", _d), ("res", _d),
-                ("bits", ctypes.POINTER(ctypes.c_uint64)), ("d2", ctypes.POINTER(ctypes.c_uint16))]
+                ("bits", ctypes.POINTER(ctypes.c_uint64)), ("d2", ctypes.POINTER(ctypes.c_uint16)),
+                ("n_slab", _i), ("slab", ctypes.POINTER(ctypes.c_uint16))]
 
 
 class Params(ctypes.Structure):
     _fields_ = [("near_r", _d), ("step", _d), ("n_pts", _i), ("max_near", _i), ("opt_thresh", _d),
                 ("tree_opt", _i), ("informed", _i), ("env_x", _d * 2), ("env_y", _d * 2),
                 ("self_", _i), ("map", _i), ("seed", ctypes.c_uint64), ("query", ctypes.c_uint32),
-                ("max_iter", _i), ("max_time", _d), ("max_checked", ctypes.c_longlong)]
+                ("max_iter", _i), ("max_time", _d), ("max_checked", ctypes.c_longlong), ("threads", _i)]
 
 
 class Result(ctypes.Structure):
@@ -170,6 +173,15 @@ class OracleRobot:
         for b in model["link_bounds"]:
             self.lb_body[b["link"]] = b["body"]
             self.lb_cb[3 * b["link"]:3 * b["link"] + 3] = b["cb"]
+        PR = model.get("prims", [])
+        self.n_prim = len(PR)
+        self.prim_type = np.array([1 if p["type"] == "box" else 2 for p in PR] or [0], np.int32)
+        self.prim_body = np.array([p["body"] for p in PR] or [0], np.int32)
+        self.prim_link = np.array([p["link"] for p in PR] or [0], np.int32)
+        self.prim_cb = np.array([p["cb"] for p in PR] or [[0.0] * 3], np.float64).ravel()
+        self.prim_ab = np.array([p["ab"] for p in PR] or [[0.0] * 3], np.float64).ravel()
+        self.prim_h = np.array([p["half"] for p in PR] or [[0.0] * 3], np.float64).ravel()
+        self.prim_rxy = np.array([p["rxy"] for p in PR] or [0.0], np.float64)
 
     def desc(self):
         d = RobotDesc()
@@ -194,6 +206,10 @@ class OracleRobot:
         d.n_body = self.n_body
         d.sph_body, d.lb_body = _p(self.sph_body, _i), _p(self.lb_body, _i)
         d.sph_cb, d.lb_cb = _p(self.sph_cb, _d), _p(self.lb_cb, _d)
+        d.n_prim = self.n_prim
+        d.prim_type, d.prim_body, d.prim_link = _p(self.prim_type, _i), _p(self.prim_body, _i), _p(self.prim_link, _i)
+        d.prim_cb, d.prim_ab = _p(self.prim_cb, _d), _p(self.prim_ab, _d)
+        d.prim_h, d.prim_rxy = _p(self.prim_h, _d), _p(self.prim_rxy, _d)
         return d
 
 
@@ -202,8 +218,8 @@ KEY_OFFSET = 32768  # octomap tree_max_val
 
 
 def grid_pad_cells(res):
-    """Padding around the occupied key bbox: robot spheres are <= 0.30 m."""
-    return int(math.ceil(0.30 / res)) + 2
+    """Padding around the occupied key bbox: sphere / primitive reaches are <= 0.45 m."""
+    return int(math.ceil(0.45 / res)) + 2
 
 
 class OracleScene:
@@ -242,19 +258,43 @@ class OracleScene:
         else:
             self.d2 = np.full(self.nx * self.ny * self.nz, 65535, np.uint16)
 
-    def desc(self):
+    def slabs(self, zranges):
+        """Per primitive, the 2-D box-gap field of the occupancy projected over the layers whose cells meet its z range
+        (zlo, zhi): squared EDT (cells) of the 3x3-dilated projection, clamped to 65535 (scipy, independent of the
+        product's C++ builder)."""
+        from scipy.ndimage import binary_dilation, distance_transform_edt
+        out = []
+        for zlo, zhi in zranges:
+            k0 = max(0, int(math.floor((zlo - self.oz) / self.res)) - 1)
+            k1 = min(self.nz - 1, int(math.floor((zhi - self.oz) / self.res)) + 1)
+            while k0 <= k1 and self.oz + (k0 + 1) * self.res < zlo:
+                k0 += 1
+            while k1 >= k0 and self.oz + k1 * self.res > zhi:
+                k1 -= 1
+            proj = self.occ[k0:k1 + 1].any(0) if k0 <= k1 else np.zeros((self.ny, self.nx), bool)
+            if proj.any():
+                d = distance_transform_edt(~binary_dilation(proj, structure=np.ones((3, 3), bool)))
+                out.append(np.minimum(np.rint(d * d), 65535).astype(np.uint16).ravel())
+            else:
+                out.append(np.full(self.nx * self.ny, 65535, np.uint16))
+        return out
+
+    def desc(self, slabs=()):
         d = SceneDesc()
         d.nx, d.ny, d.nz = self.nx, self.ny, self.nz
         d.ox, d.oy, d.oz, d.res = self.ox, self.oy, self.oz, self.res
         d.bits = _p(self.bits, ctypes.c_uint64)
         d.d2 = _p(self.d2, ctypes.c_uint16)
+        self._slab = np.ascontiguousarray(np.concatenate(slabs) if len(slabs) else np.zeros(1, np.uint16))
+        d.n_slab = len(slabs)
+        d.slab = _p(self._slab, ctypes.c_uint16)
         return d
 
 
 # ------------------------------------------------------------------------------------------ planner
 DEFAULT_PARAMS = dict(near_r=4.0, step=0.5, n_pts=20, max_near=20, opt_thresh=1.0, tree_opt=1, informed=1,
                       env_x=(0.0, 0.0), env_y=(0.0, 0.0), self_=1, map=1, seed=1, query=0, max_iter=1000,
-                      max_time=0.0, max_checked=0)
+                      max_time=0.0, max_checked=0, threads=1)
 
 
 class Oracle:
@@ -262,7 +302,25 @@ class Oracle:
         self.robot = robot if isinstance(robot, OracleRobot) else OracleRobot(robot)
         self.scene = scene
         self._rd = self.robot.desc()
-        self._sd = scene.desc() if scene is not None else None
+        self._sd = None
+        if scene is not None:
+            rb = self.robot
+            slabs = []
+            if rb.n_prim:
+                # the primitives' bodies are planar: their centre z is the one of q = 0 (margin 1e-6 m)
+                h0 = lib().orc_create(ctypes.byref(self._rd), None, None)
+                fr = np.zeros((1, rb.n_body, 12))
+                lib().orc_body_fk(h0, _p(np.zeros(8), _d), 1, _p(fr, _d))
+                lib().orc_destroy(h0)
+                zr = []
+                for k in range(rb.n_prim):
+                    B = fr[0, rb.prim_body[k]]
+                    cb = rb.prim_cb[3 * k:3 * k + 3]
+                    zc = (B[6] * cb[0] + B[7] * cb[1] + B[8] * cb[2]) + B[11]
+                    hz = rb.prim_h[3 * k + 2] if rb.prim_type[k] == 1 else rb.prim_h[3 * k + 1]
+                    zr.append((zc - hz - 1e-6, zc + hz + 1e-6))
+                slabs = scene.slabs(zr)
+            self._sd = scene.desc(slabs)
         me = None
         if map_enabled is not None:
             self._me = np.ascontiguousarray(map_enabled, np.uint8)

@@ -23,8 +23,13 @@
 #include <chrono>
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 namespace orc {
 
@@ -131,6 +136,11 @@ struct Robot {
   int n_body;
   std::vector<int> sph_body, lb_body;
   std::vector<double> sph_cb, lb_cb;
+  // exact upright primitives (URDF box / cylinder links on the planar base): type 1 box (half extents), 2 cylinder
+  // (radius, half length); centre and x axis in the body frame
+  struct Prim { int type, body, link; double cb[3], ab[3], h[3], rxy; };
+  std::vector<Prim> prims;
+  std::vector<int> link_prim;  // per link: its primitive, -1 for sphere links
 };
 
 struct Scene {
@@ -138,6 +148,7 @@ struct Scene {
   double ox, oy, oz, res;
   std::vector<uint64_t> bits;
   std::vector<uint16_t> d2;
+  std::vector<std::vector<uint16_t>> slab;  // per primitive: 2-D box-gap field of its z slab (oracle.py Oracle)
 };
 
 static inline bool occ(const Scene& s, int i, int j, int k) {
@@ -174,6 +185,67 @@ static inline bool sphere_hits_map(const Scene& s, const double* c, double r, ui
     }
   }
   return false;
+}
+
+// ---- exact primitives (DESIGN.md "Collision model"): restated term by term from the product's spec (the same
+// expressions, so both decide every case alike); the reference collides fcl::Box / fcl::Cylinder (CC:282-288).
+// prim: centre pw[0..2], horizontal x axis (pw[3], pw[4]).
+static inline bool prim_cell(int ty, const double* h, const double* pw, const Scene& s, int i, int j, int k) {
+  const double zlo = s.oz + (double)k * s.res, zhi = s.oz + (double)(k + 1) * s.res;
+  const double hz = ty == 1 ? h[2] : h[1];
+  if (zhi < pw[2] - hz || zlo > pw[2] + hz) return false;
+  const double xlo = s.ox + (double)i * s.res, xhi = s.ox + (double)(i + 1) * s.res;
+  const double ylo = s.oy + (double)j * s.res, yhi = s.oy + (double)(j + 1) * s.res;
+  if (ty == 2) {
+    const double qx = pw[0] < xlo ? xlo - pw[0] : (pw[0] > xhi ? pw[0] - xhi : 0.0);
+    const double qy = pw[1] < ylo ? ylo - pw[1] : (pw[1] > yhi ? pw[1] - yhi : 0.0);
+    return qx * qx + qy * qy <= h[0] * h[0];
+  }
+  const double c = pw[3], sn = pw[4], ac = std::fabs(c), as = std::fabs(sn), hw = 0.5 * s.res;
+  const double dx = 0.5 * (xlo + xhi) - pw[0], dy = 0.5 * (ylo + yhi) - pw[1];
+  if (std::fabs(dx) > hw + (ac * h[0] + as * h[1])) return false;
+  if (std::fabs(dy) > hw + (as * h[0] + ac * h[1])) return false;
+  if (std::fabs(c * dx + sn * dy) > h[0] + hw * (ac + as)) return false;
+  if (std::fabs(c * dy - sn * dx) > h[1] + hw * (ac + as)) return false;
+  return true;
+}
+
+// Slab prefilter, then every occupied cell of the primitive's axis-aligned reach.
+static inline bool prim_hits_map(const Scene& s, int p, int ty, const double* h, double rxy_T, const double* pw) {
+  const double fx = std::floor((pw[0] - s.ox) / s.res), fy = std::floor((pw[1] - s.oy) / s.res);
+  if (!(fx >= 0 && fx < s.nx && fy >= 0 && fy < s.ny)) return false;
+  if ((uint32_t)s.slab[p][(size_t)(int)fy * s.nx + (int)fx] > (uint32_t)rxy_T) return false;
+  const double ac = std::fabs(pw[3]), as = std::fabs(pw[4]);
+  const double ex = ty == 1 ? ac * h[0] + as * h[1] : h[0];
+  const double ey = ty == 1 ? as * h[0] + ac * h[1] : h[0];
+  const double ez = ty == 1 ? h[2] : h[1];
+  const double lo[3] = {pw[0] - ex, pw[1] - ey, pw[2] - ez}, hi[3] = {pw[0] + ex, pw[1] + ey, pw[2] + ez};
+  const double o[3] = {s.ox, s.oy, s.oz};
+  const int n[3] = {s.nx, s.ny, s.nz};
+  int a[3], b[3];
+  for (int d = 0; d < 3; ++d) {
+    a[d] = std::max((int)std::floor((lo[d] - o[d]) / s.res) - 2, 0);
+    b[d] = std::min((int)std::floor((hi[d] - o[d]) / s.res) + 2, n[d] - 1);
+  }
+  for (int k = a[2]; k <= b[2]; ++k)
+    for (int j = a[1]; j <= b[1]; ++j)
+      for (int i = a[0]; i <= b[0]; ++i)
+        if (occ(s, i, j, k) && prim_cell(ty, h, pw, s, i, j, k)) return true;
+  return false;
+}
+
+// Sphere (centre w, radius rs) vs primitive: squared distance to the solid box / cylinder against rs^2.
+static inline bool sphere_prim(int ty, const double* h, const double* pw, const double* w, double rs) {
+  const double dx = w[0] - pw[0], dy = w[1] - pw[1], dz = w[2] - pw[2];
+  const double az = std::fabs(dz);
+  if (ty == 1) {
+    const double lx = std::fabs(pw[3] * dx + pw[4] * dy), ly = std::fabs(pw[3] * dy - pw[4] * dx);
+    const double qx = lx > h[0] ? lx - h[0] : 0.0, qy = ly > h[1] ? ly - h[1] : 0.0, qz = az > h[2] ? az - h[2] : 0.0;
+    return qx * qx + qy * qy + qz * qz <= rs * rs;
+  }
+  const double rho = std::sqrt(dx * dx + dy * dy);
+  const double qr = rho > h[0] ? rho - h[0] : 0.0, qz = az > h[1] ? az - h[1] : 0.0;
+  return qr * qr + qz * qz <= rs * rs;
 }
 
 static inline uint32_t sphere_threshold(double r, double res) {
@@ -273,12 +345,17 @@ struct Checker {
   std::vector<uint8_t> map_enabled; // per link (setDisabledLinkMapCollisions, CC:90-102)
   std::vector<Frame> frames;
   std::vector<double> wc;           // world sphere centres
+  std::vector<uint32_t> pT;         // per-primitive slab threshold
+  std::vector<double> pw;           // world primitive centres + x axes (5 per primitive)
   long long calls = 0;
 
   void init(const Robot* r, const Scene* s) {
     rb = r; sc = s;
     T.resize(r->n_sph);
     for (int i = 0; i < r->n_sph; ++i) T[i] = s ? sphere_threshold(r->sph_r[i], s->res) : 0;
+    pT.resize(r->prims.size());
+    for (size_t i = 0; i < r->prims.size(); ++i) pT[i] = s ? sphere_threshold(r->prims[i].rxy, s->res) : 0;
+    pw.resize(5 * r->prims.size());
     map_enabled.assign(r->n_links, 1);
     frames.resize(r->n_body > r->n_links ? r->n_body : r->n_links);
     wc.resize(r->n_sph * 3);
@@ -290,13 +367,20 @@ struct Checker {
     if (!self && !map) return false;
     body_frames(*rb, q, frames.data());
     for (int i = 0; i < rb->n_sph; ++i) xform(frames[rb->sph_body[i]], &rb->sph_cb[i * 3], &wc[i * 3]);
+    prim_frames();
     if (map && sc) {
       for (int i = 0; i < rb->n_sph; ++i)
         if (map_enabled[rb->sph_link[i]] && sphere_hits_map(*sc, &wc[i * 3], rb->sph_r[i], T[i])) return true;
+      for (size_t p = 0; p < rb->prims.size(); ++p)
+        if (map_enabled[rb->prims[p].link] && prim_map(p)) return true;
     }
     if (self) {
       for (int pi = 0; pi < rb->n_pairs; ++pi) {
         int a = rb->pair_a[pi], b = rb->pair_b[pi];
+        if (rb->link_prim[a] >= 0 || rb->link_prim[b] >= 0) {
+          if (pair_prim(a, b)) return true;
+          continue;
+        }
         double ca[3], cb[3];  // link bounding-sphere prefilter
         xform(frames[rb->lb_body[a]], &rb->lb_cb[a * 3], ca);
         xform(frames[rb->lb_body[b]], &rb->lb_cb[b * 3], cb);
@@ -311,6 +395,29 @@ struct Checker {
           }
       }
     }
+    return false;
+  }
+
+  // world centre and x axis of every primitive (the sphere centres' KDL Frame * Vector; the axis without translation)
+  void prim_frames() {
+    for (size_t p = 0; p < rb->prims.size(); ++p) {
+      const Robot::Prim& P = rb->prims[p];
+      const Frame& B = frames[P.body];
+      xform(B, P.cb, &pw[p * 5]);
+      pw[p * 5 + 3] = B.R[0] * P.ab[0] + B.R[1] * P.ab[1] + B.R[2] * P.ab[2];
+      pw[p * 5 + 4] = B.R[3] * P.ab[0] + B.R[4] * P.ab[1] + B.R[5] * P.ab[2];
+    }
+  }
+  bool prim_map(size_t p) const {
+    const Robot::Prim& P = rb->prims[p];
+    return prim_hits_map(*sc, (int)p, P.type, P.h, pT[p], &pw[p * 5]);
+  }
+  // a primitive link against a sphere link: any sphere of it touching the primitive
+  bool pair_prim(int a, int b) const {
+    const int p = rb->link_prim[a] >= 0 ? rb->link_prim[a] : rb->link_prim[b], sl = rb->link_prim[a] >= 0 ? b : a;
+    const Robot::Prim& P = rb->prims[p];
+    for (int s : rb->link_sph[sl])
+      if (sphere_prim(P.type, P.h, &pw[p * 5], &wc[s * 3], rb->sph_r[s])) return true;
     return false;
   }
 };
@@ -352,6 +459,7 @@ struct Params {
   int max_iter = 1000;
   double max_time = 0;         // >0: time budget instead of iterations (flag_iter_or_time = 1)
   long long max_checked = 0;   // >0: budget of collision-checked configurations instead of iterations
+  int threads = 1;             // >1: the two scans run as OpenMP loops on this many threads (BS:4092, BS:4283)
 };
 
 struct Stats {
@@ -466,6 +574,26 @@ struct Planner {
   int nearest(const Tree& t, const Conf& q) const {
     int id = 0;
     double mn = 10000.0;
+#ifdef _OPENMP
+    if (P.threads > 1) {
+      // the reference's parallel scan (BS:4092-4130: omp parallel for, critical(closervertex)), with the tie the
+      // sequential loop takes: the lowest index among equal minima
+      const long long nn = (long long)t.nodes.size();
+#pragma omp parallel num_threads(P.threads)
+      {
+        int lid = 0;
+        double lmn = 10000.0;
+#pragma omp for schedule(static) nowait
+        for (long long n = 0; n < nn; ++n) {
+          double d = dist(t.nodes[n].q, q);
+          if (d < lmn) { lid = t.nodes[n].node_id; lmn = d; }
+        }
+#pragma omp critical(closervertex)
+        if (lmn < mn || (lmn == mn && lmn < 10000.0 && lid < id)) { mn = lmn; id = lid; }
+      }
+      return id;
+    }
+#endif
     for (size_t n = 0; n < t.nodes.size(); ++n) {
       double d = dist(t.nodes[n].q, q);
       if (d < mn) { id = t.nodes[n].node_id; mn = d; }
@@ -476,6 +604,23 @@ struct Planner {
   // find_near_vertices_interpolation (BS:4272-4324); order = ascending (cost, id).
   std::vector<int> near_set(const Tree& t, const Node& x) const {
     std::vector<std::pair<double, int>> v;
+#ifdef _OPENMP
+    if (P.threads > 1) {
+      // BS:4283-4302: omp parallel for, critical(nodeinsertion); the (cost, id) sort makes the order schedule-free
+      const long long nn = (long long)t.nodes.size();
+#pragma omp parallel num_threads(P.threads)
+      {
+        std::vector<std::pair<double, int>> lv;
+#pragma omp for schedule(static) nowait
+        for (long long n = 0; n < nn; ++n) {
+          double d = dist(t.nodes[n].q, x.q);
+          if (d < P.near_r && x.node_id != t.nodes[n].node_id) lv.push_back({t.nodes[n].cost.total, t.nodes[n].node_id});
+        }
+#pragma omp critical(nodeinsertion)
+        v.insert(v.end(), lv.begin(), lv.end());
+      }
+    } else
+#endif
     for (size_t n = 0; n < t.nodes.size(); ++n) {
       double d = dist(t.nodes[n].q, x.q);
       if (d < P.near_r && x.node_id != t.nodes[n].node_id) v.push_back({t.nodes[n].cost.total, t.nodes[n].node_id});
@@ -1379,6 +1524,9 @@ struct orc_robot_desc {
   int n_body;
   const int *sph_body, *lb_body;
   const double *sph_cb, *lb_cb;
+  int n_prim;
+  const int *prim_type, *prim_body, *prim_link;
+  const double *prim_cb, *prim_ab, *prim_h, *prim_rxy;
 };
 
 struct orc_scene_desc {
@@ -1386,6 +1534,8 @@ struct orc_scene_desc {
   double ox, oy, oz, res;
   const uint64_t* bits;
   const uint16_t* d2;
+  int n_slab;
+  const uint16_t* slab;  // n_slab x ny x nx
 };
 
 struct orc_params {
@@ -1400,6 +1550,7 @@ struct orc_params {
   int max_iter;
   double max_time;
   long long max_checked;
+  int threads;           // OpenMP threads of the two scans (<= 1: sequential)
 };
 
 struct orc_result {
@@ -1457,6 +1608,14 @@ static orc::Robot* mk_robot(const orc_robot_desc* d) {
   r->lb_cb.assign(d->lb_cb, d->lb_cb + 3 * d->n_links);
   r->link_sph.assign(d->n_links, {});
   for (int i = 0; i < d->n_sph; ++i) r->link_sph[d->sph_link[i]].push_back(i);
+  r->link_prim.assign(d->n_links, -1);
+  for (int k = 0; k < d->n_prim; ++k) {
+    orc::Robot::Prim P;
+    P.type = d->prim_type[k]; P.body = d->prim_body[k]; P.link = d->prim_link[k]; P.rxy = d->prim_rxy[k];
+    for (int i = 0; i < 3; ++i) { P.cb[i] = d->prim_cb[k * 3 + i]; P.ab[i] = d->prim_ab[k * 3 + i]; P.h[i] = d->prim_h[k * 3 + i]; }
+    r->prims.push_back(P);
+    r->link_prim[P.link] = k;
+  }
   return r;
 }
 
@@ -1468,6 +1627,8 @@ static orc::Scene* mk_scene(const orc_scene_desc* d) {
   size_t nw = (size_t)s->wx * d->ny * d->nz, nc = (size_t)d->nx * d->ny * d->nz;
   s->bits.assign(d->bits, d->bits + nw);
   s->d2.assign(d->d2, d->d2 + nc);
+  const size_t plane = (size_t)d->nx * d->ny;
+  for (int k = 0; k < d->n_slab; ++k) s->slab.emplace_back(d->slab + k * plane, d->slab + (k + 1) * plane);
   return s;
 }
 
@@ -1483,6 +1644,10 @@ void* orc_create(const orc_robot_desc* rd, const orc_scene_desc* sd, const uint8
   orc_handle* h = new orc_handle();
   h->rb = mk_robot(rd);
   h->sc = mk_scene(sd);
+  if (h->sc && h->sc->slab.size() < h->rb->prims.size()) {  // every primitive needs its slab field
+    fprintf(stderr, "oracle: scene without the primitives' slab fields\n");
+    std::abort();
+  }
   h->ck.init(h->rb, h->sc);
   if (map_enabled) for (int i = 0; i < rd->n_links; ++i) h->ck.map_enabled[i] = map_enabled[i];
   return h;
@@ -1511,11 +1676,19 @@ void orc_collisions(void* hp, const double* q, uint8_t* link_map, uint8_t* pair_
   const orc::Robot& rb = *ck.rb;
   orc::body_frames(rb, q, ck.frames.data());
   for (int i = 0; i < rb.n_sph; ++i) orc::xform(ck.frames[rb.sph_body[i]], &rb.sph_cb[i * 3], &ck.wc[i * 3]);
+  ck.prim_frames();
   for (int l = 0; l < rb.n_links; ++l) link_map[l] = 0;
-  if (ck.sc)
+  if (ck.sc) {
     for (int i = 0; i < rb.n_sph; ++i)
       if (orc::sphere_hits_map(*ck.sc, &ck.wc[i * 3], rb.sph_r[i], ck.T[i])) link_map[rb.sph_link[i]] = 1;
+    for (size_t p = 0; p < rb.prims.size(); ++p)
+      if (ck.prim_map(p)) link_map[rb.prims[p].link] = 1;
+  }
   for (int pi = 0; pi < rb.n_pairs; ++pi) {
+    if (rb.link_prim[rb.pair_a[pi]] >= 0 || rb.link_prim[rb.pair_b[pi]] >= 0) {
+      pair_self[pi] = ck.pair_prim(rb.pair_a[pi], rb.pair_b[pi]) ? 1 : 0;
+      continue;
+    }
     bool hit = false;
     for (int sa : rb.link_sph[rb.pair_a[pi]])
       for (int sb : rb.link_sph[rb.pair_b[pi]]) {
@@ -1584,6 +1757,7 @@ int orc_plan(void* hp, const double* start, const double* goal, const orc_params
   pl.P.env_x[0] = p->env_x[0]; pl.P.env_x[1] = p->env_x[1]; pl.P.env_y[0] = p->env_y[0]; pl.P.env_y[1] = p->env_y[1];
   pl.P.self = p->self; pl.P.map = p->map; pl.P.seed = p->seed; pl.P.query = p->query;
   pl.P.max_iter = p->max_iter; pl.P.max_time = p->max_time; pl.P.max_checked = p->max_checked;
+  pl.P.threads = p->threads;
   orc::Conf s, g;
   for (int j = 0; j < 8; ++j) { s[j] = start[j]; g[j] = goal[j]; }
   std::memset(res, 0, sizeof(*res));

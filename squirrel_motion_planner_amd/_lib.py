@@ -59,7 +59,7 @@ class Stats(ctypes.Structure):
                 ("samples_precomputed", _i64), ("phase_seconds", _d * 32), ("scout_nn_hits", _i64),
                 ("scout_near_hits", _i64), ("scout_edge_hits", _i64), ("scout_edge_misses", _i64),
                 ("scout_wait_seconds", _d), ("scout_phase_seconds", _d * 32), ("helpers", ctypes.c_int32),
-                ("scout", ctypes.c_int32)]
+                ("scout", ctypes.c_int32), ("time_first_solution_host", _d)]
 
 
 class Result(ctypes.Structure):

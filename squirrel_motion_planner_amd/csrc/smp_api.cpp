@@ -118,6 +118,7 @@ struct smp_planner {
   DBuf<uint64_t> d_bricks;
   DBuf<uint16_t> d_d2;
   DBuf<uint8_t> d_d2b;
+  DBuf<uint16_t> d_slab;           // per-primitive 2-D slab fields (SceneDev::slab), n_prim x nx x ny
   SceneDev sc{};
   bool have_scene = false;
   double scene_res = 0.05;
@@ -135,9 +136,25 @@ struct smp_planner {
   int64_t last_plan_launches = 0;
   double wall_rate_hz = 1e8;
   int num_cus = 256;
+  unsigned* h_ttff = nullptr;      // host-mapped first-solution flags, one per query (QueryDev::ttff)
+  int n_ttff = 0;
   // last plan (query 0) bookkeeping for smp_get_tree
   int last_n[2] = {0, 0};
 };
+
+// Workgroups of BLOCK threads that can be resident at once on the device, for the planner's kernels (leader / scout
+// plan_kernel and helper_kernel share the CUs): occupancy per CU (registers, LDS) x CUs.
+static int resident_slots(const smp_planner* p) {
+  int occ_plan = 0, occ_help = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_plan, reinterpret_cast<const void*>(&plan_kernel), BLOCK, 0) !=
+          hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_help, reinterpret_cast<const void*>(&helper_kernel), BLOCK, 0) !=
+          hipSuccess) {
+    (void)hipGetLastError();
+    return p->num_cus;
+  }
+  return p->num_cus * std::max(1, std::min(occ_plan, occ_help));
+}
 
 static int update_mapcfg(smp_planner* p) {
   const RobotDev& d = p->robot.dev;
@@ -147,6 +164,10 @@ static int update_mapcfg(smp_planner* p) {
     p->mc_host.T[s] = p->have_scene ? sphere_threshold(d.sph_r[s], p->scene_res) : 0;
     int link = d.cl_link[d.sph_clink[s]];
     p->mc_host.map_on[s] = p->disabled.count(p->robot.link_names[link]) ? 0 : 1;
+  }
+  for (int k = 0; k < d.n_prim; ++k) {
+    p->mc_host.pT[k] = p->have_scene ? sphere_threshold(d.prim_rxy[k], p->scene_res) : 0;
+    p->mc_host.p_map_on[k] = p->disabled.count(p->robot.link_names[d.cl_link[d.prim_clink[k]]]) ? 0 : 1;
   }
   HIPCHK(hipMemcpyAsync(p->d_mc, &p->mc_host, sizeof(MapCfg), hipMemcpyHostToDevice, p->stream));
   HIPCHK(hipStreamSynchronize(p->stream));
@@ -402,7 +423,8 @@ void smp_planner_destroy(smp_planner* p) {
   if (p->hstream) (void)hipStreamSynchronize(p->hstream);
   for (auto& q : p->qb) q.release();
   p->d_qdev.release(); p->d_counts.release(); p->d_cq.release(); p->d_valid.release();
-  p->d_bricks.release(); p->d_d2.release(); p->d_d2b.release();
+  p->d_ik_tasks.release(); p->d_ik_out.release(); p->d_ik_best.release();
+  p->d_bricks.release(); p->d_d2.release(); p->d_d2b.release(); p->d_slab.release();
   if (p->d_rb) (void)hipFree(p->d_rb);
   if (p->d_mc) (void)hipFree(p->d_mc);
   if (p->ev0) (void)hipEventDestroy(p->ev0);
@@ -410,6 +432,7 @@ void smp_planner_destroy(smp_planner* p) {
   if (p->stream) (void)hipStreamDestroy(p->stream);
   if (p->hstream) (void)hipStreamDestroy(p->hstream);
   if (p->ev_board) (void)hipEventDestroy(p->ev_board);
+  if (p->h_ttff) (void)hipHostFree(p->h_ttff);
   delete p;
 }
 
@@ -425,6 +448,26 @@ int smp_planner_set_scene(smp_planner* p, const smp_scene* s) {
   p->sc.ox = s->h.ox; p->sc.oy = s->h.oy; p->sc.oz = s->h.oz; p->sc.res = s->h.res; p->sc.inv_res = 1.0 / s->h.res;
   p->sc.bricks = p->d_bricks.p;
   p->sc.d2 = p->d_d2.p;
+  {
+    const RobotDev& d = p->robot.dev;
+    for (int k = 0; k < d.n_prim; ++k)
+      if (d.prim_rxy[k] > GRID_REACH) {  // the padding would not keep a primitive outside the grid free
+        fprintf(stderr, "smp_gpu: primitive reach %.3f m exceeds the grid padding\n", d.prim_rxy[k]);
+        return SMP_ERR_ARG;
+      }
+    for (int k = 0; k < MAX_PRIM; ++k) p->sc.slab[k] = nullptr;
+    if (d.n_prim > 0) {
+      std::vector<std::vector<uint16_t>> slabs;
+      prim_slabs(d, s->h, &slabs);
+      const size_t plane = (size_t)s->h.nx * s->h.ny;
+      std::vector<uint16_t> all(plane * d.n_prim);
+      for (int k = 0; k < d.n_prim; ++k) std::memcpy(all.data() + k * plane, slabs[k].data(), plane * sizeof(uint16_t));
+      HIPCHK(p->d_slab.reserve(all.size()));
+      HIPCHK(hipMemcpyAsync(p->d_slab.p, all.data(), all.size() * sizeof(uint16_t), hipMemcpyHostToDevice, p->stream));
+      HIPCHK(hipStreamSynchronize(p->stream));  // `all` is released on return
+      for (int k = 0; k < d.n_prim; ++k) p->sc.slab[k] = p->d_slab.p + k * plane;
+    }
+  }
   // byte copy of the field when every sphere's threshold is below 255 (SceneDev.d2b)
   uint32_t tmax = 0;
   for (int k = 0; k < p->robot.dev.n_sph; ++k) tmax = std::max(tmax, sphere_threshold(p->robot.dev.sph_r[k], s->h.res));
@@ -758,6 +801,7 @@ static QueryDev make_qdev(QueryBuffers& b, size_t cap, long long rows) {
   d.nworkers = 1;
   d.sampler = 0;
   d.trace = nullptr;
+  d.ttff = nullptr;
   return d;
 }
 
@@ -819,7 +863,10 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
       else cap = (int64_t)4 << 20;
     }
     rows_cap[i] = by_iter ? std::max<long long>(iters, 1) : 1 << 20;
-    int via_cap = 4096;
+    // via nodes one connect / choose-parent chain may add (a chain of step_factor steps across the workspace: a few
+    // dozen on a 10 m map); an eighth of the tree capacity, so that a seconds budget's stop margin (two chains) leaves
+    // three quarters of an explicit node_capacity usable.  A longer chain ends the run with SMP_ERR_CAPACITY.
+    const int via_cap = (int)std::max<int64_t>(64, std::min<int64_t>(4096, cap / 8));
     HIPCHK(alloc_query(p->qb[i], (size_t)cap, via_cap, rows_cap[i]));
     qdev[i] = make_qdev(p->qb[i], (size_t)cap, rows_cap[i]);
     init_qstate(p, q, cap, via_cap, &S[i]);
@@ -844,7 +891,10 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
   // with scouts (C2: 127 -> 200 helpers 3.65 -> 3.75 M configs/s with four scouts; 250 no longer all fit and stall).
   int nh = p->params.helpers;
   const bool want_scout = p->params.scout != 0;
-  const int cpq = std::max(1, p->num_cus / nq);
+  // Every workgroup of a query (leader, scouts, helpers) polls the others, so all of them must be resident at once:
+  // the budget is the device's co-resident capacity for these kernels (occupancy x CUs), not a fixed count.
+  const int slots = resident_slots(p);
+  const int cpq = std::max(1, slots / nq);
   int ns = 0;
   int cap_s = 200;  // SMP_HELPER_CAP: experiments with other helper caps
   if (const char* e = std::getenv("SMP_HELPER_CAP")) cap_s = std::max(1, std::atoi(e));
@@ -858,6 +908,13 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
   if (want_scout && p->params.scout > 1) ns = std::min(p->params.scout, MAX_SCOUTS);  // explicit count
   if (nh < 0) nh = 0;
   if (nh < 4) ns = 0;
+  // an explicit request larger than what can be resident is clamped: a helper that never starts would leave its tiles
+  // to the leader's 8 us timeout on every job
+  // to the automatic count (helper sweeps: 250 helpers beside four scouts no longer all start on 256 CUs and stall)
+  if (1 + ns + nh > cpq) {
+    nh = std::max(0, want_scout ? std::min(cap_s, cpq - 1 - ns) : std::min(63, cpq - 1));
+    if (nh < 4) { ns = 0; nh = std::max(0, std::min(nh, cpq - 1)); }
+  }
   // after the first solution scouts 0 and 1 check choose-parent / rewire candidate batches (many tiles); scouts 2
   // and 3 only work before it, one edge per job (3 tiles); the leader's own jobs (edges no record had) are rare
   int h_lead = 0, h_s[MAX_SCOUTS] = {};
@@ -902,6 +959,27 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
     HIPCHK(hipHostGetDevicePointer((void**)&trace_dev, trace_host, 0));
     qdev[0].trace = trace_dev;
   }
+  // first feasible path on the host's clock (from run_planner entry): the kernel sets a host-mapped flag
+  // when it commits the first solution and the launch loop below polls it
+  if (p->n_ttff < nq) {
+    if (p->h_ttff) (void)hipHostFree(p->h_ttff);
+    p->h_ttff = nullptr;
+    p->n_ttff = 0;
+    HIPCHK(hipHostMalloc(&p->h_ttff, nq * sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent));
+    p->n_ttff = nq;
+  }
+  for (int i = 0; i < nq; ++i) __atomic_store_n(&p->h_ttff[i], 0u, __ATOMIC_RELAXED);
+  {
+    unsigned* dflag = nullptr;
+    HIPCHK(hipHostGetDevicePointer((void**)&dflag, p->h_ttff, 0));
+    for (int i = 0; i < nq; ++i) qdev[i].ttff = dflag + i;
+  }
+  std::vector<double> host_ttff(nq, -1.0);
+  auto poll_ttff = [&]() {
+    for (int i = 0; i < nq; ++i)
+      if (host_ttff[i] < 0 && __atomic_load_n(&p->h_ttff[i], __ATOMIC_ACQUIRE))
+        host_ttff[i] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_entry).count();
+  };
   HIPCHK(p->d_qdev.reserve(nq));
   HIPCHK(p->d_counts.reserve(2 * nq));
   HIPCHK(hipMemcpyAsync(p->d_qdev.p, qdev.data(), nq * sizeof(QueryDev), hipMemcpyHostToDevice, p->stream));
@@ -953,6 +1031,13 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
       HIPCHK(hipGetLastError());
     }
     launches++;
+    // time the first feasible path on the host: poll the flags while the launch runs
+    {
+      hipError_t qe;
+      while ((qe = hipEventQuery(p->ev1)) == hipErrorNotReady) poll_ttff();
+      if (qe != hipSuccess) HIPCHK(qe);
+      poll_ttff();
+    }
     if (debug) {  // bounded wait: print the leader's progress markers if the launch does not finish
       auto tw = std::chrono::steady_clock::now();
       hipError_t qe;
@@ -1033,6 +1118,7 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
     st.configs_valid = s.valid;
     st.time_first_solution = s.have_sol && s.t_first >= s.t0 ? (double)(s.t_first - s.t0) / p->wall_rate_hz : -1.0;
     st.time_total = s.t_end >= s.t0 ? (double)(s.t_end - s.t0) / p->wall_rate_hz : 0.0;
+    st.time_first_solution_host = s.have_sol ? host_ttff[i] : -1.0;
     for (int k = 0; k < 3; ++k) { st.cost_best[k] = s.cbest[k]; st.cost_theoretical[k] = s.h0[k]; }
     st.nodes_start = s.n[0]; st.nodes_goal = s.n[1];
     st.edges_start = s.edges[0]; st.edges_goal = s.edges[1];

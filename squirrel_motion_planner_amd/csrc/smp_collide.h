@@ -268,6 +268,132 @@ __device__ __forceinline__ bool wave_sphere_map(const SceneDev& sc, const double
   return false;
 }
 
+// ---------------------------------------------------------------------------------------------- exact primitives
+// World centre and horizontal x axis (c, s) of primitive p from its body's frame B (R row-major, then p): the same
+// three-term sums as a sphere centre (KDL Frame * Vector); the axis is R times ab without the translation.
+__device__ __forceinline__ void prim_world(const RobotDev* __restrict__ rb, int p, const double* B, double* o) {
+  const double* cb = &rb->prim_cb[p * 3];
+  const double* ab = &rb->prim_ab[p * 3];
+  for (int r = 0; r < 3; ++r) {
+    const double m = B[r * 3 + 0] * cb[0] + B[r * 3 + 1] * cb[1] + B[r * 3 + 2] * cb[2];
+    o[r] = m + B[9 + r];
+  }
+  o[3] = B[0] * ab[0] + B[1] * ab[1] + B[2] * ab[2];
+  o[4] = B[3] * ab[0] + B[4] * ab[1] + B[5] * ab[2];
+}
+
+// Exact test of an upright primitive (ty 1 box with half extents h[0..2], 2 cylinder of radius h[0] and half length
+// h[1]; centre pw[0..2], x axis (pw[3], pw[4])) against the closed box of cell (i, j, k): z intervals overlap, and in
+// the plane the separating-axis test of the rotated rectangle against the cell's square (axes x, y, the box's own
+// two), or the circle against the square.  Shared term by term with the oracle (smp_oracle.cpp prim_cell).
+__device__ __forceinline__ bool prim_cell(int ty, const double* __restrict__ h, const double* pw, const SceneDev& sc, int i,
+                                          int j, int k) {
+  const double zlo = sc.oz + (double)k * sc.res, zhi = sc.oz + (double)(k + 1) * sc.res;
+  const double hz = ty == 1 ? h[2] : h[1];
+  if (zhi < pw[2] - hz || zlo > pw[2] + hz) return false;
+  const double xlo = sc.ox + (double)i * sc.res, xhi = sc.ox + (double)(i + 1) * sc.res;
+  const double ylo = sc.oy + (double)j * sc.res, yhi = sc.oy + (double)(j + 1) * sc.res;
+  if (ty == 2) {
+    const double qx = pw[0] < xlo ? xlo - pw[0] : (pw[0] > xhi ? pw[0] - xhi : 0.0);
+    const double qy = pw[1] < ylo ? ylo - pw[1] : (pw[1] > yhi ? pw[1] - yhi : 0.0);
+    return qx * qx + qy * qy <= h[0] * h[0];
+  }
+  const double c = pw[3], s = pw[4], ac = fabs(c), as = fabs(s), hw = 0.5 * sc.res;
+  const double dx = 0.5 * (xlo + xhi) - pw[0], dy = 0.5 * (ylo + yhi) - pw[1];
+  if (fabs(dx) > hw + (ac * h[0] + as * h[1])) return false;
+  if (fabs(dy) > hw + (as * h[0] + ac * h[1])) return false;
+  if (fabs(c * dx + s * dy) > h[0] + hw * (ac + as)) return false;
+  if (fabs(c * dy - s * dx) > h[1] + hw * (ac + as)) return false;
+  return true;
+}
+
+// Cells whose boxes can meet the primitive's axis-aligned bounds, trimmed with the cell test's own comparisons (a
+// trimmed cell fails that test), clipped to the grid.  Returns false if the range is empty.
+__device__ __forceinline__ bool prim_reach(int ty, const double* __restrict__ h, const double* pw, const SceneDev& sc,
+                                           int* lo, int* hi) {
+  const double ac = fabs(pw[3]), as = fabs(pw[4]);
+  const double ex = ty == 1 ? ac * h[0] + as * h[1] : h[0];
+  const double ey = ty == 1 ? as * h[0] + ac * h[1] : h[0];
+  const double ez = ty == 1 ? h[2] : h[1];
+  const double a[3] = {pw[0] - ex, pw[1] - ey, pw[2] - ez}, b[3] = {pw[0] + ex, pw[1] + ey, pw[2] + ez};
+  const double o[3] = {sc.ox, sc.oy, sc.oz};
+  const int n[3] = {sc.nx, sc.ny, sc.nz};
+  for (int d = 0; d < 3; ++d) {
+    int l = (int)floor((a[d] - o[d]) * sc.inv_res) - 1, u = (int)floor((b[d] - o[d]) * sc.inv_res) + 1;
+    l = max(l, 0);
+    u = min(u, n[d] - 1);
+    while (l <= u && o[d] + (double)(l + 1) * sc.res < a[d]) ++l;
+    while (u >= l && o[d] + (double)u * sc.res > b[d]) --u;
+    if (l > u) return false;
+    lo[d] = l;
+    hi[d] = u;
+  }
+  return true;
+}
+
+// Cooperative exact map test of one primitive by a wavefront: one brick word per lane over the reach, masked to the
+// reach's cells; each lane tests its brick's occupied cells in reach (ballot early exit).
+__device__ __forceinline__ bool wave_prim_map(const SceneDev& sc, int ty, const double* __restrict__ h, const double* pw,
+                                              int lane) {
+  int lo[3], hi[3];
+  if (!prim_reach(ty, h, pw, sc, lo, hi)) return false;
+  const int bi0 = lo[0] >> 2, bj0 = lo[1] >> 2, bk0 = lo[2] >> 2;
+  const int nbi = (hi[0] >> 2) - bi0 + 1, nbj = (hi[1] >> 2) - bj0 + 1, nbk = (hi[2] >> 2) - bk0 + 1;
+  const int nb = nbi * nbj * nbk;
+  for (int b0 = 0; b0 < nb; b0 += 64) {
+    const int b = b0 + lane;
+    bool hit = false;
+    if (b < nb) {
+      const int bi = bi0 + b % nbi, t = b / nbi;
+      const int bj = bj0 + t % nbj, bk = bk0 + t / nbj;
+      uint64_t w = sc.bricks[((size_t)bk * sc.bny + bj) * sc.bnx + bi];
+      if (w) {
+        const int il = max(lo[0] - 4 * bi, 0), ih = min(hi[0] - 4 * bi, 3);
+        const int jl = max(lo[1] - 4 * bj, 0), jh = min(hi[1] - 4 * bj, 3);
+        const int kl = max(lo[2] - 4 * bk, 0), kh = min(hi[2] - 4 * bk, 3);
+        const uint32_t xm = ((2u << ih) - 1u) & ~((1u << il) - 1u);
+        uint32_t row = 0;
+        for (int jj = jl; jj <= jh; ++jj) row |= xm << (4 * jj);
+        uint64_t m = 0;
+        for (int kk = kl; kk <= kh; ++kk) m |= (uint64_t)row << (16 * kk);
+        w &= m;
+        while (w && !hit) {
+          const int bit = __builtin_ctzll(w);
+          w &= w - 1;
+          hit = prim_cell(ty, h, pw, sc, 4 * bi + (bit & 3), 4 * bj + ((bit >> 2) & 3), 4 * bk + (bit >> 4));
+        }
+      }
+    }
+    if (__ballot(hit)) return true;
+  }
+  return false;
+}
+
+// Slab prefilter of primitive p (SceneDev::slab): true if p may touch the map (its centre's column holds a squared
+// gap of at most pT); a centre outside the grid is free (the grid is padded by more than any rxy).
+__device__ __forceinline__ bool prim_candidate(const SceneDev& sc, const uint16_t* __restrict__ slab, uint32_t pT,
+                                               const double* pw) {
+  const double fx = floor((pw[0] - sc.ox) * sc.inv_res), fy = floor((pw[1] - sc.oy) * sc.inv_res);
+  if (!(fx >= 0 && fx < sc.nx && fy >= 0 && fy < sc.ny)) return false;
+  return (uint32_t)slab[(size_t)(int)fy * sc.nx + (int)fx] <= pT;
+}
+
+// Exact sphere (world centre w, radius rs) vs upright primitive test: the squared distance from the centre to the
+// solid box (in the box's frame) or cylinder against rs^2.  Shared term by term with the oracle (sphere_prim).
+__device__ __forceinline__ bool sphere_prim(int ty, const double* __restrict__ h, const double* pw, const double* w,
+                                            double rs) {
+  const double dx = w[0] - pw[0], dy = w[1] - pw[1], dz = w[2] - pw[2];
+  const double az = fabs(dz);
+  if (ty == 1) {
+    const double lx = fabs(pw[3] * dx + pw[4] * dy), ly = fabs(pw[3] * dy - pw[4] * dx);
+    const double qx = lx > h[0] ? lx - h[0] : 0.0, qy = ly > h[1] ? ly - h[1] : 0.0, qz = az > h[2] ? az - h[2] : 0.0;
+    return qx * qx + qy * qy + qz * qz <= rs * rs;
+  }
+  const double rho = sqrt(dx * dx + dy * dy);
+  const double qr = rho > h[0] ? rho - h[0] : 0.0, qz = az > h[1] ? az - h[1] : 0.0;
+  return qr * qr + qz * qz <= rs * rs;
+}
+
 constexpr int NWAVE = BLOCK / 64;
 
 // LDS work area of one collision tile of CT configurations (CT a multiple of the wave count).
@@ -281,9 +407,11 @@ struct TileLds {
     double lf[CT][MAX_CHAIN][12];           // stages A/B: local frame of every chain step
     struct {
       double wc[CT][MAX_SPH][3];            // stage C: sphere world centres
+      double pw[CT][MAX_PRIM][5];           // stage C: primitive centres and x axes
     } c;
   } u;
   uint32_t cand[CT][SW];                    // spheres needing the exact map sweep
+  uint32_t pcand[CT];                       // primitives needing the exact map sweep
   int coll[CT];                             // 1 = in collision
 };
 
@@ -341,6 +469,7 @@ __device__ __forceinline__ void collide_tile(const RobotDev* __restrict__ rb, co
       o[9] = F.p[0]; o[10] = F.p[1]; o[11] = F.p[2];
     }
     for (int it = tid; it < CT * SW; it += BLOCK) (&L.cand[0][0])[it] = 0u;
+    if (tid < CT) L.pcand[tid] = 0u;
     if (tid < nc) L.coll[tid] = 0;
     wave_sync();
   }
@@ -421,6 +550,17 @@ __device__ __forceinline__ void collide_tile(const RobotDev* __restrict__ rb, co
       const int k = it / nsph, s = it - k * nsph;
       if (cell[u] >= 0 && dv[u] <= mc->T[s]) atomicOr(&L.cand[k * NWAVE + wave][s >> 5], 1u << (s & 31));
     }
+    // primitives: world frames (for the self test too) and the slab prefilter, lanes over (configuration, primitive)
+    const int npr = rb->n_prim;
+    for (int it = lane; it < CPW * npr; it += 64) {
+      const int k = it / npr, p = it - k * npr;
+      if (!((live >> k) & 1u)) continue;
+      const int c = k * NWAVE + wave;
+      double* pw = L.u.c.pw[c][p];
+      prim_world(rb, p, L.fr[c][rb->prim_body[p]], pw);
+      if (do_map && mc->p_map_on[p] && prim_candidate(sc, sc_in.slab[p], mc->pT[p], pw))
+        atomicOr(&L.pcand[c], 1u << p);
+    }
     wave_sync();
     if (prof && tid == 0) prof[2] += wall_clock64() - t1;
     // map sweeps
@@ -429,6 +569,13 @@ __device__ __forceinline__ void collide_tile(const RobotDev* __restrict__ rb, co
       if (!((live >> k) & 1u)) continue;
       const int c = k * NWAVE + wave;
       bool hit = false;
+      for (uint32_t pm = L.pcand[c]; pm && !hit;) {
+        const int p = __builtin_ctz(pm);
+        pm &= pm - 1;
+        const double pw[5] = {L.u.c.pw[c][p][0], L.u.c.pw[c][p][1], L.u.c.pw[c][p][2], L.u.c.pw[c][p][3],
+                              L.u.c.pw[c][p][4]};
+        hit = wave_prim_map(sc, rb->prim_type[p], &rb->prim_h[p * 3], pw, lane);
+      }
       for (int wd = 0; wd < SW && !hit; ++wd) {
         uint32_t m = L.cand[c][wd];
         while (m) {
@@ -459,6 +606,18 @@ __device__ __forceinline__ void collide_tile(const RobotDev* __restrict__ rb, co
             const double ex = wa[0] - wb[0], ey = wa[1] - wb[1], ez = wa[2] - wb[2];
             if (ex * ex + ey * ey + ez * ez <= rr2) sh |= 1u << k;
           }
+        }
+        // (primitive, sphere) pairs
+        const int npp = rb->n_ppairs;
+        for (int p = lane; p < npp; p += 64) {
+          const uint32_t ps = rb->pp_ps[p];
+          const int pr = ps & 0xff, sp = ps >> 8;
+          const int ty = rb->prim_type[pr];
+          const double rs = rb->sph_r[sp];
+#pragma unroll
+          for (int k = 0; k < CPW; ++k)
+            if (sphere_prim(ty, &rb->prim_h[pr * 3], L.u.c.pw[k * NWAVE + wave][pr], L.u.c.wc[k * NWAVE + wave][sp], rs))
+              sh |= 1u << k;
         }
         for (int k = 0; k < CPW; ++k)
           if (((todo >> k) & 1u) && __ballot((sh >> k) & 1u)) hitm |= 1u << k;

@@ -94,6 +94,36 @@ void robot_from_json(const std::string& text, RobotHost* out) {
     if (d.cl_nsph[c] == 0) d.cl_sph0[c] = k;
     d.cl_nsph[c]++;
   }
+  for (int j = 0; j < NJ; ++j) {
+    d.q_min[j] = m["q_min"][j].d();
+    d.q_max[j] = m["q_max"][j].d();
+    d.rev[j] = m["joint_is_revolute"][j].i();
+  }
+  // exact primitives (format 2; a format-1 model has none)
+  for (int c = 0; c < d.n_clink; ++c) d.cl_prim[c] = -1;
+  d.n_prim = 0;
+  if (m.has("prims")) {
+    const json::Value& PR = m["prims"];
+    d.n_prim = (int)PR.size();
+    if (d.n_prim > MAX_PRIM) throw std::runtime_error("model: too many primitives");
+    for (int k = 0; k < d.n_prim; ++k) {
+      const json::Value& e = PR[k];
+      const int c = out->clink_of_link[e["link"].i()];
+      if (c < 0 || d.cl_nsph[c] > 0 || d.cl_prim[c] >= 0) throw std::runtime_error("model: bad primitive link");
+      const std::string ty = e["type"].s();
+      d.prim_type[k] = ty == "box" ? 1 : ty == "cylinder" ? 2 : 0;
+      if (!d.prim_type[k]) throw std::runtime_error("model: unknown primitive type " + ty);
+      d.prim_body[k] = e["body"].i();
+      d.prim_clink[k] = c;
+      d.cl_prim[c] = k;
+      copy3(e["cb"], &d.prim_cb[k * 3]);
+      copy3(e["ab"], &d.prim_ab[k * 3]);
+      copy3(e["half"], &d.prim_h[k * 3]);
+      d.prim_rxy[k] = e["rxy"].d();
+    }
+  }
+  for (int c = 0; c < d.n_clink; ++c)
+    if (d.cl_nsph[c] == 0 && d.cl_prim[c] < 0) throw std::runtime_error("model: collision link without geometry");
   const json::Value& P = m["self_pairs"];
   d.n_pairs = (int)P.size();
   if (d.n_pairs > MAX_PAIRS) throw std::runtime_error("model: too many pairs");
@@ -102,10 +132,28 @@ void robot_from_json(const std::string& text, RobotHost* out) {
     d.pair_b[p] = out->clink_of_link[P[p][1].i()];
     if (d.pair_a[p] < 0 || d.pair_b[p] < 0) throw std::runtime_error("model: pair on a link without geometry");
   }
-  // sphere pairs in (link pair, sphere of a, sphere of b) order; (ra + rb)^2 rounded as the device would
+  finish_pairs(&d);
+}
+
+// Flat self-collision lists of the enabled link pairs: every sphere pair of two sphere links in (link pair, sphere
+// of a, sphere of b) order with (ra + rb)^2 rounded as the device would, and every (primitive, sphere) pair of a
+// primitive link and a sphere link.  Two primitive links in one pair would have to be rigidly attached (both sit on
+// the planar base), and rigid pairs are not in the model.
+void finish_pairs(RobotDev* dp) {
+  RobotDev& d = *dp;
   d.n_spairs = 0;
+  d.n_ppairs = 0;
   for (int p = 0; p < d.n_pairs; ++p) {
     int a = d.pair_a[p], b = d.pair_b[p];
+    if (d.cl_prim[a] >= 0 && d.cl_prim[b] >= 0) throw std::runtime_error("model: primitive-primitive pair");
+    if (d.cl_prim[a] >= 0 || d.cl_prim[b] >= 0) {
+      const int pr = d.cl_prim[a] >= 0 ? d.cl_prim[a] : d.cl_prim[b], sl = d.cl_prim[a] >= 0 ? b : a;
+      for (int s = d.cl_sph0[sl]; s < d.cl_sph0[sl] + d.cl_nsph[sl]; ++s) {
+        if (d.n_ppairs >= MAX_PPAIRS) throw std::runtime_error("model: too many primitive-sphere pairs");
+        d.pp_ps[d.n_ppairs++] = (uint16_t)(pr | (s << 8));
+      }
+      continue;
+    }
     for (int sa = d.cl_sph0[a]; sa < d.cl_sph0[a] + d.cl_nsph[a]; ++sa)
       for (int sb = d.cl_sph0[b]; sb < d.cl_sph0[b] + d.cl_nsph[b]; ++sb) {
         if (d.n_spairs >= MAX_SPAIRS) throw std::runtime_error("model: too many sphere pairs");
@@ -116,15 +164,62 @@ void robot_from_json(const std::string& text, RobotHost* out) {
         d.n_spairs++;
       }
   }
-  for (int j = 0; j < NJ; ++j) {
-    d.q_min[j] = m["q_min"][j].d();
-    d.q_max[j] = m["q_max"][j].d();
-    d.rev[j] = m["joint_is_revolute"][j].i();
-  }
 }
 
 // ------------------------------------------------------------------------------------------ scene
-int grid_pad_cells(double res) { return (int)std::ceil(0.30 / res) + 2; }
+// Padding around the occupied keys: more than the largest horizontal reach of any sphere (<= 0.30 m) or primitive
+// (rxy <= 0.45 m; robotino's front shell box 0.389 m) plus a cell, so a centre outside the grid is free of the map.
+int grid_pad_cells(double res) { return (int)std::ceil(GRID_REACH / res) + 2; }
+
+// World z of every primitive's centre: its body is planar (tools/gen_robot_model.py), so the body frame at q = 0
+// gives the z every configuration has (up to rounding; the slab adds a margin).
+static void prim_z(const RobotDev& d, double* zc) {
+  double R[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, P[3] = {0, 0, d.root_z};
+  double BR[MAX_BODY][9], BP[MAX_BODY][3];
+  for (int k = 0; k < d.n_chain; ++k) {
+    double LR[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, LP[3];
+    for (int i = 0; i < 3; ++i) LP[i] = d.ch_origin[k * 3 + i];
+    if (d.ch_type[k] == 0) {
+      for (int i = 0; i < 9; ++i) LR[i] = d.ch_R[k * 9 + i];
+      for (int i = 0; i < 3; ++i) LP[i] = d.ch_p[k * 3 + i];
+    }
+    double NR[9], NP[3];
+    for (int r = 0; r < 3; ++r) {
+      for (int c = 0; c < 3; ++c) NR[r * 3 + c] = R[r * 3] * LR[c] + R[r * 3 + 1] * LR[3 + c] + R[r * 3 + 2] * LR[6 + c];
+      NP[r] = (R[r * 3] * LP[0] + R[r * 3 + 1] * LP[1] + R[r * 3 + 2] * LP[2]) + P[r];
+    }
+    std::memcpy(R, NR, sizeof(R));
+    std::memcpy(P, NP, sizeof(P));
+    if (d.ch_body[k] >= 0) { std::memcpy(BR[d.ch_body[k]], R, sizeof(R)); std::memcpy(BP[d.ch_body[k]], P, sizeof(P)); }
+  }
+  for (int p = 0; p < d.n_prim; ++p) {
+    const double* B = BR[d.prim_body[p]];
+    const double* c = &d.prim_cb[p * 3];
+    zc[p] = (B[6] * c[0] + B[7] * c[1] + B[8] * c[2]) + BP[d.prim_body[p]][2];
+  }
+}
+
+void prim_slabs(const RobotDev& d, const SceneHost& s, std::vector<std::vector<uint16_t>>* out) {
+  out->assign(d.n_prim, {});
+  double zc[MAX_PRIM];
+  prim_z(d, zc);
+  for (int p = 0; p < d.n_prim; ++p) {
+    const double hz = d.prim_type[p] == 1 ? d.prim_h[p * 3 + 2] : d.prim_h[p * 3 + 1];
+    const double zlo = zc[p] - hz - 1e-6, zhi = zc[p] + hz + 1e-6;
+    // layers whose cell boxes meet [zlo, zhi]
+    int k0 = std::max(0, (int)std::floor((zlo - s.oz) / s.res) - 1), k1 = std::min(s.nz - 1, (int)std::floor((zhi - s.oz) / s.res) + 1);
+    while (k0 <= k1 && s.oz + (double)(k0 + 1) * s.res < zlo) ++k0;
+    while (k1 >= k0 && s.oz + (double)k1 * s.res > zhi) --k1;
+    std::vector<uint8_t> proj((size_t)s.nx * s.ny, 0);
+    for (int k = k0; k <= k1; ++k)
+      for (int j = 0; j < s.ny; ++j) {
+        const uint64_t* row = s.bits.data() + ((size_t)k * s.ny + j) * s.wx;
+        for (int w = 0; w < s.wx; ++w)
+          for (uint64_t m = row[w]; m; m &= m - 1) proj[(size_t)j * s.nx + w * 64 + __builtin_ctzll(m)] = 1;
+      }
+    box_gap_squared(proj, s.nx, s.ny, 1, &(*out)[p]);
+  }
+}
 
 // d2 is a lower bound of (distance from any point of the cell to any occupied box / res)^2, so a sphere of
 // radius r whose centre cell has d2 > T cannot touch an occupied box; the 1e-6 m margin absorbs rounding.

@@ -31,6 +31,7 @@ void robot_from_urdf(const std::string& urdf, const std::string& srdf, const std
 
 constexpr int KEY_OFFSET = 32768;  // octomap tree_max_val
 
+constexpr double GRID_REACH = 0.45;  // m: largest horizontal reach of a sphere or primitive from its centre
 int grid_pad_cells(double res);
 void scene_from_keys(const uint16_t* keys, int64_t n, double res, double z_offset, SceneHost* out);
 // A free octree leaf (depth, centre key, float log-odds): kept for the floor insertion, which leaves a floor cell
@@ -60,5 +61,10 @@ void box_gap_squared(const std::vector<uint8_t>& occ, int nx, int ny, int nz, st
 // 4x4x4 occupancy bricks from the bitset.
 void build_bricks(SceneHost* h);
 uint32_t sphere_threshold(double r, double res);
+// Per-primitive 2-D box-gap fields of a scene (SceneDev::slab): occupancy projected over the layers the primitive's
+// constant z range touches, dilated 3x3, squared EDT (cells).
+void prim_slabs(const RobotDev& d, const SceneHost& s, std::vector<std::vector<uint16_t>>* out);
+// Flat self-collision pair lists (sphere pairs, primitive-sphere pairs) from pair_a / pair_b.
+void finish_pairs(RobotDev* d);
 
 }  // namespace smp

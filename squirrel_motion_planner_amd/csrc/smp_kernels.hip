@@ -106,6 +106,7 @@ __global__ void __launch_bounds__(64) collisions_kernel(const RobotDev* __restri
   __shared__ double wc[MAX_SPH][3];
   __shared__ uint32_t cand[(MAX_SPH + 31) / 32];
   __shared__ int lm[MAX_CLINK];
+  __shared__ double pwl[MAX_PRIM][5];
   const int lane = threadIdx.x;
   if (lane == 0) {
     double qq[NJ];
@@ -128,6 +129,16 @@ __global__ void __launch_bounds__(64) collisions_kernel(const RobotDev* __restri
       if (dv <= mc->T[s]) atomicOr(&cand[s >> 5], 1u << (s & 31));
     }
   }
+  for (int p = lane; p < rb->n_prim; p += 64) prim_world(rb, p, &B[rb->prim_body[p]].R[0], pwl[p]);
+  __syncthreads();
+  // primitives: exact sweep of every one whose slab prefilter does not clear it (disabled links included)
+  if (map)
+    for (int p = 0; p < rb->n_prim; ++p) {
+      const double pw[5] = {pwl[p][0], pwl[p][1], pwl[p][2], pwl[p][3], pwl[p][4]};
+      if (!prim_candidate(sc, sc.slab[p], mc->pT[p], pw)) continue;
+      const bool hit = wave_prim_map(sc, rb->prim_type[p], &rb->prim_h[p * 3], pw, lane);
+      if (hit && lane == 0) lm[rb->prim_clink[p]] = 1;
+    }
   __syncthreads();
   for (int wd = 0; wd < (nsph + 31) / 32; ++wd) {
     uint32_t m = cand[wd];
@@ -146,6 +157,13 @@ __global__ void __launch_bounds__(64) collisions_kernel(const RobotDev* __restri
   for (int p = lane; p < rb->n_pairs; p += 64) {
     const int a = rb->pair_a[p], b = rb->pair_b[p];
     bool hit = false;
+    if (rb->cl_prim[a] >= 0 || rb->cl_prim[b] >= 0) {
+      const int pr = rb->cl_prim[a] >= 0 ? rb->cl_prim[a] : rb->cl_prim[b], sl = rb->cl_prim[a] >= 0 ? b : a;
+      for (int s = rb->cl_sph0[sl]; s < rb->cl_sph0[sl] + rb->cl_nsph[sl] && !hit; ++s)
+        hit = sphere_prim(rb->prim_type[pr], &rb->prim_h[pr * 3], pwl[pr], wc[s], rb->sph_r[s]);
+      pair_self[p] = hit ? 1 : 0;
+      continue;
+    }
     for (int sa = rb->cl_sph0[a]; sa < rb->cl_sph0[a] + rb->cl_nsph[a] && !hit; ++sa)
       for (int sb = rb->cl_sph0[b]; sb < rb->cl_sph0[b] + rb->cl_nsph[b]; ++sb) {
         const double rs = rb->sph_r[sa] + rb->sph_r[sb];
@@ -1563,6 +1581,11 @@ __device__ void scout_ask(const Ctx& C, long long k, int tree, bool pre, bool& f
       if (!((g_L.sc_dead >> c) & 1u)) w = c;
     }
     if (w < 0) return;
+    // a scout holds one request slot (req[0..2], newest tag wins): if it still has an outstanding request of its own,
+    // a second one could replace it before it is taken and its record would never come (the leader would wait out
+    // SCOUT_WAIT for it), so iteration k takes the full path instead
+    for (int x = 0; x < SCOUT_SLOTS; ++x)
+      if (g_L.asked[x] == 1 + w) return;
     which = 1 + w;
   }
   ScoutBoard* sb = C.Q.scbs[which - 1];
@@ -2672,6 +2695,8 @@ __device__ void connect_tail(const Ctx& C, int t) {
       if (!S.have_sol) {
         S.first_iter = S.iter;
         S.t_first = wall_clock64();
+        // host-visible flag: smp_plan times the first feasible path on its own clock (system-scope vector store)
+        if (C.Q.ttff) __hip_atomic_store(C.Q.ttff, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
       S.have_sol = 1;
       insert_node(C, t, g_L.sel_start, g_L.sel_target, g_L.sel);
@@ -3685,6 +3710,7 @@ __device__ __forceinline__ void scout_ctx(Ctx& C, int which) {
   C.Q.via = C.Q.svia;
   C.Q.rows = nullptr;
   C.Q.trace = nullptr;
+  C.Q.ttff = nullptr;
 }
 
 __device__ __forceinline__ void scout_main(Ctx& C, int which) {

@@ -264,6 +264,7 @@ struct QueryDev {
   ViaNode* svia;
   int sworkers;
   int* trace;                  // debug only (SMP_DEBUG): host-mapped progress markers of the leader
+  unsigned* ttff;              // host-mapped word set to 1 when the first feasible path is committed (null: none)
   int nworkers;                // leader + tile helper workgroups (tile w, w + nworkers, ... is worker w's)
   int sampler;                 // 1: the last helper workgroup is the run-ahead sampler
   TreeDev tr[2];

@@ -21,6 +21,10 @@ KEY_OFFSET = 32768
 ARM_FOLDED = [-0.7, 1.9, 0.0, 1.7, 0.0]
 ARM_UNFOLDED = [-0.707011701539749, 1.6149626484476989, 0.19002285249790796, 1.7589609723317974, 0.183945523562212]
 ARM_REACH = [0.6, 0.9, 0.4, 0.8, 0.0]
+# The first keyframe of folding_poses_tuw-robotino2.yaml, SURVEY C1's start ("folded arm"): the stowed hand rests its
+# fingers inside the front shell's box primitive (robotino_plan.urdf:323-329), so the start is in self-collision --
+# for the reference as well (its FCL box vs the hand meshes of squirrel-hand.dae, tools/gen_robot_model.py validate).
+ARM_STOWED = [0.29201350928033476, 2.2600188129288705, 0.19001033369874476, -1.1680354608387098, 0.5320232345529955]
 
 
 def coord_to_key(c, res):
@@ -81,9 +85,10 @@ class Scene:
         return (float(lo[0]), float(hi[0])), (float(lo[1]), float(hi[1]))
 
 
-def empty_room(res=0.05):
-    """C1: empty 5 m x 5 m map, floor only (plumbing)."""
-    start = [0.0, 0.0, 0.0] + ARM_FOLDED
+def empty_room(res=0.05, stowed=False):
+    """C1: empty 5 m x 5 m map, floor only (plumbing).  stowed=True: SURVEY's start (ARM_STOWED, in self-collision:
+    init_planner fails, birrt_star.cpp:353-357); else pose_folded_arm (parameters.yaml:38)."""
+    start = [0.0, 0.0, 0.0] + (ARM_STOWED if stowed else ARM_FOLDED)
     goal = [1.5, 1.0, 1.2] + ARM_UNFOLDED
     keys = floor_keys(start[:2], res, 2.5)
     s = Scene("C1-empty-5m", keys, res, start, goal, (0, 0), (0, 0))
@@ -120,12 +125,12 @@ def box_room(seed=42, res=0.05, n_boxes=20, start=None, goal=None):
 def narrow_passage(res=0.05, slot=0.24):
     """C4: wall at x = 0 with a slot `slot` m wide (2 x ~0.12 m arm-link width) at z 0.55-0.79.
 
-    Start: folded arm 0.9 m in front of the wall.  Goal: the hand inside the slot (hand_wrist_link at x 0.027,
-    y -0.024, z 0.613), one of the few collision-free configurations that reach into it (found by rejection
-    sampling with the oracle); the straight start->goal edge collides, so the query is planned, not connected
-    directly (birrt_star.cpp:1072-1075)."""
+    Start: folded arm 0.9 m in front of the wall.  Goal: the wrist inside the slot (hand_wrist_link at x 0.031,
+    y -0.052, z 0.597), one of the 8 collision-free configurations of 1e6 random ones with the wrist in the slot
+    (rejection sampling with the oracle, seed 4); the straight start->goal edge collides, so the query is planned,
+    not connected directly (birrt_star.cpp:1072-1075)."""
     start = [-0.9, 0.0, 0.0] + ARM_FOLDED
-    goal = [-0.351, -0.064, 1.074, -0.445, 0.83, -0.28, 0.395, -0.119]
+    goal = [-0.391, -0.227, 1.184, -0.799, -0.055, 1.581, -0.13, 1.613]
     wall = _box_keys([0.0, -5.0, 0.0], [0.1, 5.0, 2.0], res)
     rel = (wall - KEY_OFFSET + 0.5) * res
     hole = (np.abs(rel[:, 1]) < slot / 2) & (rel[:, 2] > 0.55) & (rel[:, 2] < 0.79)

@@ -66,13 +66,35 @@ def test_seconds_budget_counts_from_the_call(c2):
     assert wall < 0.05 + 0.5
 
 
-def test_seconds_budget_keeps_the_path_when_a_tree_fills(c2):
+@pytest.mark.parametrize("cap", [9000, 4000])
+def test_seconds_budget_keeps_the_path_when_a_tree_fills(c2, cap):
     sc, scene = c2
-    # 8196 nodes are held back for one iteration's via chains: the run stops once a tree holds ~800 nodes
-    gp = GpuPlanner(Robot(), path_optimality_threshold=-math.inf, node_capacity=9000)
+    # two via chains of cap/8 nodes each are held back for one iteration: the run stops once a tree holds about
+    # three quarters of the capacity, with the best path so far
+    gp = GpuPlanner(Robot(), path_optimality_threshold=-math.inf, node_capacity=cap)
     gp.set_scene(scene)
     r = gp.plan(GpuPlanner.make_query(sc.start, sc.goal, sc.env_x, sc.env_y, seconds=20.0, seed=1))
     assert r["status"] == L.SMP_OK, r["status"]
     assert len(r["path"]) > 0
-    assert max(r["nodes_start"], r["nodes_goal"]) + 8196 > 9000
+    margin = 2 * max(64, min(4096, cap // 8)) + 4
+    n = max(r["nodes_start"], r["nodes_goal"])
+    assert n + margin > cap and n > cap // 2, (n, cap)
+    assert r["iterations"] > 100
     assert r["time_total"] < 5.0
+
+
+def test_oversubscribed_helpers_are_clamped(c2):
+    # a helper request beyond the co-resident capacity (occupancy x CUs) falls back to the automatic count: every
+    # helper has to be running for the leader's jobs not to wait out its tile timeout
+    sc, scene = c2
+    q = lambda: GpuPlanner.make_query(sc.start, sc.goal, sc.env_x, sc.env_y, samples=200_000, seed=3)
+    auto = GpuPlanner(Robot(), path_optimality_threshold=-math.inf)
+    auto.set_scene(scene)
+    over = GpuPlanner(Robot(), path_optimality_threshold=-math.inf, helpers=1000)
+    over.set_scene(scene)
+    auto.plan(q()), over.plan(q())  # first-call allocation
+    ra, ro = auto.plan(q()), over.plan(q())
+    assert 0 < ro["helpers"] <= ra["helpers"], (ro["helpers"], ra["helpers"])
+    for k in ("iterations", "configs_checked", "nodes_start", "nodes_goal", "cost_best"):
+        assert ro[k] == ra[k], k
+    assert ro["time_total"] < 2.0 * ra["time_total"] + 0.01, (ro["time_total"], ra["time_total"])

@@ -202,3 +202,17 @@ def test_collision_listing_agrees_with_validity():
         assert m == sorted(m) and [pair_order[p] for p in s] == sorted(pair_order[p] for p in s)
         listed += bool(s) + bool(m)
     assert listed > 50
+
+
+def test_openmp_scans_plan_the_same_trees(orobot):
+    """The all-core CPU baseline (OpenMP scans as BS:4092 / BS:4283) plans exactly what the sequential oracle plans."""
+    sc = scenes.box_room()
+    orc = O.Oracle(orobot, O.OracleScene(sc.keys, sc.res))
+    kw = dict(env_x=sc.env_x, env_y=sc.env_y, seed=5, max_iter=400, opt_thresh=-math.inf)
+    a = orc.plan(sc.start, sc.goal, threads=1, **kw)
+    b = orc.plan(sc.start, sc.goal, threads=4, **kw)
+    for k in ("iterations", "checked", "valid", "n_start", "n_goal", "conn_a", "conn_b"):
+        assert a[k] == b[k], k
+    assert a["cost"] == b["cost"]
+    assert np.array_equal(a["start_parent"], b["start_parent"]) and np.array_equal(a["goal_conf"], b["goal_conf"])
+    assert np.array_equal(a["path"], b["path"])
