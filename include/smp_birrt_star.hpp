@@ -7,8 +7,16 @@
 // the goal search's IK controller run in the HIP kernels of libsmp_gpu.so.
 //
 // Build: include this header instead of <birrt_star_algorithm/birrt_star.h> and link -lsmp_gpu.
-// Configuration (environment, read by initialize()):
-//   SMP_ROBOT_MODEL  robot model JSON (default SMP_DEFAULT_ROBOT_MODEL, i.e. data/robotino_model.json)
+// Robot model: as the reference (birrt_star.cpp:36-73, collision_checker.hpp:176-393) initialize() builds it from the
+// robot description -- the URDF and SRDF text the node's ~robot_description / robot_description_semantic parameters
+// hold after createPlanningDescription (squirrel_8dof_planner.cpp:1744-1767) -- through smp_robot_create_urdf:
+//   * built with SMP_WITH_ROS: read from the ROS parameter server, like MoveIt's RobotModelLoader in the reference;
+//   * else given by setRobotDescription(urdf, srdf) before initialize(), or read from the files SMP_ROBOT_URDF /
+//     SMP_ROBOT_SRDF (environment);
+//   * the sphere covers of the mesh links come from SMP_ROBOT_SPHERES (default SMP_DEFAULT_ROBOT_SPHERES,
+//     data/robotino_spheres.json); the URDF's box / cylinder links are collided exactly.
+//   Without any description, SMP_ROBOT_MODEL (default SMP_DEFAULT_ROBOT_MODEL) names a prebuilt model JSON.
+// Other configuration (environment, read by initialize()):
 //   SMP_DEVICE       GPU ordinal (default 0)
 //   SMP_SEED         planner seed (default 1); the seed advances by one per run_planner call
 // Reference behaviour kept: init_planner returns false for a dimension mismatch or a colliding start/goal
@@ -32,6 +40,12 @@
 #ifndef SMP_DEFAULT_ROBOT_MODEL
 #define SMP_DEFAULT_ROBOT_MODEL "squirrel_motion_planner_amd/data/robotino_model.json"
 #endif
+#ifndef SMP_DEFAULT_ROBOT_SPHERES
+#define SMP_DEFAULT_ROBOT_SPHERES "squirrel_motion_planner_amd/data/robotino_spheres.json"
+#endif
+#ifdef SMP_WITH_ROS
+#include <ros/ros.h>
+#endif
 
 namespace birrt_star_motion_planning {
 
@@ -44,14 +58,37 @@ class BiRRTstarPlanner {
   BiRRTstarPlanner(const BiRRTstarPlanner&) = delete;
   BiRRTstarPlanner& operator=(const BiRRTstarPlanner&) = delete;
 
+  // The robot description initialize() builds the model from (URDF and SRDF text), when not read from ROS.
+  void setRobotDescription(const string& urdf, const string& srdf) {
+    urdf_ = urdf;
+    srdf_ = srdf;
+  }
+
   // birrt_star.cpp:11-326 (planning group "robotino_robot"): robot model + device planner.
   void initialize(string planning_group) {
     (void)planning_group;
     release();
-    const char* model = std::getenv("SMP_ROBOT_MODEL");
-    std::string path = model ? model : SMP_DEFAULT_ROBOT_MODEL;
-    std::string text = read_file(path);
-    check(smp_robot_create_json(text.c_str(), &robot_), "smp_robot_create_json(" + path + ")");
+#ifdef SMP_WITH_ROS
+    if (urdf_.empty()) {  // the reference's RobotModelLoader reads these two parameters (birrt_star.cpp:36-41)
+      ros::NodeHandle nh;
+      nh.getParam("robot_description", urdf_);
+      nh.getParam("robot_description_semantic", srdf_);
+    }
+#endif
+    if (urdf_.empty() && std::getenv("SMP_ROBOT_URDF")) {
+      urdf_ = read_file(std::getenv("SMP_ROBOT_URDF"));
+      srdf_ = read_file(std::getenv("SMP_ROBOT_SRDF") ? std::getenv("SMP_ROBOT_SRDF") : "");
+    }
+    if (!urdf_.empty()) {
+      const char* sp = std::getenv("SMP_ROBOT_SPHERES");
+      const std::string spheres = read_file(sp ? sp : SMP_DEFAULT_ROBOT_SPHERES);
+      check(smp_robot_create_urdf(urdf_.c_str(), srdf_.c_str(), spheres.c_str(), &robot_), "smp_robot_create_urdf");
+    } else {
+      const char* model = std::getenv("SMP_ROBOT_MODEL");
+      std::string path = model ? model : SMP_DEFAULT_ROBOT_MODEL;
+      std::string text = read_file(path);
+      check(smp_robot_create_json(text.c_str(), &robot_), "smp_robot_create_json(" + path + ")");
+    }
     const char* dev = std::getenv("SMP_DEVICE");
     const char* seed = std::getenv("SMP_SEED");
     seed_ = seed ? std::strtoull(seed, nullptr, 10) : 1;
@@ -310,6 +347,7 @@ class BiRRTstarPlanner {
   }
 
   smp_robot* robot_ = nullptr;
+  string urdf_, srdf_;
   smp_planner* planner_ = nullptr;
   smp_params params_;
   smp_stats stats_{};

@@ -10,6 +10,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SMP_LIB") or os.path.join(HERE, "lib", "libsmp_gpu.so")  # SMP_LIB: experiment builds
 MODEL_JSON = os.path.join(HERE, "data", "robotino_model.json")
+SPHERES_JSON = os.path.join(HERE, "data", "robotino_spheres.json")
 
 SMP_OK = 0
 SMP_ERR_ARG = -1
@@ -128,6 +129,8 @@ PROBES = [
     ("smp_probe_near", _i, [_i, _pd, _pd, _i, _pd, _p, _i, ctypes.c_double, _i, _p, _p, _p, _p,
                             ctypes.POINTER(ctypes.c_uint64), _pd]),
     ("smp_probe_check_latency", _i, [_p, _pd, _i64, _i, _i, _i, _i, _pd, ctypes.POINTER(ctypes.c_uint64), _pd]),
+    ("smp_probe_robot_dev", _i64, [_p, _p, _i64]),
+    ("smp_probe_scene_slabs", _i64, [_p, _p, _p, _i64]),
 ]
 
 _lib = None

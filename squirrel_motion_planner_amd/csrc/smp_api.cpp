@@ -1240,6 +1240,26 @@ extern "C" int64_t smp_get_tree(smp_planner* p, int which, int32_t* parent, doub
 }
 
 // ------------------------------------------------------------------------------------------ parity probes
+// The per-primitive slab fields a planner would build for this robot and scene (n_prim x ny x nx), host only.
+extern "C" int64_t smp_probe_scene_slabs(const smp_robot* r, const smp_scene* s, uint16_t* out, int64_t cap) {
+  if (!r || !s) return SMP_ERR_ARG;
+  std::vector<std::vector<uint16_t>> slabs;
+  prim_slabs(r->h.dev, s->h, &slabs);
+  int64_t n = 0;
+  for (auto& v : slabs) {
+    if (out && n + (int64_t)v.size() <= cap) std::memcpy(out + n, v.data(), v.size() * sizeof(uint16_t));
+    n += (int64_t)v.size();
+  }
+  return n;
+}
+
+// The device model of a robot (tests: the URDF + SRDF path and the JSON path give the same bytes).  Host only.
+extern "C" int64_t smp_probe_robot_dev(const smp_robot* r, void* out, int64_t cap) {
+  if (!r) return SMP_ERR_ARG;
+  if (out && cap >= (int64_t)sizeof(RobotDev)) std::memcpy(out, &r->h.dev, sizeof(RobotDev));
+  return (int64_t)sizeof(RobotDev);
+}
+
 // Device evaluations of the shared arithmetic (tests only): portable sin/cos, the Philox draw, body FK,
 // end-effector z and the fp64 sqrt / division used throughout.
 extern "C" int smp_probe_sincos(int device, const double* x, int n, double* s, double* c) {

@@ -25,7 +25,12 @@ static void copy3(const json::Value& v, double* o, int n = 3) {
 
 // Robot model JSON (tools/gen_robot_model.py).  Mirrors KDLRobotModel + CollisionChecker construction.
 void robot_from_json(const std::string& text, RobotHost* out) {
-  json::Value m = json::parse(text.c_str());
+  const json::Value m = json::parse(text.c_str());
+  robot_from_model_value(m, out);
+}
+
+// The model's key / value form -> RobotDev (shared by the JSON path and the URDF + SRDF path, smp_urdf.cpp).
+void robot_from_model_value(const json::Value& m, RobotHost* out) {
   RobotDev& d = out->dev;
   std::memset(&d, 0, sizeof(d));
   d.root_z = m["root_z"].d();

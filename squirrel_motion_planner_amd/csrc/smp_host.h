@@ -25,7 +25,9 @@ struct SceneHost {
   double bbox_min[3] = {0, 0, 0}, bbox_max[3] = {0, 0, 0};  // metric bbox of the occupied keys (octree frame)
 };
 
+namespace json { struct Value; }
 // Throws std::runtime_error on malformed input.
+void robot_from_model_value(const json::Value& m, RobotHost* out);
 void robot_from_json(const std::string& text, RobotHost* out);
 void robot_from_urdf(const std::string& urdf, const std::string& srdf, const std::string& spheres_json, RobotHost* out);
 

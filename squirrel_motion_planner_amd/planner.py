@@ -26,14 +26,36 @@ def default_params(**kw):
 
 
 class Robot:
-    """Robot model (KDL chain + sphere collision model) from the committed model JSON."""
+    """Robot model (KDL chain + collision model): from the committed model JSON, or (from_urdf) from the robot
+    description the node holds -- URDF and SRDF text plus the sphere covers of the mesh links."""
 
-    def __init__(self, model_json=L.MODEL_JSON):
+    def __init__(self, model_json=L.MODEL_JSON, _handle=None):
+        if _handle is not None:
+            self.h = _handle
+            return
         with open(model_json, "rb") as f:
             text = f.read()
         h = ctypes.c_void_p()
         check(lib().smp_robot_create_json(text, ctypes.byref(h)), "smp_robot_create_json")
         self.h = h
+
+    @classmethod
+    def from_urdf(cls, urdf, srdf, spheres=None):
+        """smp_robot_create_urdf: KDLRobotModel + CollisionChecker construction from the description text
+        (birrt_star.cpp:36-73, collision_checker.hpp:176-393)."""
+        if spheres is None:
+            spheres = open(L.SPHERES_JSON).read()
+        enc = lambda t: t.encode() if isinstance(t, str) else bytes(t)
+        h = ctypes.c_void_p()
+        check(lib().smp_robot_create_urdf(enc(urdf), enc(srdf), enc(spheres), ctypes.byref(h)), "smp_robot_create_urdf")
+        return cls(_handle=h)
+
+    def device_bytes(self):
+        """The device model (RobotDev) as bytes -- for comparing construction paths."""
+        n = lib().smp_probe_robot_dev(self.h, None, 0)
+        b = ctypes.create_string_buffer(n)
+        lib().smp_probe_robot_dev(self.h, b, n)
+        return b.raw
 
     @property
     def link_names(self):

@@ -1,7 +1,10 @@
 // Replays squirrel_8dof_planner.cpp's planner call sequence (SP:16, 482, 872-915, 1221-1248) through the C++
 // drop-in shim include/smp_birrt_star.hpp, the way the ROS node would after swapping the include.
 //
-//   shim_plan <robot_model.json> <scene.bt> <iterations> <seed> <start x8> <goal x8> <env_x0 env_x1 env_y0 env_y1>
+//   shim_plan <robot.urdf> <scene.bt> <iterations> <seed> <start x8> <goal x8> <env_x0 env_x1 env_y0 env_y1>
+//
+// The robot description is the URDF given and the SRDF beside it (same name, .srdf), handed to the planner as the node
+// holds them (robot_description / robot_description_semantic); a .json argument names a prebuilt model instead.
 //
 // Prints "status <0|1>" and the trajectory rows; exit 0 on success, 2 on usage error, 3 when no GPU is usable
 // (the shim throws: there is no CPU fallback).
@@ -29,14 +32,23 @@ int main(int argc, char** argv) {
     std::fprintf(stderr, "usage: shim_plan model.json scene.bt iterations seed start[8] goal[8] env[4]\n");
     return 2;
   }
-  setenv("SMP_ROBOT_MODEL", argv[1], 1);
+  const std::string robot = argv[1];
   setenv("SMP_SEED", argv[4], 1);
+  birrt_star_motion_planning::BiRRTstarPlanner planner;
+  if (robot.size() > 5 && robot.compare(robot.size() - 5, 5, ".urdf") == 0) {
+    auto slurp = [](const std::string& p) {
+      std::ifstream in(p, std::ios::binary);
+      return std::string(std::istreambuf_iterator<char>(in), std::istreambuf_iterator<char>());
+    };
+    planner.setRobotDescription(slurp(robot), slurp(robot.substr(0, robot.size() - 5) + ".srdf"));
+  } else {
+    setenv("SMP_ROBOT_MODEL", argv[1], 1);
+  }
   std::ifstream f(argv[2], std::ios::binary);
   BtFileTree tree{std::string(std::istreambuf_iterator<char>(f), std::istreambuf_iterator<char>()), 0.05};
   std::vector<double> start(8), goal(8);
   for (int j = 0; j < 8; ++j) { start[j] = std::atof(argv[5 + j]); goal[j] = std::atof(argv[13 + j]); }
   std::vector<double> ex = {std::atof(argv[21]), std::atof(argv[22])}, ey = {std::atof(argv[23]), std::atof(argv[24])};
-  birrt_star_motion_planning::BiRRTstarPlanner planner;
   try {
     planner.initialize("robotino_robot");                        // SP:16
   } catch (const std::exception& e) {

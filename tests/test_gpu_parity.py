@@ -453,3 +453,28 @@ def test_check_sequence_fold_keyframes(gp, orobot):
     assert want[:len(good[0])].all() and not want[len(good[0])]
     assert gp.check_sequence(seq) == len(good[0])
     assert gp.check_sequence(np.zeros((0, 8))) == -1
+
+
+# ------------------------------------------------------------------------------------------ C1 as SURVEY specifies it
+def test_c1_survey_start_is_in_self_collision(gp, orobot):
+    """SURVEY C1's start -- the first tuw folding keyframe -- puts the fingers inside the front shell's exact box
+    (robotino_plan.urdf:323-329; the finger meshes of squirrel-hand.dae enter it too, tools/gen_robot_model.py
+    validate): init_planner refuses it (birrt_star.cpp:353-357) on the GPU and in the oracle alike, with the same
+    collision listing.  The planning C1 cases start from pose_folded_arm instead (scenes.empty_room)."""
+    sc = scenes.empty_room(stowed=True)
+    gs = Scene.from_keys(sc.keys, sc.res)
+    gp.set_scene(gs)
+    gp.set_disabled_map_links([])
+    orc = O.Oracle(orobot, O.OracleScene(sc.keys, sc.res))
+    o = orc.plan(sc.start, sc.goal, env_x=sc.env_x, env_y=sc.env_y, max_iter=100, seed=1)
+    assert o["status"] == -2
+    r = gp.plan(GpuPlanner.make_query(sc.start, sc.goal, sc.env_x, sc.env_y, iterations=100, seed=1))
+    assert r["status"] == L.SMP_ERR_START_INVALID
+    pairs, links = gp.get_collisions(sc.start)
+    assert (pairs, links) == orc.collisions(sc.start)
+    assert all("shell_base_link_front" in p or "base_body_link" in p for p in pairs) and pairs
+    p = BiRRTstarPlanner()
+    p.initialize()
+    p.setOctree(sc.keys, resolution=sc.res)
+    assert not p.init_planner(sc.start, sc.goal, 1, True, True)
+    assert p.init_planner(sc.start, sc.goal, 1, False, True)  # without the self check the start is free

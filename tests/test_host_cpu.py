@@ -1,6 +1,7 @@
 """CPU tests of the product library's host side: ABI exports, scene builder vs the oracle, .bt decoding,
 and that compute entry points refuse to run without a GPU (no CPU fallback)."""
 import ctypes
+import json
 import os
 import re
 
@@ -106,3 +107,55 @@ def test_no_cpu_fallback_without_gpu():
     L.lib().smp_params_default(ctypes.byref(p))
     st = L.lib().smp_planner_create(0, r.h, ctypes.byref(p), ctypes.byref(h))
     assert st == L.SMP_ERR_NO_DEVICE
+
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _description():
+    return (open(os.path.join(GOLD, "robotino_plan.urdf")).read(), open(os.path.join(GOLD, "robotino_plan.srdf")).read())
+
+
+def test_urdf_path_builds_the_committed_model():
+    """smp_robot_create_urdf (C++ XML reader, KDL segment rules, float-cast limits, SRDF pairs, exact primitives, body
+    collapse) gives the device model of the committed JSON (tools/gen_robot_model.py, Python) byte for byte."""
+    urdf, srdf = _description()
+    a = Robot().device_bytes()
+    b = Robot.from_urdf(urdf, srdf).device_bytes()
+    assert len(a) == len(b) and a == b
+    assert Robot.from_urdf(urdf, srdf).link_names == Robot().link_names
+
+
+def test_urdf_path_errors():
+    urdf, srdf = _description()
+    bad = [(urdf[: len(urdf) // 2], srdf), ("<robot><link name='a'/></robot>", srdf), (urdf, "<robot/>"),
+           ("not xml", srdf), (urdf.replace('<box size="0.55 0.55 0.17"/>', '<box size="0.55 0.55"/>'), srdf)]
+    for u, s in bad:
+        h = ctypes.c_void_p()
+        assert L.lib().smp_robot_create_urdf(u.encode(), s.encode(), open(L.SPHERES_JSON, "rb").read(),
+                                             ctypes.byref(h)) == L.SMP_ERR_PARSE
+    h = ctypes.c_void_p()
+    spec = json.load(open(L.SPHERES_JSON))
+    spec["links"]["no_such_link"] = [[0, 0, 0, 0.1]]
+    assert L.lib().smp_robot_create_urdf(urdf.encode(), srdf.encode(), json.dumps(spec).encode(),
+                                         ctypes.byref(h)) == L.SMP_ERR_PARSE
+    # a box link given spheres in the spec is collided with those spheres instead of exactly
+    spec = json.load(open(L.SPHERES_JSON))
+    spec["links"]["kinect_link"] = [[0.0, 0.0, 0.0, 0.1]]
+    r = Robot.from_urdf(urdf, srdf, json.dumps(spec))
+    assert r.device_bytes() != Robot().device_bytes()
+
+
+@pytest.mark.parametrize("mk", [scenes.box_room, scenes.clutter_cloud])
+def test_primitive_slabs_match_oracle(mk, orobot):
+    """The per-primitive slab prefilter fields (C++ builder) equal the oracle's independent scipy construction."""
+    sc = mk()
+    s = Scene.from_keys(sc.keys, sc.res)
+    r = Robot()
+    n = L.lib().smp_probe_scene_slabs(r.h, s.h, None, 0)
+    got = np.zeros(n, np.uint16)
+    L.lib().smp_probe_scene_slabs(r.h, s.h, got.ctypes.data_as(ctypes.c_void_p), n)
+    orc = O.Oracle(orobot, O.OracleScene(sc.keys, sc.res))
+    want = orc.scene._slab
+    assert np.array_equal(got, want)
+    assert orobot.n_prim == 6 and (got < 65535).any()

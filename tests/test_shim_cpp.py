@@ -13,6 +13,7 @@ from squirrel_motion_planner_amd import scenes
 
 LIBDIR = os.path.join(ROOT, "squirrel_motion_planner_amd", "lib")
 MODEL = os.path.join(ROOT, "squirrel_motion_planner_amd", "data", "robotino_model.json")
+URDF = os.path.join(ROOT, "tests", "golden", "robotino_plan.urdf")  # the node's robot description (+ .srdf beside it)
 
 
 def build_shim(tmpdir):
@@ -44,7 +45,7 @@ def run_shim(exe, model, bt, sc, iters, seed):
 def test_shim_builds_and_fails_loudly_without_gpu(tmp_path):
     exe = build_shim(tmp_path)
     sc, bt = room3_case(tmp_path)
-    p = run_shim(exe, MODEL, bt, sc, 10, 1)
+    p = run_shim(exe, URDF, bt, sc, 10, 1)
     if p.returncode == 3:  # no GPU here: the shim throws, no CPU fallback
         assert "no usable GPU" in p.stdout or "NO_DEVICE" in p.stdout.upper(), p.stdout
     else:
@@ -56,7 +57,7 @@ def test_shim_node_sequence_matches_oracle(tmp_path):
     exe = build_shim(tmp_path)
     sc, bt = room3_case(tmp_path)
     iters, seed = 200, 5
-    p = run_shim(exe, MODEL, bt, sc, iters, seed)
+    p = run_shim(exe, URDF, bt, sc, iters, seed)  # initialize() builds the robot from the URDF + SRDF text
     assert p.returncode == 0, p.stdout + p.stderr
     lines = p.stdout.splitlines()
     assert lines[0] in ("status 0", "status 1")
