@@ -413,8 +413,14 @@ void floor_keys(double cx, double cy, double res, double distance, std::vector<u
 // Occupied leaf (depth, centre key) -> its depth-16 keys; a pruned leaf at depth d covers [k - h, k + h - 1],
 // h = 32768 >> d, on every axis.
 namespace {
+// Occupied voxels one stream may expand to (a pruned leaf at depth d stands for (2^(16-d))^3 of them): a corrupted or
+// hostile payload must not exhaust memory.  2^26 voxels is a 2 cm grid of 27 x 27 x 2 m fully occupied.
+size_t kMaxVoxels = (size_t)1 << 26;
+
 void emit_leaf(std::vector<uint16_t>* keys, int depth, int kx, int ky, int kz) {
   if (depth < 6) throw std::runtime_error("octomap: occupied leaf too coarse to expand");
+  const size_t side = depth >= 16 ? 1 : (size_t)2 * (KEY_OFFSET >> depth);
+  if (keys->size() / 3 + side * side * side > kMaxVoxels) throw std::runtime_error("octomap: too many occupied voxels");
   if (depth >= 16) {
     keys->push_back((uint16_t)kx); keys->push_back((uint16_t)ky); keys->push_back((uint16_t)kz);
     return;
@@ -519,6 +525,8 @@ const uint8_t* octomap_header(const uint8_t* data, size_t size, double* res, lon
   return p;
 }
 }  // namespace
+
+void set_max_octomap_voxels(size_t n) { kMaxVoxels = n; }
 
 void octomap_bt_keys(const uint8_t* data, size_t size, double* res, std::vector<uint16_t>* keys,
                      std::vector<FreeLeaf>* free, bool header) {

@@ -49,6 +49,8 @@ constexpr float kClampMinLogOdds = -2.000027830777221f;   // clamping_thres_min 
 // (expanded to depth 16) and, if `free` is given, the free leaves.  *res is read from the header.
 void octomap_bt_keys(const uint8_t* data, size_t size, double* res, std::vector<uint16_t>* keys,
                      std::vector<FreeLeaf>* free = nullptr, bool header = true);
+// Expansion limit of pruned occupied leaves per stream (default 2^26 voxels; the parser throws beyond it).
+void set_max_octomap_voxels(size_t n);
 // Octomap full stream (.ot file, or with header = false an octomap_msgs full payload), same outputs.
 void octomap_ot_keys(const uint8_t* data, size_t size, double* res, std::vector<uint16_t>* keys,
                      std::vector<FreeLeaf>* free = nullptr, bool header = true);

@@ -97,7 +97,8 @@ class XmlReader {
     }
     return o;
   }
-  XNode element() {
+  XNode element(int depth = 0) {
+    if (depth > 256) throw std::runtime_error("xml: elements nested too deeply");
     XNode n;
     ++p_;  // '<'
     n.tag = name();
@@ -137,7 +138,7 @@ class XmlReader {
         ++p_;
         return n;
       }
-      if (s_[p_] == '<') { n.kids.push_back(element()); continue; }
+      if (s_[p_] == '<') { n.kids.push_back(element(depth + 1)); continue; }
       ++p_;
     }
   }
@@ -358,7 +359,8 @@ void robot_from_urdf(const std::string& urdf_text, const std::string& srdf_text,
   std::vector<const Joint*> seq;
   for (std::string n = tip; n != base;) {
     auto it = by_child.find(n);
-    if (it == by_child.end()) throw std::runtime_error("urdf: chain tip does not lead to the base " + base);
+    if (it == by_child.end() || seq.size() > joints.size())
+      throw std::runtime_error("urdf: chain tip does not lead to the base " + base);
     seq.push_back(it->second);
     n = it->second->parent;
   }
@@ -411,6 +413,7 @@ void robot_from_urdf(const std::string& urdf_text, const std::string& srdf_text,
     const std::vector<std::string>& ch = children[top.name];
     if (top.next >= ch.size()) { stack.pop_back(); continue; }
     const std::string c = ch[top.next++];
+    if (index.count(c)) throw std::runtime_error("urdf: link " + c + " reached twice (the joints do not form a tree)");
     const Joint* j = by_child[c];
     TreeLink t;
     t.name = c;
