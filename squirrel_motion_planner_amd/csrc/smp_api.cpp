@@ -802,6 +802,10 @@ static QueryDev make_qdev(QueryBuffers& b, size_t cap, long long rows) {
   d.sampler = 0;
   d.trace = nullptr;
   d.ttff = nullptr;
+  // scans of trees of at least this many nodes are split over the helpers (DESIGN.md "Scans of large trees");
+  // SMP_SCAN_MIN overrides it (experiments and tests; 0: never)
+  d.scan_min = 12288;
+  if (const char* e = std::getenv("SMP_SCAN_MIN")) d.scan_min = std::max(0, std::atoi(e));
   return d;
 }
 

@@ -211,8 +211,32 @@ __global__ void sqrt_div_kernel(const double* a, const double* b, int n, double*
 }
 
 // ============================================================================================ planner
+// Distributed scans of large trees (DESIGN.md "Scans of large trees").  ScanLds: one workgroup's slice (the per-wave
+// lists of the near scan, the slice's merged lists, the nearest reduction); MergeLds: every participant's partial
+// result as the leader collects and merges them.
+constexpr int SCAN_K = 20;  // near-list ends a scan keeps (near_set<20>; max_near_nodes <= 20)
+struct ScanLds {
+  unsigned long long wlk[BLOCK / 64][SCAN_K], whk[BLOCK / 64][SCAN_K];
+  int wli[BLOCK / 64][SCAN_K], whi[BLOCK / 64][SCAN_K];
+  int wtot[BLOCK / 64];
+  unsigned long long blo, bhi;                       // near_batch's block bounds
+  unsigned long long lk[SCAN_K], hk[SCAN_K];        // the slice's lowest (ascending) / highest (descending) entries
+  int li[SCAN_K], hi[SCAN_K];
+  int cnt, take;
+  unsigned long long wk[BLOCK / 64];
+  int wi[BLOCK / 64];
+};
+struct MergeLds {
+  unsigned long long k[2][SCAN_P][SCAN_K];  // [0] lows ascending, [1] highs descending, per participant
+  int id[2][SCAN_P][SCAN_K];
+  int len[SCAN_P], cnt[SCAN_P], done[SCAN_P];
+  unsigned long long nk[SCAN_P];            // nearest: per participant (distance key, id)
+  int ni[SCAN_P];
+  int ndone, go[2], steal;
+};
 // LDS of job mode (leader and helper kernel): the published job + one job tile.
 struct JobLds {
+  ScanLds scan;                            // helper: its slice of a scan job
   TileLds<HELPER_CT> T;
   double tq[HELPER_CT][NJ];
   double start[MAXE][NJ], step[MAXE][NJ];  // the job's edges (needed edges of the batch, compacted)
@@ -249,6 +273,10 @@ struct PlanLds {
     JobLds job;  // job mode: the leader's LDS copy of its published job + one job tile
     double seg[MAXE][MAX_PTS][3];
     SmpLds smp;
+    struct {            // a distributed scan (never while a collision job holds u.job)
+      ScanLds s;
+      MergeLds m;
+    } sc;
   } u;
   // near_set scratch (outside the union: a near set may be computed while a collision job holds u.job)
   struct {  // near_set: per-wave sorted low / high ends of the near list
@@ -274,6 +302,7 @@ struct PlanLds {
   int tile_e[PLAN_CT], tile_i[PLAN_CT], tile_n;
   int count_slot;  // profiling: phase the checked configurations are attributed to
   int job_seq;     // last job published by this leader (this launch)
+  int in_job;      // a collision job is in flight (its helpers are busy): scans stay local
   int smp_ver, smp_have_sol, smp_hit;  // run-ahead sampler: published parameter version / snapshot, slot hit
   int smp_pub;                         // the version changed this iteration: publish the parameters
   int spec, spec_nn;                   // overlap_work: what was computed during the last collision job, its result
@@ -473,10 +502,17 @@ __device__ void insert_node(const Ctx& C, int t, const double* e_start, const do
 // sqrt is monotone, so a node can only beat the running minimum if its squared distance is below the minimum's
 // squared distance; the (correctly rounded) sqrt is taken only then and compared exactly as the reference does.
 __device__ bool spec_stage(const Ctx& C, int s, unsigned long long wait = 0);
+// Distributed scans (defined with the job protocol below): true if a scan of `nodes` nodes is split over the helpers.
+__device__ __forceinline__ bool scan_split(const Ctx& C, int nodes) {
+  return uni(C.Q.jb != nullptr && C.Q.scan_min > 0 && nodes >= C.Q.scan_min && C.Q.nworkers >= 8 && !g_L.in_job);
+}
+__device__ int nearest_dist(const Ctx& C, int t, const double* q, int i0, int n, double* d_out);
+__device__ void near_set_dist(const Ctx& C, int t, const double* q, int excl);
 // Block argmin of the nodes [i_begin, n) of tree t: the first strict minimum (d, id) of the distances, d = 10000
 // if none is below it.  All threads; result in (g_L.wd[0], g_L.wi[0]) via nearest_scan's return.
 __device__ int nearest_scan(const Ctx& C, int t, const double* q, int i_begin, double* d_out) {
   TR();
+  if (scan_split(C, uni(g_L.S.n[t]) - i_begin)) return nearest_dist(C, t, q, i_begin, uni(g_L.S.n[t]), d_out);
   const gcdptr tq = uni_gptr(C.Q.tr[t].q);
   const int n = uni(g_L.S.n[t]), cap = uni(g_L.S.cap);
   double qq[NJ];
@@ -618,9 +654,10 @@ __device__ __forceinline__ unsigned long long wave_shr1_u64(unsigned long long v
 // so a node whose key lies beyond another wave's K-th key cannot be among the block's K smallest (largest).
 template <int K>
 __device__ __forceinline__ void near_batch(bool near, unsigned long long key, int base, int lane,
-                                           unsigned long long& lk, int& li, unsigned long long& hk, int& hi) {
+                                           unsigned long long& lk, int& li, unsigned long long& hk, int& hi,
+                                           unsigned long long& blo_r, unsigned long long& bhi_r) {
   const int i = base + lane;
-  const unsigned long long blo = g_L.near_blo, bhi = g_L.near_bhi;
+  const unsigned long long blo = blo_r, bhi = bhi_r;
   {
     const unsigned long long tk = readlane_u64(lk, K - 1);
     const int ti = __builtin_amdgcn_readlane(li, K - 1);
@@ -639,7 +676,7 @@ __device__ __forceinline__ void near_batch(bool near, unsigned long long key, in
         }
       } while (m);
       const unsigned long long nk = readlane_u64(lk, K - 1);
-      if (lane == 0 && nk < blo && __builtin_amdgcn_readlane(li, K - 1) != 0x7fffffff) atomicMin(&g_L.near_blo, nk);
+      if (lane == 0 && nk < blo && __builtin_amdgcn_readlane(li, K - 1) != 0x7fffffff) atomicMin(&blo_r, nk);
     }
   }
   {
@@ -660,7 +697,7 @@ __device__ __forceinline__ void near_batch(bool near, unsigned long long key, in
         }
       } while (m);
       const unsigned long long nk = readlane_u64(hk, K - 1);
-      if (lane == 0 && nk > bhi && __builtin_amdgcn_readlane(hi, K - 1) != -1) atomicMax(&g_L.near_bhi, nk);
+      if (lane == 0 && nk > bhi && __builtin_amdgcn_readlane(hi, K - 1) != -1) atomicMax(&bhi_r, nk);
     }
   }
 }
@@ -730,7 +767,7 @@ __device__ __noinline__ void near_set_stream(const Ctx& C, int t, const double* 
       const int bb = base + b * BLOCK;
       if (bb < n) {
         wc += __popcll(__ballot(nr[b]));
-        near_batch<K>(nr[b], key[b], bb, lane, lk, li, hk, hi);
+        near_batch<K>(nr[b], key[b], bb, lane, lk, li, hk, hi, g_L.near_blo, g_L.near_bhi);
       }
     }
   }
@@ -782,6 +819,162 @@ __device__ __noinline__ void near_set_stream(const Ctx& C, int t, const double* 
     }
   }
   if (threadIdx.x == 0) { g_L.nk = tot; g_L.n_lo = take; g_L.n_hi = take; g_L.near_blo = KMAX; g_L.near_bhi = 0; }
+  __syncthreads();
+}
+
+// ------------------------------------------------------------------------------- slices of distributed scans
+// Nearest over the nodes [i0, i1): the first strict minimum as nearest_scan, reduced to (distance key, id) in X.wk[0],
+// X.wi[0] (key of 10000.0 and id INT_MAX if no node is below 10000).  All threads.
+__device__ void slice_nn(gcdptr tq, int cap, int i0, int i1, const double* q, ScanLds& X) {
+  double qq[NJ];
+  for (int j = 0; j < NJ; ++j) qq[j] = q[j];
+  double best = 10000.0, best_s = 1e300;
+  int bid = 0x7fffffff;
+  constexpr int NPT = 8;
+  for (int b0 = i0 + (int)threadIdx.x; b0 < i1; b0 += NPT * BLOCK) {
+    double a[NPT][NJ];
+#pragma unroll
+    for (int u = 0; u < NPT; ++u) {
+      const int i = b0 + u * BLOCK;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) a[u][j] = i < i1 ? (tq + (size_t)j * cap)[(unsigned)i] : 0.0;
+    }
+    double s[NPT];
+#pragma unroll
+    for (int u = 0; u < NPT; ++u) s[u] = 0.0;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+#pragma unroll
+      for (int u = 0; u < NPT; ++u) {
+        const double d = qq[j] - a[u][j];
+        s[u] += d * d;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < NPT; ++u) {
+      const int i = b0 + u * BLOCK;
+      if (i < i1 && s[u] < best_s) {
+        const double dist = sqrt(s[u]);
+        if (dist < best) { best = dist; bid = i; best_s = s[u]; }
+      }
+    }
+  }
+  const unsigned long long key = (unsigned long long)__double_as_longlong(best);
+  const unsigned long long wk = __ockl_wfred_min_u64(key);
+  const int wi = __ockl_wfred_min_i32(key == wk ? bid : 0x7fffffff);
+  if (lane_id() == 0) { X.wk[wave_id()] = wk; X.wi[wave_id()] = wi; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long bk = X.wk[0];
+    int bi = X.wi[0];
+    for (int w = 1; w < BLOCK / 64; ++w)
+      if (X.wk[w] < bk || (X.wk[w] == bk && X.wi[w] < bi)) { bk = X.wk[w]; bi = X.wi[w]; }
+    X.wk[0] = bk;
+    X.wi[0] = bi;
+  }
+  __syncthreads();
+}
+
+// Near set over the nodes [i0, i1) (find_near_vertices_interpolation's radius test, excluding `excl`): count X.cnt,
+// its SCAN_K lowest (cost, id) entries ascending in X.lk / X.li and SCAN_K highest descending in X.hk / X.hi (X.take
+// each).  near_set_stream's per-wave lists and rank merge over a range.  All threads.
+__device__ __noinline__ void slice_near(gcdptr tq, gcdptr tc, int cap, int i0, int i1, const double* q, int excl,
+                                        double r, ScanLds& X) {
+  constexpr int K = SCAN_K, NW = BLOCK / 64, NB = 4;
+  const double r2 = r * r, r2lo = r2 * (1.0 - 1e-12), r2hi = r2 * (1.0 + 1e-12);
+  const int lane = lane_id(), wave = wave_id();
+  double qq[NJ];
+  for (int j = 0; j < NJ; ++j) qq[j] = q[j];
+  const unsigned long long KMAX = ~0ull;
+  if (threadIdx.x == 0) { X.blo = KMAX; X.bhi = 0; }
+  __syncthreads();
+  unsigned long long lk = KMAX, hk = 0;
+  int li = 0x7fffffff, hi = -1;
+  int wc = 0;
+  for (int base = i0 + wave * 64; base < i1; base += NB * BLOCK) {
+    double x[NB][NJ];
+    unsigned long long key[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const int i = base + b * BLOCK + lane;
+      const bool v = i < i1;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) x[b][j] = v ? (tq + (size_t)j * cap)[(unsigned)i] : 0.0;
+      key[b] = v ? (unsigned long long)__double_as_longlong(tc[(unsigned)i]) : 0ull;
+    }
+    bool nr[NB], amb[NB];
+    bool any_amb = false;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const int i = base + b * BLOCK + lane;
+      double sb = 0.0;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        double d = qq[j] - x[b][j];
+        sb += d * d;
+      }
+      nr[b] = near_radius(i < i1 && i != excl, sb, r, r2lo, r2hi, amb[b]);
+      x[b][0] = sb;
+      any_amb |= amb[b];
+    }
+    if (__ballot(any_amb)) {
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+        if (amb[b]) nr[b] = sqrt(x[b][0]) < r;
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const int bb = base + b * BLOCK;
+      if (bb < i1) {
+        wc += __popcll(__ballot(nr[b]));
+        near_batch<K>(nr[b], key[b], bb, lane, lk, li, hk, hi, X.blo, X.bhi);
+      }
+    }
+  }
+  if (lane < K) {
+    X.wlk[wave][lane] = lk; X.wli[wave][lane] = li;
+    X.whk[wave][lane] = hk; X.whi[wave][lane] = hi;
+  }
+  if (lane == 0) X.wtot[wave] = wc;
+  __syncthreads();
+  int tot = 0;
+  for (int w = 0; w < NW; ++w) tot += X.wtot[w];
+  const int take = min(K, tot);
+  static_assert(NW * K <= 256, "rank merge thread map");
+  const int hsel = threadIdx.x >= 256;
+  const int e = threadIdx.x - hsel * 256;
+  if (e < NW * K) {
+    const int w = e / K, k = e - w * K;
+    const unsigned long long ck = hsel ? X.whk[w][k] : X.wlk[w][k];
+    const int ci = hsel ? X.whi[w][k] : X.wli[w][k];
+    if (ci != (hsel ? -1 : 0x7fffffff)) {
+      int lo[NW];
+#pragma unroll
+      for (int o = 0; o < NW; ++o) lo[o] = 0;
+#pragma unroll
+      for (int step = 16; step > 0; step >>= 1) {
+#pragma unroll
+        for (int o = 0; o < NW; ++o) {
+          const int m = lo[o] + step - 1;
+          if (m < K) {
+            const unsigned long long ok = hsel ? X.whk[o][m] : X.wlk[o][m];
+            const int oi = hsel ? X.whi[o][m] : X.wli[o][m];
+            const bool ahead = hsel ? ki_less(ck, ci, ok, oi) : ki_less(ok, oi, ck, ci);
+            if (ahead) lo[o] += step;
+          }
+        }
+      }
+      int rank = k;
+#pragma unroll
+      for (int o = 0; o < NW; ++o)
+        if (o != w) rank += lo[o];
+      if (rank < take) {
+        if (!hsel) { X.lk[rank] = ck; X.li[rank] = ci; }
+        else { X.hk[rank] = ck; X.hi[rank] = ci; }
+      }
+    }
+  }
+  if (threadIdx.x == 0) { X.cnt = tot; X.take = take; }
   __syncthreads();
 }
 
@@ -862,6 +1055,11 @@ __device__ void near_set(const Ctx& C, int t, const double* q, int excl, bool sp
         return;
       }
     }
+  }
+  if (K == SCAN_K && scan_split(C, n)) {
+    near_set_dist(C, t, q, excl);
+    TR();
+    return;
   }
   double qq[NJ];
   for (int j = 0; j < NJ; ++j) qq[j] = q[j];
@@ -1258,7 +1456,10 @@ __device__ __forceinline__ void edge_validity_job(const Ctx& C, int E, int pslot
   PROF_BEGIN();
   if (threadIdx.x == 0) { g_L.S.prof[P_TFK] += _pt - tj0; g_L.S.prof[P_TTEST]++; }  // job publication
   TR();
+  if (threadIdx.x == 0) g_L.in_job = 1;  // the helpers are on this job's tiles: overlap scans stay local
+  __syncthreads();
   overlap_work(C, ov, ovt);
+  if (threadIdx.x == 0) g_L.in_job = 0;
   TR();
   // the leader's own tiles
   for (int t = W - 1; t < nt; t += W) {
@@ -1343,6 +1544,301 @@ __device__ __forceinline__ void edge_validity_job(const Ctx& C, int E, int pslot
   __syncthreads();
 }
 
+// --------------------------------------------------------------------------------------- distributed scans
+// A nearest or near scan of a large tree (scan_split: at least QueryDev::scan_min nodes, eight or more workers, no
+// collision job in flight) is split into P = min(workers, SCAN_P) slices of equal size: the workgroup publishes a scan
+// job (header + the query configuration, range, excluded id and radius: 33 payload words, within the helpers' first
+// poll), scans slice 0 itself, and collects the helpers' partial results (data-tagged granules of JobBoard::sres).
+// A slice whose result does not arrive within 20 us of the last progress is scanned here (a duplicate is identical).
+// The merge is exact: nearest takes the (distance, id) minimum of the slices -- the slices partition the range, and
+// each slice's answer is its first strict minimum; the near lists take every entry whose rank over all slices' lists
+// is below SCAN_K (an entry beyond a slice's K-th cannot rank below K: K entries are ahead of it).
+constexpr unsigned SCAN_HDR = 1u | 1u << 18;  // edge-count field 1 (33 payload words), scan job bit
+constexpr unsigned long long SCAN_WAIT = 2000;  // device-clock ticks (20 us) without progress before stealing a slice
+
+__device__ __forceinline__ void scan_range(int i0, int n, int P, int w, int* lo, int* hi) {
+  int chunk = (n - i0 + P - 1) / P;
+  chunk = (chunk + 63) & ~63;
+  *lo = min(n, i0 + w * chunk);
+  *hi = min(n, *lo + chunk);
+}
+
+// Publishes scan job `seq` (all threads).
+__device__ void scan_publish(const Ctx& C, int seq, int near, int t, const double* q, int i0, int n, int excl, double r,
+                             int P) {
+  JobBoard* jb = C.Q.jb;
+  const int i = threadIdx.x;
+  if (i < 33) {
+    unsigned w = 0;
+    if (i == 0) {
+      w = SCAN_HDR | (unsigned)near << 19 | (unsigned)t << 20;
+    } else if (i <= 16) {
+      const unsigned long long b = (unsigned long long)__double_as_longlong(q[(i - 1) >> 1]);
+      w = ((i - 1) & 1) ? (unsigned)(b >> 32) : (unsigned)b;
+    } else if (i == 17) {
+      w = (unsigned)i0;
+    } else if (i == 18) {
+      w = (unsigned)n;
+    } else if (i == 19) {
+      w = (unsigned)excl;
+    } else if (i == 20 || i == 21) {
+      const unsigned long long b = (unsigned long long)__double_as_longlong(r);
+      w = i == 21 ? (unsigned)(b >> 32) : (unsigned)b;
+    } else if (i == 22) {
+      w = (unsigned)P;
+    }
+    st_agent(&jb->pay[i], granule(seq, w));
+  }
+}
+
+// Participant w's slice of a scan, its result as granules of sres[w] (helper) or into the merge area (workgroup).
+__device__ void scan_slice(const Ctx& C, int near, int t, const double* q, int i0, int n, int excl, double r, int P, int w,
+                           ScanLds& X) {
+  const gcdptr tq = uni_gptr(C.Q.tr[t].q), tc = uni_gptr(C.Q.tr[t].cost);
+  const int cap = uni(__hip_atomic_load(&C.Q.st->cap, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  int lo, hi;
+  scan_range(i0, n, P, w, &lo, &hi);
+  if (near) slice_near(tq, tc, cap, lo, hi, q, excl, r, X);
+  else slice_nn(tq, cap, lo, hi, q, X);
+}
+
+// Helper side of a scan job already in J.words (seq): its slice, then the result granules.
+__device__ void scan_helper(const Ctx& C, JobLds& J, int w, int seq) {
+  const unsigned hdr = J.words[0];
+  const int near = (hdr >> 19) & 1, t = (hdr >> 20) & 1;
+  double q[NJ];
+  for (int j = 0; j < NJ; ++j) q[j] = __hiloint2double((int)J.words[2 + 2 * j], (int)J.words[1 + 2 * j]);
+  const int i0 = (int)J.words[17], n = (int)J.words[18], excl = (int)J.words[19], P = (int)J.words[22];
+  const double r = __hiloint2double((int)J.words[21], (int)J.words[20]);
+  if (w >= P) return;
+  // tree words stored by the leader since this CU last cached them: drop stale copies (consumer form: one acquire,
+  // its wait, a barrier, then plain loads)
+  if (threadIdx.x < 64) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    drain();
+  }
+  __syncthreads();
+  ScanLds& X = J.scan;
+  scan_slice(C, near, t, q, i0, n, excl, r, P, w, X);
+  unsigned long long* out = C.Q.jb->sres[w];
+  if (!near) {
+    if (threadIdx.x == 0) {
+      st_agent(&out[0], granule(seq, (unsigned)X.wk[0]));
+      st_agent(&out[1], granule(seq, (unsigned)(X.wk[0] >> 32)));
+      st_agent(&out[2], granule(seq, (unsigned)X.wi[0]));
+    }
+  } else {
+    const int take = X.take;
+    const int i = threadIdx.x;
+    if (i == 0) st_agent(&out[0], granule(seq, (unsigned)X.cnt));
+    if (i == 1) st_agent(&out[1], granule(seq, (unsigned)take | (unsigned)take << 16));
+    if (i < 6 * take) {
+      const int side = i >= 3 * take, e = (i - side * 3 * take) / 3, f = i - side * 3 * take - 3 * e;
+      const unsigned long long k = side ? X.hk[e] : X.lk[e];
+      const int id = side ? X.hi[e] : X.li[e];
+      const unsigned v = f == 0 ? (unsigned)k : f == 1 ? (unsigned)(k >> 32) : (unsigned)id;
+      st_agent(&out[2 + i], granule(seq, v));
+    }
+  }
+  __syncthreads();
+}
+
+// Slot w of the merge area from a slice result in X (all threads).
+__device__ __forceinline__ void merge_put(MergeLds& M, const ScanLds& X, int near, int w) {
+  if (!near) {
+    if (threadIdx.x == 0) { M.nk[w] = X.wk[0]; M.ni[w] = X.wi[0]; }
+  } else {
+    const int take = X.take;
+    if (threadIdx.x < SCAN_K) {
+      const int e = threadIdx.x;
+      if (e < take) {
+        M.k[0][w][e] = X.lk[e]; M.id[0][w][e] = X.li[e];
+        M.k[1][w][e] = X.hk[e]; M.id[1][w][e] = X.hi[e];
+      }
+    }
+    if (threadIdx.x == 0) { M.len[w] = take; M.cnt[w] = X.cnt; }
+  }
+  if (threadIdx.x == 0) M.done[w] = 1;
+}
+
+// Publishes a scan of [i0, n), scans slice 0, collects (or steals) the other slices into g_L.u.sc.m.  All threads.
+__device__ void scan_run(const Ctx& C, int near, int t, const double* q, int i0, int n, int excl, double r) {
+  MergeLds& M = g_L.u.sc.m;
+  ScanLds& X = g_L.u.sc.s;
+  const int P = uni(min(C.Q.nworkers, SCAN_P));
+  __syncthreads();
+  const int seq = uni(g_L.job_seq) + 1;
+  if (threadIdx.x < SCAN_P) M.done[threadIdx.x] = 0;
+  __syncthreads();
+  if (threadIdx.x == 0) { g_L.job_seq = seq; M.ndone = 0; }
+  // the helpers read the tree through their own CUs and XCDs: the tree stores (this workgroup's, or the leader's on
+  // this XCD for a scout) are written back before the job is published (MI355X_MICROARCH.md producer form)
+  drain();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    drain();
+  }
+  __syncthreads();
+  scan_publish(C, seq, near, t, q, i0, n, excl, r, P);
+  scan_slice(C, near, t, q, i0, n, excl, r, P, 0, X);
+  merge_put(M, X, near, 0);
+  __syncthreads();
+  const JobBoard* jb = C.Q.jb;
+  unsigned long long t_prog = wall_clock64();
+  const unsigned long long t_start = t_prog;
+  int last_done = 0;
+  for (int k = 0;; k ^= 1) {
+    // wave v reads participants 1 + v, 1 + v + 8, ...: every granule of a result must carry this job's number
+    const int lane = lane_id();
+    for (int w = 1 + wave_id(); w < P; w += BLOCK / 64) {
+      if (M.done[w]) continue;
+      const unsigned long long* g = jb->sres[w];
+      if (!near) {
+        const unsigned long long v = lane < 3 ? ld_agent(&g[lane]) : 0ull;
+        const bool ok = !__ballot(lane < 3 && (int)(v >> 32) != seq);
+        const unsigned v0 = __shfl((unsigned)v, 0), v1 = __shfl((unsigned)v, 1), v2 = __shfl((unsigned)v, 2);
+        if (ok && lane == 0) {
+          M.nk[w] = (unsigned long long)v1 << 32 | v0;
+          M.ni[w] = (int)v2;
+          M.done[w] = 1;
+          atomicAdd(&M.ndone, 1);
+        }
+      } else {
+        const unsigned long long h = lane < 2 ? ld_agent(&g[lane]) : 0ull;
+        if (__ballot(lane < 2 && (int)(h >> 32) != seq)) continue;
+        const unsigned cnt = __shfl((unsigned)h, 0), tk = __shfl((unsigned)h, 1) & 0xffff;
+        const int take = (int)min(tk, (unsigned)SCAN_K);
+        bool ok = true;
+        unsigned vv[2] = {0, 0};
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int i = lane + 64 * u;
+          if (i < 6 * take) {
+            const unsigned long long v = ld_agent(&g[2 + i]);
+            ok &= (int)(v >> 32) == seq;
+            vv[u] = (unsigned)v;
+          }
+        }
+        if (__ballot(!ok)) continue;
+        // entry e of side s: granules 3e .. 3e + 2 of the side's block; granule i sits in lane i % 64 of vv[i / 64].
+        // Every lane takes part in the shuffles (uniform control flow), lanes < 2 * take keep an entry.
+        const int sd = lane >= take ? 1 : 0, e = lane - sd * take;
+        const int g0 = lane < 2 * take ? sd * 3 * take + 3 * e : 0;
+        auto fetch = [&](int gi) {
+          const unsigned a = __shfl(vv[0], gi & 63), b = __shfl(vv[1], gi & 63);
+          return gi < 64 ? a : b;
+        };
+        const unsigned klo = fetch(g0), khi = fetch(g0 + 1), idv = fetch(g0 + 2);
+        if (lane < 2 * take) {
+          M.k[sd][w][e] = (unsigned long long)khi << 32 | klo;
+          M.id[sd][w][e] = (int)idv;
+        }
+        if (lane == 0) {
+          M.len[w] = take;
+          M.cnt[w] = (int)cnt;
+          M.done[w] = 1;
+          atomicAdd(&M.ndone, 1);
+        }
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned long long now = wall_clock64();
+      const int nd = M.ndone;
+      if (nd != last_done) { last_done = nd; t_prog = now; }
+      int st = nd >= P - 1 ? 1 : (now - t_prog > SCAN_WAIT ? 2 : 0);
+      if (st != 1 && now - t_start > 200000000ull) {  // 2 s: never hang (the slices are then scanned here)
+        g_L.S.status = -5;
+        g_L.S.phase = 2;
+        st = 2;
+      }
+      if (st == 2) {
+        int w = 1;
+        while (w < P && M.done[w]) ++w;
+        M.steal = w < P ? w : -1;
+        if (M.steal < 0) st = 1;
+      }
+      M.go[k] = st;
+    }
+    __syncthreads();
+    const int go = uni(M.go[k]);
+    if (go == 1) break;
+    if (go == 2) {
+      const int w = uni(M.steal);
+      scan_slice(C, near, t, q, i0, n, excl, r, P, w, X);
+      merge_put(M, X, near, w);
+      if (threadIdx.x == 0) { M.ndone++; t_prog = wall_clock64(); }
+      __syncthreads();
+      continue;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  __syncthreads();
+}
+
+__device__ int nearest_dist(const Ctx& C, int t, const double* q, int i0, int n, double* d_out) {
+  scan_run(C, 0, t, q, i0, n, -1, 0.0);
+  const MergeLds& M = g_L.u.sc.m;
+  const int P = uni(min(C.Q.nworkers, SCAN_P));
+  unsigned long long bk = M.nk[0];
+  int bi = M.ni[0];
+  for (int w = 1; w < P; ++w)
+    if (M.nk[w] < bk || (M.nk[w] == bk && M.ni[w] < bi)) { bk = M.nk[w]; bi = M.ni[w]; }
+  __syncthreads();
+  *d_out = __longlong_as_double((long long)bk);
+  return bi;
+}
+
+// near_set's outputs (g_L.nk, n_lo, n_hi, lo_*, hi_*) from the merged slices: an entry of participant w's list at
+// position j ranks j + (entries of the other lists ahead of it); the lists are sorted, so each count is a binary
+// search.  Threads [0, 256) the low lists, [256, 512) the high lists, candidates strided.
+__device__ void near_set_dist(const Ctx& C, int t, const double* q, int excl) {
+  const int n = uni(g_L.S.n[t]);
+  scan_run(C, 1, t, q, 0, n, excl, g_L.S.near_r);
+  const MergeLds& M = g_L.u.sc.m;
+  const int P = uni(min(C.Q.nworkers, SCAN_P));
+  int tot = 0;
+  for (int w = 0; w < P; ++w) tot += M.cnt[w];
+  tot = uni(tot);
+  const int take = min(SCAN_K, tot);
+  const int side = threadIdx.x >= 256;
+  for (int c = threadIdx.x & 255; c < P * SCAN_K; c += 256) {
+    const int w = c / SCAN_K, j = c - w * SCAN_K;
+    if (j >= M.len[w]) continue;
+    const unsigned long long ck = M.k[side][w][j];
+    const int ci = M.id[side][w][j];
+    int rank = j;
+    for (int o0 = 0; o0 < P && rank < take; o0 += 8) {
+      int lo[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) lo[u] = 0;
+#pragma unroll
+      for (int step = 16; step > 0; step >>= 1) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int o = o0 + u;
+          const int m = lo[u] + step - 1;
+          if (o < P && o != w && m < M.len[o]) {
+            const unsigned long long ok = M.k[side][o][m];
+            const int oi = M.id[side][o][m];
+            const bool ahead = side ? ki_less(ck, ci, ok, oi) : ki_less(ok, oi, ck, ci);
+            if (ahead) lo[u] += step;
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) rank += lo[u];
+    }
+    if (rank < take) {
+      if (!side) { g_L.lo_c[rank] = __longlong_as_double((long long)ck); g_L.lo_i[rank] = ci; }
+      else { g_L.hi_c[take - 1 - rank] = __longlong_as_double((long long)ck); g_L.hi_i[take - 1 - rank] = ci; }
+    }
+  }
+  if (threadIdx.x == 0) { g_L.nk = tot; g_L.n_lo = take; g_L.n_hi = take; g_L.S.near_nodes += n; }
+  __syncthreads();
+}
+
 #ifndef SMP_HELPER_SLEEP
 #define SMP_HELPER_SLEEP 2  // s_sleep units (64 clocks) between an idle helper's polls of its job board
 #endif
@@ -1386,6 +1882,12 @@ __device__ __forceinline__ void helper_main(const Ctx& C, int hidx, JobLds& J) {
     }
     const int seq = uni(J.seq);
     const unsigned hdr = J.words[0];
+    if (uni((int)((hdr >> 18) & 1u))) {  // scan job: this helper's slice (the payload fits the first poll)
+      scan_helper(C, J, w, seq);
+      last = seq;
+      t_last = wall_clock64();
+      continue;
+    }
     const int ne = min((int)(hdr & 255), MAXE), nw = 1 + 32 * ne;
     if (go == -2) {
       // the rest of a long payload (one read; granules not yet current abandon the job to the next poll, which
@@ -3724,6 +4226,7 @@ __device__ __forceinline__ void scout_main(Ctx& C, int which) {
   if (threadIdx.x == 0) {
     g_L.count_slot = 0;
     g_L.job_seq = 0;
+    g_L.in_job = 0;
     g_L.n_via = 0;
     g_L.near_blo = ~0ull;
     g_L.near_bhi = 0;
@@ -3864,6 +4367,7 @@ __global__ void __launch_bounds__(BLOCK) plan_kernel(const RobotDev* __restrict_
     g_L.rec_grp = -1;
     g_L.count_slot = 0;
     g_L.job_seq = 0;
+    g_L.in_job = 0;
     g_L.S = *C.Q.st;
     if (g_L.S.phase == 0 && g_L.S.t0 == 0) {
       g_L.S.t0 = wall_clock64();
@@ -4057,9 +4561,12 @@ __global__ void __launch_bounds__(BLOCK) near_probe_kernel(const double* tq, con
                                                            int reps, int* nn, int* nk, int* lo, int* hi,
                                                            unsigned long long* ticks) {
   Ctx C;
+  C.Q.jb = nullptr;  // single workgroup: no helpers, scans stay local
+  C.Q.scan_min = 0;
   C.Q.tr[0].q = const_cast<double*>(tq);
   C.Q.tr[0].cost = const_cast<double*>(tcost);
   if (threadIdx.x == 0) {
+    g_L.in_job = 0;
     g_L.S.n[0] = n;
     g_L.S.cap = cap;
     g_L.S.near_r = r;

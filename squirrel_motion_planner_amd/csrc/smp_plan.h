@@ -84,6 +84,12 @@ constexpr int JOB_SLOTS = MAXE * (MAX_PTS + 1); // (edge, point) slots of one jo
 constexpr int JOB_TILES = (JOB_SLOTS + HELPER_CT - 1) / HELPER_CT;
 constexpr int JOB_WORDS = 1 + 4 * NJ * MAXE;     // payload words: header + (start, step) halves per edge
 constexpr int SMP_RING = 16;                     // run-ahead sampler: samples kept ahead of the leader
+// Distributed tree scans (DESIGN.md "Scans of large trees"): a workgroup splits a nearest / near scan of a large tree
+// over itself and up to SCAN_P - 1 of its helpers; participant w's partial result is SCAN_W granules of sres[w]:
+// nearest: key low / high half, id; near set: count, list lengths (lo | hi << 16), then per entry of the low and the
+// high list (key low half, key high half, id).
+constexpr int SCAN_P = 64;
+constexpr int SCAN_W = 2 + 2 * 3 * MAX_NEAR;
 // Tag of the run-ahead sampler's ring granules: iteration (low 24 bits) and parameter version (low 8 bits).  A slot
 // holds only iteration i (mod SMP_RING) and the version changes at most once per iteration, so the short fields
 // cannot alias within a run of fewer than 2^24 iterations.
@@ -115,6 +121,7 @@ struct JobBoard {
   struct {
     unsigned long long g[2 * NJ];
   } ring[SMP_RING];
+  unsigned long long sres[SCAN_P][SCAN_W];  // scan jobs: participant w's partial result (w >= 1)
 };
 
 // Scout (DESIGN.md "Scout"): a second workgroup per query computes the expand / near / choose-parent / rewire
@@ -265,6 +272,7 @@ struct QueryDev {
   int sworkers;
   int* trace;                  // debug only (SMP_DEBUG): host-mapped progress markers of the leader
   unsigned* ttff;              // host-mapped word set to 1 when the first feasible path is committed (null: none)
+  int scan_min;                // nodes in a scan's range from which it is split over the helpers (0: never)
   int nworkers;                // leader + tile helper workgroups (tile w, w + nworkers, ... is worker w's)
   int sampler;                 // 1: the last helper workgroup is the run-ahead sampler
   TreeDev tr[2];

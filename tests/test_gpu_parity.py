@@ -478,3 +478,45 @@ def test_c1_survey_start_is_in_self_collision(gp, orobot):
     p.setOctree(sc.keys, resolution=sc.res)
     assert not p.init_planner(sc.start, sc.goal, 1, True, True)
     assert p.init_planner(sc.start, sc.goal, 1, False, True)  # without the self check the start is free
+
+
+# ------------------------------------------------------------------------------------------ distributed scans
+@pytest.mark.parametrize("scan_min,helpers,scouts,iters,seed", [(64, 0, 1, 3000, 5), (64, 63, 0, 1500, 9),
+                                                               (600, 0, 1, 3000, 13)])
+def test_distributed_scans_parity(orobot, robot, monkeypatch, scan_min, helpers, scouts, iters, seed):
+    """Nearest and near scans split over the helper workgroups (DESIGN.md "Scans of large trees"), forced onto small
+    trees (SMP_SCAN_MIN): trees, costs, counters and path bit for bit against the oracle."""
+    monkeypatch.setenv("SMP_SCAN_MIN", str(scan_min))
+    gp2 = GpuPlanner(robot, helpers=helpers, scout=scouts, path_optimality_threshold=-np.inf)
+    sc, gscene, osc = scene_pair("c2")
+    gp2.set_scene(gscene)
+    r = gp2.plan(GpuPlanner.make_query(sc.start, sc.goal, sc.env_x, sc.env_y, iterations=iters, seed=seed))
+    o = O.Oracle(orobot, osc).plan(sc.start, sc.goal, env_x=sc.env_x, env_y=sc.env_y, max_iter=iters, seed=seed,
+                                   opt_thresh=-np.inf)
+    assert max(r["nodes_start"], r["nodes_goal"]) > scan_min
+    assert_same_run(gp2, r, o)
+
+
+def test_large_tree_run_matches_golden(robot):
+    """One C2 query for 1e5 iterations (trees of ~50k nodes per side, the distributed scans at the default split)
+    against the committed oracle run (tests/golden/make_large_golden.py): counters, c_best, both trees' SHA-256
+    digests and the path."""
+    import hashlib
+    g = np.load(os.path.join(GOLD, "plan_c2_1e5.npz"))
+    gp2 = GpuPlanner(robot, path_optimality_threshold=-np.inf)
+    sc, gscene, osc = scene_pair("c2")
+    gp2.set_scene(gscene)
+    r = gp2.plan(GpuPlanner.make_query(sc.start, sc.goal, sc.env_x, sc.env_y, iterations=int(g["iterations"]),
+                                       seed=int(g["seed"])))
+    dig = lambda a: hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+    assert r["iterations"] == int(g["iterations"]) and r["first_solution_iter"] == int(g["first_iter"])
+    assert r["configs_checked"] == int(g["checked"]) and r["configs_valid"] == int(g["valid"])
+    assert r["nodes_start"] == int(g["n_start"]) and r["nodes_goal"] == int(g["n_goal"])
+    assert [r["rewires_start"], r["rewires_goal"]] == g["rewires"].tolist()
+    assert r["cost_best"] == g["cost"].tolist()
+    for w, name in ((0, "start"), (1, "goal")):
+        par, conf, cost = gp2.tree(w)
+        assert dig(par) == str(g[name + "_parent_sha"]), name
+        assert dig(conf) == str(g[name + "_conf_sha"]), name
+        assert dig(cost) == str(g[name + "_cost_sha"]), name
+    assert np.array_equal(r["path"], g["path"])

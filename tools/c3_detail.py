@@ -11,7 +11,8 @@ from squirrel_motion_planner_amd.planner import GpuPlanner, Scene  # noqa: E402
 sc = scenes.box_room()
 nq = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 samples = int(sys.argv[2]) if len(sys.argv) > 2 else 300000
-gp = GpuPlanner(path_optimality_threshold=-math.inf)
+gp = GpuPlanner(path_optimality_threshold=-math.inf, helpers=int(os.environ.get("SMP_HELPERS", "0")),
+                scout=int(os.environ.get("SMP_SCOUT", "1")))
 gp.set_scene(Scene.from_keys(sc.keys, sc.res))
 pairs = scenes.random_queries(sc, nq, seed=7, check=lambda q: bool(gp.check_configs([q])[0]))
 qs = [GpuPlanner.make_query(s, g, sc.env_x, sc.env_y, samples=samples, seed=1, query_id=i) for i, (s, g) in enumerate(pairs)]
