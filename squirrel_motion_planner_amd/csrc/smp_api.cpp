@@ -806,6 +806,14 @@ static QueryDev make_qdev(QueryBuffers& b, size_t cap, long long rows) {
   // SMP_SCAN_MIN overrides it (experiments and tests; 0: never)
   d.scan_min = 12288;
   if (const char* e = std::getenv("SMP_SCAN_MIN")) d.scan_min = std::max(0, std::atoi(e));
+  // participants of one split scan: a nearest result is 3 granules, a near result 122, and the near merge ranks
+  // every list entry against the other lists -- fewer, longer slices for near (SMP_SCAN_PNN / SMP_SCAN_PNEAR)
+  d.scan_pnn = 64;
+  d.scan_pnear = 8;
+  if (const char* e = std::getenv("SMP_SCAN_PNN")) d.scan_pnn = std::atoi(e);
+  if (const char* e = std::getenv("SMP_SCAN_PNEAR")) d.scan_pnear = std::atoi(e);
+  d.scan_pnn = std::min(SCAN_P, std::max(2, d.scan_pnn));
+  d.scan_pnear = std::min(SCAN_P, std::max(2, d.scan_pnear));
   return d;
 }
 

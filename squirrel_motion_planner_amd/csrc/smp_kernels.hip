@@ -227,13 +227,17 @@ struct ScanLds {
   int wi[BLOCK / 64];
 };
 struct MergeLds {
-  unsigned long long k[2][SCAN_P][SCAN_K];  // [0] lows ascending, [1] highs descending, per participant
+  unsigned kw[2][SCAN_P][SCAN_K][2];  // [0] lows ascending, [1] highs descending, per participant: key halves
   int id[2][SCAN_P][SCAN_K];
-  int len[SCAN_P], cnt[SCAN_P], done[SCAN_P];
-  unsigned long long nk[SCAN_P];            // nearest: per participant (distance key, id)
+  int len[SCAN_P], cnt[SCAN_P], done[SCAN_P], bad[SCAN_P];
+  unsigned hv[SCAN_P][3];             // collection: near header (count, take) / nearest (key halves, id)
+  unsigned long long nk[SCAN_P];      // nearest: per participant (distance key, id)
   int ni[SCAN_P];
   int ndone, go[2], steal;
 };
+__device__ __forceinline__ unsigned long long merge_key(const MergeLds& M, int s, int w, int e) {
+  return (unsigned long long)M.kw[s][w][e][1] << 32 | M.kw[s][w][e][0];
+}
 // LDS of job mode (leader and helper kernel): the published job + one job tile.
 struct JobLds {
   ScanLds scan;                            // helper: its slice of a scan job
@@ -503,6 +507,9 @@ __device__ void insert_node(const Ctx& C, int t, const double* e_start, const do
 // squared distance; the (correctly rounded) sqrt is taken only then and compared exactly as the reference does.
 __device__ bool spec_stage(const Ctx& C, int s, unsigned long long wait = 0);
 // Distributed scans (defined with the job protocol below): true if a scan of `nodes` nodes is split over the helpers.
+__device__ __forceinline__ int scan_parts(const Ctx& C, int near) {
+  return uni(min(min(C.Q.nworkers, SCAN_P), near ? C.Q.scan_pnear : C.Q.scan_pnn));
+}
 __device__ __forceinline__ bool scan_split(const Ctx& C, int nodes) {
   return uni(C.Q.jb != nullptr && C.Q.scan_min > 0 && nodes >= C.Q.scan_min && C.Q.nworkers >= 8 && !g_L.in_job);
 }
@@ -1628,16 +1635,18 @@ __device__ void scan_helper(const Ctx& C, JobLds& J, int w, int seq) {
       st_agent(&out[2], granule(seq, (unsigned)X.wi[0]));
     }
   } else {
+    // fixed places: entry e of side s in granules 2 + 3 * (s * SCAN_K + e) .. + 2, so that the collector can
+    // load a whole result at once
     const int take = X.take;
     const int i = threadIdx.x;
     if (i == 0) st_agent(&out[0], granule(seq, (unsigned)X.cnt));
-    if (i == 1) st_agent(&out[1], granule(seq, (unsigned)take | (unsigned)take << 16));
+    if (i == 1) st_agent(&out[1], granule(seq, (unsigned)take));
     if (i < 6 * take) {
-      const int side = i >= 3 * take, e = (i - side * 3 * take) / 3, f = i - side * 3 * take - 3 * e;
+      const int side = i >= 3 * take, j = i - side * 3 * take, e = j / 3, f = j - 3 * e;
       const unsigned long long k = side ? X.hk[e] : X.lk[e];
       const int id = side ? X.hi[e] : X.li[e];
       const unsigned v = f == 0 ? (unsigned)k : f == 1 ? (unsigned)(k >> 32) : (unsigned)id;
-      st_agent(&out[2 + i], granule(seq, v));
+      st_agent(&out[2 + 3 * side * SCAN_K + j], granule(seq, v));
     }
   }
   __syncthreads();
@@ -1652,8 +1661,8 @@ __device__ __forceinline__ void merge_put(MergeLds& M, const ScanLds& X, int nea
     if (threadIdx.x < SCAN_K) {
       const int e = threadIdx.x;
       if (e < take) {
-        M.k[0][w][e] = X.lk[e]; M.id[0][w][e] = X.li[e];
-        M.k[1][w][e] = X.hk[e]; M.id[1][w][e] = X.hi[e];
+        M.kw[0][w][e][0] = (unsigned)X.lk[e]; M.kw[0][w][e][1] = (unsigned)(X.lk[e] >> 32); M.id[0][w][e] = X.li[e];
+        M.kw[1][w][e][0] = (unsigned)X.hk[e]; M.kw[1][w][e][1] = (unsigned)(X.hk[e] >> 32); M.id[1][w][e] = X.hi[e];
       }
     }
     if (threadIdx.x == 0) { M.len[w] = take; M.cnt[w] = X.cnt; }
@@ -1661,14 +1670,14 @@ __device__ __forceinline__ void merge_put(MergeLds& M, const ScanLds& X, int nea
   if (threadIdx.x == 0) M.done[w] = 1;
 }
 
-// Publishes a scan of [i0, n), scans slice 0, collects (or steals) the other slices into g_L.u.sc.m.  All threads.
-__device__ void scan_run(const Ctx& C, int near, int t, const double* q, int i0, int n, int excl, double r) {
+// Publishes a scan of [i0, n) over P participants, scans slice 0, collects (or steals) the other slices into
+// g_L.u.sc.m.  All threads.
+__device__ void scan_run(const Ctx& C, int near, int t, const double* q, int i0, int n, int excl, double r, int P) {
   MergeLds& M = g_L.u.sc.m;
   ScanLds& X = g_L.u.sc.s;
-  const int P = uni(min(C.Q.nworkers, SCAN_P));
   __syncthreads();
   const int seq = uni(g_L.job_seq) + 1;
-  if (threadIdx.x < SCAN_P) M.done[threadIdx.x] = 0;
+  if (threadIdx.x < SCAN_P) { M.done[threadIdx.x] = 0; M.bad[threadIdx.x] = 0; }
   __syncthreads();
   if (threadIdx.x == 0) { g_L.job_seq = seq; M.ndone = 0; }
   // the helpers read the tree through their own CUs and XCDs: the tree stores (this workgroup's, or the leader's on
@@ -1688,58 +1697,75 @@ __device__ void scan_run(const Ctx& C, int near, int t, const double* q, int i0,
   unsigned long long t_prog = wall_clock64();
   const unsigned long long t_start = t_prog;
   int last_done = 0;
+  // One collection round loads every granule of every outstanding result at once (up to 4 per thread per pass:
+  // independent loads, one round trip), then keeps the results whose needed granules all carry this job's number.
+  const int per = near ? 2 + 6 * SCAN_K : 3;
+  const int total = (P - 1) * per;
   for (int k = 0;; k ^= 1) {
-    // wave v reads participants 1 + v, 1 + v + 8, ...: every granule of a result must carry this job's number
-    const int lane = lane_id();
-    for (int w = 1 + wave_id(); w < P; w += BLOCK / 64) {
-      if (M.done[w]) continue;
-      const unsigned long long* g = jb->sres[w];
-      if (!near) {
-        const unsigned long long v = lane < 3 ? ld_agent(&g[lane]) : 0ull;
-        const bool ok = !__ballot(lane < 3 && (int)(v >> 32) != seq);
-        const unsigned v0 = __shfl((unsigned)v, 0), v1 = __shfl((unsigned)v, 1), v2 = __shfl((unsigned)v, 2);
-        if (ok && lane == 0) {
-          M.nk[w] = (unsigned long long)v1 << 32 | v0;
-          M.ni[w] = (int)v2;
-          M.done[w] = 1;
-          atomicAdd(&M.ndone, 1);
-        }
-      } else {
-        const unsigned long long h = lane < 2 ? ld_agent(&g[lane]) : 0ull;
-        if (__ballot(lane < 2 && (int)(h >> 32) != seq)) continue;
-        const unsigned cnt = __shfl((unsigned)h, 0), tk = __shfl((unsigned)h, 1) & 0xffff;
-        const int take = (int)min(tk, (unsigned)SCAN_K);
-        bool ok = true;
-        unsigned vv[2] = {0, 0};
+    for (int base = 0; base < total; base += 4 * BLOCK) {
+      unsigned val[4];
+      unsigned okm = 0;
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int i = lane + 64 * u;
-          if (i < 6 * take) {
-            const unsigned long long v = ld_agent(&g[2 + i]);
-            ok &= (int)(v >> 32) == seq;
-            vv[u] = (unsigned)v;
+      for (int u = 0; u < 4; ++u) {
+        const int g = base + u * BLOCK + (int)threadIdx.x;
+        val[u] = 0;
+        if (g < total) {
+          const int w = 1 + g / per;
+          if (!M.done[w]) {
+            const unsigned long long v = ld_agent(&jb->sres[w][g - (w - 1) * per]);
+            val[u] = (unsigned)v;
+            if ((int)(v >> 32) == seq) okm |= 1u << u;
           }
         }
-        if (__ballot(!ok)) continue;
-        // entry e of side s: granules 3e .. 3e + 2 of the side's block; granule i sits in lane i % 64 of vv[i / 64].
-        // Every lane takes part in the shuffles (uniform control flow), lanes < 2 * take keep an entry.
-        const int sd = lane >= take ? 1 : 0, e = lane - sd * take;
-        const int g0 = lane < 2 * take ? sd * 3 * take + 3 * e : 0;
-        auto fetch = [&](int gi) {
-          const unsigned a = __shfl(vv[0], gi & 63), b = __shfl(vv[1], gi & 63);
-          return gi < 64 ? a : b;
-        };
-        const unsigned klo = fetch(g0), khi = fetch(g0 + 1), idv = fetch(g0 + 2);
-        if (lane < 2 * take) {
-          M.k[sd][w][e] = (unsigned long long)khi << 32 | klo;
-          M.id[sd][w][e] = (int)idv;
+      }
+      // nearest values and near headers (every granule needed)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int g = base + u * BLOCK + (int)threadIdx.x;
+        if (g < total) {
+          const int w = 1 + g / per, i = g - (w - 1) * per;
+          if (!M.done[w] && i < (near ? 2 : 3)) {
+            M.hv[w][i] = val[u];
+            if (!((okm >> u) & 1u)) M.bad[w] = 1;
+          }
         }
-        if (lane == 0) {
-          M.len[w] = take;
-          M.cnt[w] = (int)cnt;
+      }
+      if (near) {
+        __syncthreads();
+        // near entries: needed below the result's take
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int g = base + u * BLOCK + (int)threadIdx.x;
+          if (g < total) {
+            const int w = 1 + g / per, i = g - (w - 1) * per;
+            if (!M.done[w] && i >= 2) {
+              const int j = i - 2, side = j >= 3 * SCAN_K ? 1 : 0, jj = j - side * 3 * SCAN_K, e = jj / 3, f = jj - 3 * e;
+              if (e < min((int)M.hv[w][1], SCAN_K)) {
+                if (!((okm >> u) & 1u)) M.bad[w] = 1;
+                else if (f < 2) M.kw[side][w][e][f] = val[u];
+                else M.id[side][w][e] = (int)val[u];
+              }
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+    {
+      const int w = threadIdx.x;
+      if (w >= 1 && w < P && !M.done[w]) {
+        if (!M.bad[w]) {
+          if (near) {
+            M.len[w] = min((int)M.hv[w][1], SCAN_K);
+            M.cnt[w] = (int)M.hv[w][0];
+          } else {
+            M.nk[w] = (unsigned long long)M.hv[w][1] << 32 | M.hv[w][0];
+            M.ni[w] = (int)M.hv[w][2];
+          }
           M.done[w] = 1;
           atomicAdd(&M.ndone, 1);
         }
+        M.bad[w] = 0;
       }
     }
     __syncthreads();
@@ -1778,9 +1804,9 @@ __device__ void scan_run(const Ctx& C, int near, int t, const double* q, int i0,
 }
 
 __device__ int nearest_dist(const Ctx& C, int t, const double* q, int i0, int n, double* d_out) {
-  scan_run(C, 0, t, q, i0, n, -1, 0.0);
+  const int P = scan_parts(C, 0);
+  scan_run(C, 0, t, q, i0, n, -1, 0.0, P);
   const MergeLds& M = g_L.u.sc.m;
-  const int P = uni(min(C.Q.nworkers, SCAN_P));
   unsigned long long bk = M.nk[0];
   int bi = M.ni[0];
   for (int w = 1; w < P; ++w)
@@ -1795,9 +1821,9 @@ __device__ int nearest_dist(const Ctx& C, int t, const double* q, int i0, int n,
 // search.  Threads [0, 256) the low lists, [256, 512) the high lists, candidates strided.
 __device__ void near_set_dist(const Ctx& C, int t, const double* q, int excl) {
   const int n = uni(g_L.S.n[t]);
-  scan_run(C, 1, t, q, 0, n, excl, g_L.S.near_r);
+  const int P = scan_parts(C, 1);
+  scan_run(C, 1, t, q, 0, n, excl, g_L.S.near_r, P);
   const MergeLds& M = g_L.u.sc.m;
-  const int P = uni(min(C.Q.nworkers, SCAN_P));
   int tot = 0;
   for (int w = 0; w < P; ++w) tot += M.cnt[w];
   tot = uni(tot);
@@ -1806,7 +1832,7 @@ __device__ void near_set_dist(const Ctx& C, int t, const double* q, int excl) {
   for (int c = threadIdx.x & 255; c < P * SCAN_K; c += 256) {
     const int w = c / SCAN_K, j = c - w * SCAN_K;
     if (j >= M.len[w]) continue;
-    const unsigned long long ck = M.k[side][w][j];
+    const unsigned long long ck = merge_key(M, side, w, j);
     const int ci = M.id[side][w][j];
     int rank = j;
     for (int o0 = 0; o0 < P && rank < take; o0 += 8) {
@@ -1820,7 +1846,7 @@ __device__ void near_set_dist(const Ctx& C, int t, const double* q, int excl) {
           const int o = o0 + u;
           const int m = lo[u] + step - 1;
           if (o < P && o != w && m < M.len[o]) {
-            const unsigned long long ok = M.k[side][o][m];
+            const unsigned long long ok = merge_key(M, side, o, m);
             const int oi = M.id[side][o][m];
             const bool ahead = side ? ki_less(ck, ci, ok, oi) : ki_less(ok, oi, ck, ci);
             if (ahead) lo[u] += step;

@@ -273,6 +273,7 @@ struct QueryDev {
   int* trace;                  // debug only (SMP_DEBUG): host-mapped progress markers of the leader
   unsigned* ttff;              // host-mapped word set to 1 when the first feasible path is committed (null: none)
   int scan_min;                // nodes in a scan's range from which it is split over the helpers (0: never)
+  int scan_pnn, scan_pnear;    // participants (this workgroup + helpers) of a split nearest / near scan, <= SCAN_P
   int nworkers;                // leader + tile helper workgroups (tile w, w + nworkers, ... is worker w's)
   int sampler;                 // 1: the last helper workgroup is the run-ahead sampler
   TreeDev tr[2];
