@@ -137,6 +137,47 @@ def cpu_baseline(sc, pair, a, step0_seed, step_seeds=()):
             "time_first_solution_stats_s": stats3(ttff)}
 
 
+def _oracle_worker(args):
+    """One independent oracle process of the many-query CPU baseline: plans its share of the queries."""
+    workload, jobs, budget = args
+    from oracle import oracle as O
+    from squirrel_motion_planner_amd import scenes
+    sc = scenes.clutter_cloud() if workload == "c5" else scenes.box_room()
+    rob = O.OracleRobot(os.path.join(ROOT, "squirrel_motion_planner_amd", "data", "robotino_model.json"))
+    orc = O.Oracle(rob, O.OracleScene(sc.keys, sc.res))
+    out = []
+    for qid, s, g, seed in jobs:
+        t = time.perf_counter()
+        r = orc.plan(s, g, env_x=sc.env_x, env_y=sc.env_y, seed=seed, query=qid, opt_thresh=-math.inf, threads=1,
+                     **budget)
+        out.append((qid, r["checked"], r["iterations"], r["valid"], time.perf_counter() - t))
+    return out
+
+
+def cpu_many_queries(a, pairs, seed, procs, gpu_results):
+    """The many-query CPU baseline (C3 / C5): `procs` independent single-thread oracle processes, each planning its
+    share of this rank's queries (same pairs, seeds, query ids and budget as the GPU step 0), the whole set timed
+    on the wall clock from the first process start to the last result (scene set-up excluded: each process builds
+    its scene before its clock starts)."""
+    import multiprocessing as mp
+    budget = dict(max_iter=a.iterations) if a.iterations else dict(max_checked=a.samples, max_iter=0)
+    jobs = [(k, list(pairs[k][0]), list(pairs[k][1]), seed) for k in range(len(gpu_results))]
+    shares = [jobs[i::procs] for i in range(procs)]
+    ctx = mp.get_context("spawn")  # fresh interpreters: nothing of this (GPU) process is inherited
+    with ctx.Pool(procs) as pool:
+        res = pool.map(_oracle_worker, [(a.workload, sh, budget) for sh in shares if sh])
+    flat = sorted(x for part in res for x in part)
+    busy = [sum(x[4] for x in part) for part in res]
+    span = max(busy)
+    checked = sum(x[1] for x in flat)
+    same = all(x[1] == r["configs_checked"] and x[2] == r["iterations"] for x, r in zip(flat, gpu_results))
+    return {"value": checked / span, "unit": "configs/s", "cores": procs, "processes": procs,
+            "queries": len(flat), "checked": checked, "span_s": span,
+            "how": "%d independent oracle processes (one thread each), the %d queries dealt round-robin; value = all "
+                   "configurations checked / the busiest process's planning time" % (procs, len(flat)),
+            "same_results_as_gpu_step0": bool(same)}
+
+
 def stats3(v):
     v = sorted(x for x in v if x is not None)
     if not v:
@@ -204,6 +245,7 @@ def main():
     totals = dict(checked=0, valid=0, iters=0, nn=0, near=0, plan_ms=0.0, launches=0)
     first_t, first_host = [], []
     step0 = None
+    step0_all = None
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -212,6 +254,7 @@ def main():
         rs = gp.plan_batch(queries(step, a.samples))
         if step0 is None:
             step0 = rs[0]
+            step0_all = rs
         for r in rs:
             if r["status"] not in (0, -4):
                 raise RuntimeError("plan failed with status %d" % r["status"])
@@ -310,6 +353,9 @@ def main():
             cb["same_result_as_gpu_step0"] = bool(not cb["bounded_sample"] and cb["checked"] == step0["configs_checked"] and
                                                   cb["iterations"] == step0["iterations"] and
                                                   cb["cost_best"] == step0["cost_best"][0])
+            if a.queries_per_gpu > 1:
+                # many queries: the host's answer is one oracle per core, not OpenMP scans inside one query
+                cb["all_cores"] = cpu_many_queries(a, pairs, a.seed, host_cpu()[1], step0_all)
             out["cpu_baseline"] = cb
         else:
             out["cpu_baseline"] = None

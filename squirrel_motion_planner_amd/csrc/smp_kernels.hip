@@ -250,6 +250,8 @@ struct JobLds {
   int emap[MAXE];                          // leader: job edge -> batch edge
   int first[MAXE];                         // leader: first colliding point per job edge
   int E, np1, nslots, ntiles, self, map, seq, steal, hidx, left;
+  int skip, sfv, tskip;                    // job in skip mode / stop-first-valid; tile wholly skipped
+  int tgrp[HELPER_CT], tord[HELPER_CT];    // skip mode: the tile's TileOrder (edge, point or "skip")
   unsigned long long tprof[4];             // SMP_JOB_PROF builds: this helper's tile stage clocks
   int go[2];  // poll-loop decisions, double-buffered by iteration parity (a slow wave may still read the last one)
 };
@@ -1368,17 +1370,76 @@ __device__ __forceinline__ unsigned long long granule(int seq, unsigned w) {
   return ((unsigned long long)(unsigned)seq << 32) | w;
 }
 
+// Skip mode (a job of more tiles than workers, JobLds::skip): before tile t of its second or later round, a worker
+// reads the results of tiles [0, t) that have arrived (JobBoard::res, the leader's own included) -> each job edge's
+// lowest known colliding point (J.first) and, for a stop-first-valid job (choose-parent, the connect near loop), the
+// first edge known to be free (every tile of it arrived without a collision).  A configuration beyond its edge's
+// known collision, or on an edge after a known free one, cannot change what the job's consumer reads (the first
+// collision of each edge up to the first free one: eg_first of later edges is undefined, as in the local path), so
+// it is not checked.  Returns true if no configuration of the tile is left; else J.tgrp / J.tord / J.first are the
+// tile's TileOrder.  All threads.
+__device__ __forceinline__ bool job_tile_skip(const Ctx& C, JobLds& J, int t, int seq) {
+  const JobBoard* jb = C.Q.jb;
+  const int np1 = uni(J.np1), ne = uni(J.E);
+  for (int u = threadIdx.x; u < t; u += BLOCK) {
+    if (!J.rdone[u]) {
+      const unsigned long long v = ld_agent(&jb->res[u]);
+      if ((int)(v >> 32) == seq) { J.rmask[u] = (unsigned)v; J.rdone[u] = 1; }
+    }
+  }
+  if (threadIdx.x < ne) J.first[threadIdx.x] = np1;
+  __syncthreads();
+  for (int u = threadIdx.x; u < t; u += BLOCK) {
+    if (!J.rdone[u]) continue;
+    unsigned m = J.rmask[u];
+    while (m) {
+      const int sl = u * HELPER_CT + __builtin_ctz(m), k = sl / np1;
+      m &= m - 1;
+      atomicMin(&J.first[k], sl - k * np1);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    bool fr = false;
+    if (J.sfv && lane < ne && (lane + 1) * np1 <= t * HELPER_CT && J.first[lane] >= np1) {
+      fr = true;
+      for (int u = (lane * np1) / HELPER_CT; u <= ((lane + 1) * np1 - 1) / HELPER_CT; ++u)
+        if (!J.rdone[u]) { fr = false; break; }
+    }
+    const unsigned long long fb = __ballot(fr);
+    const int ff = fb ? __builtin_ctzll(fb) : (1 << 30);
+    const int base = t * HELPER_CT, nc = min(HELPER_CT, J.nslots - base);
+    bool live = false;
+    if (lane < nc) {
+      const int sl = base + lane, k = sl / np1, i = sl - k * np1;
+      live = k <= ff && i <= J.first[k];
+      J.tgrp[lane] = k;
+      J.tord[lane] = live ? i : (1 << 30);
+    }
+    const unsigned long long lb = __ballot(live);
+    if (lane == 0) J.tskip = lb == 0;
+  }
+  __syncthreads();
+  return uni(J.tskip) != 0;
+}
+
 // Configurations of job tile t -> J.tq: slot s = job edge s / np1, point s % np1, configuration start + i * step
 // (the leader's arithmetic).  Then the collision tile; returns the tile's collision mask in every thread.
-__device__ __forceinline__ unsigned job_tile_mask(const Ctx& C, JobLds& J, int t, unsigned long long* prof = nullptr) {
+// `seq` >= 0 in skip mode: configurations skipped by job_tile_skip report no collision.
+__device__ __forceinline__ unsigned job_tile_mask(const Ctx& C, JobLds& J, int t, unsigned long long* prof = nullptr,
+                                                  int seq = -1) {
   const int base = t * HELPER_CT, nc = min(HELPER_CT, uni(J.nslots) - base);
+  const bool sk = seq >= 0 && uni(J.skip) && t >= uni(C.Q.nworkers);
+  if (sk && job_tile_skip(C, J, t, seq)) return 0u;
   if (threadIdx.x < nc * NJ) {
     const int c = threadIdx.x / NJ, j = threadIdx.x - c * NJ;
     const int sl = base + c, k = sl / J.np1, i = sl - k * J.np1;
     J.tq[c][j] = J.start[k][j] + i * J.step[k][j];
   }
   __syncthreads();
-  collide_tile<HELPER_CT>((&g_rb), C.sc, (&g_mc), nc, J.tq, J.self, J.map, J.T, nullptr, prof);
+  const TileOrder order{J.tgrp, J.tord, J.first, false};
+  collide_tile<HELPER_CT>((&g_rb), C.sc, (&g_mc), nc, J.tq, J.self, J.map, J.T, sk ? &order : nullptr, prof);
   unsigned m = 0;
   for (int c = 0; c < nc; ++c) m |= (J.T.coll[c] ? 1u : 0u) << c;
   __syncthreads();
@@ -1406,7 +1467,7 @@ __device__ __forceinline__ bool take_spec(int ov) {
 // tile results and reduces them to the first collision of each edge (eg_first).  A helper's tile that does not
 // arrive within 8 us of the last progress is checked by the leader itself (a duplicate result is identical, so
 // no claim is needed).
-__device__ __forceinline__ void edge_validity_job(const Ctx& C, int E, int pslot, int ov, int ovt) {
+__device__ __forceinline__ void edge_validity_job(const Ctx& C, int E, int pslot, int ov, int ovt, bool sfv) {
   JobBoard* jb = C.Q.jb;
   auto& J = g_L.u.job;
   const int np1 = g_L.S.n_pts + 1;
@@ -1425,6 +1486,8 @@ __device__ __forceinline__ void edge_validity_job(const Ctx& C, int E, int pslot
       J.ntiles = (ne * np1 + HELPER_CT - 1) / HELPER_CT;
       J.self = g_L.S.self; J.map = g_L.S.map;
       J.seq = ++g_L.job_seq;
+      J.skip = J.ntiles > W;  // more tiles than workers: later rounds skip what earlier ones decided
+      J.sfv = J.skip && sfv;
     }
   }
   if (threadIdx.x < E) g_L.eg_first[threadIdx.x] = np1;
@@ -1449,7 +1512,8 @@ __device__ __forceinline__ void edge_validity_job(const Ctx& C, int E, int pslot
   for (int i = threadIdx.x; i < 1 + 32 * ne; i += BLOCK) {
     unsigned w;
     if (i == 0) {
-      w = (unsigned)ne | (unsigned)np1 << 8 | (unsigned)(J.self != 0) << 16 | (unsigned)(J.map != 0) << 17;
+      w = (unsigned)ne | (unsigned)np1 << 8 | (unsigned)(J.self != 0) << 16 | (unsigned)(J.map != 0) << 17 |
+          (unsigned)J.skip << 19 | (unsigned)J.sfv << 20;
     } else {
       const int m = i - 1, k = m >> 5, r = m & 31, j = (r & 15) >> 1;
       const unsigned long long bits = (unsigned long long)__double_as_longlong(r < 16 ? J.start[k][j] : J.step[k][j]);
@@ -1468,10 +1532,15 @@ __device__ __forceinline__ void edge_validity_job(const Ctx& C, int E, int pslot
   overlap_work(C, ov, ovt);
   if (threadIdx.x == 0) g_L.in_job = 0;
   TR();
-  // the leader's own tiles
+  // the leader's own tiles (in skip mode published too: the helpers' skip decisions read every earlier tile)
+  const bool skip = uni(J.skip) != 0;
   for (int t = W - 1; t < nt; t += W) {
-    const unsigned m = job_tile_mask(C, J, t);
-    if (threadIdx.x == 0) { J.rmask[t] = m; J.rdone[t] = 1; }
+    const unsigned m = job_tile_mask(C, J, t, nullptr, skip ? seq : -1);
+    if (threadIdx.x == 0) {
+      J.rmask[t] = m;
+      J.rdone[t] = 1;
+      if (skip) st_agent(&jb->res[t], granule(seq, m));
+    }
   }
   __syncthreads();
   const unsigned long long tj1 = threadIdx.x == 0 ? wall_clock64() : 0;
@@ -1941,9 +2010,13 @@ __device__ __forceinline__ void helper_main(const Ctx& C, int hidx, JobLds& J) {
       J.np1 = (int)((hdr >> 8) & 255);
       J.self = (hdr >> 16) & 1;
       J.map = (hdr >> 17) & 1;
+      J.skip = (hdr >> 19) & 1;
+      J.sfv = (hdr >> 20) & 1;
       J.nslots = ne * J.np1;
       J.ntiles = (J.nslots + HELPER_CT - 1) / HELPER_CT;
     }
+    if (hdr & (1u << 19))
+      for (int t = threadIdx.x; t < JOB_TILES; t += BLOCK) J.rdone[t] = 0;
     __syncthreads();
     last = seq;
     const int nt = uni(J.ntiles);
@@ -1961,7 +2034,7 @@ __device__ __forceinline__ void helper_main(const Ctx& C, int hidx, JobLds& J) {
     unsigned long long* tp = nullptr;
 #endif
     for (int t = w - 1; t < nt; t += W) {
-      const unsigned m = job_tile_mask(C, J, t, tp);
+      const unsigned m = job_tile_mask(C, J, t, tp, seq);
       if (threadIdx.x == 0) st_agent(&jb->res[t], granule(seq, m));
 #ifdef SMP_JOB_PROF
       if (threadIdx.x == 0) atomicAdd(&jb->dbg[3], wall_clock64() - ld_agent(&jb->dbg[0]));
@@ -2310,7 +2383,7 @@ __device__ void edge_validity(const Ctx& C, int E, bool stop_first_valid, int ps
     }
     __syncthreads();
     if (!uni(g_L.ev_job)) { TR(); return; }
-    edge_validity_job(C, E, pslot, ov, ovt);
+    edge_validity_job(C, E, pslot, ov, ovt, stop_first_valid);
     if (threadIdx.x < E && g_L.eg_hit[threadIdx.x] >= 0) g_L.eg_first[threadIdx.x] = g_L.eg_hit[threadIdx.x];
     __syncthreads();
     TR();

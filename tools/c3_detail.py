@@ -31,6 +31,14 @@ def row(r, tag):
               r["time_total"] * 1e6 / n, *[ph[k] * 1e6 / n for k in ("sample", "nearest", "expand", "near",
                                                                           "choose_parent", "rewire", "connect")],
               r["scout_wait_seconds"] * 1e6 / n), flush=True)
+    print("           checked configurations per slot checked (reference-semantics / actual tile slots): " +
+          " ".join("%s %.2f" % (k, ph["checked_" + k] / max(ph["slots_" + k], 1))
+                   for k in ("expand", "choose", "rewire", "connect")) +
+          " | tiles %d" % ph["n_tiles"], flush=True)
+    raw = r["phase_raw"]
+    nj = max(raw[15] * 1e8, 1)
+    print("           jobs %.1f/iter: publish %.1f us, own tiles %.1f us, wait %.1f us per job; tiles/job %.1f" % (
+        nj / n, raw[12] * 1e6 / nj, raw[13] * 1e6 / nj, raw[14] * 1e6 / nj, ph["n_tiles"] / nj), flush=True)
 
 
 for i, r in enumerate(rs):
