@@ -52,6 +52,8 @@ def pmc(kernel, out, dbs):
         "write_bytes_per_launch": write_kb * 1024.0 / nw,
         "hbm_bytes_per_launch": 2.0 * fetch_kb * 1024.0 / nf + write_kb * 1024.0 / nw,
         "correction": "FETCH_SIZE (KB) x1024 x2 (gfx950 half-count, MI355X_MICROARCH.md HBM section); WRITE_SIZE x1024",
+        # every collected counter per launch (raw units; see the correction above for FETCH_SIZE)
+        "per_launch": {k: v / max(launches.get(k, 1), 1) for k, v in totals.items()},
         "per_dispatch": per,
     }
     json.dump(res, open(out, "w"), indent=1)

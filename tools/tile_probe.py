@@ -12,7 +12,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from squirrel_motion_planner_amd import _lib as L, scenes  # noqa: E402
 from squirrel_motion_planner_amd.planner import GpuPlanner, Scene  # noqa: E402
 
-sc = scenes.box_room()
+# SMP_SCENE=c5: the 2 cm clutter scene (BASELINE configs[4]) instead of C2's box room
+sc = scenes.clutter_cloud() if os.environ.get("SMP_SCENE") == "c5" else scenes.box_room()
 gp = GpuPlanner(path_optimality_threshold=-math.inf)
 gp.set_scene(Scene.from_keys(sc.keys, sc.res))
 r = gp.plan(GpuPlanner.make_query(sc.start, sc.goal, sc.env_x, sc.env_y, iterations=1500, seed=1))
