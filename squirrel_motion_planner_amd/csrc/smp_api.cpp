@@ -126,6 +126,7 @@ struct smp_planner {
   std::vector<QueryBuffers> qb;
   DBuf<QueryDev> d_qdev;
   DBuf<int> d_counts;
+  DBuf<unsigned> d_lfin;  // finished queries of the current launch
   DBuf<double> d_cq;
   DBuf<uint8_t> d_valid;
   DBuf<IkTaskDev> d_ik_tasks;
@@ -422,7 +423,7 @@ void smp_planner_destroy(smp_planner* p) {
   if (p->stream) (void)hipStreamSynchronize(p->stream);
   if (p->hstream) (void)hipStreamSynchronize(p->hstream);
   for (auto& q : p->qb) q.release();
-  p->d_qdev.release(); p->d_counts.release(); p->d_cq.release(); p->d_valid.release();
+  p->d_qdev.release(); p->d_counts.release(); p->d_lfin.release(); p->d_cq.release(); p->d_valid.release();
   p->d_ik_tasks.release(); p->d_ik_out.release(); p->d_ik_best.release();
   p->d_bricks.release(); p->d_d2.release(); p->d_d2b.release(); p->d_slab.release();
   if (p->d_rb) (void)hipFree(p->d_rb);
@@ -802,6 +803,8 @@ static QueryDev make_qdev(QueryBuffers& b, size_t cap, long long rows) {
   d.sampler = 0;
   d.trace = nullptr;
   d.ttff = nullptr;
+  d.lfin = nullptr;
+  d.lquota = 0;
   // scans of trees of at least this many nodes are split over the helpers (DESIGN.md "Scans of large trees");
   // SMP_SCAN_MIN overrides it (experiments and tests; 0: never)
   d.scan_min = 12288;
@@ -901,67 +904,84 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
   // iteration before the first solution and retire after it: time to first path 2.1 -> 1.7 ms on C2), 2 from 18,
   // 1 from 6).  Helpers: the leader's tile helpers, each scout's, and the run-ahead sampler (the last one); up to 200
   // with scouts (C2: 127 -> 200 helpers 3.65 -> 3.75 M configs/s with four scouts; 250 no longer all fit and stall).
-  int nh = p->params.helpers;
-  const bool want_scout = p->params.scout != 0;
   // Every workgroup of a query (leader, scouts, helpers) polls the others, so all of them must be resident at once:
-  // the budget is the device's co-resident capacity for these kernels (occupancy x CUs), not a fixed count.
+  // the budget is the device's co-resident capacity for these kernels (occupancy x CUs), not a fixed count.  With
+  // automatic helpers the provisioning is redone for the queries still running whenever a launch ends with some of
+  // them finished (DESIGN.md "Many queries").
+  const int nh_req = p->params.helpers;
+  const bool want_scout = p->params.scout != 0;
   const int slots = resident_slots(p);
-  const int cpq = std::max(1, slots / nq);
-  int ns = 0;
   int cap_s = 200;  // SMP_HELPER_CAP: experiments with other helper caps
   if (const char* e = std::getenv("SMP_HELPER_CAP")) cap_s = std::max(1, std::atoi(e));
-  if (nh == 0) {
-    if (want_scout) ns = cpq >= 64 ? 4 : cpq >= 18 ? 2 : cpq >= 6 ? 1 : 0;
-    if (want_scout && p->params.scout > 1) ns = std::min(p->params.scout, MAX_SCOUTS);
-    nh = want_scout ? std::min(cap_s, std::max(0, cpq - 1 - ns)) : std::min(63, std::max(0, cpq - 1));
-  } else if (nh > 0 && want_scout) {
-    ns = nh >= 16 ? 2 : nh >= 4 ? 1 : 0;
-  }
-  if (want_scout && p->params.scout > 1) ns = std::min(p->params.scout, MAX_SCOUTS);  // explicit count
-  if (nh < 0) nh = 0;
-  if (nh < 4) ns = 0;
-  // an explicit request larger than what can be resident is clamped: a helper that never starts would leave its tiles
-  // to the leader's 8 us timeout on every job
-  // to the automatic count (helper sweeps: 250 helpers beside four scouts no longer all start on 256 CUs and stall)
-  if (1 + ns + nh > cpq) {
-    nh = std::max(0, want_scout ? std::min(cap_s, cpq - 1 - ns) : std::min(63, cpq - 1));
-    if (nh < 4) { ns = 0; nh = std::max(0, std::min(nh, cpq - 1)); }
-  }
-  // after the first solution scouts 0 and 1 check choose-parent / rewire candidate batches (many tiles); scouts 2
-  // and 3 only work before it, one edge per job (3 tiles); the leader's own jobs (edges no record had) are rare
-  int h_lead = 0, h_s[MAX_SCOUTS] = {};
-  if (ns > 0) {
-    const int avail = nh - 1;  // minus the sampler
-    int lead_div = 3;  // SMP_LEAD_DIV: the leader's share of the helpers (C2: 1/3 3.82, 1/5 3.75, 1/8 3.73 M configs/s)
-    if (const char* e = std::getenv("SMP_LEAD_DIV")) lead_div = std::max(1, std::atoi(e));
-    h_lead = ns >= 2 ? avail / lead_div : avail / 2;
-    int rest = avail - h_lead;
-    int pre_h = 6;  // SMP_PRE_HELPERS: helpers of each pre-solution-only scout (its jobs: expand + connect edge, 6 tiles)
-    if (const char* e = std::getenv("SMP_PRE_HELPERS")) pre_h = std::max(0, std::atoi(e));
-    for (int s = 2; s < ns; ++s) { h_s[s] = std::min(pre_h, rest); rest -= h_s[s]; }
-    if (ns >= 2) { h_s[0] = rest - rest / 2; h_s[1] = rest / 2; } else { h_s[0] = rest; }
-  }
+  int lead_div = 3;  // SMP_LEAD_DIV: the leader's share of the helpers (C2: 1/3 3.82, 1/5 3.75, 1/8 3.73 M configs/s)
+  if (const char* e = std::getenv("SMP_LEAD_DIV")) lead_div = std::max(1, std::atoi(e));
+  int pre_h = 6;  // SMP_PRE_HELPERS: helpers of each pre-solution-only scout (its jobs: expand + connect edge, 6 tiles)
+  if (const char* e = std::getenv("SMP_PRE_HELPERS")) pre_h = std::max(0, std::atoi(e));
   // before the first solution a scout starts record k when the leader reaches k - pre_delay (DESIGN.md "Pre-solution
   // commits"); SMP_PRE_DELAY overrides it for experiments (0: at the request)
   int pre_delay = 3;
   if (const char* e = std::getenv("SMP_PRE_DELAY")) pre_delay = std::atoi(e);
   int pre_commit = 1;  // SMP_PRE_COMMIT=0: every iteration runs the full path (experiments)
   if (const char* e = std::getenv("SMP_PRE_COMMIT")) pre_commit = std::atoi(e);
-  for (int i = 0; i < nq; ++i) {
-    qdev[i].jb = nh > 0 ? p->qb[i].jb.p : nullptr;
-    qdev[i].sampler = nh >= 2;              // with two or more helpers, the last one runs ahead sampling
-    qdev[i].nworkers = ns > 0 ? 1 + h_lead : (nh >= 2 ? nh : 1 + nh);
-    qdev[i].nscouts = ns;
-    qdev[i].pre_delay = pre_delay;
-    qdev[i].pre_commit = pre_commit;
-    qdev[i].sampler_jb = p->qb[i].jb.p;
-    for (int s = 0; s < ns; ++s) {
-      qdev[i].sjbs[s] = p->qb[i].sjb[s].p;
-      qdev[i].scbs[s] = p->qb[i].scb[s].p;
-      qdev[i].svias[s] = p->qb[i].svia[s].p;
-      qdev[i].sworkers_s[s] = 1 + h_s[s];
+  int rebalance = nh_req == 0 ? 1 : 0;  // SMP_REBALANCE=0: keep the first launch's provisioning (experiments)
+  if (const char* e = std::getenv("SMP_REBALANCE")) rebalance = rebalance && std::atoi(e) != 0;
+  int nh = 0, ns = 0;
+  auto provision = [&](const std::vector<int>& act) {
+    const int na = std::max(1, (int)act.size());
+    const int cpq = std::max(1, slots / na);
+    nh = nh_req;
+    ns = 0;
+    if (nh == 0) {
+      if (want_scout) ns = cpq >= 64 ? 4 : cpq >= 18 ? 2 : cpq >= 6 ? 1 : 0;
+      if (want_scout && p->params.scout > 1) ns = std::min(p->params.scout, MAX_SCOUTS);
+      nh = want_scout ? std::min(cap_s, std::max(0, cpq - 1 - ns)) : std::min(63, std::max(0, cpq - 1));
+    } else if (nh > 0 && want_scout) {
+      ns = nh >= 16 ? 2 : nh >= 4 ? 1 : 0;
     }
-  }
+    if (want_scout && p->params.scout > 1) ns = std::min(p->params.scout, MAX_SCOUTS);  // explicit count
+    if (nh < 0) nh = 0;
+    if (nh < 4) ns = 0;
+    // an explicit request larger than what can be resident is clamped to the automatic count: a helper that never
+    // starts would leave its tiles to the leader's 8 us timeout on every job (helper sweeps: 250 helpers beside four
+    // scouts no longer all start on 256 CUs and stall)
+    if (1 + ns + nh > cpq) {
+      nh = std::max(0, want_scout ? std::min(cap_s, cpq - 1 - ns) : std::min(63, cpq - 1));
+      if (nh < 4) { ns = 0; nh = std::max(0, std::min(nh, cpq - 1)); }
+    }
+    // after the first solution scouts 0 and 1 check choose-parent / rewire candidate batches (many tiles); scouts 2
+    // and 3 only work before it, one edge per job (3 tiles); the leader's own jobs (edges no record had) are rare
+    int h_lead = 0, h_s[MAX_SCOUTS] = {};
+    if (ns > 0) {
+      const int avail = nh - 1;  // minus the sampler
+      h_lead = ns >= 2 ? avail / lead_div : avail / 2;
+      int rest = avail - h_lead;
+      for (int s = 2; s < ns; ++s) { h_s[s] = std::min(pre_h, rest); rest -= h_s[s]; }
+      if (ns >= 2) { h_s[0] = rest - rest / 2; h_s[1] = rest / 2; } else { h_s[0] = rest; }
+    }
+    for (int i : act) {
+      qdev[i].jb = nh > 0 ? p->qb[i].jb.p : nullptr;
+      qdev[i].sampler = nh >= 2;              // with two or more helpers, the last one runs ahead sampling
+      qdev[i].nworkers = ns > 0 ? 1 + h_lead : (nh >= 2 ? nh : 1 + nh);
+      qdev[i].nscouts = ns;
+      qdev[i].pre_delay = pre_delay;
+      qdev[i].pre_commit = pre_commit;
+      qdev[i].sampler_jb = p->qb[i].jb.p;
+      for (int s = 0; s < ns; ++s) {
+        qdev[i].sjbs[s] = p->qb[i].sjb[s].p;
+        qdev[i].scbs[s] = p->qb[i].scb[s].p;
+        qdev[i].svias[s] = p->qb[i].svia[s].p;
+        qdev[i].sworkers_s[s] = 1 + h_s[s];
+      }
+    }
+  };
+  // the queries to launch: those not decided on the host (an invalid start / goal or argument)
+  std::vector<int> act;
+  for (int i = 0; i < nq; ++i)
+    if (S[i].phase != 2 && S[i].status == 0) act.push_back(i);
+  std::vector<int> all(nq);
+  for (int i = 0; i < nq; ++i) all[i] = i;
+  provision(act.empty() ? all : act);
+  const int nh_first = nh, ns_first = ns;
   static int* trace_host = nullptr;
   const bool debug = std::getenv("SMP_DEBUG") != nullptr;
   if (debug && !trace_host) HIPCHK(hipHostMalloc(&trace_host, 256 * sizeof(int), hipHostMallocMapped));
@@ -994,10 +1014,27 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
   };
   HIPCHK(p->d_qdev.reserve(nq));
   HIPCHK(p->d_counts.reserve(2 * nq));
-  HIPCHK(hipMemcpyAsync(p->d_qdev.p, qdev.data(), nq * sizeof(QueryDev), hipMemcpyHostToDevice, p->stream));
-  HIPCHK(hipStreamSynchronize(p->stream));
+  HIPCHK(p->d_lfin.reserve(1));
+  // the launch's query records, compacted to the queries still running
+  std::vector<QueryDev> qlaunch;
+  auto upload_active = [&]() -> int {
+    qlaunch.clear();
+    const int quota = rebalance && act.size() >= 2 ? (int)act.size() / 2 : 0;
+    for (int i : act) {
+      qdev[i].lfin = p->d_lfin.p;
+      qdev[i].lquota = quota;
+      qlaunch.push_back(qdev[i]);
+    }
+    if (!qlaunch.empty())
+      HIPCHK(hipMemcpyAsync(p->d_qdev.p, qlaunch.data(), qlaunch.size() * sizeof(QueryDev), hipMemcpyHostToDevice,
+                            p->stream));
+    HIPCHK(hipStreamSynchronize(p->stream));
+    return SMP_OK;
+  };
+  if (int st = upload_active()) return st;
 
-  // launch loop: each launch advances every query by `chunk` iterations; time budgets use a device deadline
+  // launch loop: each launch advances every running query by up to `chunk` iterations; time budgets use a device
+  // deadline
   double tmax = 0;
   for (int i = 0; i < nq; ++i) if (qs[i].budget_kind == SMP_BUDGET_SECONDS) tmax = std::max(tmax, qs[i].budget);
   auto t_begin = std::chrono::steady_clock::now();
@@ -1009,14 +1046,17 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
   long long max_iters = 0;
   for (int i = 0; i < nq; ++i)
     if (qs[i].budget_kind != SMP_BUDGET_SECONDS) max_iters = std::max(max_iters, (long long)qs[i].budget);
-  for (;;) {
-    if (tmax == 0 && launches > max_iters / 256 + 64) return SMP_ERR_HIP;  // no progress: never spin forever
+  while (!act.empty()) {
+    // no progress: never spin forever (a launch ended early by finished queries counts too)
+    if (tmax == 0 && launches > max_iters / 256 + 64 + 2 * nq) return SMP_ERR_HIP;
     if (tmax > 0 && std::chrono::duration<double>(std::chrono::steady_clock::now() - t_begin).count() > tmax * 4 + 60)
       return SMP_ERR_HIP;
+    const int na = (int)act.size();
+    HIPCHK(hipMemsetAsync(p->d_lfin.p, 0, sizeof(unsigned), p->stream));
     if (nh > 0) {
       // fresh boards, then the helpers on their own (high-priority, separate hardware queue) stream; they wait
       // for the reset and leave when the leader signals stop
-      for (int i = 0; i < nq; ++i) {
+      for (int i : act) {
         HIPCHK(hipMemsetAsync(qdev[i].jb, 0, sizeof(JobBoard), p->stream));
         for (int s = 0; s < ns; ++s) {
           HIPCHK(hipMemsetAsync(qdev[i].sjbs[s], 0, sizeof(JobBoard), p->stream));
@@ -1029,17 +1069,17 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
     // scout s of query q at block scout_base + s * round8(nq) + q, scout_base a multiple of 8: blocks b and b + 8
     // are dealt to the same XCD (plan_kernel).  The leaders and scouts are queued before the helpers, so their
     // workgroups find CUs first (a scout queued behind 200 helpers was seen to start only when they left).
-    const int r8 = (nq + 7) / 8 * 8;
+    const int r8 = (na + 7) / 8 * 8;
     const int scout_base = ns > 0 ? r8 : 0;
-    const int grid = ns > 0 ? scout_base + (ns - 1) * r8 + nq : nq;
+    const int grid = ns > 0 ? scout_base + (ns - 1) * r8 + na : na;
     hipLaunchKernelGGL(plan_kernel, dim3(grid), dim3(BLOCK), 0, p->stream, p->d_rb, p->sc,
-                       p->d_mc, p->d_qdev.p, nq, scout_base, chunk);
+                       p->d_mc, p->d_qdev.p, na, scout_base, chunk);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(p->ev1, p->stream));
     if (nh > 0) {  // the helpers on their own (high-priority, separate hardware queue) stream, after the board reset
       HIPCHK(hipStreamWaitEvent(p->hstream, p->ev_board, 0));
-      hipLaunchKernelGGL(helper_kernel, dim3(nq * nh), dim3(BLOCK), 0, p->hstream, p->d_rb, p->sc, p->d_mc,
-                         p->d_qdev.p, nq);
+      hipLaunchKernelGGL(helper_kernel, dim3(na * nh), dim3(BLOCK), 0, p->hstream, p->d_rb, p->sc, p->d_mc,
+                         p->d_qdev.p, na);
       HIPCHK(hipGetLastError());
     }
     launches++;
@@ -1063,11 +1103,11 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
         }
       }
     }
-    for (int i = 0; i < nq; ++i)
+    for (int i : act)
       HIPCHK(hipMemcpyAsync(&S[i], qdev[i].st, sizeof(QState), hipMemcpyDeviceToHost, p->stream));
     if (ns > 0) {  // every scout's phase clocks, summed (per-pass averages divide by the summed pass count)
       HIPCHK(hipStreamSynchronize(p->stream));
-      for (int i = 0; i < nq; ++i)
+      for (int i : act)
         for (int sc = 0; sc < ns; ++sc) {
           unsigned long long sp[32];
           HIPCHK(hipMemcpy(sp, qdev[i].scbs[sc]->prof, sizeof(sp), hipMemcpyDeviceToHost));
@@ -1094,19 +1134,29 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
     total_ms += ms;
     if (std::getenv("SMP_DEBUG")) {
       JobBoard jbh;
-      if (nh > 0) HIPCHK(hipMemcpy(&jbh, qdev[0].jb, sizeof(JobBoard), hipMemcpyDeviceToHost));
-      std::fprintf(stderr, "[smp] launch %lld grid %d chunk %d: %.3f ms phase %d status %d iter %lld checked %lld"
-                   " board stop %d job %u tile0 %llx\n", (long long)launches, nq * (1 + nh), chunk, ms, S[0].phase,
-                   S[0].status, S[0].iter, S[0].checked, nh ? jbh.stop : -1, nh ? (unsigned)(jbh.pay[0] >> 32) : 0u,
+      const int i0 = act[0];
+      if (nh > 0) HIPCHK(hipMemcpy(&jbh, qdev[i0].jb, sizeof(JobBoard), hipMemcpyDeviceToHost));
+      std::fprintf(stderr, "[smp] launch %lld queries %d grid %d chunk %d: %.3f ms phase %d status %d iter %lld checked %lld"
+                   " board stop %d job %u tile0 %llx\n", (long long)launches, na, na * (1 + nh), chunk, ms, S[i0].phase,
+                   S[i0].status, S[i0].iter, S[i0].checked, nh ? jbh.stop : -1, nh ? (unsigned)(jbh.pay[0] >> 32) : 0u,
                    nh ? jbh.res[0] : 0ull);
     }
-    bool all_done = true;
-    for (int i = 0; i < nq; ++i) all_done &= (S[i].phase == 2 || S[i].status != 0);
-    if (all_done) break;
+    std::vector<int> still;
+    for (int i : act)
+      if (!(S[i].phase == 2 || S[i].status != 0)) still.push_back(i);
+    const bool shrank = still.size() < act.size();
+    act.swap(still);
+    if (act.empty()) break;
+    if (shrank) {
+      if (rebalance) provision(act);
+      if (int st = upload_active()) return st;
+    }
     if (chunk < 4096) chunk *= 2;
-    double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_begin).count();
-    (void)el;
   }
+  // path extraction reads every query's record: the full array again
+  HIPCHK(hipMemcpyAsync(p->d_qdev.p, qdev.data(), nq * sizeof(QueryDev), hipMemcpyHostToDevice, p->stream));
+  nh = nh_first;
+  ns = ns_first;
   p->last_plan_ms = total_ms;
   p->last_plan_launches = launches;
 

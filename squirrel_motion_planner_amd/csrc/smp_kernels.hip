@@ -309,6 +309,7 @@ struct PlanLds {
   int count_slot;  // profiling: phase the checked configurations are attributed to
   int job_seq;     // last job published by this leader (this launch)
   int in_job;      // a collision job is in flight (its helpers are busy): scans stay local
+  int go_end;      // the launch's finished-query quota is reached
   int smp_ver, smp_have_sol, smp_hit;  // run-ahead sampler: published parameter version / snapshot, slot hit
   int smp_pub;                         // the version changed this iteration: publish the parameters
   int spec, spec_nn;                   // overlap_work: what was computed during the last collision job, its result
@@ -4505,9 +4506,16 @@ __global__ void __launch_bounds__(BLOCK) plan_kernel(const RobotDev* __restrict_
   }
   for (int k = 0; k < iters; ++k) {
     if (uni(g_L.S.status != 0 || g_L.S.phase != 1)) break;
+    if (C.Q.lquota > 0 && (k & 7) == 7) {  // enough of the launch's queries finished: end it (resumable)
+      if (threadIdx.x == 0) g_L.go_end = ld_agent(C.Q.lfin) >= (unsigned)C.Q.lquota;
+      __syncthreads();
+      if (uni(g_L.go_end)) break;
+    }
     iteration(C);
   }
   if (threadIdx.x == 0) {
+    if (C.Q.lquota > 0 && (g_L.S.phase == 2 || g_L.S.status != 0))
+      __hip_atomic_fetch_add(C.Q.lfin, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (g_L.S.phase == 2 && g_L.S.t_end == 0) g_L.S.t_end = wall_clock64();
 #ifdef SMP_JOB_PROF
     if (C.Q.jb) {

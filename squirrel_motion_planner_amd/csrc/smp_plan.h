@@ -271,6 +271,11 @@ struct QueryDev {
   ViaNode* svia;
   int sworkers;
   int* trace;                  // debug only (SMP_DEBUG): host-mapped progress markers of the leader
+  // queries of this launch that finished in it (shared by all of the launch's queries); once it reaches lquota > 0
+  // every leader ends the launch after its current iteration, so that the host re-provisions the CUs of the
+  // finished queries to the others (DESIGN.md "Many queries")
+  unsigned* lfin;
+  int lquota;
   unsigned* ttff;              // host-mapped word set to 1 when the first feasible path is committed (null: none)
   int scan_min;                // nodes in a scan's range from which it is split over the helpers (0: never)
   int scan_pnn, scan_pnear;    // participants (this workgroup + helpers) of a split nearest / near scan, <= SCAN_P
