@@ -19,7 +19,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-S_SPHERES = 64          # spheres per configuration in the collision model
+S_SPHERES = 50 + 6      # collision model 2: 50 spheres + 6 exact box / cylinder primitives (one map test each)
 BYTES_PER_CONFIG = 64 + 8 * S_SPHERES   # config in + one 8-byte occupancy word per sphere
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8 TB/s
 
@@ -317,7 +317,7 @@ def main():
                        "queries_per_gpu": a.queries_per_gpu,
                        "budget_per_query": ("%d iterations" % a.iterations) if a.iterations else
                                            ("%d collision-checked samples" % a.samples),
-                       "robot": "robotino 8-DoF, 64-sphere model",
+                       "robot": "robotino 8-DoF, 50 spheres + 6 exact box / cylinder primitives (collision model 2)",
                        # helper workgroups per query as the library resolved them (0 = auto: the CUs left over by
                        # the queries; with a scout, split between the leader's and the scout's tiles + the sampler)
                        "helpers_per_query": int(step0["helpers"]), "scout": int(step0["scout"]),

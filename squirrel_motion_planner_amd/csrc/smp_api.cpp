@@ -925,6 +925,10 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
   if (const char* e = std::getenv("SMP_PRE_COMMIT")) pre_commit = std::atoi(e);
   int rebalance = nh_req == 0 ? 1 : 0;  // SMP_REBALANCE=0: keep the first launch's provisioning (experiments)
   if (const char* e = std::getenv("SMP_REBALANCE")) rebalance = rebalance && std::atoi(e) != 0;
+  // SMP_REBALANCE_DIV: a launch ends once 1/rb_div of its queries finished (C3, 64 queries: 2 / 4 / 8 all 10.1-10.3
+  // M configs/s; C5, 8 queries: 0.49 / 0.61 / 0.62 M)
+  int rb_div = 4;
+  if (const char* e = std::getenv("SMP_REBALANCE_DIV")) rb_div = std::max(1, std::atoi(e));
   int nh = 0, ns = 0;
   auto provision = [&](const std::vector<int>& act) {
     const int na = std::max(1, (int)act.size());
@@ -1019,7 +1023,7 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
   std::vector<QueryDev> qlaunch;
   auto upload_active = [&]() -> int {
     qlaunch.clear();
-    const int quota = rebalance && act.size() >= 2 ? (int)act.size() / 2 : 0;
+    const int quota = rebalance && act.size() >= 2 ? std::max(1, (int)act.size() / rb_div) : 0;
     for (int i : act) {
       qdev[i].lfin = p->d_lfin.p;
       qdev[i].lquota = quota;
