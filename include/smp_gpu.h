@@ -205,7 +205,12 @@ int smp_is_config_valid(smp_planner* p, const double q[8], int check_self, int c
 /* Every self pair that collides (2 link indices each, smp_robot_link_name, in the model's pair order -- the SRDF-enabled
  * link pairs i < j in link order, CC:378-388) and every collision link that touches the map (link indices in name
  * order, as the reference's std::map; disabled links included, CC:610-630).  Writes at most max_self pairs /
- * max_map links; *n_self / *n_map receive the full counts (the caller compares them with its capacity). */
+ * max_map links; *n_self / *n_map receive the full counts (the caller compares them with its capacity).
+ * Rigid pairs are left out, here as in every validity check: the 65 SRDF-enabled pairs of links on one rigid body
+ * (the reference's getSelfCollisions, CC:594-608, tests all 230) have the same relative pose in every configuration,
+ * so their outcome does not depend on it; an overlapping one would make every configuration invalid in the
+ * reference, and 7 of them overlap only under the conservative sphere covers (hand couplers / cranks against the
+ * hand base and finger links, door against shell) -- tests/test_host_cpu.py pins both facts. */
 int smp_get_collisions(smp_planner* p, const double q[8], int32_t* self_pairs, int max_self, int* n_self,
                        int32_t* map_links, int max_map, int* n_map);
 /* n poses, row-major n x 8: *first_invalid = index of the first pose in collision, -1 if all are valid. */
@@ -235,6 +240,12 @@ typedef struct smp_ik_result {
   double manipulability;    /* last manipulability measure (control_laws.cpp:6050-6089) */
 } smp_ik_result;
 
+/* Parity: bit for bit against the oracle (oracle/smp_oracle.cpp), which is unpinned against the reference here:
+ * the reference's manipulability (float Eigen::JacobiSVD, CL:6061-6084) and damped pseudo-inverse (fp64 SVD,
+ * CL:5574-5596) are restated as det / Gauss-Jordan with a Jacobi eigen-decomposition fallback (DESIGN.md "IK goal
+ * search"), equal in exact arithmetic; near singular Jacobians the iteration counts and REACHED / ADVANCED can
+ * differ from the reference binaries.  fallback_iterations counts the fallback branch; tests/test_gpu_ik.py checks
+ * that kernel and oracle take the same branch on singular starts. */
 int smp_ik_solve(smp_planner* p, const smp_ik_request* reqs, int n, smp_ik_result* out);
 
 typedef struct smp_goal_search {
@@ -250,6 +261,7 @@ typedef struct smp_goal_search {
  * current pose, candidate spacing in degrees (goal_pose_search_discretization, default 20; values < 1 count as 1).
  * *result: 0 = pose found (pose_goal written), 1 = every pose the controller reached collides (COLLISION_GOAL_POSE),
  * 2 = the controller reached no pose (INVALID_END_EFFECTOR_POSE) -- the reference's return codes.  info may be NULL. */
+/* (Unpinned against the reference near singular Jacobians as smp_ik_solve.) */
 int smp_find_goal_pose(smp_planner* p, const double ee_pose[6], const double pose_current[8], double discretization_deg,
                        int check_self, int check_map, double pose_goal[8], int* result, smp_goal_search* info);
 

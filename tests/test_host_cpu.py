@@ -159,3 +159,27 @@ def test_primitive_slabs_match_oracle(mk, orobot):
     want = orc.scene._slab
     assert np.array_equal(got, want)
     assert orobot.n_prim == 6 and (got < 65535).any()
+
+
+def test_rigid_pairs_are_configuration_independent():
+    """The SRDF-enabled pairs the model leaves out (smp_get_collisions, smp_gpu.h) are pairs of links on one rigid
+    body: their relative pose, and so their overlap, is the same in every configuration.  Under the sphere covers
+    exactly the 7 listed in smp_gpu.h overlap (cover artefacts of touching hand parts and of door / shell)."""
+    m = json.load(open(os.path.join(ROOT, "squirrel_motion_planner_amd", "data", "robotino_model.json")))
+    names = [e["name"] for e in m["links"]]
+    body = {e["link"]: e["body"] for e in m["link_bounds"]}
+    rigid = m["self_pairs_rigid_dropped"]
+    assert len(rigid) == 65 and m["self_pairs_srdf_enabled"] == len(rigid) + len(m["self_pairs"])
+    over = []
+    for a, b in rigid:
+        ia, ib = names.index(a), names.index(b)
+        assert body[ia] == body[ib], (a, b)
+        sa = [s for s in m["spheres"] if s["link"] == ia]
+        sb = [s for s in m["spheres"] if s["link"] == ib]
+        if sa and sb and min(np.linalg.norm(np.subtract(x["cb"], y["cb"])) - x["r"] - y["r"] for x in sa for y in sb) <= 0:
+            over.append((a, b))
+    assert sorted(over) == sorted([
+        ("hand_base_link", "hand_left_coupler"), ("hand_base_link", "hand_left_finger_lower_link"),
+        ("hand_base_link", "hand_right_coupler"), ("hand_left_crank", "hand_left_finger_lower_link"),
+        ("hand_left_coupler", "hand_right_coupler"), ("hand_right_crank", "hand_right_finger_lower_link"),
+        ("door_link", "shell_base_link")])
