@@ -28,6 +28,7 @@ __global__ void plan_kernel(const RobotDev* rb, SceneDev sc, const MapCfg* mc, Q
                             int iters);
 __global__ void helper_kernel(const RobotDev* rb, SceneDev sc, const MapCfg* mc, QueryDev* qs, int nq);
 __global__ void path_kernel(QueryDev* qs, int* counts);
+__global__ void boards_reset_kernel(const QueryDev* qs, int ns);
 size_t check_kernels_private_bytes();
 size_t ik_kernels_private_bytes();
 void launch_collisions(hipStream_t st, const RobotDev* rb, SceneDev sc, const MapCfg* mc, const double* q, int map,
@@ -141,11 +142,13 @@ struct smp_planner {
   int n_ttff = 0;
   // last plan (query 0) bookkeeping for smp_get_tree
   int last_n[2] = {0, 0};
+  int slots_cache = 0;  // resident_slots (occupancy queries) once per planner
 };
 
 // Workgroups of BLOCK threads that can be resident at once on the device, for the planner's kernels (leader / scout
 // plan_kernel and helper_kernel share the CUs): occupancy per CU (registers, LDS) x CUs.
-static int resident_slots(const smp_planner* p) {
+static int resident_slots(smp_planner* p) {
+  if (p->slots_cache > 0) return p->slots_cache;
   int occ_plan = 0, occ_help = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_plan, reinterpret_cast<const void*>(&plan_kernel), BLOCK, 0) !=
           hipSuccess ||
@@ -154,7 +157,8 @@ static int resident_slots(const smp_planner* p) {
     (void)hipGetLastError();
     return p->num_cus;
   }
-  return p->num_cus * std::max(1, std::min(occ_plan, occ_help));
+  p->slots_cache = p->num_cus * std::max(1, std::min(occ_plan, occ_help));
+  return p->slots_cache;
 }
 
 static int update_mapcfg(smp_planner* p) {
@@ -820,49 +824,28 @@ static QueryDev make_qdev(QueryBuffers& b, size_t cap, long long rows) {
   return d;
 }
 
-static int upload_roots(smp_planner* p, QueryBuffers& b, const QueryDev& d, const smp_query& q, size_t cap) {
-  for (int t = 0; t < 2; ++t) {
-    const double* root = t == 0 ? q.start : q.goal;
-    double col[NJ];
-    for (int j = 0; j < NJ; ++j) col[j] = root[j];
-    for (int j = 0; j < NJ; ++j)
-      HIPCHK(hipMemcpyAsync(d.tr[t].q + (size_t)j * cap, &col[j], sizeof(double), hipMemcpyHostToDevice, p->stream));
-    double zero = 0.0;
-    for (int k = 0; k < 3; ++k)
-      HIPCHK(hipMemcpyAsync(d.tr[t].cost + (size_t)k * cap, &zero, sizeof(double), hipMemcpyHostToDevice, p->stream));
-    int z = 0, m1 = -1;
-    HIPCHK(hipMemcpyAsync(d.tr[t].parent, &z, sizeof(int), hipMemcpyHostToDevice, p->stream));
-    HIPCHK(hipMemcpyAsync(d.tr[t].first_child, &m1, sizeof(int), hipMemcpyHostToDevice, p->stream));
-    HIPCHK(hipMemcpyAsync(d.tr[t].next_sib, &m1, sizeof(int), hipMemcpyHostToDevice, p->stream));
-    HIPCHK(hipMemcpyAsync(d.tr[t].prev_sib, &m1, sizeof(int), hipMemcpyHostToDevice, p->stream));
-  }
-  (void)b;
-  return SMP_OK;
-}
-
 // smp_plan_batch's body.  done[i] is set once out[i] holds query i's complete result; a call that fails on the way
 // (a HIP error, the no-progress guard) returns early, and smp_plan_batch then reports that status in every
 // result not yet complete.
 static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_result* out, std::vector<char>& done) {
   const auto t_entry = std::chrono::steady_clock::now();
   HIPCHK(hipSetDevice(p->device));
-  // init_planner validity of start and goal (birrt_star.cpp:350-362)
+  // arguments; init_planner's validity of start and goal (birrt_star.cpp:350-362) is the kernel's first step (its
+  // first launch checks both with the query's own self / map flags: no separate check launch and wait here)
   std::vector<int> status(nq, SMP_OK);
-  {
-    // per-query self/map flags may differ: check each query's pair with its own flags
-    for (int i = 0; i < nq; ++i) {
-      double pair[NJ * 2];
-      for (int j = 0; j < NJ; ++j) { pair[j * 2] = qs[i].start[j]; pair[j * 2 + 1] = qs[i].goal[j]; }
-      uint8_t v[2];
-      int st = smp_check_configs(p, pair, 2, qs[i].check_self, qs[i].check_map, v);
-      if (st) return st;
-      if (!v[0]) status[i] = SMP_ERR_START_INVALID;
-      else if (!v[1]) status[i] = SMP_ERR_GOAL_INVALID;
-      const int bk = qs[i].budget_kind;
-      if (!(qs[i].budget >= 0) || (bk != SMP_BUDGET_ITERATIONS && bk != SMP_BUDGET_SECONDS && bk != SMP_BUDGET_SAMPLES))
-        status[i] = SMP_ERR_ARG;
-    }
+  for (int i = 0; i < nq; ++i) {
+    const int bk = qs[i].budget_kind;
+    if (!(qs[i].budget >= 0) || (bk != SMP_BUDGET_ITERATIONS && bk != SMP_BUDGET_SECONDS && bk != SMP_BUDGET_SAMPLES))
+      status[i] = SMP_ERR_ARG;
   }
+  // SMP_HOST_PROF: microseconds from smp_plan entry to each host stage of the first launch (experiments)
+  const bool hprof = std::getenv("SMP_HOST_PROF") != nullptr;
+  auto hstamp = [&](const char* what) {
+    if (hprof)
+      std::fprintf(stderr, "[smp host] %-22s %8.1f us\n", what,
+                   std::chrono::duration<double>(std::chrono::steady_clock::now() - t_entry).count() * 1e6);
+  };
+  hstamp("arguments checked");
   if ((int)p->qb.size() < nq) p->qb.resize(nq);
   std::vector<QueryDev> qdev(nq);
   std::vector<QState> S(nq);
@@ -895,8 +878,7 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
     }
     if (status[i] != SMP_OK) { S[i].status = status[i]; S[i].phase = 2; }
     if (by_iter && iters <= 0 && S[i].phase == 0) S[i].max_iter = 0;
-    int st = upload_roots(p, p->qb[i], qdev[i], q, (size_t)cap);
-    if (st) return st;
+    // (the two roots are written by the kernel's first launch from QState::qs / qg: no per-word uploads)
     HIPCHK(hipMemcpyAsync(qdev[i].st, &S[i], sizeof(QState), hipMemcpyHostToDevice, p->stream));
   }
   // Workgroups per query (one per CU): the leader, its scouts and the helpers (DESIGN.md "Helpers", "Scouts").
@@ -1029,13 +1011,15 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
       qdev[i].lquota = quota;
       qlaunch.push_back(qdev[i]);
     }
+    // (qlaunch outlives the copy: it changes only after the next launch has completed)
     if (!qlaunch.empty())
       HIPCHK(hipMemcpyAsync(p->d_qdev.p, qlaunch.data(), qlaunch.size() * sizeof(QueryDev), hipMemcpyHostToDevice,
                             p->stream));
-    HIPCHK(hipStreamSynchronize(p->stream));
     return SMP_OK;
   };
+  hstamp("queries uploaded");
   if (int st = upload_active()) return st;
+  hstamp("provisioned");
 
   // launch loop: each launch advances every running query by up to `chunk` iterations; time budgets use a device
   // deadline
@@ -1060,15 +1044,11 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
     if (nh > 0) {
       // fresh boards, then the helpers on their own (high-priority, separate hardware queue) stream; they wait
       // for the reset and leave when the leader signals stop
-      for (int i : act) {
-        HIPCHK(hipMemsetAsync(qdev[i].jb, 0, sizeof(JobBoard), p->stream));
-        for (int s = 0; s < ns; ++s) {
-          HIPCHK(hipMemsetAsync(qdev[i].sjbs[s], 0, sizeof(JobBoard), p->stream));
-          HIPCHK(hipMemsetAsync(qdev[i].scbs[s], 0, sizeof(ScoutBoard), p->stream));
-        }
-      }
+      hipLaunchKernelGGL(boards_reset_kernel, dim3(na * (1 + 2 * ns)), dim3(BLOCK), 0, p->stream, p->d_qdev.p, ns);
+      HIPCHK(hipGetLastError());
       HIPCHK(hipEventRecord(p->ev_board, p->stream));
     }
+    if (launches == 0) hstamp("boards reset issued");
     HIPCHK(hipEventRecord(p->ev0, p->stream));
     // scout s of query q at block scout_base + s * round8(nq) + q, scout_base a multiple of 8: blocks b and b + 8
     // are dealt to the same XCD (plan_kernel).  The leaders and scouts are queued before the helpers, so their
@@ -1086,6 +1066,7 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
                          p->d_qdev.p, na);
       HIPCHK(hipGetLastError());
     }
+    if (launches == 0) hstamp("kernels launched");
     launches++;
     // time the first feasible path on the host: poll the flags while the launch runs
     {

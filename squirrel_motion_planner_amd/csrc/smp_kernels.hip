@@ -4485,6 +4485,32 @@ __global__ void __launch_bounds__(BLOCK) plan_kernel(const RobotDev* __restrict_
 #endif
   }
   __syncthreads();
+  if (uni(g_L.S.status == 0 && g_L.S.phase == 0)) {
+    // first launch: init_planner's validity of start and goal (birrt_star.cpp:350-362), one collision tile
+    if (threadIdx.x < 2 * NJ) {
+      const int c = threadIdx.x / NJ, j = threadIdx.x - c * NJ;
+      g_L.u.tile.tq[c][j] = c == 0 ? g_L.S.qs[j] : g_L.S.qg[j];
+    }
+    __syncthreads();
+    collide_tile<PLAN_CT>((&g_rb), C.sc, (&g_mc), 2, g_L.u.tile.tq, g_L.S.self, g_L.S.map, g_L.u.tile.T);
+    if (threadIdx.x == 0 && (g_L.u.tile.T.coll[0] || g_L.u.tile.T.coll[1])) {
+      g_L.S.status = g_L.u.tile.T.coll[0] ? -2 : -3;  // SMP_ERR_START_INVALID / SMP_ERR_GOAL_INVALID
+      g_L.S.phase = 2;
+    }
+    __syncthreads();
+  }
+  if (uni(g_L.S.status == 0 && g_L.S.phase == 0) && threadIdx.x < 2) {
+    // first launch: the two roots (init_planner, birrt_star.cpp:386-443) from the query's start / goal
+    const int t = threadIdx.x, cap = g_L.S.cap;
+    const TreeDev& T = C.Q.tr[t];
+    for (int j = 0; j < NJ; ++j) T.q[(size_t)j * cap] = t == 0 ? g_L.S.qs[j] : g_L.S.qg[j];
+    for (int k = 0; k < 3; ++k) T.cost[(size_t)k * cap] = 0.0;
+    T.parent[0] = 0;
+    T.first_child[0] = -1;
+    T.next_sib[0] = -1;
+    T.prev_sib[0] = -1;
+  }
+  __syncthreads();
   // the last PATCH_K nodes of each tree -> the LDS copy kept by insert_node / insert_via
   for (int it = threadIdx.x; it < 2 * PATCH_K * NJ; it += BLOCK) {
     const int t = it / (PATCH_K * NJ), r = it - t * (PATCH_K * NJ), k = r / NJ, j = r - k * NJ;
@@ -4637,6 +4663,20 @@ __global__ void __launch_bounds__(BLOCK) helper_kernel(const RobotDev* __restric
     return;
   }
   helper_main(g_ctx, role, J);
+}
+
+// Fresh job / scout boards for a launch (all zero: no granule carries a job number, no stop flag): block b clears
+// board b % (1 + 2 ns) of query b / (1 + 2 ns) -- the leader's job board, then each scout's job and record board.
+// One launch instead of a memset per board (each costs the host a few microseconds before the planner starts).
+__global__ void __launch_bounds__(BLOCK) boards_reset_kernel(const QueryDev* qs, int ns) {
+  const int per = 1 + 2 * ns, q = (int)blockIdx.x / per, w = (int)blockIdx.x - q * per;
+  const QueryDev& Q = qs[q];
+  char* base = w == 0 ? (char*)Q.jb : w <= ns ? (char*)Q.sjbs[w - 1] : (char*)Q.scbs[w - 1 - ns];
+  const size_t bytes = w == 0 || w <= ns ? sizeof(JobBoard) : sizeof(ScoutBoard);
+  uint4* p4 = reinterpret_cast<uint4*>(base);
+  const size_t n4 = bytes / sizeof(uint4);
+  for (size_t i = threadIdx.x; i < n4; i += BLOCK) p4[i] = make_uint4(0u, 0u, 0u, 0u);
+  for (size_t i = n4 * sizeof(uint4) + threadIdx.x; i < bytes; i += BLOCK) base[i] = 0;
 }
 
 __global__ void path_kernel(QueryDev* qs, int* counts) {
