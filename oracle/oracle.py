@@ -90,6 +90,8 @@ def lib():
         L.orc_get_tree.restype = _i
         L.orc_get_cost_rows.argtypes = [ctypes.c_void_p, _pd]
         L.orc_get_cost_rows.restype = _i
+        L.orc_get_cost_row_times.argtypes = [ctypes.c_void_p, _pd]
+        L.orc_get_cost_row_times.restype = _i
         L.orc_ik_solve.argtypes = [ctypes.c_void_p, _pd, _i, _i, _pd, _pi]
         L.orc_ik_goal.argtypes = [_pd, _pd]
         L.orc_ik_fk_jac.argtypes = [ctypes.c_void_p, _pd, _i, _pd, _pd]
@@ -425,6 +427,11 @@ class Oracle:
             if nr:
                 lib().orc_get_cost_rows(self.h, _p(rows, _d))
             out["cost_rows"] = rows
+            # wall-clock seconds of each row from the planning start (reports only; the rows keep time 0)
+            tr = np.zeros(nr)
+            if nr:
+                lib().orc_get_cost_row_times(self.h, _p(tr, _d))
+            out["cost_row_times"] = tr
         return out
 
 

@@ -483,6 +483,7 @@ struct Planner {
   long long iter = 0;
   Stats st;
   std::vector<std::array<double, 5>> cost_rows;  // BS:1325-1331 (time column = 0 for determinism)
+  std::vector<double> cost_row_time;              // the rows' wall-clock seconds from the planning start (reports)
   std::chrono::steady_clock::time_point t0;
 
   double dist(const Conf& a, const Conf& b) const {  // DH:128-156
@@ -1061,6 +1062,7 @@ struct Planner {
       std::swap(A, B);
       iter++;
       cost_rows.push_back({(double)iter, 0.0, cbest, cbest_rev, cbest_prism});
+      cost_row_time.push_back(std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
       if ((cbest - h0.total) < P.opt_thresh) break;  // BS:1333-1338 (start root cost_h.total = h0.total)
     }
     st.iterations = iter;
@@ -1878,6 +1880,12 @@ int orc_find_goal_pose(void* hp, const double* ee, const double* cur, double dis
   }
   if (info) { info[0] = (long long)ts.size(); info[1] = -1; info[2] = iters; }
   return found ? 1 : 2;
+}
+
+int orc_get_cost_row_times(void* hp, double* t) {
+  orc_handle* h = (orc_handle*)hp;
+  if (t) for (size_t i = 0; i < h->pl->cost_row_time.size(); ++i) t[i] = h->pl->cost_row_time[i];
+  return (int)h->pl->cost_row_time.size();
 }
 
 int orc_get_cost_rows(void* hp, double* rows) {

@@ -49,7 +49,8 @@ def c4(a):
         max_iter=int(r["iterations"]))
     same = bool(o["iterations"] == r["iterations"] and o["checked"] == r["configs_checked"] and
                 o["cost"] == r["cost_best"])
-    rg, ro = changes(r["cost_rows"]), changes(o["cost_rows"])
+    orows = [[row[0], t, row[2], row[3], row[4]] for row, t in zip(o["cost_rows"], o["cost_row_times"])]
+    rg, ro = changes(r["cost_rows"]), changes(orows)
     out = {"config": "C4 narrow passage, slot 0.24 m at z 0.55-0.79, seed %d, path_optimality_threshold=-inf"
                      % a.seed,
            "gpu": {"seconds_budget": a.seconds, "wall_s": wall, "iterations": int(r["iterations"]),
