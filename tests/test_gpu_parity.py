@@ -341,6 +341,27 @@ def test_c3_bench_share_full_budget(orobot, robot):
         _same_query_result(r, o)
 
 
+def test_many_queries_reprovisioned_match_oracle(orobot, robot):
+    """Many queries with staggered budgets (24 random C3 pairs, 40 .. 730 iterations): launches end as quarters of
+    the running queries finish and the finished queries' CUs go to the others (more helpers, scouts appearing), several
+    times in one call (DESIGN.md "Many queries"); every query still equals its oracle run."""
+    gp2 = GpuPlanner(robot)
+    sc, gscene, osc = scene_pair("c2")
+    gp2.set_scene(gscene)
+    pairs = scenes.random_queries(sc, 24, seed=7, check=lambda q: bool(gp2.check_configs([q])[0]))
+    assert len(pairs) == 24
+    budgets = [40 + 30 * k for k in range(24)]
+    qs = [GpuPlanner.make_query(s, g, sc.env_x, sc.env_y, iterations=b, seed=5, query_id=k)
+          for k, ((s, g), b) in enumerate(zip(pairs, budgets))]
+    rs = gp2.plan_batch(qs)
+    _, _, launches = gp2.last_kernel_ms()
+    assert launches >= 4  # re-provisioned more than once
+    orc = O.Oracle(orobot, osc)
+    for k, ((s, g), r) in enumerate(zip(pairs, rs)):
+        o = orc.plan(s, g, env_x=sc.env_x, env_y=sc.env_y, max_iter=budgets[k], seed=5, query=k)
+        _same_query_result(r, o)
+
+
 @pytest.fixture(scope="module")
 def c5_pair():
     sc = scenes.clutter_cloud()
