@@ -212,12 +212,13 @@ def main():
         a.queries_per_gpu = 8
     # every rank builds the same scene description (seeded); only rank 0 turns it into the grid
     sc = scenes.clutter_cloud() if a.workload == "c5" else scenes.box_room()
-    # scene: rank 0 builds the grid (octomap keys -> bitset + box-gap field) and broadcasts it once (RCCL/xGMI)
-    s0 = Scene.from_keys(sc.keys, sc.res) if rank == 0 else None
-    scene = D.broadcast_scene(s0, device="cuda") if world > 1 else s0
-
+    # scene: rank 0 builds the grid (octomap keys -> bitset + box-gap field + slab fields) and sets it on its GPU;
+    # the other ranks receive its device arrays in one RCCL broadcast over xGMI, device to device (no host rebuild)
     gp = GpuPlanner(device=local, path_optimality_threshold=-math.inf, helpers=a.helpers, scout=a.scout)
-    gp.set_scene(scene)
+    if rank == 0:
+        gp.set_scene(Scene.from_keys(sc.keys, sc.res))
+    if world > 1:
+        D.broadcast_planner_scene(gp, src=0)
 
     # (start, goal) of every query of the job: C2 repeats its own pair; C3/C5 draw world * queries_per_gpu
     # collision-free pairs (scenes.random_queries, seed 7) and each rank takes its own slice (no collective)

@@ -22,6 +22,11 @@
  *                              + getJointTrajectoryRef (squirrel_8dof_planner.cpp:1221-1248,
  *                              birrt_star.cpp:335-536, 983-1407, 1688-1691)
  *   smp_plan_batch             independent queries against one scene (one workgroup each)
+ *   smp_plan_multi             the same over several planners / GPUs of one process (the node is one process:
+ *                              squirrel_8dof_planner_node.cpp:6-15), queries dealt round-robin
+ *   smp_planner_scene_device   setOctree's copy of the map for further GPUs: the planner's device-resident scene
+ *   smp_planner_set_scene_device  (RCCL broadcast between ranks, xGMI peer copies between planners) instead of a
+ *   smp_planners_share_scene   host rebuild per GPU
  *   smp_check_configs          batched isConfigValid (birrt_star.cpp:6897-6908) -> valid flags
  *   smp_is_config_valid        BiRRTstarPlanner::isConfigValid for one configuration
  *   smp_get_collisions         BiRRTstarPlanner::getCollisions (birrt_star.cpp:6910-6914 -> collision_checker.hpp:
@@ -193,8 +198,40 @@ int smp_planner_set_params(smp_planner* p, const smp_params* params);
 int smp_planner_get_params(const smp_planner* p, smp_params* params);
 int smp_set_disabled_map_links(smp_planner* p, const char* const* link_names, int n);
 
+/* Multi-GPU (queries shard, the scene is sent once per scene, no per-iteration collective).
+ * The device-resident form of a planner's scene: the arrays smp_planner_set_scene derived for the planner's robot
+ * (4x4x4 occupancy bricks, the box-gap field, its byte copy when every sphere threshold is below 255, one 2-D slab field
+ * per exact primitive).  They move device to device: between ranks by an RCCL broadcast into caller buffers
+ * (squirrel_motion_planner_amd/distributed.py), between the planners of one process by peer copies over xGMI
+ * (smp_planners_share_scene).  The sender's and the receiver's robot must be the same model. */
+typedef struct smp_scene_device {
+  int dims[3];             /* cells x, y, z */
+  double origin[3];
+  double resolution;
+  int64_t n_bricks;        /* uint64 words: ceil(x/4) * ceil(y/4) * ceil(z/4) */
+  int64_t n_cells;         /* x * y * z: uint16 box-gap values (and bytes of the byte copy) */
+  int n_prim;              /* slab planes of x * y uint16 values */
+  int has_d2b;             /* the byte copy is part of the scene */
+  uint64_t* bricks;        /* device pointers (any GPU of this process, or caller-owned buffers on the planner's GPU) */
+  uint16_t* d2;
+  uint8_t* d2b;
+  uint16_t* slab;
+} smp_scene_device;
+/* Geometry and sizes of the planner's device scene; each non-NULL pointer of *io receives a device-to-device copy of
+ * that array (caller-allocated, on any GPU).  SMP_ERR_ARG if the planner has no scene. */
+int smp_planner_scene_device(const smp_planner* p, smp_scene_device* io);
+/* Sets the planner's scene from device arrays laid out as above (copied: the caller keeps ownership); the robot-derived
+ * parts must match this planner's robot (SMP_ERR_ARG otherwise).  Replaces smp_planner_set_scene on receiving ranks. */
+int smp_planner_set_scene_device(smp_planner* p, const smp_scene_device* in);
+/* ps[src]'s scene to every other planner of the array (peer copies over xGMI for planners on other GPUs). */
+int smp_planners_share_scene(smp_planner* const* ps, int n, int src);
+
 int smp_plan(smp_planner* p, const smp_query* q, smp_result* out);
 int smp_plan_batch(smp_planner* p, const smp_query* q, int n, smp_result* out);
+/* Independent queries over several planners (typically one per GPU, sharing a scene): query i runs on planner
+ * i % n_planners, all planners concurrently (one host thread each); out[i] is query i's result, identical to what
+ * smp_plan on that planner returns.  Each planner may appear once. */
+int smp_plan_multi(smp_planner* const* planners, int n_planners, const smp_query* q, int n, smp_result* out);
 void smp_result_free(smp_result* r);
 
 /* Tree dump of the last smp_plan (which: 0 start tree, 1 goal tree) for parity checks; arrays may be NULL. */

@@ -81,6 +81,12 @@ class GoalSearch(ctypes.Structure):
     _fields_ = [("n_candidates", _i), ("n_reached", _i), ("chosen", _i), ("downward", _i), ("kernel_ms", _d)]
 
 
+class SceneDevice(ctypes.Structure):
+    """smp_scene_device: a planner's device-resident scene (geometry, sizes, device pointers)."""
+    _fields_ = [("dims", _i * 3), ("origin", _d * 3), ("resolution", _d), ("n_bricks", _i64), ("n_cells", _i64),
+                ("n_prim", _i), ("has_d2b", _i), ("bricks", _p), ("d2", _p), ("d2b", _p), ("slab", _p)]
+
+
 # (name, restype, argtypes) of every symbol declared in include/smp_gpu.h
 EXPORTS = [
     ("smp_params_default", None, [ctypes.POINTER(Params)]),
@@ -107,6 +113,10 @@ EXPORTS = [
     ("smp_set_disabled_map_links", _i, [_p, ctypes.POINTER(ctypes.c_char_p), _i]),
     ("smp_plan", _i, [_p, ctypes.POINTER(Query), ctypes.POINTER(Result)]),
     ("smp_plan_batch", _i, [_p, ctypes.POINTER(Query), _i, ctypes.POINTER(Result)]),
+    ("smp_plan_multi", _i, [ctypes.POINTER(_p), _i, ctypes.POINTER(Query), _i, ctypes.POINTER(Result)]),
+    ("smp_planner_scene_device", _i, [_p, ctypes.POINTER(SceneDevice)]),
+    ("smp_planner_set_scene_device", _i, [_p, ctypes.POINTER(SceneDevice)]),
+    ("smp_planners_share_scene", _i, [ctypes.POINTER(_p), _i, _i]),
     ("smp_result_free", None, [ctypes.POINTER(Result)]),
     ("smp_get_tree", _i64, [_p, _i, _p, _p, _p]),
     ("smp_check_configs", _i, [_p, _pd, _i64, _i, _i, _p]),

@@ -12,6 +12,7 @@
 #include <stdexcept>
 #include <string>
 #include <array>
+#include <thread>
 #include <vector>
 
 #include "../../include/smp_gpu.h"
@@ -488,6 +489,115 @@ int smp_planner_set_scene(smp_planner* p, const smp_scene* s) {
   p->have_scene = true;
   p->scene_res = s->h.res;
   return update_mapcfg(p);
+}
+
+// Device-resident scene of a planner (multi-GPU): the arrays smp_planner_set_scene derived for
+// this robot (bricks, box-gap field, its byte copy, the primitives' slab fields) travel device to device -- an RCCL
+// broadcast between ranks, or peer copies over xGMI between the planners of one process -- instead of being rebuilt
+// from a host scene on every GPU.
+static void scene_layout(const smp_planner* p, smp_scene_device* o) {
+  o->dims[0] = p->sc.nx; o->dims[1] = p->sc.ny; o->dims[2] = p->sc.nz;
+  o->origin[0] = p->sc.ox; o->origin[1] = p->sc.oy; o->origin[2] = p->sc.oz;
+  o->resolution = p->sc.res;
+  o->n_bricks = (int64_t)p->sc.bnx * p->sc.bny * (((int64_t)p->sc.nz + 3) / 4);
+  o->n_cells = (int64_t)p->sc.nx * p->sc.ny * p->sc.nz;
+  o->n_prim = p->robot.dev.n_prim;
+  o->has_d2b = p->sc.d2b != nullptr;
+}
+
+int smp_planner_scene_device(const smp_planner* p, smp_scene_device* io) {
+  if (!p || !io) return SMP_ERR_ARG;
+  if (!p->have_scene) return SMP_ERR_ARG;
+  HIPCHK(hipSetDevice(p->device));
+  uint64_t* bricks = io->bricks;
+  uint16_t* d2 = io->d2;
+  uint8_t* d2b = io->d2b;
+  uint16_t* slab = io->slab;
+  scene_layout(p, io);
+  io->bricks = bricks; io->d2 = d2; io->d2b = d2b; io->slab = slab;
+  const size_t plane = (size_t)p->sc.nx * p->sc.ny;
+  if (bricks) HIPCHK(hipMemcpyAsync(bricks, p->sc.bricks, io->n_bricks * sizeof(uint64_t), hipMemcpyDefault, p->stream));
+  if (d2) HIPCHK(hipMemcpyAsync(d2, p->sc.d2, io->n_cells * sizeof(uint16_t), hipMemcpyDefault, p->stream));
+  if (d2b && io->has_d2b) HIPCHK(hipMemcpyAsync(d2b, p->sc.d2b, io->n_cells, hipMemcpyDefault, p->stream));
+  if (slab && io->n_prim > 0)
+    HIPCHK(hipMemcpyAsync(slab, p->d_slab.p, plane * io->n_prim * sizeof(uint16_t), hipMemcpyDefault, p->stream));
+  HIPCHK(hipStreamSynchronize(p->stream));
+  return SMP_OK;
+}
+
+int smp_planner_set_scene_device(smp_planner* p, const smp_scene_device* in) {
+  if (!p || !in || !in->bricks || !in->d2) return SMP_ERR_ARG;
+  const int nx = in->dims[0], ny = in->dims[1], nz = in->dims[2];
+  if (nx <= 0 || ny <= 0 || nz <= 0 || !(in->resolution > 0)) return SMP_ERR_ARG;
+  const RobotDev& d = p->robot.dev;
+  const int bnx = (nx + 3) / 4, bny = (ny + 3) / 4, bnz = (nz + 3) / 4;
+  const size_t nb = (size_t)bnx * bny * bnz, nc = (size_t)nx * ny * nz, plane = (size_t)nx * ny;
+  // the derived arrays depend on the robot (slab z ranges, the byte field's threshold condition): the sender's
+  // robot must be this one's
+  uint32_t tmax = 0;
+  for (int k = 0; k < d.n_sph; ++k) tmax = std::max(tmax, sphere_threshold(d.sph_r[k], in->resolution));
+  if (in->n_bricks != (int64_t)nb || in->n_cells != (int64_t)nc || in->n_prim != d.n_prim ||
+      (in->has_d2b != 0) != (tmax < 255) || (in->has_d2b && !in->d2b) || (d.n_prim > 0 && !in->slab))
+    return SMP_ERR_ARG;
+  for (int k = 0; k < d.n_prim; ++k)
+    if (d.prim_rxy[k] > GRID_REACH) return SMP_ERR_ARG;
+  HIPCHK(hipSetDevice(p->device));
+  HIPCHK(p->d_bricks.reserve(nb));
+  HIPCHK(p->d_d2.reserve(nc));
+  // hipMemcpyDefault: a source on another GPU is a peer copy (xGMI), one on this GPU a device copy
+  HIPCHK(hipMemcpyAsync(p->d_bricks.p, in->bricks, nb * sizeof(uint64_t), hipMemcpyDefault, p->stream));
+  HIPCHK(hipMemcpyAsync(p->d_d2.p, in->d2, nc * sizeof(uint16_t), hipMemcpyDefault, p->stream));
+  p->sc.d2b = nullptr;
+  if (in->has_d2b) {
+    HIPCHK(p->d_d2b.reserve(nc));
+    HIPCHK(hipMemcpyAsync(p->d_d2b.p, in->d2b, nc, hipMemcpyDefault, p->stream));
+    p->sc.d2b = p->d_d2b.p;
+  }
+  for (int k = 0; k < MAX_PRIM; ++k) p->sc.slab[k] = nullptr;
+  if (d.n_prim > 0) {
+    HIPCHK(p->d_slab.reserve(plane * d.n_prim));
+    HIPCHK(hipMemcpyAsync(p->d_slab.p, in->slab, plane * d.n_prim * sizeof(uint16_t), hipMemcpyDefault, p->stream));
+    for (int k = 0; k < d.n_prim; ++k) p->sc.slab[k] = p->d_slab.p + k * plane;
+  }
+  HIPCHK(hipStreamSynchronize(p->stream));  // the caller may release its buffers on return
+  p->sc.nx = nx; p->sc.ny = ny; p->sc.nz = nz;
+  p->sc.bnx = bnx; p->sc.bny = bny;
+  p->sc.ox = in->origin[0]; p->sc.oy = in->origin[1]; p->sc.oz = in->origin[2];
+  p->sc.res = in->resolution; p->sc.inv_res = 1.0 / in->resolution;
+  p->sc.bricks = p->d_bricks.p;
+  p->sc.d2 = p->d_d2.p;
+  p->have_scene = true;
+  p->scene_res = in->resolution;
+  return update_mapcfg(p);
+}
+
+int smp_planners_share_scene(smp_planner* const* ps, int n, int src) {
+  if (!ps || n <= 0 || src < 0 || src >= n || !ps[src]) return SMP_ERR_ARG;
+  smp_scene_device v{};
+  int rc = smp_planner_scene_device(ps[src], &v);
+  if (rc != SMP_OK) return rc;
+  v.bricks = ps[src]->d_bricks.p;
+  v.d2 = ps[src]->d_d2.p;
+  v.d2b = ps[src]->sc.d2b ? ps[src]->d_d2b.p : nullptr;
+  v.slab = v.n_prim > 0 ? ps[src]->d_slab.p : nullptr;
+  for (int i = 0; i < n; ++i) {
+    if (i == src) continue;
+    if (!ps[i]) return SMP_ERR_ARG;
+    if (ps[i]->device != ps[src]->device) {
+      // direct peer reads over xGMI where the pair allows it (else the runtime stages the copy)
+      int can = 0;
+      HIPCHK(hipDeviceCanAccessPeer(&can, ps[i]->device, ps[src]->device));
+      if (can) {
+        HIPCHK(hipSetDevice(ps[i]->device));
+        const hipError_t e = hipDeviceEnablePeerAccess(ps[src]->device, 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIPCHK(e);
+        (void)hipGetLastError();
+      }
+    }
+    rc = smp_planner_set_scene_device(ps[i], &v);
+    if (rc != SMP_OK) return rc;
+  }
+  return SMP_OK;
 }
 
 int smp_set_disabled_map_links(smp_planner* p, const char* const* names, int n) {
@@ -1255,6 +1365,40 @@ extern "C" int smp_plan_batch(smp_planner* p, const smp_query* qs, int nq, smp_r
 }
 
 extern "C" int smp_plan(smp_planner* p, const smp_query* q, smp_result* out) { return smp_plan_batch(p, q, 1, out); }
+
+// Queries dealt round-robin over the planners (query i -> planner i % np), one host thread per planner, so the
+// planners' GPUs plan concurrently; out[i] is query i's result.  The return code is the first non-OK status in query
+// order, as smp_plan_batch's.
+extern "C" int smp_plan_multi(smp_planner* const* ps, int np, const smp_query* qs, int nq, smp_result* out) {
+  if (!ps || np <= 0 || !qs || nq <= 0 || !out) return SMP_ERR_ARG;
+  for (int i = 0; i < nq; ++i) std::memset(&out[i], 0, sizeof(smp_result));
+  for (int k = 0; k < np; ++k)
+    for (int j = 0; j <= k; ++j)
+      if (!ps[k] || (j < k && ps[k] == ps[j])) {  // a planner is not thread-safe: each at most once
+        for (int i = 0; i < nq; ++i) out[i].status = SMP_ERR_ARG;
+        return SMP_ERR_ARG;
+      }
+  const int used = std::min(np, nq);
+  std::vector<std::vector<smp_query>> part(used);
+  std::vector<std::vector<smp_result>> res(used);
+  for (int i = 0; i < nq; ++i) part[i % used].push_back(qs[i]);
+  std::vector<int> rcs(used, SMP_OK);
+  std::vector<std::thread> th;
+  th.reserve(used);
+  for (int k = 0; k < used; ++k) {
+    res[k].resize(part[k].size());
+    th.emplace_back([&, k] { rcs[k] = smp_plan_batch(ps[k], part[k].data(), (int)part[k].size(), res[k].data()); });
+  }
+  for (auto& t : th) t.join();
+  int rc = SMP_OK;
+  for (int i = 0; i < nq; ++i) {
+    out[i] = res[i % used][i / used];
+    if (rc == SMP_OK && out[i].status != SMP_OK) rc = out[i].status;
+  }
+  for (int k = 0; k < used; ++k)
+    if (rc == SMP_OK && rcs[k] != SMP_OK) rc = rcs[k];
+  return rc;
+}
 
 extern "C" void smp_result_free(smp_result* r) {
   if (!r) return;

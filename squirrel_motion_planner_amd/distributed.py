@@ -18,7 +18,8 @@ def shard_queries(n_queries, world, rank):
 
 
 def broadcast_scene(scene, device="cpu", src=0):
-    """Rank `src` passes its Scene (others None); every rank returns an equivalent Scene.
+    """Rank `src` passes its Scene (others None); every rank returns an equivalent Scene (host form, for ranks that
+    need the host grid; planners take broadcast_planner_scene's device-to-device path instead).
 
     One broadcast of the header (dims, origin, resolution) and one each of the occupancy bitset and the
     box-gap field; ranks other than `src` rebuild their brick masks from the bitset (smp_scene_from_grid).
@@ -49,6 +50,56 @@ def broadcast_scene(scene, device="cpu", src=0):
         return scene
     d2 = td.cpu().numpy().view(np.uint16)[:nc].copy()
     return Scene.from_grid(tb.cpu().numpy().view(np.uint64), d2, dims, origin, res)
+
+
+def _scene_offsets(n_bricks, n_cells, n_prim, plane, has_d2b):
+    """Byte offsets of the arrays of a device scene in one flat broadcast buffer (8-byte aligned) and its size."""
+    al = lambda n: (n + 7) // 8 * 8
+    o_bricks = 0
+    o_d2 = o_bricks + al(8 * n_bricks)
+    o_d2b = o_d2 + al(2 * n_cells)
+    o_slab = o_d2b + (al(n_cells) if has_d2b else 0)
+    return o_bricks, o_d2, o_d2b, o_slab, o_slab + al(2 * plane * n_prim)
+
+
+def broadcast_planner_scene(gp, src=0, device=None):
+    """The scene of rank `src`'s planner to every rank's planner, device to device: one broadcast of a small header
+    and ONE broadcast of the device-resident arrays (bricks, box-gap field, its byte copy, the primitives' slab fields)
+    -- RCCL over xGMI with the nccl backend -- straight from the sender's planner buffers into the receivers'
+    (smp_planner_scene_device / smp_planner_set_scene_device); nothing is rebuilt or staged on a host.
+
+    Rank `src` must have set its planner's scene (GpuPlanner.set_scene); the ranks' robots must be the same model.
+    Returns the number of payload bytes broadcast."""
+    from . import _lib as L
+    rank = dist.get_rank()
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    meta = torch.zeros(11, dtype=torch.float64, device=dev)
+    if rank == src:
+        v = gp.scene_device()
+        meta[:] = torch.tensor(list(v.dims) + list(v.origin) + [v.resolution, v.n_bricks, v.n_cells, v.n_prim,
+                                                                 v.has_d2b], dtype=torch.float64)
+    dist.broadcast(meta, src)
+    m = meta.tolist()
+    dims = [int(x) for x in m[0:3]]
+    n_bricks, n_cells, n_prim, has_d2b = int(m[7]), int(m[8]), int(m[9]), int(m[10])
+    plane = dims[0] * dims[1]
+    o_b, o_d, o_db, o_s, total = _scene_offsets(n_bricks, n_cells, n_prim, plane, has_d2b)
+    buf = torch.empty(total, dtype=torch.uint8, device=dev)
+    base = buf.data_ptr()
+    ptrs = dict(bricks=base + o_b, d2=base + o_d, d2b=base + o_db if has_d2b else 0, slab=base + o_s if n_prim else 0)
+    if rank == src:
+        gp.scene_device(**ptrs)  # the planner's arrays into the broadcast buffer (device copies)
+    dist.broadcast(buf, src)
+    if rank != src:
+        v = L.SceneDevice()
+        for k in range(3):
+            v.dims[k] = dims[k]
+            v.origin[k] = m[3 + k]
+        v.resolution = m[6]
+        v.n_bricks, v.n_cells, v.n_prim, v.has_d2b = n_bricks, n_cells, n_prim, has_d2b
+        torch.cuda.synchronize(dev)  # the broadcast has landed before the library's stream reads the buffer
+        gp.set_scene_device(v, **ptrs)
+    return total
 
 
 def reduce_counters(values, device="cpu"):

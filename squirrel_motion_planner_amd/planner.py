@@ -184,6 +184,23 @@ class GpuPlanner:
         check(lib().smp_planner_set_scene(self.h, scene.h), "smp_planner_set_scene")
         self.scene = scene
 
+    def scene_device(self, bricks=0, d2=0, d2b=0, slab=0):
+        """smp_planner_scene_device: geometry and sizes of the planner's device-resident scene; each non-zero device
+        address (e.g. a torch tensor's data_ptr() on any GPU) receives a device-to-device copy of that array."""
+        v = L.SceneDevice()
+        v.bricks, v.d2, v.d2b, v.slab = bricks or None, d2 or None, d2b or None, slab or None
+        check(lib().smp_planner_scene_device(self.h, ctypes.byref(v)), "smp_planner_scene_device")
+        return v
+
+    def set_scene_device(self, layout, bricks, d2, d2b=0, slab=0):
+        """smp_planner_set_scene_device: the scene from device arrays laid out as `layout` (scene_device() of the
+        sending planner), given by device address; copied, so the caller may release them afterwards."""
+        v = L.SceneDevice()
+        ctypes.pointer(v)[0] = layout
+        v.bricks, v.d2, v.d2b, v.slab = bricks or None, d2 or None, d2b or None, slab or None
+        check(lib().smp_planner_set_scene_device(self.h, ctypes.byref(v)), "smp_planner_set_scene_device")
+        self.scene = None
+
     def set_disabled_map_links(self, names):
         arr = (ctypes.c_char_p * max(len(names), 1))(*[n.encode() for n in names])
         check(lib().smp_set_disabled_map_links(self.h, arr, len(names)))
@@ -311,6 +328,36 @@ class GpuPlanner:
 
     def plan(self, query):
         return self.plan_batch([query])[0]
+
+    @staticmethod
+    def share_scene(planners, src=0):
+        """smp_planners_share_scene: planners[src]'s scene to the others (xGMI peer copies across GPUs)."""
+        arr = (ctypes.c_void_p * len(planners))(*[p.h.value for p in planners])
+        check(lib().smp_planners_share_scene(arr, len(planners), int(src)), "smp_planners_share_scene")
+        for k, p in enumerate(planners):
+            if k != src:
+                p.scene = planners[src].scene
+
+    @staticmethod
+    def plan_multi(planners, queries):
+        """smp_plan_multi: query i on planners[i % len(planners)], all planners concurrently; results in query
+        order (per-query outcomes in the dicts, call failures raise as plan_batch)."""
+        n = len(queries)
+        arr = (ctypes.c_void_p * len(planners))(*[p.h.value for p in planners])
+        qa = (L.Query * n)(*queries)
+        ra = (L.Result * n)()
+        rc = lib().smp_plan_multi(arr, len(planners), qa, n, ra)
+        if rc == L.SMP_ERR_ARG and all(r.status == L.SMP_ERR_ARG for r in ra):
+            raise L.SmpError(rc, "smp_plan_multi")
+        out = []
+        for r in ra:
+            d = _result_dict(r)
+            lib().smp_result_free(ctypes.byref(r))
+            out.append(d)
+        failed = [d["status"] for d in out if d["status"] in _CALL_FAILURES]
+        if rc in _CALL_FAILURES or failed:
+            raise L.SmpError(rc if rc in _CALL_FAILURES else failed[0], "smp_plan_multi")
+        return out
 
     def tree(self, which):
         n = lib().smp_get_tree(self.h, which, None, None, None)
