@@ -362,6 +362,144 @@ class BiRRTstarPlanner {
 
 namespace smp_node {
 
+// Several GPUs behind one node process (independent queries shard, the scene is sent once): one planner per
+// listed device (a device may be listed more than once), the octree set on the first and copied to the others over
+// xGMI (smp_planners_share_scene), and a batch of queries dealt round-robin and planned concurrently (smp_plan_multi).
+// The robot model comes from the same places as BiRRTstarPlanner::initialize() (setRobotDescription, SMP_ROBOT_URDF /
+// SMP_ROBOT_SRDF / SMP_ROBOT_SPHERES, else SMP_ROBOT_MODEL).  Errors of the GPU runtime throw std::runtime_error.
+class MultiGpuPlanner {
+ public:
+  struct Query {
+    std::vector<double> start, goal;  // 8 values each
+    double env_x[2] = {0, 0}, env_y[2] = {0, 0};
+    bool check_self = true, check_map = true;
+    bool budget_is_time = false;      // run_planner's flag_iter_or_time
+    double budget = 1000;             // iterations or seconds
+    unsigned long long seed = 1;
+  };
+  struct Outcome {
+    bool success = false;             // run_planner's return value
+    int status = SMP_OK;              // SMP_OK, SMP_ERR_NO_SOLUTION, SMP_ERR_START_INVALID, ...
+    std::vector<std::vector<double> > trajectory;
+    smp_stats stats{};
+  };
+
+  explicit MultiGpuPlanner(const std::vector<int>& devices) : devices_(devices) {
+    if (devices_.empty()) throw std::runtime_error("smp: MultiGpuPlanner: no device");
+  }
+  ~MultiGpuPlanner() { release(); }
+  MultiGpuPlanner(const MultiGpuPlanner&) = delete;
+  MultiGpuPlanner& operator=(const MultiGpuPlanner&) = delete;
+
+  void setRobotDescription(const std::string& urdf, const std::string& srdf) { urdf_ = urdf; srdf_ = srdf; }
+
+  void initialize() {
+    release();
+    const char* env_urdf = std::getenv("SMP_ROBOT_URDF");
+    if (urdf_.empty() && env_urdf) {
+      urdf_ = read_file(env_urdf);
+      srdf_ = read_file(std::getenv("SMP_ROBOT_SRDF") ? std::getenv("SMP_ROBOT_SRDF") : "");
+    }
+    if (!urdf_.empty()) {
+      const char* sp = std::getenv("SMP_ROBOT_SPHERES");
+      const std::string spheres = read_file(sp ? sp : SMP_DEFAULT_ROBOT_SPHERES);
+      check(smp_robot_create_urdf(urdf_.c_str(), srdf_.c_str(), spheres.c_str(), &robot_), "smp_robot_create_urdf");
+    } else {
+      const char* model = std::getenv("SMP_ROBOT_MODEL");
+      const std::string text = read_file(model ? model : SMP_DEFAULT_ROBOT_MODEL);
+      check(smp_robot_create_json(text.c_str(), &robot_), "smp_robot_create_json");
+    }
+    smp_params params;
+    smp_params_default(&params);
+    for (int d : devices_) {
+      smp_planner* p = nullptr;
+      check(smp_planner_create(d, robot_, &params, &p), "smp_planner_create");
+      planners_.push_back(p);
+    }
+  }
+
+  // The octree (octomap binary stream) on the first planner's GPU, then device to device to the others.
+  void setOctreeBinary(const uint8_t* data, size_t size, double resolution) {
+    need();
+    smp_scene_opts o;
+    smp_scene_opts_default(&o);
+    o.resolution = resolution;
+    o.insert_floor = 0;
+    smp_scene* s = nullptr;
+    check(smp_scene_from_bt(data, size, &o, &s), "smp_scene_from_bt");
+    const int st = smp_planner_set_scene(planners_[0], s);
+    smp_scene_destroy(s);
+    check(st, "smp_planner_set_scene");
+    check(smp_planners_share_scene(planners_.data(), (int)planners_.size(), 0), "smp_planners_share_scene");
+  }
+
+  // Query i runs on planner i % planners (query_id i); the outcomes come back in query order.
+  std::vector<Outcome> plan(const std::vector<Query>& queries) {
+    need();
+    std::vector<smp_query> qs(queries.size());
+    for (size_t i = 0; i < queries.size(); ++i) {
+      const Query& a = queries[i];
+      if (a.start.size() != 8 || a.goal.size() != 8) throw std::runtime_error("smp: MultiGpuPlanner: dimension");
+      smp_query& q = qs[i];
+      std::memset(&q, 0, sizeof(q));
+      for (int j = 0; j < 8; ++j) { q.start[j] = a.start[j]; q.goal[j] = a.goal[j]; }
+      for (int k = 0; k < 2; ++k) { q.env_x[k] = a.env_x[k]; q.env_y[k] = a.env_y[k]; }
+      q.check_self = a.check_self;
+      q.check_map = a.check_map;
+      q.budget_kind = a.budget_is_time ? SMP_BUDGET_SECONDS : SMP_BUDGET_ITERATIONS;
+      q.budget = a.budget;
+      q.seed = a.seed;
+      q.query_id = (uint32_t)i;
+    }
+    std::vector<Outcome> out(queries.size());
+    if (queries.empty()) return out;
+    std::vector<smp_result> rs(queries.size());
+    const int rc = smp_plan_multi(planners_.data(), (int)planners_.size(), qs.data(), (int)qs.size(), rs.data());
+    for (size_t i = 0; i < rs.size(); ++i) {
+      Outcome& o = out[i];
+      o.status = rs[i].status;
+      o.success = rs[i].status == SMP_OK;
+      o.stats = rs[i].stats;
+      for (int64_t k = 0; o.success && k < rs[i].n_waypoints; ++k)
+        o.trajectory.push_back(std::vector<double>(rs[i].waypoints + k * 8, rs[i].waypoints + (k + 1) * 8));
+      smp_result_free(&rs[i]);
+    }
+    if (rc == SMP_ERR_HIP || rc == SMP_ERR_NO_DEVICE || rc == SMP_ERR_ARG) check(rc, "smp_plan_multi");
+    return out;
+  }
+
+  size_t size() const { return planners_.size(); }
+
+ private:
+  static std::string read_file(const std::string& path) {
+    FILE* f = std::fopen(path.c_str(), "rb");
+    if (!f) throw std::runtime_error("smp: cannot open " + path);
+    std::string s;
+    char buf[65536];
+    size_t n;
+    while ((n = std::fread(buf, 1, sizeof(buf), f)) > 0) s.append(buf, n);
+    std::fclose(f);
+    return s;
+  }
+  static void check(int st, const std::string& what) {
+    if (st != SMP_OK) throw std::runtime_error("smp: " + what + ": " + smp_strerror(st));
+  }
+  void need() const {
+    if (planners_.empty()) throw std::runtime_error("smp: MultiGpuPlanner::initialize() not called");
+  }
+  void release() {
+    for (smp_planner* p : planners_) smp_planner_destroy(p);
+    planners_.clear();
+    if (robot_) smp_robot_destroy(robot_);
+    robot_ = nullptr;
+  }
+
+  std::vector<int> devices_;
+  std::string urdf_, srdf_;
+  smp_robot* robot_ = nullptr;
+  std::vector<smp_planner*> planners_;
+};
+
 // Planner::normalizeTrajectory (squirrel_8dof_planner.cpp:1557-1637), same signature and the same behaviour: the
 // output is left untouched for an empty normalized pose, a single pose or a dimension mismatch.  Host only.
 inline void normalizeTrajectory(const std::vector<std::vector<double> >& trajectoryRaw,

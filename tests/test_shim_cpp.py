@@ -137,3 +137,59 @@ def test_shim_normalize_trajectory_matches_oracle(tmp_path):
         got = np.array([[float(v) for v in ln.split()] for ln in lines[i + 1:i + 1 + len(want)]])
         assert np.array_equal(got, np.array(want))
         i += 1 + len(want)
+
+
+def build_multi(tmpdir):
+    exe = os.path.join(str(tmpdir), "shim_multi")
+    subprocess.run(["g++", "-std=c++11", "-O2", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "cpp", "shim_multi.cpp"), "-L", LIBDIR, "-lsmp_gpu",
+                    "-Wl,-rpath," + LIBDIR, "-o", exe], check=True, capture_output=True, text=True)
+    return exe
+
+
+def run_multi(exe, bt, sc, devices, iters, nq):
+    args = [exe, URDF, bt, devices, str(iters), str(nq)] + ["%.17g" % v for v in list(sc.start) + list(sc.goal)]
+    args += ["%.17g" % v for v in list(sc.env_x) + list(sc.env_y)]
+    return subprocess.run(args, capture_output=True, text=True, timeout=300)
+
+
+def parse_multi(out):
+    lines, res, i = out.splitlines(), [], 0
+    while i < len(lines):
+        f = lines[i].split()
+        assert f[0] == "query"
+        n = int(f[4])
+        res.append((int(f[2]), int(f[3]), np.array([[float(v) for v in ln.split()] for ln in lines[i + 1:i + 1 + n]])))
+        i += 1 + n
+    return res
+
+
+def test_shim_multi_builds_and_fails_loudly_without_gpu(tmp_path):
+    exe = build_multi(tmp_path)
+    sc, bt = room3_case(tmp_path)
+    p = run_multi(exe, bt, sc, "0", 10, 2)
+    if p.returncode == 3:
+        assert "no usable GPU" in p.stdout or "NO_DEVICE" in p.stdout.upper(), p.stdout
+    else:
+        assert p.returncode == 0, p.stderr
+
+
+@pytest.mark.gpu
+def test_shim_multi_gpu_planner_matches_single_planner(tmp_path):
+    """smp_node::MultiGpuPlanner: the scene shared device to device to a second planner (listed on the same GPU here)
+    and 5 queries dealt over both give exactly what one planner gives, and query 0 equals the oracle's run."""
+    exe = build_multi(tmp_path)
+    sc, bt = room3_case(tmp_path)
+    two = run_multi(exe, bt, sc, "0,0", 150, 5)
+    one = run_multi(exe, bt, sc, "0", 150, 5)
+    assert two.returncode == 0 and one.returncode == 0, two.stdout + two.stderr + one.stderr
+    a, b = parse_multi(two.stdout), parse_multi(one.stdout)
+    assert len(a) == len(b) == 5
+    for x, y in zip(a, b):
+        assert x[0] == y[0] and x[1] == y[1] and np.array_equal(x[2], y[2])
+    res, keys = octomap_bt.read_bt(open(bt, "rb").read())
+    orc = O.Oracle(O.OracleRobot(MODEL), O.OracleScene(keys, res))
+    o = orc.plan(sc.start, sc.goal, env_x=sc.env_x, env_y=sc.env_y, max_iter=150, seed=100, query=0)
+    assert a[0][1] == o["checked"]
+    if o["status"] == 0:
+        assert a[0][0] == 0 and np.array_equal(a[0][2], o["path"].reshape(-1, 8))
