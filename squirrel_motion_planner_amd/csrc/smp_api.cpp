@@ -29,6 +29,7 @@ __global__ void plan_kernel(const RobotDev* rb, SceneDev sc, const MapCfg* mc, Q
                             int iters);
 __global__ void helper_kernel(const RobotDev* rb, SceneDev sc, const MapCfg* mc, QueryDev* qs, int nq);
 __global__ void path_kernel(QueryDev* qs, int* counts);
+__global__ void path_edges_kernel(const QueryDev* qs, int q, int ns, int ng, double* out);
 __global__ void boards_reset_kernel(const QueryDev* qs, int ns);
 size_t check_kernels_private_bytes();
 size_t ik_kernels_private_bytes();
@@ -134,6 +135,7 @@ struct smp_planner {
   DBuf<IkTaskDev> d_ik_tasks;
   DBuf<IkOutDev> d_ik_out;
   DBuf<int> d_ik_best;
+  DBuf<double> d_path_edges;       // path_edges_kernel output (the path's edges, one copy to the host)
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   double last_check_ms = 0, last_plan_ms = 0;
   int64_t last_plan_launches = 0;
@@ -429,7 +431,7 @@ void smp_planner_destroy(smp_planner* p) {
   if (p->hstream) (void)hipStreamSynchronize(p->hstream);
   for (auto& q : p->qb) q.release();
   p->d_qdev.release(); p->d_counts.release(); p->d_lfin.release(); p->d_cq.release(); p->d_valid.release();
-  p->d_ik_tasks.release(); p->d_ik_out.release(); p->d_ik_best.release();
+  p->d_ik_tasks.release(); p->d_ik_out.release(); p->d_ik_best.release(); p->d_path_edges.release();
   p->d_bricks.release(); p->d_d2.release(); p->d_d2b.release(); p->d_slab.release();
   if (p->d_rb) (void)hipFree(p->d_rb);
   if (p->d_mc) (void)hipFree(p->d_mc);
@@ -1136,7 +1138,11 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
   double tmax = 0;
   for (int i = 0; i < nq; ++i) if (qs[i].budget_kind == SMP_BUDGET_SECONDS) tmax = std::max(tmax, qs[i].budget);
   auto t_begin = std::chrono::steady_clock::now();
-  int chunk = 256;
+  // a single query runs its whole budget in one launch (the loop state is resumable, but a relaunch costs the host
+  // round trip, the board reset and the scouts' restart: C2, 5 launches of 256 .. 4096 iterations, ~1 ms each);
+  // several queries start at 256 iterations and double, so that finished ones free their CUs early (rebalance)
+  int chunk = nq == 1 ? (1 << 30) : 256;
+  if (const char* e = std::getenv("SMP_CHUNK0")) chunk = std::max(1, std::atoi(e));  // experiments
   std::vector<std::array<unsigned long long, 32>> scout_prof(nq);
   for (auto& a : scout_prof) a.fill(0);
   float total_ms = 0;
@@ -1248,6 +1254,7 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
     }
     if (chunk < 4096) chunk *= 2;
   }
+  hstamp("launch loop done");
   // path extraction reads every query's record: the full array again
   HIPCHK(hipMemcpyAsync(p->d_qdev.p, qdev.data(), nq * sizeof(QueryDev), hipMemcpyHostToDevice, p->stream));
   nh = nh_first;
@@ -1308,33 +1315,37 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
     }
     if (r.status != SMP_OK) { done[i] = 1; continue; }
     int ns = counts[2 * i], ng = counts[2 * i + 1];
-    std::vector<int> ids(ns + ng);
-    if (ns) HIPCHK(hipMemcpy(ids.data(), qdev[i].path_nodes, ns * sizeof(int), hipMemcpyDeviceToHost));
-    if (ng) HIPCHK(hipMemcpy(ids.data() + ns, qdev[i].path_nodes + cap, ng * sizeof(int), hipMemcpyDeviceToHost));
     const int np = p->params.num_traj_segments;
-    std::vector<double> wp;
-    auto edge_of = [&](int t, int id, double* st8, double* tg8) -> int {
-      for (int j = 0; j < NJ; ++j) {
-        HIPCHK(hipMemcpy(&st8[j], qdev[i].tr[t].e_start + (size_t)j * cap + id, sizeof(double), hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(&tg8[j], qdev[i].tr[t].e_target + (size_t)j * cap + id, sizeof(double), hipMemcpyDeviceToHost));
-      }
-      return SMP_OK;
-    };
-    for (int k = 0; k < ns; ++k) {  // start-tree edges contribute points 0 .. np-1
-      double a[NJ], b[NJ], stp[NJ];
-      if (edge_of(0, ids[k], a, b)) return SMP_ERR_HIP;
-      for (int j = 0; j < NJ; ++j) stp[j] = (b[j] - a[j]) / double(np);
-      for (int inc = 0; inc < np; ++inc)
-        for (int j = 0; j < NJ; ++j) wp.push_back(a[j] + inc * stp[j]);
+    // the path's edges (e_start, e_target of every path node, start-tree nodes root first, then the goal-tree nodes
+    // from the connection) gathered on the device: one copy instead of one per value
+    std::vector<double> pe((size_t)(ns + ng) * 2 * NJ);
+    if (ns + ng > 0) {
+      HIPCHK(p->d_path_edges.reserve(pe.size()));
+      const int nthr = (int)pe.size();
+      hipLaunchKernelGGL(path_edges_kernel, dim3((nthr + 255) / 256), dim3(256), 0, p->stream, p->d_qdev.p, i, ns, ng,
+                         p->d_path_edges.p);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipMemcpyAsync(pe.data(), p->d_path_edges.p, pe.size() * sizeof(double), hipMemcpyDeviceToHost, p->stream));
+      HIPCHK(hipStreamSynchronize(p->stream));
     }
-    for (int k = 0; k < ng; ++k) {  // goal-tree edges reversed: points np .. 1, then point 0 of the last
-      double a[NJ], b[NJ], stp[NJ];
-      if (edge_of(1, ids[ns + k], a, b)) return SMP_ERR_HIP;
+    (void)cap;
+    std::vector<double> wp;
+    for (int k = 0; k < ns + ng; ++k) {
+      // start-tree edges contribute points 0 .. np-1; goal-tree edges reversed: points np .. 1, then point 0 of the
+      // last one (computeFinalSolutionPathTrajectories, birrt_star.cpp:6173-6274)
+      const double* a = &pe[(size_t)k * 2 * NJ];
+      const double* b = a + NJ;
+      double stp[NJ];
       for (int j = 0; j < NJ; ++j) stp[j] = (b[j] - a[j]) / double(np);
-      for (int inc = np; inc > 0; --inc)
-        for (int j = 0; j < NJ; ++j) wp.push_back(a[j] + inc * stp[j]);
-      if (k == ng - 1)
-        for (int j = 0; j < NJ; ++j) wp.push_back(a[j] + 0 * stp[j]);
+      if (k < ns) {
+        for (int inc = 0; inc < np; ++inc)
+          for (int j = 0; j < NJ; ++j) wp.push_back(a[j] + inc * stp[j]);
+      } else {
+        for (int inc = np; inc > 0; --inc)
+          for (int j = 0; j < NJ; ++j) wp.push_back(a[j] + inc * stp[j]);
+        if (k == ns + ng - 1)
+          for (int j = 0; j < NJ; ++j) wp.push_back(a[j] + 0 * stp[j]);
+      }
     }
     r.n_waypoints = (int64_t)(wp.size() / NJ);
     if (!wp.empty()) {
@@ -1344,6 +1355,7 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
     done[i] = 1;
   }
   for (int i = 0; i < nq; ++i) if (out[i].status != SMP_OK && rc == SMP_OK) rc = out[i].status;
+  hstamp("results assembled");
   return rc;
 }
 

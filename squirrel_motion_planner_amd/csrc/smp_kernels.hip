@@ -4699,6 +4699,20 @@ __global__ void path_kernel(QueryDev* qs, int* counts) {
 }
 
 
+// The edges of query q's path (path_kernel's node lists: ns start-tree nodes, then ng goal-tree nodes) gathered for
+// one device-to-host copy: per path node its edge's e_start[0..7] then e_target[0..7].
+__global__ void path_edges_kernel(const QueryDev* qs, int q, int ns, int ng, double* out) {
+  const QueryDev& Q = qs[q];
+  const int cap = Q.st->cap;
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < (ns + ng) * 2 * NJ; k += gridDim.x * blockDim.x) {
+    const int e = k / (2 * NJ), w = k - e * (2 * NJ), j = w % NJ;
+    const int t = e < ns ? 0 : 1;
+    const int id = e < ns ? Q.path_nodes[e] : Q.path_nodes[cap + (e - ns)];
+    const double* src = w < NJ ? Q.tr[t].e_start : Q.tr[t].e_target;
+    out[k] = src[(size_t)j * cap + id];
+  }
+}
+
 // Probe of the tree scans alone (tests and tools/near_probe.py): one workgroup runs nearest() and
 // near_set<20>() for m query configurations against one tree (SoA q [NJ][cap], total cost [cap]), `reps` times
 // each; out: nearest id, near count, the first / last 20 near ids; ticks[0] / ticks[1] = device-clock ticks of

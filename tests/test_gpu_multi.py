@@ -64,16 +64,24 @@ def test_share_scene_and_plan_multi(c2):
         GpuPlanner.plan_multi([a, a], qs[:2])
 
 
-def test_scene_device_roundtrip_through_torch(c2):
+def _roundtrip(rank, out_dir):
+    """Body of test_scene_device_roundtrip_through_torch, in a fresh process: torch's HIP runtime initialises before
+    the library's there (torch ships its own libamdhip64 beside /opt/rocm's; in a process where the library already
+    ran many planners, torch's later initialisation was seen to find no GPU)."""
+    import sys
     import torch
-    sc, scene = c2
-    robot = Robot()
-    a = GpuPlanner(robot, device=0)
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from squirrel_motion_planner_amd import _lib as LL, scenes as S
+    from squirrel_motion_planner_amd.planner import GpuPlanner as G, Robot as R, Scene as Sc
+    dev = torch.device("cuda", 0)
+    torch.empty(1, device=dev)
+    sc = S.box_room()
+    scene = Sc.from_keys(sc.keys, sc.res)
+    robot = R()
+    a = G(robot, device=0)
     a.set_scene(scene)
     v = a.scene_device()
-    assert tuple(v.dims) == scene.info()["dims"] and v.n_cells == int(np.prod(v.dims))
-    assert v.n_prim == 6 and v.has_d2b == 1
-    dev = torch.device("cuda", 0)
+    checks = [tuple(v.dims) == scene.info()["dims"], v.n_cells == int(np.prod(v.dims)), v.n_prim == 6, v.has_d2b == 1]
     bricks = torch.empty(v.n_bricks, dtype=torch.int64, device=dev)
     d2 = torch.empty(v.n_cells, dtype=torch.int16, device=dev)
     d2b = torch.empty(v.n_cells, dtype=torch.uint8, device=dev)
@@ -82,23 +90,34 @@ def test_scene_device_roundtrip_through_torch(c2):
     torch.cuda.synchronize()
     # the device arrays are the host builder's: the box-gap field equals the host scene's export
     _, d2_host = scene.export()
-    assert np.array_equal(d2.cpu().numpy().view(np.uint16), d2_host)
-    assert np.array_equal(d2b.cpu().numpy(), np.minimum(d2_host, 255).astype(np.uint8))
-    c = GpuPlanner(robot, device=0)
+    checks.append(bool(np.array_equal(d2.cpu().numpy().view(np.uint16), d2_host)))
+    checks.append(bool(np.array_equal(d2b.cpu().numpy(), np.minimum(d2_host, 255).astype(np.uint8))))
+    c = G(robot, device=0)
     c.set_scene_device(v, bricks.data_ptr(), d2.data_ptr(), d2b.data_ptr(), slab.data_ptr())
     del bricks, d2, d2b, slab  # copied by the library
     q = _configs(sc, 20000, 5)
-    assert np.array_equal(a.check_configs(q), c.check_configs(q))
+    checks.append(bool(np.array_equal(a.check_configs(q), c.check_configs(q))))
     qs = _queries(sc, 1, iters=200)
-    _same_result(a.plan(qs[0]), c.plan(qs[0]))
-    # a layout that does not fit this robot / grid is refused
+    ra, rc = a.plan(qs[0]), c.plan(qs[0])
+    checks.append(all(ra[k] == rc[k] for k in ("status", "iterations", "configs_checked", "nodes_start", "nodes_goal")))
+    checks.append(bool(np.array_equal(ra["path"], rc["path"])) and ra["cost_best"] == rc["cost_best"])
+    # a layout that does not fit this robot / grid is refused; no scene yet: nothing to export
     bad = a.scene_device()
     bad.n_prim = 5
-    with pytest.raises(L.SmpError):
-        c.set_scene_device(bad, 1, 1, 1, 1)
-    # no scene yet: nothing to export
-    with pytest.raises(L.SmpError):
-        GpuPlanner(robot, device=0).scene_device()
+    for f in (lambda: c.set_scene_device(bad, 1, 1, 1, 1), lambda: G(robot, device=0).scene_device()):
+        try:
+            f()
+            checks.append(False)
+        except LL.SmpError:
+            checks.append(True)
+    np.save(os.path.join(out_dir, "roundtrip.npy"), np.array(checks))
+
+
+def test_scene_device_roundtrip_through_torch(tmp_path):
+    import torch.multiprocessing as mp
+    mp.spawn(_roundtrip, args=(str(tmp_path),), nprocs=1, join=True)
+    checks = np.load(os.path.join(str(tmp_path), "roundtrip.npy"))
+    assert checks.all(), checks.tolist()
 
 
 def _free_port():

@@ -362,6 +362,33 @@ def test_many_queries_reprovisioned_match_oracle(orobot, robot):
         _same_query_result(r, o)
 
 
+def test_single_query_relaunched_equals_one_launch(orobot, robot, monkeypatch):
+    """A single query runs its whole budget in one launch; forced into launches of 64 iterations (SMP_CHUNK0, the loop
+    state resumed from QState each time, scouts and helpers restarted) it plans the identical trees, path and counters,
+    and both equal the oracle."""
+    gp2 = GpuPlanner(robot, path_optimality_threshold=-math.inf)
+    sc, gscene, osc = scene_pair("c2")
+    gp2.set_scene(gscene)
+    q = GpuPlanner.make_query(sc.start, sc.goal, sc.env_x, sc.env_y, iterations=700, seed=3)
+    one = gp2.plan(q)
+    assert gp2.last_kernel_ms()[2] == 1
+    t_one = [gp2.tree(w) for w in (0, 1)]
+    monkeypatch.setenv("SMP_CHUNK0", "64")
+    many = gp2.plan(q)
+    assert gp2.last_kernel_ms()[2] >= 4
+    for k in ("status", "iterations", "configs_checked", "configs_valid", "nodes_start", "nodes_goal",
+              "first_solution_iter", "rewires_start", "rewires_goal"):
+        assert one[k] == many[k], k
+    assert np.array_equal(one["path"], many["path"]) and one["cost_best"] == many["cost_best"]
+    for w in (0, 1):
+        par, conf, cost = gp2.tree(w)
+        assert np.array_equal(par, t_one[w][0]) and np.array_equal(conf, t_one[w][1])
+        assert np.array_equal(cost, t_one[w][2])
+    o = O.Oracle(orobot, osc).plan(sc.start, sc.goal, env_x=sc.env_x, env_y=sc.env_y, max_iter=700, seed=3,
+                                   opt_thresh=-np.inf)
+    _same_query_result(one, o)
+
+
 @pytest.fixture(scope="module")
 def c5_pair():
     sc = scenes.clutter_cloud()
