@@ -1680,7 +1680,7 @@ __device__ void scan_slice(const Ctx& C, int near, int t, const double* q, int i
 }
 
 // Helper side of a scan job already in J.words (seq): its slice, then the result granules.
-__device__ void scan_helper(const Ctx& C, JobLds& J, int w, int seq) {
+__device__ __noinline__ void scan_helper(const Ctx& C, JobLds& J, int w, int seq) {
   const unsigned hdr = J.words[0];
   const int near = (hdr >> 19) & 1, t = (hdr >> 20) & 1;
   double q[NJ];
@@ -4575,7 +4575,9 @@ struct SamplerLds {
 // the ring, computed with the latest published parameters and tagged (iteration, version); a parameter change
 // restarts the window.  Never writes the slot of an iteration the leader may be reading: it fills iterations
 // up to (published iteration) + SMP_RING - 1 only.  Leaves on the stop flag or after two idle seconds.
-__device__ void sampler_main(const Ctx& C, SamplerLds& L) {
+// (not inlined into helper_kernel, like scan_helper: the tile helpers' loop is compiled without the sampler's and the
+// scan slices' registers live around it -- C2 73.1 -> 71.8 us per iteration, tools/gpu_r03s7.sh)
+__device__ __noinline__ void sampler_main(const Ctx& C, SamplerLds& L) {
   JobBoard* jb = C.Q.jb;
   {
     const int* src = reinterpret_cast<const int*>(C.Q.st);
