@@ -268,6 +268,124 @@ __device__ __forceinline__ bool wave_sphere_map(const SceneDev& sc, const double
   return false;
 }
 
+// The brick box of a sphere's reach (sphere_reach, then the 4x4x4 bricks covering it): first brick and counts.
+__device__ __forceinline__ int sphere_bricks(const SceneDev& sc, const double* cc, double r, int* lo, int* hi, int* b0,
+                                             int* nbx) {
+  sphere_reach(sc, cc, r, lo, hi);
+  b0[0] = lo[0] >> 2; b0[1] = lo[1] >> 2; b0[2] = lo[2] >> 2;
+  nbx[0] = (hi[0] >> 2) - b0[0] + 1; nbx[1] = (hi[1] >> 2) - b0[1] + 1; nbx[2] = (hi[2] >> 2) - b0[2] + 1;
+  return nbx[0] * nbx[1] * nbx[2];
+}
+
+constexpr int MAP_STAGE_W = 96;  // brick words staged per configuration (its dead body-frame rows, TileLds::fr)
+
+// Exact map tests of all candidate spheres of one configuration by one wavefront, their brick words fetched in ONE
+// memory round trip: lanes over spheres give each candidate (<= 64 bricks) its slot range of the staging buffer `buf`
+// (MAP_STAGE_W words, in sphere order; owner[w] = the sphere of word w, off[s] = its first slot), lanes over slots
+// load the words, then the candidates are swept in sphere order from LDS (the cells and the exact box test of
+// wave_sphere_map).  A candidate that does not fit (more than 64 bricks, or the buffer full) is swept by
+// wave_sphere_map itself.  The outcome (any candidate touching an occupied cell) is the same as sweeping them one
+// after the other; wave_sphere_map pays one load round trip per candidate.
+__device__ __forceinline__ bool wave_map_staged(const RobotDev* __restrict__ rb, const SceneDev& sc, const double (*wc)[3],
+                                                const uint32_t* cand, int nsph, uint64_t* buf, uint8_t* owner,
+                                                uint8_t* off, int lane) {
+  // slots: sphere s = g * 64 + lane of group g.  Staged are the candidates (of at most 64 bricks) whose inclusive
+  // prefix of brick counts still ends within the buffer: a prefix of them in sphere order, so the words [0, base)
+  // all have an owner; off[s] = first slot of a staged candidate, else 255
+  int base = 0;
+  uint64_t spill[2] = {0, 0};  // candidates of group 0 / 1 (bit per lane) swept by wave_sphere_map
+  for (int g = 0; g < 2 && g * 64 < nsph; ++g) {
+    const int s = g * 64 + lane;
+    const bool is_c = s < nsph && ((cand[s >> 5] >> (s & 31)) & 1u);
+    int nb = 0;
+    if (is_c) {
+      int lo[3], hi[3], b0[3], nbx[3];
+      nb = sphere_bricks(sc, wc[s], rb->sph_r[s], lo, hi, b0, nbx);
+      if (nb > 64) nb = 0;  // swept by wave_sphere_map (its per-cell loads)
+    }
+    int inc = nb;
+    for (int d = 1; d < 64; d <<= 1) {
+      const int v = __shfl_up(inc, d);
+      if (lane >= d) inc += v;
+    }
+    const bool staged = nb > 0 && base + inc <= MAP_STAGE_W;
+    const int start = base + inc - nb;
+    if (s < nsph) off[s] = staged ? (uint8_t)start : (uint8_t)255;
+    if (staged)
+      for (int b = 0; b < nb; ++b) owner[start + b] = (uint8_t)s;
+    spill[g] = __ballot(is_c && !staged);
+    const uint64_t sm = __ballot(staged);
+    if (sm) base += __shfl(inc, 63 - __builtin_clzll(sm));
+  }
+  wave_sync();
+  // one round: every staged word loaded (two slots per lane), then stored
+  uint64_t v[2] = {0, 0};
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int w = u * 64 + lane;
+    if (w < base) {
+      const int s = owner[w];
+      int lo[3], hi[3], b0[3], nbx[3];
+      sphere_bricks(sc, wc[s], rb->sph_r[s], lo, hi, b0, nbx);
+      const int b = w - off[s], bi = b % nbx[0], t = b / nbx[0];
+      const int bj = t % nbx[1], bk = t / nbx[1];
+      v[u] = sc.bricks[((size_t)(b0[2] + bk) * sc.bny + (b0[1] + bj)) * sc.bnx + (b0[0] + bi)];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+    if (u * 64 + lane < base) buf[u * 64 + lane] = v[u];
+  wave_sync();
+  // sweeps of the staged candidates in sphere order (scalar loop over the candidate mask)
+  for (int wd = 0; wd * 32 < nsph; ++wd) {
+    uint32_t m = cand[wd];
+    while (m) {
+      const int s = wd * 32 + __builtin_ctz(m);
+      m &= m - 1;
+      const int o = off[s];
+      if (o == 255) continue;
+      const double cc[3] = {wc[s][0], wc[s][1], wc[s][2]};
+      const double r = rb->sph_r[s], r2 = r * r;
+      int lo[3], hi[3], b0[3], nbx[3];
+      sphere_bricks(sc, cc, r, lo, hi, b0, nbx);
+      const int ni = hi[0] - lo[0] + 1, nj = hi[1] - lo[1] + 1, nk = hi[2] - lo[2] + 1;
+      const int nv = ni * nj * nk;
+      for (int v0 = 0; v0 < nv; v0 += 64) {
+        const int vv = v0 + lane;
+        bool hit = false;
+        if (vv < nv) {
+          const int t = vv / ni;
+          const int i = lo[0] + (vv - t * ni), j = lo[1] + t % nj, k = lo[2] + t / nj;
+          const int src = ((k >> 2) - b0[2]) * nbx[1] * nbx[0] + ((j >> 2) - b0[1]) * nbx[0] + ((i >> 2) - b0[0]);
+          const uint64_t word = buf[o + src];
+          const int bit = ((k & 3) << 4) | ((j & 3) << 2) | (i & 3);
+          if ((word >> bit) & 1ull) {
+            const double xlo = sc.ox + (double)i * sc.res, xhi = sc.ox + (double)(i + 1) * sc.res;
+            const double ylo = sc.oy + (double)j * sc.res, yhi = sc.oy + (double)(j + 1) * sc.res;
+            const double zlo = sc.oz + (double)k * sc.res, zhi = sc.oz + (double)(k + 1) * sc.res;
+            const double dx = cc[0] < xlo ? xlo - cc[0] : (cc[0] > xhi ? cc[0] - xhi : 0.0);
+            const double dy = cc[1] < ylo ? ylo - cc[1] : (cc[1] > yhi ? cc[1] - yhi : 0.0);
+            const double dz = cc[2] < zlo ? zlo - cc[2] : (cc[2] > zhi ? cc[2] - zhi : 0.0);
+            hit = dx * dx + dy * dy + dz * dz <= r2;
+          }
+        }
+        if (__ballot(hit)) return true;
+      }
+    }
+  }
+  // candidates that did not fit the staging buffer
+  for (int g = 0; g < 2; ++g) {
+    uint64_t m = spill[g];
+    while (m) {
+      const int s = g * 64 + __builtin_ctzll(m);
+      m &= m - 1;
+      const double cc[3] = {wc[s][0], wc[s][1], wc[s][2]};
+      if (wave_sphere_map(sc, cc, rb->sph_r[s], lane)) return true;
+    }
+  }
+  return false;
+}
+
 // ---------------------------------------------------------------------------------------------- exact primitives
 // World centre and horizontal x axis (c, s) of primitive p from its body's frame B (R row-major, then p): the same
 // three-term sums as a sphere centre (KDL Frame * Vector); the axis is R times ab without the translation.
@@ -576,14 +694,16 @@ __device__ __forceinline__ void collide_tile(const RobotDev* __restrict__ rb, co
                               L.u.c.pw[c][p][4]};
         hit = wave_prim_map(sc, rb->prim_type[p], &rb->prim_h[p * 3], pw, lane);
       }
-      for (int wd = 0; wd < SW && !hit; ++wd) {
-        uint32_t m = L.cand[c][wd];
-        while (m) {
-          const int s = wd * 32 + __builtin_ctz(m);
-          m &= m - 1;
-          const double cc[3] = {L.u.c.wc[c][s][0], L.u.c.wc[c][s][1], L.u.c.wc[c][s][2]};
-          if (wave_sphere_map(sc, cc, rb->sph_r[s], lane)) { hit = true; break; }
-        }
+      // the candidate spheres' brick words in one round trip, staged in this configuration's body-frame rows (dead
+      // once its centres and primitive frames are formed) -- one round trip per candidate before
+      uint32_t any = 0;
+      for (int wd = 0; wd < SW; ++wd) any |= L.cand[c][wd];
+      if (!hit && any) {
+        static_assert(sizeof(L.fr[0]) >= MAP_STAGE_W * sizeof(uint64_t), "staging buffer in the body-frame rows");
+        static_assert(sizeof(L.tf[0]) >= MAP_STAGE_W + MAX_SPH, "slot owners and offsets in the stage-B rows");
+        uint8_t* tb = reinterpret_cast<uint8_t*>(&L.tf[c][0][0]);
+        hit = wave_map_staged(rb, sc, L.u.c.wc[c], L.cand[c], nsph, reinterpret_cast<uint64_t*>(&L.fr[c][0][0]), tb,
+                              tb + MAP_STAGE_W, lane);
       }
       if (hit) hitm |= 1u << k;
     }
