@@ -76,8 +76,9 @@ for rl in sorted(set(role.tolist())):
             s / max(len(its), 1), s / c, c, l0, func_of(l0)[:22], l1, func_of(l1)[:22]))
 
 # raw timeline of two leader iterations with the scouts' records interleaved
-w0 = 20
-sel = (it >= w0) & (it < w0 + 2)
+w0 = int(os.environ.get("SMP_TRACE_W0", "20"))
+nw = int(os.environ.get("SMP_TRACE_NW", "2"))
+sel = (it >= w0) & (it < w0 + nw)
 order = np.argsort(clk[sel], kind="stable")
 t0 = clk[sel][order][0] if sel.any() else 0
 print("\n=== timeline (iterations %d-%d of the window), us from the first record" % (w0, w0 + 1))
