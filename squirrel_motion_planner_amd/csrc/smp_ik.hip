@@ -7,13 +7,14 @@
 // joint update with the joint-limit check (control_laws.cpp:3504-3550), forward kinematics and the clamped error
 // (control_laws.cpp:2167-2245).  An iteration is a dependent chain of small steps, and gfx950 fp64 has ~40 cycles
 // of dependent latency, so a run stays on one wavefront and each step is laid out to be short and wide:
-//   J    lanes 0-7: Jacobian column c (the joint rotations come from the previous FK); lanes 8-13: the
-//        quaternion and error component of the previous FK (divergent lanes of one wave run one after the other);
+//   J    lanes 0-7: Jacobian column c (the joint rotations come from the previous FK) and, in the same
+//        instruction stream, the quaternion and error component min(c, 5) of the previous FK (the goal terms in
+//        registers for the whole run);
 //   A    lanes 0-35: J J^T; lanes 36-41: the error column of the augmented system;
 //   GJ   6 Gauss-Jordan steps on [J J^T | e] (lanes 0-41, one entry each); when det < 1e-10 tr^5 also the
 //        symmetric elimination of J J^T - 1e-10 I, whose pivot signs decide the manipulability path;
-//   q    lanes 0-7: q_dot_c = (J^T z)_c, joint update with the limit check;
-//   FK   lanes 0-11: local frame of every segment; lanes 0-2: one frame row each through the chain.
+//   FK   lanes 0-11: joint update of the segment's column (q_dot_c = (J^T z)_c, limit check) and the local frame
+//        of every segment; lanes 0-2: one frame row each through the chain.
 // Robot constants live in registers (each lane always owns the same segment / column), the iteration touches
 // only LDS, and phases are separated by wavefront syncs (one wave per workgroup: no s_barrier).  Every value is
 // computed with the same operations in the same order as oracle/smp_oracle.cpp (ik_solve): -ffp-contract=off,
@@ -57,47 +58,42 @@ struct IkLds {
   double ql[8][NJ];           // goal search: the pose to check (collide_tile input)
 };
 
-// KDL Rotation::GetQuaternion (frames.cpp), as compute_FK uses it (kdl_kuka_model.cpp:302): q = x, y, z, w.
-__device__ __forceinline__ void get_quaternion(const double* R, double* q) {
-  double trace = R[0] + R[4] + R[8];
-  if (trace > 1e-12) {
-    double s = 0.5 / sqrt(trace + 1.0);
-    q[3] = 0.25 / s;
-    q[0] = (R[7] - R[5]) * s;
-    q[1] = (R[2] - R[6]) * s;
-    q[2] = (R[3] - R[1]) * s;
-  } else if (R[0] > R[4] && R[0] > R[8]) {
-    double s = 2.0 * sqrt(1.0 + R[0] - R[4] - R[8]);
-    q[3] = (R[7] - R[5]) / s;
-    q[0] = 0.25 * s;
-    q[1] = (R[1] + R[3]) / s;
-    q[2] = (R[2] + R[6]) / s;
-  } else if (R[4] > R[8]) {
-    double s = 2.0 * sqrt(1.0 + R[4] - R[0] - R[8]);
-    q[3] = (R[2] - R[6]) / s;
-    q[0] = (R[1] + R[3]) / s;
-    q[1] = 0.25 * s;
-    q[2] = (R[5] + R[7]) / s;
-  } else {
-    double s = 2.0 * sqrt(1.0 + R[8] - R[0] - R[4]);
-    q[3] = (R[3] - R[1]) / s;
-    q[0] = (R[2] + R[6]) / s;
-    q[1] = (R[5] + R[7]) / s;
-    q[2] = 0.25 * s;
-  }
+// KDL Rotation::GetQuaternion (frames.cpp), as compute_FK uses it (kdl_kuka_model.cpp:302): q = x, y, z, w.  Written
+// without branches: the trace selects one of KDL's four cases, and the case's own operations are applied (the
+// square root's argument, s, and per component either x * s or x / s), so that it runs in one instruction stream
+// beside the Jacobian column.
+__device__ __forceinline__ void get_quaternion_sel(const double* R, double* q) {
+  const double trace = R[0] + R[4] + R[8];
+  const bool c0 = trace > 1e-12;
+  const bool c1 = !c0 && R[0] > R[4] && R[0] > R[8];
+  const bool c2 = !c0 && !c1 && R[4] > R[8];
+  const double a1 = 1.0 + R[0] - R[4] - R[8], a2 = 1.0 + R[4] - R[0] - R[8], a3 = 1.0 + R[8] - R[0] - R[4];
+  const double r = sqrt(c0 ? trace + 1.0 : (c1 ? a1 : (c2 ? a2 : a3)));
+  const double s = c0 ? 0.5 / r : 2.0 * r;
+  const double d75 = R[7] - R[5], d26 = R[2] - R[6], d31 = R[3] - R[1];
+  const double s13 = R[1] + R[3], s26 = R[2] + R[6], s57 = R[5] + R[7];
+  const double x3 = c0 ? 0.25 : (c1 ? d75 : (c2 ? d26 : d31));
+  const double x0 = c0 ? d75 : (c1 ? 0.25 : (c2 ? s13 : s26));
+  const double x1 = c0 ? d26 : (c1 ? s13 : (c2 ? 0.25 : s57));
+  const double x2 = c0 ? d31 : (c1 ? s26 : (c2 ? s57 : 0.25));
+  const double v0 = x0 / s, v1 = x1 / s, v2 = x2 / s, m0 = x0 * s, m1 = x1 * s, m2 = x2 * s;
+  q[3] = x3 / s;
+  q[0] = (c0 || c1) ? m0 : v0;
+  q[1] = (c0 || c2) ? m1 : v1;
+  q[2] = c0 ? m2 : (c1 || c2 ? v2 : m2);
 }
 
 // Constants of the segment a lane owns in the FK (lane s < n_seg) and of the Jacobian column it owns (lane c < 8).
 struct LaneConst {
-  int f_ty, f_jn;
-  double f_ax[3], f_org[3], f_R[9], f_p[3];
-  int j_s, j_ty, j_jn;
-  double j_ax[3], j_fp[3], j_lo, j_hi;
+  int f_ty, f_jn, f_col;  // f_col: the segment's Jacobian column (movable segments)
+  double f_ax[3], f_org[3], f_R[9], f_p[3], f_lo, f_hi;
+  int j_s, j_ty;
+  double j_ax[3], j_fp[3];
 };
 
 __device__ __forceinline__ void load_const(const RobotDev* __restrict__ rb, int lane, LaneConst& k) {
   const int ns = rb->n_seg;
-  k.f_ty = 0; k.f_jn = 0;
+  k.f_ty = 0; k.f_jn = 0; k.f_col = 0; k.f_lo = 0.0; k.f_hi = 0.0;
   for (int d = 0; d < 3; ++d) { k.f_ax[d] = 0.0; k.f_org[d] = 0.0; k.f_p[d] = 0.0; k.j_ax[d] = 0.0; k.j_fp[d] = 0.0; }
   for (int i = 0; i < 9; ++i) k.f_R[i] = 0.0;
   if (lane < ns) {
@@ -109,9 +105,12 @@ __device__ __forceinline__ void load_const(const RobotDev* __restrict__ rb, int 
       k.f_p[d] = rb->seg_p[lane * 3 + d];
     }
     for (int i = 0; i < 9; ++i) k.f_R[i] = rb->seg_R[lane * 9 + i];
+    for (int s = 0; s < lane; ++s) k.f_col += rb->seg_type[s] != 0 ? 1 : 0;
+    k.f_lo = rb->q_min[k.f_jn];
+    k.f_hi = rb->q_max[k.f_jn];
   }
   // the lane-th movable segment
-  k.j_s = 0; k.j_ty = 0; k.j_jn = 0; k.j_lo = 0.0; k.j_hi = 0.0;
+  k.j_s = 0; k.j_ty = 0;
   int c = 0;
   for (int s = 0; s < ns; ++s) {
     if (rb->seg_type[s] == 0) continue;
@@ -121,25 +120,39 @@ __device__ __forceinline__ void load_const(const RobotDev* __restrict__ rb, int 
   if (lane < NJ) {
     const int s = k.j_s;
     k.j_ty = rb->seg_type[s];
-    k.j_jn = rb->seg_joint[s];
     for (int d = 0; d < 3; ++d) { k.j_ax[d] = rb->seg_axis[s * 3 + d]; k.j_fp[d] = rb->seg_p[s * 3 + d]; }
-    k.j_lo = rb->q_min[k.j_jn];
-    k.j_hi = rb->q_max[k.j_jn];
   }
 }
 
 // Segment frames of S.q (ChainFkSolverPos_recursive, kdl_kuka_model.cpp:278-305 -- the same products as the T_tmp
 // chain of ChainJntToJacSolver): T[0] = I, T[s+1] = T[s] * (joint(q) * f_tip).
-__device__ __forceinline__ void chain_fk(int ns, unsigned rid, IkLds& S, int lane, const LaneConst& k) {
+// upd (after an iteration's solve): the lane of a movable segment first applies the joint update of its column,
+// q_dot_c = (J^T z)_c and the limit check (control_laws.cpp:3455-3550), z = [J J^T (+ d^2 I) | e] solved (upd 1)
+// or the fallback's z (upd 2) -- the update and the frame it moves in one step, no LDS round trip between them.
+__device__ __forceinline__ void chain_fk(int ns, unsigned rid, IkLds& S, int lane, const LaneConst& k, int upd) {
   if (lane < ns) {
+    double qq = S.q[k.f_jn];
+    if (upd != 0 && k.f_ty != 0) {
+      double z[6];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) z[i] = upd == 1 ? S.M[i][6] / S.M[i][i] : S.z[i];
+      double pz[6];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) pz[i] = S.J[i][k.f_col] * z[i];
+      const double v = ((pz[0] + pz[1]) + (pz[2] + pz[3])) + (pz[4] + pz[5]);
+      const double nv = qq + v * IK_DT;
+      if (!(nv < k.f_lo || nv > k.f_hi)) {
+        qq = nv;
+        S.q[k.f_jn] = nv;
+      }
+    }
     Frame Jf;
     frame_identity(&Jf);
     if (k.f_ty == 1) {
-      rot2(k.f_ax, S.q[k.f_jn], Jf.R);
+      rot2(k.f_ax, qq, Jf.R);
       for (int d = 0; d < 3; ++d) Jf.p[d] = k.f_org[d];
       for (int i = 0; i < 9; ++i) S.JR[lane][i] = Jf.R[i];
     } else if (k.f_ty == 2) {
-      const double qq = S.q[k.f_jn];
       for (int d = 0; d < 3; ++d) Jf.p[d] = k.f_org[d] + k.f_ax[d] * qq;
     }
     Frame F, Lf;
@@ -181,17 +194,52 @@ __device__ __forceinline__ void chain_fk(int ns, unsigned rid, IkLds& S, int lan
 // Lanes 0-7: KDL ChainJntToJacSolver::JntToJac column of movable segment s = T[s].M * (joint twist referred to
 // the tip of s), referred to the chain tip (KDL's Twist::RefPoint(T[i+1].p - T[i].p) for every later segment i,
 // telescoped); cast to float (getJacobian).
-// Lanes 8-13: error component lane-8 of the end-effector pose T[ns] (set_EE_goal_pose unclamped, update_error_vec
+// Lanes 0-5 also: error component lane of the end-effector pose T[ns] (set_EE_goal_pose unclamped, update_error_vec
 // clamped).  Returns the ballot of components outside the 1e-4 bound (is_error_within_bounds).
-__device__ __forceinline__ unsigned long long jacobian_and_error(int ns, const IkTaskDev& t, IkLds& S, int lane,
+// The goal terms of a lane's error component (lanes 0-7: component min(lane, 5)), read once per run: in the
+// iteration they were global loads on the error's dependent chain.
+struct ErrConst {
+  double di, g6, s0, s1, s2, lo, hi;
+};
+
+__device__ __forceinline__ void load_err_const(const IkTaskDev& t, int lane, ErrConst& ec) {
+  const int i = lane < 6 ? lane : 5;
+  const int rr = i < 3 ? 0 : i - 3;
+  const double* g = t.goal;
+  ec.di = g[i];
+  ec.g6 = g[6];
+  ec.s0 = rr == 0 ? 0.0 : (rr == 1 ? g[5] : -g[4]);
+  ec.s1 = rr == 0 ? -g[5] : (rr == 1 ? 0.0 : g[3]);
+  ec.s2 = rr == 0 ? g[4] : (rr == 1 ? -g[3] : 0.0);
+  ec.lo = t.lo[i];
+  ec.hi = t.hi[i];
+}
+
+__device__ __forceinline__ unsigned long long jacobian_and_error(int ns, const ErrConst& ec, IkLds& S, int lane,
                                                                  const LaneConst& k, bool clamp) {
   bool out = false;
   if (lane < NJ) {
+    // error component i (lanes 6 and 7 repeat component 5 and keep it to themselves) in the same instruction stream
+    // as the Jacobian column: the two dependent chains overlap instead of running as two divergent lane groups
+    const int i = lane < 6 ? lane : 5;
+    const double* E = S.T[ns];
+    double c[7] = {E[9], E[10], E[11], 0.0, 0.0, 0.0, 0.0};
+    get_quaternion_sel(E, &c[3]);
+    const int rr = i < 3 ? 0 : i - 3;
+    const double ci = i < 3 ? (i == 0 ? c[0] : (i == 1 ? c[1] : c[2])) : (rr == 0 ? c[3] : (rr == 1 ? c[4] : c[5]));
+    const double di = ec.di;
+    const double e_lin = di - ci;
+    const double e_rot = c[6] * di - ec.g6 * ci - (ec.s0 * c[3] + ec.s1 * c[4] + ec.s2 * c[5]);
+    double e = i < 3 ? e_lin : e_rot;
+    if (clamp) e = (e < ec.lo || e > ec.hi) ? e : 0.0;
+
     const int s = k.j_s;
-    double M[9] = {1.0, 0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 1.0};
-    if (k.j_ty == 1)
+    double M[9];
 #pragma unroll
-      for (int i = 0; i < 9; ++i) M[i] = S.JR[s][i];
+    for (int x = 0; x < 9; ++x) {
+      const double jr = S.JR[s][x];  // (unwritten for a prismatic segment: not selected)
+      M[x] = k.j_ty == 1 ? jr : (x % 4 == 0 ? 1.0 : 0.0);
+    }
     double v[3], rl[3], vl[3];
     for (int r = 0; r < 3; ++r) v[r] = M[r * 3 + 0] * k.j_fp[0] + M[r * 3 + 1] * k.j_fp[1] + M[r * 3 + 2] * k.j_fp[2];
     for (int d = 0; d < 3; ++d) {
@@ -216,25 +264,10 @@ __device__ __forceinline__ unsigned long long jacobian_and_error(int ns, const I
       S.J[d][lane] = (double)(float)vel[d];
       S.J[3 + d][lane] = (double)(float)rot[d];
     }
-  } else if (lane >= 8 && lane < 14) {
-    const int i = lane - 8;
-    const double* E = S.T[ns];
-    double c[7] = {E[9], E[10], E[11], 0.0, 0.0, 0.0, 0.0};
-    get_quaternion(E, &c[3]);
-    const double* d = t.goal;
-    double e;
-    if (i < 3) {
-      e = d[i] - c[i];
-    } else {
-      const int r = i - 3;
-      const double s0 = r == 0 ? 0.0 : (r == 1 ? d[5] : -d[4]);
-      const double s1 = r == 0 ? -d[5] : (r == 1 ? 0.0 : d[3]);
-      const double s2 = r == 0 ? d[4] : (r == 1 ? -d[3] : 0.0);
-      e = c[6] * d[i] - d[6] * c[i] - (s0 * c[3] + s1 * c[4] + s2 * c[5]);
+    if (lane < 6) {
+      S.err[i] = e;
+      out = fabs(e) > IK_BOUND;
     }
-    if (clamp) e = (e < t.lo[i] || e > t.hi[i]) ? e : 0.0;
-    S.err[i] = e;
-    out = fabs(e) > IK_BOUND;
   }
   const unsigned long long b = __ballot(out);
   wave_sync();
@@ -315,6 +348,8 @@ __global__ void __launch_bounds__(IK_THREADS) ik_kernel_t(const RobotDev* __rest
   const int ns = rb->n_seg;
   LaneConst k;
   load_const(rb, lane, k);
+  ErrConst ec;
+  load_err_const(t, lane, ec);
   const int max_iter = t.max_iter;
   const double tau = IK_SV_EPS * IK_SV_EPS;
   // main Gauss-Jordan lane (gi, gj) of the 6 x 7 system, or shifted-elimination lane (si, sj) of the upper triangle
@@ -331,13 +366,13 @@ __global__ void __launch_bounds__(IK_THREADS) ik_kernel_t(const RobotDev* __rest
   }
   if (lane < NJ) S.q[lane] = t.q[lane];
   wave_sync();
-  chain_fk(ns, rid, S, lane, k);
+  chain_fk(ns, rid, S, lane, k, 0);
   int iter = 0, fallback = 0, abandoned = 0;
 #ifdef SMP_IK_PROF
   unsigned long long _pf[8] = {0, 0, 0, 0, 0, 0, 0, 0}, _tp = __builtin_amdgcn_s_memtime();
 #endif
   while (true) {
-    const unsigned long long outb = jacobian_and_error(ns, t, S, lane, k, iter > 0);
+    const unsigned long long outb = jacobian_and_error(ns, ec, S, lane, k, iter > 0);
     IKP(0);
     if (iter > 0) {
       if (iter == max_iter) break;
@@ -445,21 +480,9 @@ __global__ void __launch_bounds__(IK_THREADS) ik_kernel_t(const RobotDev* __rest
         wave_sync();
       }
     }
-    // q_dot = J_vdls e = J^T z (control_laws.cpp:3455-3497), joint update with the limit check (:3504-3550)
-    if (lane < NJ) {
-      double z[6];
-#pragma unroll
-      for (int i = 0; i < 6; ++i) z[i] = normal ? S.M[i][6] / S.M[i][i] : S.z[i];
-      double pz[6];
-#pragma unroll
-      for (int i = 0; i < 6; ++i) pz[i] = S.J[i][lane] * z[i];
-      const double v = ((pz[0] + pz[1]) + (pz[2] + pz[3])) + (pz[4] + pz[5]);
-      const double nv = S.q[k.j_jn] + v * IK_DT;
-      if (!(nv < k.j_lo || nv > k.j_hi)) S.q[k.j_jn] = nv;
-    }
-    wave_sync();
     IKP(4);
-    chain_fk(ns, rid, S, lane, k);
+    // q_dot = J_vdls e = J^T z (control_laws.cpp:3455-3497), joint update with the limit check (:3504-3550), FK
+    chain_fk(ns, rid, S, lane, k, normal ? 1 : 2);
     IKP(5);
     ++iter;
     if (SEARCH && bst < b) {  // a lower candidate is REACHED and valid: this run can no longer be chosen
