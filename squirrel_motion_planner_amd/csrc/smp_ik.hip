@@ -133,9 +133,22 @@ __device__ __forceinline__ void chain_fk(int ns, unsigned rid, IkLds& S, int lan
   if (lane < ns) {
     double qq = S.q[k.f_jn];
     if (upd != 0 && k.f_ty != 0) {
+      // (one uniform branch around all six: a select per term compiled to six branches, each one LDS round trip
+      // and one division after the other)
       double z[6];
+      if (upd == 1) {
+        double nu[6], de[6];
 #pragma unroll
-      for (int i = 0; i < 6; ++i) z[i] = upd == 1 ? S.M[i][6] / S.M[i][i] : S.z[i];
+        for (int i = 0; i < 6; ++i) {
+          nu[i] = S.M[i][6];
+          de[i] = S.M[i][i];
+        }
+#pragma unroll
+        for (int i = 0; i < 6; ++i) z[i] = nu[i] / de[i];
+      } else {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) z[i] = S.z[i];
+      }
       double pz[6];
 #pragma unroll
       for (int i = 0; i < 6; ++i) pz[i] = S.J[i][k.f_col] * z[i];
