@@ -76,8 +76,9 @@ class BiRRTstarPlanner {
     }
 #endif
     if (urdf_.empty() && std::getenv("SMP_ROBOT_URDF")) {
+      if (!std::getenv("SMP_ROBOT_SRDF")) throw std::runtime_error("SMP_ROBOT_URDF is set but SMP_ROBOT_SRDF is not");
       urdf_ = read_file(std::getenv("SMP_ROBOT_URDF"));
-      srdf_ = read_file(std::getenv("SMP_ROBOT_SRDF") ? std::getenv("SMP_ROBOT_SRDF") : "");
+      srdf_ = read_file(std::getenv("SMP_ROBOT_SRDF"));
     }
     if (!urdf_.empty()) {
       const char* sp = std::getenv("SMP_ROBOT_SPHERES");
@@ -397,8 +398,9 @@ class MultiGpuPlanner {
     release();
     const char* env_urdf = std::getenv("SMP_ROBOT_URDF");
     if (urdf_.empty() && env_urdf) {
+      if (!std::getenv("SMP_ROBOT_SRDF")) throw std::runtime_error("SMP_ROBOT_URDF is set but SMP_ROBOT_SRDF is not");
       urdf_ = read_file(env_urdf);
-      srdf_ = read_file(std::getenv("SMP_ROBOT_SRDF") ? std::getenv("SMP_ROBOT_SRDF") : "");
+      srdf_ = read_file(std::getenv("SMP_ROBOT_SRDF"));
     }
     if (!urdf_.empty()) {
       const char* sp = std::getenv("SMP_ROBOT_SPHERES");

@@ -230,7 +230,10 @@ int smp_plan(smp_planner* p, const smp_query* q, smp_result* out);
 int smp_plan_batch(smp_planner* p, const smp_query* q, int n, smp_result* out);
 /* Independent queries over several planners (typically one per GPU, sharing a scene): query i runs on planner
  * i % n_planners, all planners concurrently (one host thread each); out[i] is query i's result, identical to what
- * smp_plan on that planner returns.  Each planner may appear once. */
+ * smp_plan on that planner returns.  Each planner may appear once; planners on one GPU split that GPU's co-resident
+ * workgroups among them for the call (each query's workgroups must all be resident).  Scenes set from grids
+ * (smp_planner_set_scene / _device) must keep every occupied cell 0.45 m plus one cell from the grid's faces
+ * (SMP_ERR_ARG otherwise): a sphere or primitive centred outside the grid is taken as free of the map. */
 int smp_plan_multi(smp_planner* const* planners, int n_planners, const smp_query* q, int n, smp_result* out);
 void smp_result_free(smp_result* r);
 

@@ -139,6 +139,7 @@ PROBES = [
     ("smp_probe_near", _i, [_i, _pd, _pd, _i, _pd, _p, _i, ctypes.c_double, _i, _p, _p, _p, _p,
                             ctypes.POINTER(ctypes.c_uint64), _pd]),
     ("smp_probe_check_latency", _i, [_p, _pd, _i64, _i, _i, _i, _i, _pd, ctypes.POINTER(ctypes.c_uint64), _pd]),
+    ("smp_probe_check_shape", _i, [_p, _pd, _i64, _i, _i, _i, _i, _p]),
     ("smp_probe_robot_dev", _i64, [_p, _p, _i64]),
     ("smp_probe_scene_slabs", _i64, [_p, _p, _p, _i64]),
 ]

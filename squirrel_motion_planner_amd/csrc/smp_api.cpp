@@ -146,12 +146,13 @@ struct smp_planner {
   // last plan (query 0) bookkeeping for smp_get_tree
   int last_n[2] = {0, 0};
   int slots_cache = 0;  // resident_slots (occupancy queries) once per planner
+  int slot_share = 1;   // planners planning on this planner's GPU at once (smp_plan_multi): its share of the slots
 };
 
 // Workgroups of BLOCK threads that can be resident at once on the device, for the planner's kernels (leader / scout
 // plan_kernel and helper_kernel share the CUs): occupancy per CU (registers, LDS) x CUs.
 static int resident_slots(smp_planner* p) {
-  if (p->slots_cache > 0) return p->slots_cache;
+  if (p->slots_cache > 0) return std::max(1, p->slots_cache / std::max(1, p->slot_share));
   int occ_plan = 0, occ_help = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_plan, reinterpret_cast<const void*>(&plan_kernel), BLOCK, 0) !=
           hipSuccess ||
@@ -161,7 +162,7 @@ static int resident_slots(smp_planner* p) {
     return p->num_cus;
   }
   p->slots_cache = p->num_cus * std::max(1, std::min(occ_plan, occ_help));
-  return p->slots_cache;
+  return std::max(1, p->slots_cache / std::max(1, p->slot_share));
 }
 
 static int update_mapcfg(smp_planner* p) {
@@ -444,8 +445,38 @@ void smp_planner_destroy(smp_planner* p) {
   delete p;
 }
 
+// The collision tests treat a sphere or primitive whose centre lies outside the grid as free of the map (centre_cell,
+// prim_candidate): exact only while every occupied cell keeps GRID_REACH (+ one cell of rounding margin) from every
+// face of the grid, which scene_from_keys' padding guarantees.  Grids from elsewhere (smp_scene_from_grid, a device
+// scene) are checked here: false if an occupied cell of the 4x4x4 bricks lies closer to a face.
+static bool occupancy_clear_of_faces(const uint64_t* bricks, int nx, int ny, int nz, double res) {
+  const int m = (int)std::ceil(GRID_REACH / res) + 1;
+  const int bnx = (nx + 3) / 4, bny = (ny + 3) / 4, bnz = (nz + 3) / 4;
+  const int lo[3] = {m, m, m}, hi[3] = {nx - 1 - m, ny - 1 - m, nz - 1 - m};
+  for (int bk = 0; bk < bnz; ++bk)
+    for (int bj = 0; bj < bny; ++bj)
+      for (int bi = 0; bi < bnx; ++bi) {
+        uint64_t w = bricks[((size_t)bk * bny + bj) * bnx + bi];
+        if (!w) continue;
+        if (4 * bi >= lo[0] && 4 * bi + 3 <= hi[0] && 4 * bj >= lo[1] && 4 * bj + 3 <= hi[1] && 4 * bk >= lo[2] &&
+            4 * bk + 3 <= hi[2])
+          continue;
+        for (; w; w &= w - 1) {
+          const int bit = __builtin_ctzll(w);
+          const int c[3] = {4 * bi + (bit & 3), 4 * bj + ((bit >> 2) & 3), 4 * bk + (bit >> 4)};
+          for (int d = 0; d < 3; ++d)
+            if (c[d] < lo[d] || c[d] > hi[d]) return false;
+        }
+      }
+  return true;
+}
+
 int smp_planner_set_scene(smp_planner* p, const smp_scene* s) {
   if (!p || !s) return SMP_ERR_ARG;
+  if (!occupancy_clear_of_faces(s->h.bricks.data(), s->h.nx, s->h.ny, s->h.nz, s->h.res)) {
+    fprintf(stderr, "smp_gpu: an occupied cell lies within %.2f m of the grid's faces (pad the grid)\n", GRID_REACH);
+    return SMP_ERR_ARG;
+  }
   HIPCHK(hipSetDevice(p->device));
   HIPCHK(p->d_bricks.reserve(s->h.bricks.size()));
   HIPCHK(p->d_d2.reserve(s->h.d2.size()));
@@ -544,6 +575,11 @@ int smp_planner_set_scene_device(smp_planner* p, const smp_scene_device* in) {
   for (int k = 0; k < d.n_prim; ++k)
     if (d.prim_rxy[k] > GRID_REACH) return SMP_ERR_ARG;
   HIPCHK(hipSetDevice(p->device));
+  {  // the occupancy must keep the collision tests' reach from the grid's faces (occupancy_clear_of_faces)
+    std::vector<uint64_t> hb(nb);
+    HIPCHK(hipMemcpy(hb.data(), in->bricks, nb * sizeof(uint64_t), hipMemcpyDefault));
+    if (!occupancy_clear_of_faces(hb.data(), nx, ny, nz, in->resolution)) return SMP_ERR_ARG;
+  }
   HIPCHK(p->d_bricks.reserve(nb));
   HIPCHK(p->d_d2.reserve(nc));
   // hipMemcpyDefault: a source on another GPU is a peer copy (xGMI), one on this GPU a device copy
@@ -916,6 +952,12 @@ static QueryDev make_qdev(QueryBuffers& b, size_t cap, long long rows) {
   d.svia = nullptr;
   d.sworkers = 1;
   d.nworkers = 1;
+  // configurations per job tile: by job size (smp_plan.h job_tile_ct); SMP_TILE_CT = 1 / 2 / 4 / 8 fixes it (experiments)
+  d.tile_ct = 0;
+  if (const char* e = std::getenv("SMP_TILE_CT")) {
+    const int v = std::atoi(e);
+    if (v == 1 || v == 2 || v == 4 || v == 8) d.tile_ct = v;
+  }
   d.sampler = 0;
   d.trace = nullptr;
   d.ttff = nullptr;
@@ -1184,10 +1226,20 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
     }
     if (launches == 0) hstamp("kernels launched");
     launches++;
-    // time the first feasible path on the host: poll the flags while the launch runs
-    {
+    // time the first feasible path on the host: poll the flags while the launch runs -- spinning (with a yield) until
+    // every query has its first path, then sleeping between polls; a seconds budget bounds the wait (SMP_DEBUG builds
+    // skip this loop for the bounded diagnostic wait below)
+    if (!debug) {
       hipError_t qe;
-      while ((qe = hipEventQuery(p->ev1)) == hipErrorNotReady) poll_ttff();
+      while ((qe = hipEventQuery(p->ev1)) == hipErrorNotReady) {
+        poll_ttff();
+        bool all = true;
+        for (int i : act) all = all && host_ttff[i] >= 0;
+        if (all) std::this_thread::sleep_for(std::chrono::microseconds(50));
+        else std::this_thread::yield();
+        if (tmax > 0 && std::chrono::duration<double>(std::chrono::steady_clock::now() - t_begin).count() > tmax * 4 + 60)
+          return SMP_ERR_HIP;
+      }
       if (qe != hipSuccess) HIPCHK(qe);
       poll_ttff();
     }
@@ -1395,6 +1447,13 @@ extern "C" int smp_plan_multi(smp_planner* const* ps, int np, const smp_query* q
   std::vector<std::vector<smp_result>> res(used);
   for (int i = 0; i < nq; ++i) part[i % used].push_back(qs[i]);
   std::vector<int> rcs(used, SMP_OK);
+  // planners on the same GPU run at once: each provisions its share of that GPU's co-resident workgroups (every
+  // workgroup of a query polls the others, so all of them must be resident)
+  for (int k = 0; k < used; ++k) {
+    int same = 0;
+    for (int j = 0; j < used; ++j) same += ps[j]->device == ps[k]->device;
+    ps[k]->slot_share = same;
+  }
   std::vector<std::thread> th;
   th.reserve(used);
   for (int k = 0; k < used; ++k) {
@@ -1402,6 +1461,7 @@ extern "C" int smp_plan_multi(smp_planner* const* ps, int np, const smp_query* q
     th.emplace_back([&, k] { rcs[k] = smp_plan_batch(ps[k], part[k].data(), (int)part[k].size(), res[k].data()); });
   }
   for (auto& t : th) t.join();
+  for (int k = 0; k < used; ++k) ps[k]->slot_share = 1;
   int rc = SMP_OK;
   for (int i = 0; i < nq; ++i) {
     out[i] = res[i % used][i / used];
@@ -1533,6 +1593,25 @@ extern "C" int smp_probe_check_latency(smp_planner* p, const double* q_soa, int6
   HIPCHK(hipMemcpy(ticks, dprof, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   (void)hipFree(dprof);
   *clock_hz = p->wall_rate_hz;
+  return SMP_OK;
+}
+
+// Validity flags of n configurations checked in tiles of the given shape (launch_check: 8 / 16 / 32 = the batch
+// checker's collide_tile, -1 / -2 / -4 / -8 = the job tiles' collide_wide with that many configurations): the parity
+// test of the job-tile shapes against the batch checker (tests/test_gpu_parity.py).
+extern "C" int smp_probe_check_shape(smp_planner* p, const double* q_soa, int64_t n, int check_self, int check_map,
+                                     int tile, int grid, uint8_t* valid) {
+  if (!p || n <= 0 || !q_soa || !valid || grid <= 0) return SMP_ERR_ARG;
+  if (!(tile == 8 || tile == 16 || tile == 32 || tile == -1 || tile == -2 || tile == -4 || tile == -8)) return SMP_ERR_ARG;
+  HIPCHK(hipSetDevice(p->device));
+  HIPCHK(p->d_cq.reserve((size_t)n * NJ));
+  HIPCHK(p->d_valid.reserve((size_t)n));
+  HIPCHK(hipMemcpyAsync(p->d_cq.p, q_soa, (size_t)n * NJ * sizeof(double), hipMemcpyHostToDevice, p->stream));
+  launch_check(tile, grid, p->stream, p->d_rb, p->sc, p->d_mc, p->d_cq.p, (long long)n, check_self,
+               check_map && p->have_scene, p->d_valid.p, nullptr);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(valid, p->d_valid.p, (size_t)n, hipMemcpyDeviceToHost, p->stream));
+  HIPCHK(hipStreamSynchronize(p->stream));
   return SMP_OK;
 }
 

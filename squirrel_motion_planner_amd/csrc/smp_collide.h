@@ -764,4 +764,192 @@ __device__ __forceinline__ void collide_tile(const RobotDev* __restrict__ rb, co
   }
 }
 
+// ------------------------------------------------------------------------------------------ job tiles (collide_wide)
+// LDS of one wavefront of collide_wide: the configuration's kinematics, centres and staging, private to the wavefront.
+struct WideWave {
+  union {
+    double lf[MAX_CHAIN][12];               // stages A/B: local frame of every chain step
+    struct {
+      double wc[MAX_SPH][3];                // C: sphere world centres
+      double pw[MAX_PRIM][5];               // C: primitive centres and x axes
+    } c;
+  } u;
+  union {
+    double fr[MAX_BODY][12];                // B -> centres: body frames (R row-major, p)
+    uint64_t stage[MAP_STAGE_W];            // map sweeps: the candidates' brick words (wave_map_staged)
+  } v;
+  uint32_t cand[(MAX_SPH + 31) / 32];       // this wavefront's candidate spheres (map sweep)
+  uint32_t pcand;                           // this wavefront's candidate primitives
+  uint8_t owner[MAP_STAGE_W], off[MAX_SPH];  // wave_map_staged: slot owners, first slot per sphere
+};
+static_assert(sizeof(WideWave::v) == MAP_STAGE_W * sizeof(uint64_t), "staging buffer = the body-frame rows");
+struct WideLds {
+  WideWave w[NWAVE];
+  int coll[NWAVE];                          // configuration c: 1 = in collision
+};
+
+// Collision test of nc <= ct configurations q_lds[c], ct in {1, 2, 4, 8}, all block threads.  Configuration c belongs
+// to the G = 8 / ct wavefronts c*G .. c*G + G - 1 (its group): a job tile of one configuration is spread over the whole
+// workgroup instead of one wavefront.  Every wavefront of a group computes the configuration's kinematics, all sphere
+// centres and all primitive frames by itself (the same values; the stages A/B/centres need no block barrier), then
+// takes its share of the tests -- the map tests of spheres and primitives s with s % G == g (g = its rank in the group:
+// box-gap / slab prefilter, exact sweeps of the candidates in one load round trip, as collide_tile) and the self pairs
+// of the 64-pair chunks k with k % G == g.  A configuration collides iff any test hits (the reference's
+// isInCollision is map || self, collision_checker.hpp:104-121), so the split changes no result; a wavefront stops
+// after its first hit or once another wavefront of the group reported one.  The caller zeroes L.coll[0 .. ct) before
+// the barrier that publishes q_lds; on return (after a block barrier) L.coll[c] is 1 for the colliding configurations.
+// prof (thread 0): stage clocks A, B, centres + prefilter loads, whole tile, as collide_tile's.
+__device__ __forceinline__ void collide_wide(const RobotDev* __restrict__ rb, const SceneDev& sc_in,
+                                             const MapCfg* __restrict__ mc, int ct, int nc, const double (*q_lds)[NJ],
+                                             int self, int map, WideLds& L, const TileOrder* ord = nullptr,
+                                             unsigned long long* prof = nullptr) {
+  const SceneDev sc = uniform_scene(sc_in);
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int G = __builtin_amdgcn_readfirstlane(NWAVE / ct);
+  const int c = wave / G, g = wave - c * G;
+  WideWave& W = L.w[wave];
+  const unsigned long long t0 = (prof && threadIdx.x == 0) ? wall_clock64() : 0;
+  unsigned long long ta = t0, tb = t0, tc = t0;
+  int live = c < nc;
+  if (live && ord) live = !(ord->ord[c] > ord->first(ord->grp[c]));
+  if (__builtin_amdgcn_readfirstlane(live)) {
+    const double* q = q_lds[c];
+    const int nch = rb->n_chain;
+    // A: local frame of every chain step (sin/cos included), one lane each
+    if (lane < nch) {
+      double st = 0.0, cs = 1.0;
+      if (rb->ch_type[lane] == 1) psincos(q[rb->ch_joint[lane]], &st, &cs);
+      Frame F;
+      chain_local(rb, lane, q, st, cs, &F);
+      double* o = W.u.lf[lane];
+      for (int i = 0; i < 9; ++i) o[i] = F.R[i];
+      o[9] = F.p[0]; o[10] = F.p[1]; o[11] = F.p[2];
+    }
+    if (lane < (MAX_SPH + 31) / 32) W.cand[lane] = 0u;
+    if (lane == 0) W.pcand = 0u;
+    wave_sync();
+    if (prof && threadIdx.x == 0) ta = wall_clock64();
+    // B: the chain product, one lane per element (rows r = 0..2 of four lanes: columns 0..2 of R, then p), as
+    // collide_tile's stage B (fmul's three-term sums in KDL order; row r of T from the lane's quad by DPP broadcasts)
+    if (lane < 12) {
+      const int r = lane >> 2, col = lane & 3;
+      const int lo = col < 3 ? col : 9, ls = col < 3 ? 3 : 1;
+      double v = col < 3 ? (r == col ? 1.0 : 0.0) : (r == 2 ? rb->root_z : 0.0);
+      double l0 = W.u.lf[0][lo], l1 = W.u.lf[0][lo + ls], l2 = W.u.lf[0][lo + 2 * ls];
+      int bd = rb->ch_body[0];
+      const int oidx = col < 3 ? r * 3 + col : 9 + r;
+      for (int k = 0; k < nch; ++k) {
+        const int kn = k + 1 < nch ? k + 1 : k;
+        const double* ln = W.u.lf[kn];
+        const double n0 = ln[lo], n1 = ln[lo + ls], n2 = ln[lo + 2 * ls];
+        const int bdn = rb->ch_body[kn];
+        const double t0v = quad_bcast<0>(v), t1v = quad_bcast<1>(v), t2v = quad_bcast<2>(v);
+        const double s = t0v * l0 + t1v * l1 + t2v * l2;
+        const double sp = s + v;
+        v = col < 3 ? s : sp;
+        if (bd >= 0) W.v.fr[bd][oidx] = v;
+        l0 = n0; l1 = n1; l2 = n2;
+        bd = bdn;
+      }
+    }
+    wave_sync();
+    if (prof && threadIdx.x == 0) tb = wall_clock64();
+    // centres of every sphere and frames of every primitive (the self pairs need them all); the prefilter loads of
+    // this wavefront's share, all issued together
+    const int nsph = rb->n_sph, npr = rb->n_prim;
+    const bool do_map = map && mc->has_map;
+    long long cell[2];
+    bool pc[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int it = u * 64 + lane;
+      cell[u] = -1;
+      pc[u] = false;
+      if (it < nsph) {
+        const double* B = W.v.fr[rb->sph_body[it]];
+        const double* p = &rb->sph_cb[it * 3];
+        double w[3];
+        for (int r = 0; r < 3; ++r) {
+          const double m = B[r * 3 + 0] * p[0] + B[r * 3 + 1] * p[1] + B[r * 3 + 2] * p[2];
+          w[r] = m + B[9 + r];
+        }
+        W.u.c.wc[it][0] = w[0]; W.u.c.wc[it][1] = w[1]; W.u.c.wc[it][2] = w[2];
+        if (do_map && mc->map_on[it] && it % G == g) cell[u] = centre_cell(sc, w);
+      } else if (it < nsph + npr) {
+        const int p = it - nsph;
+        double pw[5];
+        prim_world(rb, p, W.v.fr[rb->prim_body[p]], pw);
+        for (int i = 0; i < 5; ++i) W.u.c.pw[p][i] = pw[i];
+        pc[u] = do_map && mc->p_map_on[p] && p % G == g && prim_candidate(sc, sc_in.slab[p], mc->pT[p], pw);
+      }
+    }
+    uint32_t dv[2];
+    if (sc.d2b) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) dv[u] = cell[u] >= 0 ? (uint32_t)sc.d2b[cell[u]] : 0xffffffffu;
+    } else {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) dv[u] = cell[u] >= 0 ? (uint32_t)sc.d2[cell[u]] : 0xffffffffu;
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int it = u * 64 + lane;
+      if (cell[u] >= 0 && dv[u] <= mc->T[it]) atomicOr(&W.cand[it >> 5], 1u << (it & 31));
+      if (pc[u]) atomicOr(&W.pcand, 1u << (it - nsph));
+    }
+    wave_sync();
+    if (prof && threadIdx.x == 0) tc = wall_clock64();
+    // map: this wavefront's candidate primitives, then its candidate spheres (their brick words in one round trip)
+    bool hit = false;
+    for (uint32_t pm = (uint32_t)__builtin_amdgcn_readfirstlane((int)W.pcand); pm && !hit;) {
+      const int p = __builtin_ctz(pm);
+      pm &= pm - 1;
+      if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&L.coll[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))
+        break;
+      const double pw[5] = {W.u.c.pw[p][0], W.u.c.pw[p][1], W.u.c.pw[p][2], W.u.c.pw[p][3], W.u.c.pw[p][4]};
+      hit = wave_prim_map(sc, rb->prim_type[p], &rb->prim_h[p * 3], pw, lane);
+    }
+    uint32_t any = 0;
+    for (int wd = 0; wd < (MAX_SPH + 31) / 32; ++wd) any |= W.cand[wd];
+    if (!hit && __builtin_amdgcn_readfirstlane((int)(any != 0)) &&
+        !__builtin_amdgcn_readfirstlane(__hip_atomic_load(&L.coll[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))
+      hit = wave_map_staged(rb, sc, W.u.c.wc, W.cand, nsph, W.v.stage, W.owner, W.off, lane);
+    // self: this wavefront's 64-pair chunks of the sphere pairs, then of the (primitive, sphere) pairs
+    if (self && !hit &&
+        !__builtin_amdgcn_readfirstlane(__hip_atomic_load(&L.coll[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) {
+      const int nsp = rb->n_spairs, npp = rb->n_ppairs, ks = (nsp + 63) >> 6;
+      bool sh = false;
+#pragma unroll 4
+      for (int k = g; k < ks; k += G) {
+        const int p = k * 64 + lane;
+        if (p < nsp) {
+          const uint32_t ab = rb->sp_ab[p];
+          const double* wa = W.u.c.wc[ab & 0xff];
+          const double* wb = W.u.c.wc[ab >> 8];
+          const double ex = wa[0] - wb[0], ey = wa[1] - wb[1], ez = wa[2] - wb[2];
+          sh |= ex * ex + ey * ey + ez * ez <= rb->sp_rr2[p];
+        }
+      }
+      // chunk numbers continue after the sphere pairs', so that G > ks wavefronts share the primitive pairs
+      for (int k = (g - ks % G + G) % G; k * 64 < npp; k += G) {
+        const int p = k * 64 + lane;
+        if (p < npp) {
+          const uint32_t ps = rb->pp_ps[p];
+          const int pr = ps & 0xff, sp = ps >> 8;
+          sh |= sphere_prim(rb->prim_type[pr], &rb->prim_h[pr * 3], W.u.c.pw[pr], W.u.c.wc[sp], rb->sph_r[sp]);
+        }
+      }
+      hit = __ballot(sh) != 0;
+    }
+    if (hit && lane == 0) {
+      atomicOr(&L.coll[c], 1);
+      if (ord) atomicMin(&ord->grp_first[ord->grp[c]], ord->ord[c]);
+    }
+  }
+  __syncthreads();
+  if (prof && threadIdx.x == 0) {
+    prof[0] += ta - t0; prof[1] += tb - ta; prof[2] += tc - tb; prof[3] += wall_clock64() - tb;
+  }
+}
+
 }  // namespace smp

@@ -71,6 +71,35 @@ __global__ void __launch_bounds__(BLOCK) check_kernel_t(const RobotDev* __restri
   if (pr && threadIdx.x == 0) { pr[4] = __builtin_amdgcn_s_memtime() - c0; pr[5] = wall_clock64() - w0; }
 }
 
+// The job tiles' shape (collide_wide, ct configurations spread over the workgroup) as a batch check: grid-stride over
+// tiles of ct configurations.  Latency / rate probe of the helpers' tiles (smp_probe_check_latency, tile = -ct).
+__global__ void __launch_bounds__(BLOCK) check_wide_kernel(const RobotDev* __restrict__ rb, SceneDev sc,
+                                                           const MapCfg* __restrict__ mc, const double* __restrict__ q,
+                                                           long long n, int ct, int self, int map,
+                                                           uint8_t* __restrict__ valid, unsigned long long* prof) {
+  __shared__ WideLds L;
+  __shared__ double ql[TILE_CT_MAX][NJ];
+  unsigned long long* pr = blockIdx.x == 0 ? prof : nullptr;
+  unsigned long long c0 = 0, w0 = 0;
+  if (pr && threadIdx.x == 0) { c0 = __builtin_amdgcn_s_memtime(); w0 = wall_clock64(); }
+  stage_model(rb, mc, &g_rb, &g_mc);
+  const long long ntiles = (n + ct - 1) / ct;
+  for (long long t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const long long base = t * ct;
+    const int nc = (int)min((long long)ct, n - base);
+    if (threadIdx.x < nc * NJ) {
+      const int c = threadIdx.x / NJ, j = threadIdx.x - c * NJ;
+      ql[c][j] = q[(long long)j * n + base + c];
+    }
+    if (threadIdx.x < TILE_CT_MAX) L.coll[threadIdx.x] = 0;
+    __syncthreads();
+    collide_wide(&g_rb, sc, &g_mc, ct, nc, ql, self, map, L, nullptr, pr);
+    if (threadIdx.x < nc) valid[base + threadIdx.x] = L.coll[threadIdx.x] ? 0 : 1;
+    __syncthreads();
+  }
+  if (pr && threadIdx.x == 0) { pr[4] = __builtin_amdgcn_s_memtime() - c0; pr[5] = wall_clock64() - w0; }
+}
+
 // Batched isConfigValid (birrt_star.cpp:6897-6908): grid-stride over tiles of CT configurations.
 // Largest per-work-item private segment (scratch) of the batch check kernels (smp_planner_create raises the
 // device stack limit to cover every kernel of the library).
@@ -78,7 +107,8 @@ size_t check_kernels_private_bytes() {
   size_t need = 0;
   hipFuncAttributes fa;
   const void* ks[] = {reinterpret_cast<const void*>(&check_kernel_t<8>), reinterpret_cast<const void*>(&check_kernel_t<16>),
-                      reinterpret_cast<const void*>(&check_kernel_t<CHECK_CT>)};
+                      reinterpret_cast<const void*>(&check_kernel_t<CHECK_CT>),
+                      reinterpret_cast<const void*>(&check_wide_kernel)};
   for (const void* k : ks)
     if (hipFuncGetAttributes(&fa, k) == hipSuccess && (size_t)fa.localSizeBytes > need) need = fa.localSizeBytes;
   return need;
@@ -86,6 +116,10 @@ size_t check_kernels_private_bytes() {
 
 void launch_check(int ct, int grid, hipStream_t st, const RobotDev* rb, SceneDev sc, const MapCfg* mc, const double* q,
                   long long n, int self, int map, uint8_t* valid, unsigned long long* prof) {
+  if (ct == -1 || ct == -2 || ct == -4 || ct == -8) {  // job-tile shape (collide_wide)
+    hipLaunchKernelGGL(check_wide_kernel, dim3(grid), dim3(BLOCK), 0, st, rb, sc, mc, q, n, -ct, self, map, valid, prof);
+    return;
+  }
   switch (ct) {
     case 8: hipLaunchKernelGGL(check_kernel_t<8>, dim3(grid), dim3(BLOCK), 0, st, rb, sc, mc, q, n, self, map, valid, prof); break;
     case 16: hipLaunchKernelGGL(check_kernel_t<16>, dim3(grid), dim3(BLOCK), 0, st, rb, sc, mc, q, n, self, map, valid, prof); break;
@@ -241,17 +275,17 @@ __device__ __forceinline__ unsigned long long merge_key(const MergeLds& M, int s
 // LDS of job mode (leader and helper kernel): the published job + one job tile.
 struct JobLds {
   ScanLds scan;                            // helper: its slice of a scan job
-  TileLds<HELPER_CT> T;
-  double tq[HELPER_CT][NJ];
+  WideLds T;                               // one job tile (collide_wide)
+  double tq[TILE_CT_MAX][NJ];
   double start[MAXE][NJ], step[MAXE][NJ];  // the job's edges (needed edges of the batch, compacted)
   unsigned words[JOB_WORDS];               // helper: the payload words as received
-  unsigned rmask[JOB_TILES];               // leader: collision mask per tile
-  int rdone[JOB_TILES];                    // leader: tile result known
+  uint8_t rmask[JOB_TILES];                // leader: collision mask per tile
+  uint8_t rdone[JOB_TILES];                // leader: tile result known
   int emap[MAXE];                          // leader: job edge -> batch edge
   int first[MAXE];                         // leader: first colliding point per job edge
-  int E, np1, nslots, ntiles, self, map, seq, steal, hidx, left;
+  int E, np1, nslots, ntiles, ct, self, map, seq, steal, hidx, left;  // ct: configurations per tile
   int skip, sfv, tskip;                    // job in skip mode / stop-first-valid; tile wholly skipped
-  int tgrp[HELPER_CT], tord[HELPER_CT];    // skip mode: the tile's TileOrder (edge, point or "skip")
+  int tgrp[TILE_CT_MAX], tord[TILE_CT_MAX];  // skip mode: the tile's TileOrder (edge, point or "skip")
   unsigned long long tprof[4];             // SMP_JOB_PROF builds: this helper's tile stage clocks
   int go[2];  // poll-loop decisions, double-buffered by iteration parity (a slow wave may still read the last one)
 };
@@ -1381,7 +1415,7 @@ __device__ __forceinline__ unsigned long long granule(int seq, unsigned w) {
 // tile's TileOrder.  All threads.
 __device__ __forceinline__ bool job_tile_skip(const Ctx& C, JobLds& J, int t, int seq) {
   const JobBoard* jb = C.Q.jb;
-  const int np1 = uni(J.np1), ne = uni(J.E);
+  const int np1 = uni(J.np1), ne = uni(J.E), ct = uni(J.ct);
   for (int u = threadIdx.x; u < t; u += BLOCK) {
     if (!J.rdone[u]) {
       const unsigned long long v = ld_agent(&jb->res[u]);
@@ -1394,7 +1428,7 @@ __device__ __forceinline__ bool job_tile_skip(const Ctx& C, JobLds& J, int t, in
     if (!J.rdone[u]) continue;
     unsigned m = J.rmask[u];
     while (m) {
-      const int sl = u * HELPER_CT + __builtin_ctz(m), k = sl / np1;
+      const int sl = u * ct + __builtin_ctz(m), k = sl / np1;
       m &= m - 1;
       atomicMin(&J.first[k], sl - k * np1);
     }
@@ -1403,14 +1437,14 @@ __device__ __forceinline__ bool job_tile_skip(const Ctx& C, JobLds& J, int t, in
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
     bool fr = false;
-    if (J.sfv && lane < ne && (lane + 1) * np1 <= t * HELPER_CT && J.first[lane] >= np1) {
+    if (J.sfv && lane < ne && (lane + 1) * np1 <= t * ct && J.first[lane] >= np1) {
       fr = true;
-      for (int u = (lane * np1) / HELPER_CT; u <= ((lane + 1) * np1 - 1) / HELPER_CT; ++u)
+      for (int u = (lane * np1) / ct; u <= ((lane + 1) * np1 - 1) / ct; ++u)
         if (!J.rdone[u]) { fr = false; break; }
     }
     const unsigned long long fb = __ballot(fr);
     const int ff = fb ? __builtin_ctzll(fb) : (1 << 30);
-    const int base = t * HELPER_CT, nc = min(HELPER_CT, J.nslots - base);
+    const int base = t * ct, nc = min(ct, J.nslots - base);
     bool live = false;
     if (lane < nc) {
       const int sl = base + lane, k = sl / np1, i = sl - k * np1;
@@ -1430,7 +1464,7 @@ __device__ __forceinline__ bool job_tile_skip(const Ctx& C, JobLds& J, int t, in
 // `seq` >= 0 in skip mode: configurations skipped by job_tile_skip report no collision.
 __device__ __forceinline__ unsigned job_tile_mask(const Ctx& C, JobLds& J, int t, unsigned long long* prof = nullptr,
                                                   int seq = -1) {
-  const int base = t * HELPER_CT, nc = min(HELPER_CT, uni(J.nslots) - base);
+  const int ct = uni(J.ct), base = t * ct, nc = min(ct, uni(J.nslots) - base);
   const bool sk = seq >= 0 && uni(J.skip) && t >= uni(C.Q.nworkers);
   if (sk && job_tile_skip(C, J, t, seq)) return 0u;
   if (threadIdx.x < nc * NJ) {
@@ -1438,9 +1472,10 @@ __device__ __forceinline__ unsigned job_tile_mask(const Ctx& C, JobLds& J, int t
     const int sl = base + c, k = sl / J.np1, i = sl - k * J.np1;
     J.tq[c][j] = J.start[k][j] + i * J.step[k][j];
   }
+  if (threadIdx.x < TILE_CT_MAX) J.T.coll[threadIdx.x] = 0;
   __syncthreads();
   const TileOrder order{J.tgrp, J.tord, J.first, false};
-  collide_tile<HELPER_CT>((&g_rb), C.sc, (&g_mc), nc, J.tq, J.self, J.map, J.T, sk ? &order : nullptr, prof);
+  collide_wide((&g_rb), C.sc, (&g_mc), ct, nc, J.tq, J.self, J.map, J.T, sk ? &order : nullptr, prof);
   unsigned m = 0;
   for (int c = 0; c < nc; ++c) m |= (J.T.coll[c] ? 1u : 0u) << c;
   __syncthreads();
@@ -1484,7 +1519,8 @@ __device__ __forceinline__ void edge_validity_job(const Ctx& C, int E, int pslot
       J.E = ne;
       J.np1 = np1;
       J.nslots = ne * np1;
-      J.ntiles = (ne * np1 + HELPER_CT - 1) / HELPER_CT;
+      J.ct = job_tile_ct(ne * np1, W, C.Q.tile_ct);
+      J.ntiles = (ne * np1 + J.ct - 1) / J.ct;
       J.self = g_L.S.self; J.map = g_L.S.map;
       J.seq = ++g_L.job_seq;
       J.skip = J.ntiles > W;  // more tiles than workers: later rounds skip what earlier ones decided
@@ -1493,7 +1529,7 @@ __device__ __forceinline__ void edge_validity_job(const Ctx& C, int E, int pslot
   }
   if (threadIdx.x < E) g_L.eg_first[threadIdx.x] = np1;
   __syncthreads();
-  const int ne = uni(J.E), nt = uni(J.ntiles), seq = uni(J.seq);
+  const int ne = uni(J.E), nt = uni(J.ntiles), seq = uni(J.seq), ct = uni(J.ct);
   if (ne == 0) {
     // nothing to check (the scout's record had every edge): no job whose latency the scan would hide, and its
     // result may not be needed (OV_NEAR_EXPAND when the expand edge collides) -- the caller scans if it must
@@ -1514,7 +1550,7 @@ __device__ __forceinline__ void edge_validity_job(const Ctx& C, int E, int pslot
     unsigned w;
     if (i == 0) {
       w = (unsigned)ne | (unsigned)np1 << 8 | (unsigned)(J.self != 0) << 16 | (unsigned)(J.map != 0) << 17 |
-          (unsigned)J.skip << 19 | (unsigned)J.sfv << 20;
+          (unsigned)J.skip << 19 | (unsigned)J.sfv << 20 | (unsigned)__builtin_ctz((unsigned)J.ct) << 21;
     } else {
       const int m = i - 1, k = m >> 5, r = m & 31, j = (r & 15) >> 1;
       const unsigned long long bits = (unsigned long long)__double_as_longlong(r < 16 ? J.start[k][j] : J.step[k][j]);
@@ -1606,7 +1642,7 @@ __device__ __forceinline__ void edge_validity_job(const Ctx& C, int E, int pslot
     while (m) {
       const int c = __builtin_ctz(m);
       m &= m - 1;
-      const int sl = t * HELPER_CT + c, kk = sl / np1;
+      const int sl = t * ct + c, kk = sl / np1;
       atomicMin(&J.first[kk], sl - kk * np1);
     }
   }
@@ -1765,7 +1801,6 @@ __device__ void scan_run(const Ctx& C, int near, int t, const double* q, int i0,
   __syncthreads();
   const JobBoard* jb = C.Q.jb;
   unsigned long long t_prog = wall_clock64();
-  const unsigned long long t_start = t_prog;
   int last_done = 0;
   // One collection round loads every granule of every outstanding result at once (up to 4 per thread per pass:
   // independent loads, one round trip), then keeps the results whose needed granules all carry this job's number.
@@ -1843,12 +1878,9 @@ __device__ void scan_run(const Ctx& C, int near, int t, const double* q, int i0,
       const unsigned long long now = wall_clock64();
       const int nd = M.ndone;
       if (nd != last_done) { last_done = nd; t_prog = now; }
+      // a slice missing SCAN_WAIT after the last progress is scanned here (stealing guarantees progress: no timeout
+      // status is needed, and a slow scan is not an error)
       int st = nd >= P - 1 ? 1 : (now - t_prog > SCAN_WAIT ? 2 : 0);
-      if (st != 1 && now - t_start > 200000000ull) {  // 2 s: never hang (the slices are then scanned here)
-        g_L.S.status = -5;
-        g_L.S.phase = 2;
-        st = 2;
-      }
       if (st == 2) {
         int w = 1;
         while (w < P && M.done[w]) ++w;
@@ -2014,7 +2046,8 @@ __device__ __forceinline__ void helper_main(const Ctx& C, int hidx, JobLds& J) {
       J.skip = (hdr >> 19) & 1;
       J.sfv = (hdr >> 20) & 1;
       J.nslots = ne * J.np1;
-      J.ntiles = (J.nslots + HELPER_CT - 1) / HELPER_CT;
+      J.ct = 1 << ((hdr >> 21) & 3);
+      J.ntiles = (J.nslots + J.ct - 1) / J.ct;
     }
     if (hdr & (1u << 19))
       for (int t = threadIdx.x; t < JOB_TILES; t += BLOCK) J.rdone[t] = 0;

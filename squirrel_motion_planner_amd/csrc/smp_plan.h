@@ -75,13 +75,23 @@ struct ViaNode {               // via node pending insertion (selected_via_nodes
 // "data-tagged granules"; an aligned 8-byte store is single-copy atomic): the high 32 bits of every granule are
 // the job number, the low 32 bits data, so a reader knows a granule is current without any flag, fence or
 // drain.  Granules are stored and read with agent-scope (sc1) relaxed atomics.
-#ifndef SMP_HELPER_CT
-#define SMP_HELPER_CT 8
-#endif
-constexpr int HELPER_CT = SMP_HELPER_CT;          // configurations per job tile
-static_assert(HELPER_CT <= 32, "a tile's collision mask is one 32-bit word");
+// Job tiles (DESIGN.md "Helpers"): a job of S configurations (its slots) checked by W workers (the leader + W - 1
+// helpers) is cut into tiles of ct configurations, ct the smallest of 1, 2, 4 whose tiles the helpers take in one
+// round, else 8 (the tiles of one round then exceed the helpers: skip mode).  A tile of ct configurations is spread
+// over the whole workgroup (collide_wide: 8 / ct wavefronts per configuration), so the fewer configurations per tile,
+// the shorter the tile and the job's round trip.
+constexpr int TILE_CT_MAX = BLOCK / 64;         // configurations per tile at most (one per wavefront)
 constexpr int JOB_SLOTS = MAXE * (MAX_PTS + 1); // (edge, point) slots of one job
-constexpr int JOB_TILES = (JOB_SLOTS + HELPER_CT - 1) / HELPER_CT;
+constexpr int JOB_TILES = 256;                  // tiles of one job at most (W - 1 <= 255 for ct < 8)
+static_assert(JOB_TILES * TILE_CT_MAX >= JOB_SLOTS, "a job of 8-configuration tiles fits the result granules");
+// ct of a job of `slots` configurations and W workers; `fixed` > 0 forces 1, 2, 4 or 8 (QueryDev::tile_ct, experiments).
+__host__ __device__ inline int job_tile_ct(int slots, int W, int fixed) {
+  if (fixed > 0) return (slots + fixed - 1) / fixed <= JOB_TILES ? fixed : TILE_CT_MAX;
+  const int helpers = W - 1 < JOB_TILES ? W - 1 : JOB_TILES;
+  for (int ct = 1; ct < TILE_CT_MAX; ct <<= 1)
+    if ((slots + ct - 1) / ct <= helpers) return ct;
+  return TILE_CT_MAX;
+}
 constexpr int JOB_WORDS = 1 + 4 * NJ * MAXE;     // payload words: header + (start, step) halves per edge
 constexpr int SMP_RING = 16;                     // run-ahead sampler: samples kept ahead of the leader
 // Distributed tree scans (DESIGN.md "Scans of large trees"): a workgroup splits a nearest / near scan of a large tree
@@ -101,8 +111,9 @@ struct JobBoard {
   int pad0[7];
   unsigned long long dbg[12];  // SMP_JOB_PROF builds: publish time, helper pickup / finish delay sums and counts,
                                // helper tile stage clocks (collide_tile A, B, C-centres, C)
-  // leader -> helpers: word 0 = header (edges | np1 << 8 | self << 16 | map << 17); word 1 + 32k + 2j (+1) =
-  // low (high) half of edge k's start[j], word 1 + 32k + 16 + 2j (+1) = of its step[j]
+  // leader -> helpers: word 0 = header (edges | np1 << 8 | self << 16 | map << 17 | scan job << 18 | skip << 19 |
+  // stop-first-valid << 20 | log2(tile ct) << 21); word 1 + 32k + 2j (+1) = low (high) half of edge k's start[j],
+  // word 1 + 32k + 16 + 2j (+1) = of its step[j]
   unsigned long long pay[JOB_WORDS];
   int pad1[32 - (2 * JOB_WORDS) % 32];
   // helpers -> leader: tile t's collision mask (bit c = configuration c of the tile collides)
@@ -280,6 +291,7 @@ struct QueryDev {
   int scan_min;                // nodes in a scan's range from which it is split over the helpers (0: never)
   int scan_pnn, scan_pnear;    // participants (this workgroup + helpers) of a split nearest / near scan, <= SCAN_P
   int nworkers;                // leader + tile helper workgroups (tile w, w + nworkers, ... is worker w's)
+  int tile_ct;                 // configurations per job tile: 0 = by job size (job_tile_ct), else 1 / 2 / 4 / 8
   int sampler;                 // 1: the last helper workgroup is the run-ahead sampler
   TreeDev tr[2];
   ViaNode* via;                // [via_cap]

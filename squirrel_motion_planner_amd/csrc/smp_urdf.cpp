@@ -273,6 +273,7 @@ struct Joint {
       double a[3];
       rot_vec(Fo.R, au.data(), a);
       const double nn = kdl_norm(a);
+      if (!(nn > 0.0)) throw std::runtime_error("urdf: joint axis of zero length");
       for (int i = 0; i < 3; ++i) axis[i] = a[i] / nn;
       kdl = type == "prismatic" ? 2 : 1;
     }
@@ -529,7 +530,10 @@ void robot_from_urdf(const std::string& urdf_text, const std::string& srdf_text,
 
   // ---- rigid-body collapse (collision_checker.hpp:519-539 recursion, pre-composed into body frames)
   auto body_of = [&](int i) {
-    while (tree[i].joint < 0) i = tree[i].parent;
+    const int i0 = i;
+    while (i >= 0 && tree[i].joint < 0) i = tree[i].parent;
+    // a collision link on the root, or fixed to it, has no planning joint above it: the model cannot place it
+    if (i < 0) throw std::runtime_error("urdf: no planning joint above collision link " + tree[i0].name);
     return i;
   };
   auto offset = [&](int body, int i, bool* ident) {
@@ -556,6 +560,7 @@ void robot_from_urdf(const std::string& urdf_text, const std::string& srdf_text,
   for (const Sph& s : S) bset.insert(body_of(s.link));
   for (int i : prim_links) bset.insert(body_of(i));
   const std::vector<int> bodies(bset.begin(), bset.end());
+  if (bodies.empty()) throw std::runtime_error("urdf: no collision link below a planning joint");
   auto bidx = [&](int b) { return (int)(std::find(bodies.begin(), bodies.end(), b) - bodies.begin()); };
   json::Value body_chain = arr();
   for (int k = 1; k <= bodies.back(); ++k) {

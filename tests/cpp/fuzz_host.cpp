@@ -96,6 +96,31 @@ int main(int argc, char** argv) {
     if (argc < 5) return 2;
     srdf = slurp(argv[3]);
     spheres = slurp(argv[4]);
+    // structural mutations byte flips rarely reach: collision geometry moved onto each link in turn (the root and the
+    // links fixed to it have no planning joint above them), each joint axis zeroed, every collision element removed
+    const std::string col = "<collision><geometry><box size=\"0.1 0.1 0.1\"/></geometry></collision>";
+    for (size_t p = data.find("<link name="); p != std::string::npos; p = data.find("<link name=", p + 1)) {
+      const size_t e = data.find('>', p);
+      if (e == std::string::npos) break;
+      std::string m = data;
+      if (m[e - 1] == '/') m.replace(e - 1, 2, ">" + col + "</link>");
+      else m.insert(e + 1, col);
+      inputs.push_back(m);
+    }
+    for (size_t p = data.find("<axis xyz=\""); p != std::string::npos; p = data.find("<axis xyz=\"", p + 1)) {
+      const size_t q = data.find('"', p + 11);
+      if (q == std::string::npos) break;
+      std::string m = data;
+      m.replace(p + 11, q - (p + 11), "0 0 0");
+      inputs.push_back(m);
+    }
+    std::string nc = data;
+    for (size_t p; (p = nc.find("<collision")) != std::string::npos;) {
+      const size_t q = nc.find("</collision>", p);
+      if (q == std::string::npos) break;
+      nc.erase(p, q + 12 - p);
+    }
+    inputs.push_back(nc);
   }
   for (const std::string& in : inputs) {
     if (kind == "bt" || kind == "ot") {

@@ -114,6 +114,32 @@ def test_check_configs_parity(gp, orobot, name, flags):
     assert 0.05 < v.mean() < 0.99
 
 
+@pytest.mark.parametrize("name", ["c2", "room3"])
+@pytest.mark.parametrize("tile", [-1, -2, -4, -8, 8])
+def test_job_tile_shapes_parity(gp, orobot, name, tile):
+    """The helpers' job tiles (collide_wide: ct = -tile configurations spread over the workgroup's 8 wavefronts, the map
+    and self tests split among them) decide every configuration as the oracle does, with self / map on and off.  The
+    configurations include points along tree-like edges near obstacles (many candidate spheres per configuration)."""
+    sc, gscene, osc = scene_pair(name)
+    gp.set_scene(gscene)
+    gp.set_disabled_map_links([])
+    rng = np.random.default_rng(5)
+    q = random_configs(sc, 20000, 11, orobot)
+    a, b = q[rng.integers(0, len(q), 500)], q[rng.integers(0, len(q), 500)]
+    t = np.linspace(0.0, 1.0, 21)[None, :, None]
+    q = np.concatenate([q, (a[:, None, :] + t * (b - a)[:, None, :]).reshape(-1, 8)])
+    soa = np.ascontiguousarray(q.T)
+    orc = O.Oracle(orobot, osc)
+    for flags in [(1, 1), (1, 0), (0, 1)]:
+        v = np.zeros(len(q), np.uint8)
+        L.check(L.lib().smp_probe_check_shape(gp.h, soa.ctypes.data_as(_pd), len(q), flags[0], flags[1], tile, 2048,
+                                              v.ctypes.data_as(ctypes.c_void_p)))
+        ov = orc.check_configs(q, *flags)
+        mism = np.flatnonzero(v != ov)
+        assert len(mism) == 0, "tile %d flags %s: mismatches at %s" % (tile, flags, mism[:10])
+        assert 0.05 < v.mean() < 0.99
+
+
 def test_disabled_map_links(gp, orobot):
     sc, gscene, osc = scene_pair("c2")
     gp.set_scene(gscene)

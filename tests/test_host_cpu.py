@@ -139,6 +139,18 @@ def test_urdf_path_errors():
     spec["links"]["no_such_link"] = [[0, 0, 0, 0.1]]
     assert L.lib().smp_robot_create_urdf(urdf.encode(), srdf.encode(), json.dumps(spec).encode(),
                                          ctypes.byref(h)) == L.SMP_ERR_PARSE
+    # descriptions the model cannot place are parse errors, never out-of-bounds reads: collision geometry on the root
+    # link (no planning joint above it), a joint axis of zero length, no collision link at all
+    m = re.search(r'<link name="base_link_origin"\s*/?>', urdf)
+    col = '<link name="base_link_origin"><collision><geometry><box size="0.1 0.1 0.1"/></geometry></collision>'
+    root_box = urdf.replace(m.group(0), col + ("</link>" if m.group(0).endswith("/>") else ""))
+    zero_axis = urdf.replace('<axis xyz="0 0 1"', '<axis xyz="0 0 0"', 1)
+    no_col = re.sub(r"<collision>.*?</collision>", "", urdf, flags=re.S)
+    spec0 = json.load(open(L.SPHERES_JSON))
+    spec0["links"] = {}
+    for u, sp in [(root_box, open(L.SPHERES_JSON).read()), (zero_axis, open(L.SPHERES_JSON).read()),
+                  (no_col, json.dumps(spec0))]:
+        assert L.lib().smp_robot_create_urdf(u.encode(), srdf.encode(), sp.encode(), ctypes.byref(h)) == L.SMP_ERR_PARSE
     # a box link given spheres in the spec is collided with those spheres instead of exactly
     spec = json.load(open(L.SPHERES_JSON))
     spec["links"]["kinect_link"] = [[0.0, 0.0, 0.0, 0.1]]

@@ -32,13 +32,16 @@ lib = L.lib()
 for name, X in (("tree-edges", Q), ("random", R)):
     soa = np.ascontiguousarray(X.T)
     n = len(X)
-    for tile, grid in ((32, 1), (16, 1), (8, 1), (32, 2048)):
+    # tile < 0: the helpers' job tiles (collide_wide, -tile configurations spread over the workgroup)
+    shapes = [(int(v), 1) for v in os.environ.get("SMP_TILES", "8,-8,-4,-2,-1").split(",")] + [(32, 2048), (-1, 2048)]
+    for tile, grid in shapes:
         ms = ctypes.c_double()
         hz = ctypes.c_double()
         ticks = (ctypes.c_uint64 * 8)()
         L.check(lib.smp_probe_check_latency(gp.h, soa.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), n, 1, 1, grid, tile,
                                             ctypes.byref(ms), ticks, ctypes.byref(hz)))
-        tiles = (n + tile - 1) // tile
+        ct = abs(tile)
+        tiles = (n + ct - 1) // ct
         per_tile_us = [t / hz.value * 1e6 / (tiles if grid == 1 else max(1, tiles // grid)) for t in ticks]
         print("%-10s tile %2d n %7d grid %5d: %.2f ms  %.3g configs/s  per tile %.2f us  stages(us) A %.2f B %.2f C0 %.2f C %.2f"
               % (name, tile, n, grid, ms.value, n / (ms.value * 1e-3), ms.value * 1e3 / tiles * (grid if grid > 1 else 1) /
