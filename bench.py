@@ -41,9 +41,10 @@ def parse():
     ap.add_argument("--scout", type=int, default=1,
                     help="scout workgroups per query (1 automatic, 0 none, 2..8 that many)")
     ap.add_argument("--seed", type=int, default=1)
-    ap.add_argument("--workload", choices=("c2", "c3", "c5"), default="c2",
-                    help="c2 (default, BASELINE configs[1]): the single C2 query; c3: random (start, goal) pairs on "
-                         "the C2 scene, 8 per GPU (configs[2]); c5: 2 cm dense clutter, 8 random queries per GPU "
+    ap.add_argument("--workload", choices=("c2", "c3", "c5"), default=None,
+                    help="c2 (default on one GPU, BASELINE configs[1]): the single C2 query; c3 (default with "
+                         "WORLD_SIZE > 1, configs[2]: 64 queries sharded 8 per GPU at 8 GPUs): random (start, goal) "
+                         "pairs on the C2 scene, 8 per GPU; c5: 2 cm dense clutter, 8 random queries per GPU "
                          "(configs[4])")
     ap.add_argument("--iterations", type=int, default=None,
                     help="iteration budget per query instead of --samples (C3: 1e5 in SURVEY.md 8d)")
@@ -208,6 +209,10 @@ def main():
     from squirrel_motion_planner_amd import distributed as D, scenes
     from squirrel_motion_planner_amd.planner import GpuPlanner, Scene
 
+    # one GPU: the headline C2 query (configs[1]); several: BASELINE configs[2], the C3 share of 8 random queries per
+    # GPU (64 at 8 GPUs), so that the driver's scaling runs measure the multi-GPU configuration
+    if a.workload is None:
+        a.workload = "c3" if world > 1 else "c2"
     if a.workload != "c2" and a.queries_per_gpu == 1:
         a.queries_per_gpu = 8
     # every rank builds the same scene description (seeded); only rank 0 turns it into the grid
@@ -221,8 +226,10 @@ def main():
         D.broadcast_planner_scene(gp, src=0)
 
     # (start, goal) of every query of the job: C2 repeats its own pair; C3/C5 draw world * queries_per_gpu
-    # collision-free pairs (scenes.random_queries, seed 7) and each rank takes its own slice (no collective)
+    # collision-free pairs (scenes.random_queries, seed 7: the first k pairs are the same for any job size) and each
+    # rank plans the ones D.shard_queries deals it (no collective)
     n_job = world * a.queries_per_gpu
+    mine = D.shard_queries(n_job, world, rank)
     if a.workload == "c2":
         pairs = [(sc.start, sc.goal)] * n_job
     else:
@@ -232,8 +239,7 @@ def main():
 
     def queries(step, samples):
         out = []
-        for k in range(a.queries_per_gpu):
-            qid = rank * a.queries_per_gpu + k
+        for qid in mine:
             s, g = pairs[qid]
             budget = dict(iterations=a.iterations) if a.iterations else dict(samples=samples)
             out.append(GpuPlanner.make_query(s, g, sc.env_x, sc.env_y, seed=a.seed + 1000 * step, query_id=qid,

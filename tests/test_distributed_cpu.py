@@ -41,6 +41,55 @@ def _worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
+def _plan_worker(rank, world, port, out_dir):
+    """bench.py's multi-GPU dealing with the oracle in place of the GPU: each rank plans the queries
+    D.shard_queries deals it (C3 pairs, short budgets) and the counters are reduced as bench.py reduces them."""
+    import math
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import oracle as O
+    from squirrel_motion_planner_amd import distributed as D, scenes
+    sc = scenes.box_room()
+    orc = O.Oracle(O.OracleRobot(os.path.join(ROOT, "squirrel_motion_planner_amd", "data", "robotino_model.json")),
+                   O.OracleScene(sc.keys, sc.res))
+    pairs = scenes.random_queries(sc, 8, seed=7, check=lambda q: bool(orc.check_configs(np.array([q]))[0]))
+    mine = D.shard_queries(len(pairs), world, rank)
+    vals = [0.0, 0.0, 0.0]
+    for qid in mine:
+        r = orc.plan(pairs[qid][0], pairs[qid][1], env_x=sc.env_x, env_y=sc.env_y, seed=1, query=qid,
+                     opt_thresh=-math.inf, max_iter=40)
+        vals = [vals[0] + r["checked"], vals[1] + r["iterations"], vals[2] + r["valid"]]
+    s, m = D.reduce_counters(vals)
+    np.save(os.path.join(out_dir, "plan%d.npy" % rank), np.array(s + [float(q) for q in mine]))
+    dist.destroy_process_group()
+
+
+def test_bench_dealing_reduces_to_single_rank_totals(tmp_path, orobot):
+    """With WORLD_SIZE > 1 bench.py plans the C3 share: the dealt queries partition the job's pairs, and the reduced
+    per-rank counters equal one rank planning every query."""
+    import math
+    from oracle import oracle as O
+    from squirrel_motion_planner_amd import scenes
+    world, port = 2, _free_port()
+    mp.spawn(_plan_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)
+    got = [np.load(os.path.join(str(tmp_path), "plan%d.npy" % r)) for r in range(world)]
+    assert got[0][:3].tolist() == got[1][:3].tolist()
+    ids = sorted(int(v) for g in got for v in g[3:])
+    assert ids == list(range(8))
+    sc = scenes.box_room()
+    orc = O.Oracle(orobot, O.OracleScene(sc.keys, sc.res))
+    pairs = scenes.random_queries(sc, 8, seed=7, check=lambda q: bool(orc.check_configs(np.array([q]))[0]))
+    tot = [0.0, 0.0, 0.0]
+    for qid in range(8):
+        r = orc.plan(pairs[qid][0], pairs[qid][1], env_x=sc.env_x, env_y=sc.env_y, seed=1, query=qid,
+                     opt_thresh=-math.inf, max_iter=40)
+        tot = [tot[0] + r["checked"], tot[1] + r["iterations"], tot[2] + r["valid"]]
+    assert got[0][:3].tolist() == tot and tot[0] > 0
+
+
 def test_scene_broadcast_and_sharding_world2(tmp_path):
     world, port = 2, _free_port()
     mp.spawn(_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)
