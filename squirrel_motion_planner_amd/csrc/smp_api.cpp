@@ -1570,7 +1570,9 @@ extern "C" int smp_probe_fk(smp_planner* p, const double* q, int n, double* fram
 
 // Latency probe of the collision tile: check_kernel with `grid` workgroups (grid 1: one workgroup streams
 // every tile back to back); ticks[0..3] = block 0's device-clock ticks in tile stages A, B, C-centres, C;
-// ticks[4] / ticks[5] = block 0's shader cycles / device-clock ticks over the kernel (effective shader clock).
+// ticks[4] / ticks[5] = block 0's shader cycles / device-clock ticks over the kernel (effective shader clock);
+// ticks[6..8] = wave 0's detail clocks (collide_tile: centres + map sweeps, self test; collide_wide (tile < 0):
+// primitive sweeps, sphere sweeps, self test).  `ticks` holds 12 entries.
 extern "C" int smp_probe_check_latency(smp_planner* p, const double* q_soa, int64_t n, int check_self, int check_map,
                                        int grid, int tile, double* ms, unsigned long long* ticks, double* clock_hz) {
   if (!p || n <= 0 || !q_soa || grid <= 0) return SMP_ERR_ARG;
@@ -1578,8 +1580,8 @@ extern "C" int smp_probe_check_latency(smp_planner* p, const double* q_soa, int6
   HIPCHK(p->d_cq.reserve((size_t)n * NJ));
   HIPCHK(p->d_valid.reserve((size_t)n));
   unsigned long long* dprof = nullptr;
-  HIPCHK(hipMalloc(&dprof, 8 * sizeof(unsigned long long)));
-  HIPCHK(hipMemset(dprof, 0, 8 * sizeof(unsigned long long)));
+  HIPCHK(hipMalloc(&dprof, 16 * sizeof(unsigned long long)));
+  HIPCHK(hipMemset(dprof, 0, 16 * sizeof(unsigned long long)));
   HIPCHK(hipMemcpy(p->d_cq.p, q_soa, (size_t)n * NJ * sizeof(double), hipMemcpyHostToDevice));
   HIPCHK(hipEventRecord(p->ev0, p->stream));
   launch_check(tile, grid, p->stream, p->d_rb, p->sc, p->d_mc, p->d_cq.p, (long long)n, check_self,
@@ -1590,7 +1592,7 @@ extern "C" int smp_probe_check_latency(smp_planner* p, const double* q_soa, int6
   float f = 0;
   HIPCHK(hipEventElapsedTime(&f, p->ev0, p->ev1));
   *ms = f;
-  HIPCHK(hipMemcpy(ticks, dprof, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(ticks, dprof, 12 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   (void)hipFree(dprof);
   *clock_hz = p->wall_rate_hz;
   return SMP_OK;

@@ -449,8 +449,41 @@ __device__ __forceinline__ bool prim_reach(int ty, const double* __restrict__ h,
   return true;
 }
 
+// Relation of an upright primitive to the axis-aligned box [x0, x1] x [y0, y1] x [z0, z1] (a brick's cells in reach),
+// decided with a margin eps far above the rounding of prim_cell: 0 = separated by more than eps (every cell of the box
+// fails prim_cell: a separating axis of the box separates each of its cells by at least as much), 2 = inside by more
+// than eps (every cell of the box passes prim_cell), 1 = undecided (the cells are tested one by one).
+__device__ __forceinline__ int prim_box_relation(int ty, const double* __restrict__ h, const double* pw, double x0,
+                                                 double x1, double y0, double y1, double z0, double z1) {
+  constexpr double eps = 1e-9;
+  const double hz = ty == 1 ? h[2] : h[1];
+  if (z1 < pw[2] - hz - eps || z0 > pw[2] + hz + eps) return 0;
+  const bool zin = z0 > pw[2] - hz + eps && z1 < pw[2] + hz - eps;
+  const double wx = 0.5 * (x1 - x0), wy = 0.5 * (y1 - y0);
+  const double dx = 0.5 * (x0 + x1) - pw[0], dy = 0.5 * (y0 + y1) - pw[1];
+  if (ty == 2) {
+    const double qx = fmax(fabs(dx) - wx, 0.0), qy = fmax(fabs(dy) - wy, 0.0);
+    const double re = h[0] + eps;
+    if (qx * qx + qy * qy > re * re) return 0;
+    const double fx = fabs(dx) + wx, fy = fabs(dy) + wy, ri = h[0] - eps;  // the farthest corner
+    return zin && ri > 0.0 && fx * fx + fy * fy < ri * ri ? 2 : 1;
+  }
+  const double c = pw[3], s = pw[4], ac = fabs(c), as = fabs(s);
+  if (fabs(dx) > wx + (ac * h[0] + as * h[1]) + eps) return 0;
+  if (fabs(dy) > wy + (as * h[0] + ac * h[1]) + eps) return 0;
+  if (fabs(c * dx + s * dy) > h[0] + (wx * ac + wy * as) + eps) return 0;
+  if (fabs(c * dy - s * dx) > h[1] + (wx * as + wy * ac) + eps) return 0;
+  // inside: the box's extent along the primitive's two axes lies within its half extents
+  const bool xin = fabs(c * dx + s * dy) + (wx * ac + wy * as) < h[0] - eps;
+  const bool yin = fabs(c * dy - s * dx) + (wx * as + wy * ac) < h[1] - eps;
+  return zin && xin && yin ? 2 : 1;
+}
+
 // Cooperative exact map test of one primitive by a wavefront: one brick word per lane over the reach, masked to the
-// reach's cells; each lane tests its brick's occupied cells in reach (ballot early exit).
+// reach's cells, and each brick's cells in reach classified at once (prim_box_relation): a brick with an occupied cell
+// inside the primitive is a hit, a separated brick is skipped, and the undecided bricks are swept one after the other
+// with a lane per cell (prim_cell, ballot early exit).  The outcome is the exhaustive per-cell test's; a lane no longer
+// walks its brick's occupied cells serially (up to 64 dependent prim_cell tests next to a solid obstacle).
 __device__ __forceinline__ bool wave_prim_map(const SceneDev& sc, int ty, const double* __restrict__ h, const double* pw,
                                               int lane) {
   int lo[3], hi[3];
@@ -460,11 +493,14 @@ __device__ __forceinline__ bool wave_prim_map(const SceneDev& sc, int ty, const 
   const int nb = nbi * nbj * nbk;
   for (int b0 = 0; b0 < nb; b0 += 64) {
     const int b = b0 + lane;
-    bool hit = false;
+    uint64_t w = 0;
+    int bi = 0, bj = 0, bk = 0, rel = 0;
     if (b < nb) {
-      const int bi = bi0 + b % nbi, t = b / nbi;
-      const int bj = bj0 + t % nbj, bk = bk0 + t / nbj;
-      uint64_t w = sc.bricks[((size_t)bk * sc.bny + bj) * sc.bnx + bi];
+      bi = bi0 + b % nbi;
+      const int t = b / nbi;
+      bj = bj0 + t % nbj;
+      bk = bk0 + t / nbj;
+      w = sc.bricks[((size_t)bk * sc.bny + bj) * sc.bnx + bi];
       if (w) {
         const int il = max(lo[0] - 4 * bi, 0), ih = min(hi[0] - 4 * bi, 3);
         const int jl = max(lo[1] - 4 * bj, 0), jh = min(hi[1] - 4 * bj, 3);
@@ -475,14 +511,23 @@ __device__ __forceinline__ bool wave_prim_map(const SceneDev& sc, int ty, const 
         uint64_t m = 0;
         for (int kk = kl; kk <= kh; ++kk) m |= (uint64_t)row << (16 * kk);
         w &= m;
-        while (w && !hit) {
-          const int bit = __builtin_ctzll(w);
-          w &= w - 1;
-          hit = prim_cell(ty, h, pw, sc, 4 * bi + (bit & 3), 4 * bj + ((bit >> 2) & 3), 4 * bk + (bit >> 4));
-        }
+        if (w)
+          rel = prim_box_relation(ty, h, pw, sc.ox + (double)(4 * bi + il) * sc.res, sc.ox + (double)(4 * bi + ih + 1) * sc.res,
+                                  sc.oy + (double)(4 * bj + jl) * sc.res, sc.oy + (double)(4 * bj + jh + 1) * sc.res,
+                                  sc.oz + (double)(4 * bk + kl) * sc.res, sc.oz + (double)(4 * bk + kh + 1) * sc.res);
       }
     }
-    if (__ballot(hit)) return true;
+    if (__ballot(rel == 2)) return true;
+    // the undecided bricks, a lane per cell
+    for (uint64_t um = __ballot(rel == 1); um;) {
+      const int src = __builtin_ctzll(um);
+      um &= um - 1;
+      const uint32_t wlo = shfl_u32((uint32_t)w, src), whi = shfl_u32((uint32_t)(w >> 32), src);
+      const int sbi = __shfl(bi, src), sbj = __shfl(bj, src), sbk = __shfl(bk, src);
+      const bool set = ((lane < 32 ? wlo >> lane : whi >> (lane - 32)) & 1u) != 0;
+      const bool hit = set && prim_cell(ty, h, pw, sc, 4 * sbi + (lane & 3), 4 * sbj + ((lane >> 2) & 3), 4 * sbk + (lane >> 4));
+      if (__ballot(hit)) return true;
+    }
   }
   return false;
 }
@@ -802,7 +847,7 @@ struct WideLds {
 __device__ __forceinline__ void collide_wide(const RobotDev* __restrict__ rb, const SceneDev& sc_in,
                                              const MapCfg* __restrict__ mc, int ct, int nc, const double (*q_lds)[NJ],
                                              int self, int map, WideLds& L, const TileOrder* ord = nullptr,
-                                             unsigned long long* prof = nullptr) {
+                                             unsigned long long* prof = nullptr, unsigned long long* prof2 = nullptr) {
   const SceneDev sc = uniform_scene(sc_in);
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int G = __builtin_amdgcn_readfirstlane(NWAVE / ct);
@@ -901,6 +946,7 @@ __device__ __forceinline__ void collide_wide(const RobotDev* __restrict__ rb, co
     if (prof && threadIdx.x == 0) tc = wall_clock64();
     // map: this wavefront's candidate primitives, then its candidate spheres (their brick words in one round trip)
     bool hit = false;
+    unsigned long long tp0 = (prof2 && threadIdx.x == 0) ? wall_clock64() : 0, tp1 = tp0, tp2 = tp0;
     for (uint32_t pm = (uint32_t)__builtin_amdgcn_readfirstlane((int)W.pcand); pm && !hit;) {
       const int p = __builtin_ctz(pm);
       pm &= pm - 1;
@@ -909,11 +955,13 @@ __device__ __forceinline__ void collide_wide(const RobotDev* __restrict__ rb, co
       const double pw[5] = {W.u.c.pw[p][0], W.u.c.pw[p][1], W.u.c.pw[p][2], W.u.c.pw[p][3], W.u.c.pw[p][4]};
       hit = wave_prim_map(sc, rb->prim_type[p], &rb->prim_h[p * 3], pw, lane);
     }
+    if (prof2 && threadIdx.x == 0) tp1 = wall_clock64();
     uint32_t any = 0;
     for (int wd = 0; wd < (MAX_SPH + 31) / 32; ++wd) any |= W.cand[wd];
     if (!hit && __builtin_amdgcn_readfirstlane((int)(any != 0)) &&
         !__builtin_amdgcn_readfirstlane(__hip_atomic_load(&L.coll[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))
       hit = wave_map_staged(rb, sc, W.u.c.wc, W.cand, nsph, W.v.stage, W.owner, W.off, lane);
+    if (prof2 && threadIdx.x == 0) tp2 = wall_clock64();
     // self: this wavefront's 64-pair chunks of the sphere pairs, then of the (primitive, sphere) pairs
     if (self && !hit &&
         !__builtin_amdgcn_readfirstlane(__hip_atomic_load(&L.coll[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) {
@@ -940,6 +988,10 @@ __device__ __forceinline__ void collide_wide(const RobotDev* __restrict__ rb, co
         }
       }
       hit = __ballot(sh) != 0;
+    }
+    if (prof2 && threadIdx.x == 0) {  // wave 0: primitive sweeps, sphere sweeps, self test
+      const unsigned long long tp3 = wall_clock64();
+      prof2[0] += tp1 - tp0; prof2[1] += tp2 - tp1; prof2[2] += tp3 - tp2;
     }
     if (hit && lane == 0) {
       atomicOr(&L.coll[c], 1);

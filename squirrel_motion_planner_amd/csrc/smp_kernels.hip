@@ -93,7 +93,7 @@ __global__ void __launch_bounds__(BLOCK) check_wide_kernel(const RobotDev* __res
     }
     if (threadIdx.x < TILE_CT_MAX) L.coll[threadIdx.x] = 0;
     __syncthreads();
-    collide_wide(&g_rb, sc, &g_mc, ct, nc, ql, self, map, L, nullptr, pr);
+    collide_wide(&g_rb, sc, &g_mc, ct, nc, ql, self, map, L, nullptr, pr, pr ? pr + 6 : nullptr);
     if (threadIdx.x < nc) valid[base + threadIdx.x] = L.coll[threadIdx.x] ? 0 : 1;
     __syncthreads();
   }

@@ -2,6 +2,7 @@
 set -e
 OUT=gpurun_out
 mkdir -p $OUT
-export SMP_LIB=squirrel_motion_planner_amd/lib/libsmp_gpu_jp.so SMP_JOB_PROF=1
-timeout -k 10 120 python -u tools/perf_probe.py 4000 > $OUT/jp_adaptive.txt 2>&1
-SMP_TILE_CT=8 timeout -k 10 120 python -u tools/perf_probe.py 4000 > $OUT/jp_ct8.txt 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 200 --timeout-method thread -k "job_tile_shapes or check_configs_parity or disabled" > $OUT/t_tiles.log 2>&1
+SMP_TILES=8,-8,-1 timeout -k 10 200 python -u tools/tile_probe.py > $OUT/tile_probe.txt 2>&1
+timeout -k 10 120 python -u tools/perf_probe.py 4000 > $OUT/perf_probe_4k.txt 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $OUT/gpu_tests.log 2>&1

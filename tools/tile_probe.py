@@ -28,8 +28,22 @@ Q = np.array(qs)
 rng = np.random.default_rng(0)
 R = np.column_stack([rng.uniform(-5, 5, len(Q)), rng.uniform(-5, 5, len(Q))] +
                     [rng.uniform(-2, 2, len(Q)) for _ in range(6)])
+# planner-like expand edges: from a random tree node one step (0.5) towards a uniform sample, 21 points each -- the
+# configurations the planner's collision jobs check (new edges, often near or into obstacles)
+from oracle import oracle as O  # noqa: E402  (joint limits of the model; test infrastructure, not the path measured)
+orob = O.OracleRobot(L.MODEL_JSON)
+nodes = np.concatenate([gp.tree(w)[1] for w in (0, 1)])
+E = []
+while len(E) * 21 < len(Q):
+    a = nodes[rng.integers(len(nodes))]
+    x = np.concatenate([[rng.uniform(*sc.env_x), rng.uniform(*sc.env_y)],
+                        [rng.uniform(orob.q_min[j], orob.q_max[j]) for j in range(2, 8)]])
+    d = np.linalg.norm(x - a)
+    b = a + (x - a) * (0.5 / d) if d > 0.5 else x
+    E.append(a + np.linspace(0.0, 1.0, 21)[:, None] * (b - a)[None, :])
+P = np.concatenate(E)
 lib = L.lib()
-for name, X in (("tree-edges", Q), ("random", R)):
+for name, X in (("tree-edges", Q), ("expand-edges", P), ("random", R)):
     soa = np.ascontiguousarray(X.T)
     n = len(X)
     # tile < 0: the helpers' job tiles (collide_wide, -tile configurations spread over the workgroup)
@@ -37,7 +51,7 @@ for name, X in (("tree-edges", Q), ("random", R)):
     for tile, grid in shapes:
         ms = ctypes.c_double()
         hz = ctypes.c_double()
-        ticks = (ctypes.c_uint64 * 8)()
+        ticks = (ctypes.c_uint64 * 12)()
         L.check(lib.smp_probe_check_latency(gp.h, soa.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), n, 1, 1, grid, tile,
                                             ctypes.byref(ms), ticks, ctypes.byref(hz)))
         ct = abs(tile)
@@ -46,5 +60,9 @@ for name, X in (("tree-edges", Q), ("random", R)):
         print("%-10s tile %2d n %7d grid %5d: %.2f ms  %.3g configs/s  per tile %.2f us  stages(us) A %.2f B %.2f C0 %.2f C %.2f"
               % (name, tile, n, grid, ms.value, n / (ms.value * 1e-3), ms.value * 1e3 / tiles * (grid if grid > 1 else 1) /
                  (1 if grid == 1 else min(grid, tiles)), *per_tile_us[:4]), flush=True)
-        print("   shader clock %.3f GHz; wave 0 in C: centres + map sweeps %.2f us, self test %.2f us per tile" % (
-            ticks[4] / (ticks[5] / hz.value) / 1e9 if ticks[5] else 0, per_tile_us[6], per_tile_us[7]), flush=True)
+        if tile > 0:
+            print("   shader clock %.3f GHz; wave 0 in C: centres + map sweeps %.2f us, self test %.2f us per tile" % (
+                ticks[4] / (ticks[5] / hz.value) / 1e9 if ticks[5] else 0, per_tile_us[6], per_tile_us[7]), flush=True)
+        else:
+            print("   shader clock %.3f GHz; wave 0: primitive sweeps %.2f us, sphere sweeps %.2f us, self %.2f us per "
+                  "tile" % (ticks[4] / (ticks[5] / hz.value) / 1e9 if ticks[5] else 0, *per_tile_us[6:9]), flush=True)
