@@ -963,6 +963,7 @@ static QueryDev make_qdev(QueryBuffers& b, size_t cap, long long rows) {
   d.ttff = nullptr;
   d.lfin = nullptr;
   d.lquota = 0;
+  d.end_on_sol = 0;
   // scans of trees of at least this many nodes are split over the helpers (DESIGN.md "Scans of large trees");
   // SMP_SCAN_MIN overrides it (experiments and tests; 0: never)
   d.scan_min = 12288;
@@ -1065,10 +1066,42 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
   // M configs/s; C5, 8 queries: 0.49 / 0.61 / 0.62 M)
   int rb_div = 4;
   if (const char* e = std::getenv("SMP_REBALANCE_DIV")) rb_div = std::max(1, std::atoi(e));
+  // A single query with automatic helpers and scouts ends its first launch once it has a solution and continues
+  // re-provisioned for the post-solution phase (DESIGN.md "Post-solution provisioning"): scouts 2 and 3 have retired
+  // and the leader's own jobs are rare, so the leader keeps SMP_POST_LEAD helpers and scouts 0 and 1 (every
+  // iteration's choose-parent and rewire jobs) share the rest, up to SMP_POST_CAP helpers in all.  SMP_POST=0 keeps
+  // the first launch's provisioning (experiments).
+  int post_mode = nq == 1 && nh_req == 0 && want_scout && p->params.scout == 1 ? 1 : 0;
+  if (const char* e = std::getenv("SMP_POST")) post_mode = post_mode && std::atoi(e) != 0;
+  int post_lead = 16, post_cap = 220;
+  if (const char* e = std::getenv("SMP_POST_LEAD")) post_lead = std::max(1, std::atoi(e));
+  if (const char* e = std::getenv("SMP_POST_CAP")) post_cap = std::max(8, std::atoi(e));
   int nh = 0, ns = 0;
+  auto provision_post = [&](int i) {
+    const int cpq = slots;
+    ns = 2;
+    nh = std::min(post_cap, std::max(0, cpq - 1 - ns));
+    const int h_lead = std::min(post_lead, std::max(1, nh / 4));
+    const int rest = nh - 1 - h_lead;  // minus the sampler
+    qdev[i].jb = p->qb[i].jb.p;
+    qdev[i].sampler = 1;
+    qdev[i].nworkers = 1 + h_lead;
+    qdev[i].nscouts = ns;
+    qdev[i].end_on_sol = 0;
+    for (int sct = 0; sct < ns; ++sct) {
+      qdev[i].sjbs[sct] = p->qb[i].sjb[sct].p;
+      qdev[i].scbs[sct] = p->qb[i].scb[sct].p;
+      qdev[i].svias[sct] = p->qb[i].svia[sct].p;
+      qdev[i].sworkers_s[sct] = 1 + (sct == 0 ? rest - rest / 2 : rest / 2);
+    }
+  };
   auto provision = [&](const std::vector<int>& act) {
     const int na = std::max(1, (int)act.size());
     const int cpq = std::max(1, slots / na);
+    if (post_mode && na == 1 && S[act[0]].have_sol) {
+      provision_post(act[0]);
+      return;
+    }
     nh = nh_req;
     ns = 0;
     if (nh == 0) {
@@ -1105,6 +1138,7 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
       qdev[i].nscouts = ns;
       qdev[i].pre_delay = pre_delay;
       qdev[i].pre_commit = pre_commit;
+      qdev[i].end_on_sol = post_mode && ns >= 2 && !S[i].have_sol;
       qdev[i].sampler_jb = p->qb[i].jb.p;
       for (int s = 0; s < ns; ++s) {
         qdev[i].sjbs[s] = p->qb[i].sjb[s].p;
@@ -1298,10 +1332,12 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
     for (int i : act)
       if (!(S[i].phase == 2 || S[i].status != 0)) still.push_back(i);
     const bool shrank = still.size() < act.size();
+    // the single query's first launch ended at its first solution: the post-solution provisioning
+    const bool to_post = post_mode && still.size() == 1 && qdev[still[0]].end_on_sol && S[still[0]].have_sol;
     act.swap(still);
     if (act.empty()) break;
-    if (shrank) {
-      if (rebalance) provision(act);
+    if (shrank || to_post) {
+      if (rebalance || to_post) provision(act);
       if (int st = upload_active()) return st;
     }
     if (chunk < 4096) chunk *= 2;

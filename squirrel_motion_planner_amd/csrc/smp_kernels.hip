@@ -4571,6 +4571,7 @@ __global__ void __launch_bounds__(BLOCK) plan_kernel(const RobotDev* __restrict_
       if (uni(g_L.go_end)) break;
     }
     iteration(C);
+    if (C.Q.end_on_sol && uni(g_L.S.have_sol)) break;  // re-provisioned for the post-solution phase (resumable)
   }
   if (threadIdx.x == 0) {
     if (C.Q.lquota > 0 && (g_L.S.phase == 2 || g_L.S.status != 0))
@@ -4609,7 +4610,7 @@ struct SamplerLds {
 // restarts the window.  Never writes the slot of an iteration the leader may be reading: it fills iterations
 // up to (published iteration) + SMP_RING - 1 only.  Leaves on the stop flag or after two idle seconds.
 // (not inlined into helper_kernel, like scan_helper: the tile helpers' loop is compiled without the sampler's and the
-// scan slices' registers live around it -- C2 73.1 -> 71.8 us per iteration, tools/gpu_r03s7.sh)
+// scan slices' registers live around it -- C2 73.1 -> 71.8 us per iteration, perf_probe.py with SMP_JOB_PROF, round 3)
 __device__ __noinline__ void sampler_main(const Ctx& C, SamplerLds& L) {
   JobBoard* jb = C.Q.jb;
   {

@@ -42,8 +42,20 @@ while len(E) * 21 < len(Q):
     b = a + (x - a) * (0.5 / d) if d > 0.5 else x
     E.append(a + np.linspace(0.0, 1.0, 21)[:, None] * (b - a)[None, :])
 P = np.concatenate(E)
+# connect-like edges (the leader's connect near loop): a node of one tree to a node of the other within the near
+# radius (4.0), 21 points each -- long edges, often through obstacles
+t0, t1 = gp.tree(0)[1], gp.tree(1)[1]
+K = []
+while len(K) * 21 < len(Q):
+    a = t0[rng.integers(len(t0))]
+    b = t1[rng.integers(len(t1))]
+    if np.linalg.norm(b - a) < 4.0:
+        K.append(a + np.linspace(0.0, 1.0, 21)[:, None] * (b - a)[None, :])
+K = np.concatenate(K)
 lib = L.lib()
-for name, X in (("tree-edges", Q), ("expand-edges", P), ("random", R)):
+sets = {"tree-edges": Q, "expand-edges": P, "connect-edges": K, "random": R}
+for name in os.environ.get("SMP_SETS", "tree-edges,expand-edges,connect-edges,random").split(","):
+    X = sets[name]
     soa = np.ascontiguousarray(X.T)
     n = len(X)
     # tile < 0: the helpers' job tiles (collide_wide, -tile configurations spread over the workgroup)
