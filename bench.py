@@ -49,8 +49,11 @@ def parse():
     ap.add_argument("--iterations", type=int, default=None,
                     help="iteration budget per query instead of --samples (C3: 1e5 in SURVEY.md 8d)")
     ap.add_argument("--cpu-iterations", type=int, default=20000,
-                    help="with --iterations above this, the CPU baseline is timed on the first this-many iterations "
-                         "of the same query (a bounded sample: the oracle needs ~11 min for 1e5 C2 iterations)")
+                    help="with --iterations above this, the CPU baseline is a bounded window at the end of the run: "
+                         "the oracle continues the GPU's own state at iteration N - --cpu-window (same trees) to N, "
+                         "timed against the GPU's time for the same iterations (its cost rows)")
+    ap.add_argument("--cpu-window", type=int, default=1000,
+                    help="iterations of the CPU window of --iterations runs above --cpu-iterations")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
 
@@ -136,6 +139,51 @@ def cpu_baseline(sc, pair, a, step0_seed, step_seeds=()):
             # timed from run() entry), beside the GPU's per-step lists
             "time_first_solution_steps_s": ttff or None,
             "time_first_solution_stats_s": stats3(ttff)}
+
+
+def cpu_window(a, gp, sc, pair, seed, step0):
+    """CPU baseline of a long run (--iterations above --cpu-iterations), at the run's own tree sizes: the GPU plans
+    the same query to N - K iterations (untimed, after the timed region) and hands its state to the oracle
+    (GpuPlanner.export_state -> Oracle.resume: both trees, child order, in-edges, loop scalars), which continues it to
+    N on one thread and with its scans on all of this process's cores.  The window's GPU time is the timed step 0's
+    device clock between the cost rows of iterations N - K and N; both sides check the same configurations in it
+    (the oracle's end state is compared with the GPU's step 0)."""
+    import numpy as np
+    from oracle import oracle as O
+    from squirrel_motion_planner_amd.planner import GpuPlanner
+    n, k = a.iterations, min(a.cpu_window, a.iterations - 1)
+    gp.plan(GpuPlanner.make_query(pair[0], pair[1], sc.env_x, sc.env_y, iterations=n - k, seed=seed, query_id=0))
+    st = gp.export_state()
+    rob = O.OracleRobot(os.path.join(ROOT, "squirrel_motion_planner_amd", "data", "robotino_model.json"))
+    orc = O.Oracle(rob, O.OracleScene(sc.keys, sc.res))
+    cpu, cores = host_cpu()
+    kw = dict(env_x=sc.env_x, env_y=sc.env_y, seed=seed, query=0, opt_thresh=-math.inf, max_iter=n)
+    r1 = orc.resume(pair[0], pair[1], st, threads=1, **kw)
+    rm = orc.resume(pair[0], pair[1], st, threads=cores, **kw) if cores > 1 else r1
+    rows = step0["cost_rows"]
+    gpu_s = float(rows[n - 1][1] - rows[n - k - 1][1]) if len(rows) >= n else None
+    checked = r1["checked"] - int(st["iv"][1])
+    same = bool(r1["checked"] == step0["configs_checked"] and r1["n_start"] == step0["nodes_start"] and
+                r1["n_goal"] == step0["nodes_goal"] and r1["cost"][0] == step0["cost_best"][0])
+    nodes = (len(st["start"]["parent"]), len(st["goal"]["parent"]))
+    return {"value": checked / r1["t_total"], "unit": "configs/s", "cores": 1, "kind": "port",
+            "sample": "C2 query 0 (seed %d), oracle/smp_oracle.cpp single thread, continuing the GPU's state at "
+                      "iteration %d (trees of %d / %d nodes) to %d: %d configs checked in %.2f s on %s" % (
+                          seed, n - k, nodes[0], nodes[1], n, checked, r1["t_total"], cpu),
+            "bounded_sample": True, "window": {"from_iteration": n - k, "to_iteration": n, "tree_nodes": nodes,
+                                                "configs_checked": checked, "gpu_seconds": gpu_s,
+                                                "gpu_configs_per_s": checked / gpu_s if gpu_s else None,
+                                                "cpu_seconds_1_thread": r1["t_total"],
+                                                "cpu_seconds_all_cores": rm["t_total"]},
+            "cpu_model": cpu, "valid_configs_per_s": (r1["valid"] - int(st["iv"][2])) / r1["t_total"],
+            "iterations": k, "checked": checked, "iters_per_s": k / r1["t_total"], "cost_best": r1["cost"][0],
+            "all_cores": {"value": checked / rm["t_total"], "unit": "configs/s", "cores": cores,
+                          "t_total_s": rm["t_total"],
+                          "same_trees_as_1_thread": bool(rm["checked"] == r1["checked"] and
+                                                         rm["n_start"] == r1["n_start"]),
+                          "how": "oracle with the nearest / near scans as OpenMP loops on %d threads "
+                                 "(BS:4092, BS:4283), the same window" % cores},
+            "same_result_as_gpu_step0": same}
 
 
 def _oracle_worker(args):
@@ -298,13 +346,18 @@ def main():
         achieved = alg_bytes_rank0 / (plan_ms_rank0 * 1e-3) / 1e9 if plan_ms_rank0 > 0 else 0.0
         traffic, traffic_src = None, None
         # HBM bytes per launch: not measurable inside this run (counter passes serialise dispatches and need
-        # rocprofv3); taken from the newest committed FETCH_SIZE + WRITE_SIZE passes of this bench, named below
+        # rocprofv3); taken from the newest committed FETCH_SIZE + WRITE_SIZE passes of THIS workload
+        # (profiles/r*_pmc_<tag>.json, tools/profile_round.sh), else null.  Counter collection serialises the
+        # dispatches, so those passes run the same queries with --helpers -1 (all tiles in plan_kernel): the bytes are
+        # that configuration's, as traffic_source says.
         import glob
-        pmcs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_plan_kernel.json")))
+        tag = a.workload + ("_iter%d" % a.iterations if a.iterations else "")
+        pmcs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_%s.json" % tag)))
         if pmcs:
             try:
                 traffic = json.load(open(pmcs[-1])).get("hbm_bytes_per_launch")
-                traffic_src = "profiles/" + os.path.basename(pmcs[-1]) + " (rocprofv3 --pmc passes, --helpers -1)"
+                traffic_src = ("profiles/" + os.path.basename(pmcs[-1]) +
+                               " (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this workload with --helpers -1)")
             except (OSError, ValueError):
                 traffic = None
         out = {
@@ -350,7 +403,9 @@ def main():
                          "launches_rank0": totals["launches"],
                          "algorithmic_bytes_rank0": alg_bytes_rank0},
         }
-        if not a.no_cpu and world == 1:
+        if not a.no_cpu and world == 1 and a.workload == "c2" and a.iterations and a.iterations > a.cpu_iterations:
+            out["cpu_baseline"] = cpu_window(a, gp, sc, pairs[0], a.seed, step0)
+        elif not a.no_cpu and world == 1:
             cb = cpu_baseline(sc, pairs[0], a, step0_seed=a.seed, step_seeds=[a.seed + 1000 * step for step in
                                                                              range(a.steps)]
                               if a.queries_per_gpu == 1 else ())

@@ -100,6 +100,14 @@ def lib():
         L.orc_find_goal_pose.argtypes = [ctypes.c_void_p, _pd, _pd, _d, _i, _i, _pd,
                                          ctypes.POINTER(ctypes.c_longlong)]
         L.orc_find_goal_pose.restype = _i
+        L.orc_resume_begin.argtypes = [ctypes.c_void_p, _pd, _pd, ctypes.POINTER(Params)]
+        L.orc_resume_begin.restype = _i
+        L.orc_resume_tree.argtypes = [ctypes.c_void_p, _i, _i, _pi, _pd, _pd, _pd, _pd, _pi, _pi, _i, _i]
+        L.orc_resume_run.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_longlong), _pd, ctypes.POINTER(Result)]
+        L.orc_resume_run.restype = _i
+        L.orc_export_tree.argtypes = [ctypes.c_void_p, _i, _pd, _pd, _pi, _pi]
+        L.orc_export_tree.restype = _i
+        L.orc_export_state.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_longlong), _pd]
         _lib = L
     return _lib
 
@@ -394,6 +402,57 @@ class Oracle:
                                      _p(pose, _d), info)
         return r, (pose if r == 0 else None), info[0], info[1], info[2]
 
+    def export_state(self, res):
+        """The last run's state in the form resume() takes (res: that run's plan() / resume() output)."""
+        st = {"iv": np.zeros(12, np.int64), "dv": np.zeros(25)}
+        lib().orc_export_state(self.h, st["iv"].ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)), _p(st["dv"], _d))
+        for which, name in ((0, "start"), (1, "goal")):
+            n = len(res[name + "_parent"])
+            es, et = np.zeros((n, 8)), np.zeros((n, 8))
+            off = np.zeros(n + 1, np.int32)
+            k = lib().orc_export_tree(self.h, which, None, None, None, None)
+            ids = np.zeros(max(k, 1), np.int32)
+            lib().orc_export_tree(self.h, which, _p(es, _d), _p(et, _d), _p(off, _i), _p(ids, _i))
+            st[name] = {"parent": res[name + "_parent"], "conf": res[name + "_conf"], "cost": res[name + "_cost"],
+                        "e_start": es, "e_target": et, "child_off": off, "child_ids": ids[:k],
+                        "edges": res["edges_" + name], "rewires": res["rewires_" + name]}
+        return st
+
+    def resume(self, start, goal, state, **kw):
+        """Continues a run from `state` (export_state, or the GPU planner's GpuPlanner.export_state) to the budget of
+        **kw (max_iter counts from the run's start); the output is plan()'s, timed from the resume."""
+        p = dict(DEFAULT_PARAMS)
+        p.update(kw)
+        P = Params()
+        for k, v in p.items():
+            if k in ("env_x", "env_y"):
+                getattr(P, k)[0], getattr(P, k)[1] = v
+            else:
+                setattr(P, k, v)
+        s = np.ascontiguousarray(start, np.float64)
+        g = np.ascontiguousarray(goal, np.float64)
+        st = lib().orc_resume_begin(self.h, _p(s, _d), _p(g, _d), ctypes.byref(P))
+        if st:
+            raise ValueError("resume: init_planner failed (%d)" % st)
+        for which, name in ((0, "start"), (1, "goal")):
+            t = state[name]
+            par = np.ascontiguousarray(t["parent"], np.int32)
+            conf = np.ascontiguousarray(t["conf"], np.float64)
+            cost = np.ascontiguousarray(t["cost"], np.float64)
+            es = np.ascontiguousarray(t["e_start"], np.float64)
+            et = np.ascontiguousarray(t["e_target"], np.float64)
+            off = np.ascontiguousarray(t["child_off"], np.int32)
+            ids = np.ascontiguousarray(t["child_ids"], np.int32)
+            if len(ids) == 0:
+                ids = np.zeros(1, np.int32)
+            lib().orc_resume_tree(self.h, which, len(par), _p(par, _i), _p(conf, _d), _p(cost, _d), _p(es, _d),
+                                  _p(et, _d), _p(off, _i), _p(ids, _i), int(t["edges"]), int(t["rewires"]))
+        iv = np.ascontiguousarray(state["iv"], np.int64)
+        dv = np.ascontiguousarray(state["dv"], np.float64)
+        R = Result()
+        lib().orc_resume_run(self.h, iv.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)), _p(dv, _d), ctypes.byref(R))
+        return self._collect(R)
+
     def plan(self, start, goal, **kw):
         p = dict(DEFAULT_PARAMS)
         p.update(kw)
@@ -407,6 +466,9 @@ class Oracle:
         g = np.ascontiguousarray(goal, np.float64)
         R = Result()
         lib().orc_plan(self.h, _p(s, _d), _p(g, _d), ctypes.byref(P), ctypes.byref(R))
+        return self._collect(R)
+
+    def _collect(self, R):
         out = {f: getattr(R, f) for f, _ in Result._fields_}
         out["cost"] = list(R.cost)
         out["h0"] = list(R.h0)

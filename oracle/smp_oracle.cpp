@@ -430,6 +430,7 @@ struct Costs { double total = 0, rev = 0, prism = 0; };
 struct Edge {                 // DS:11-19 (ee trajectory dropped: output-only in C-space)
   int root_node_id = 0, child_node_id = 0;
   std::vector<Conf> traj;     // 21 interpolated configs (BS:4443-4526)
+  Conf s{}, g{};              // interpolation start / target (export for orc_resume_*; the GPU's in-edge)
 };
 
 struct Node {                 // DS:29-45
@@ -513,6 +514,8 @@ struct Planner {
     e.traj.resize(P.n_pts + 1);
     for (int inc = 0; inc <= P.n_pts; ++inc)
       for (int j = 0; j < 8; ++j) e.traj[inc][j] = near.q[j] + inc * step[j];
+    e.s = near.q;
+    e.g = end.q;
     double ct = 0, cr = 0, cp = 0;
     for (int wp = 0; wp < P.n_pts; ++wp) {
       double st_ = 0, sr = 0, sp = 0;
@@ -1030,8 +1033,23 @@ struct Planner {
     Tree* B = &tb;
     iter = 0;
     connect_graphs(*A, A->nodes[0], B->nodes[0]);
-    bool no_planning = have_sol;
-    while (!no_planning) {
+    if (have_sol) {
+      st.iterations = iter;
+      st.t_total = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      return have_sol;
+    }
+    return loop(A, B);
+  }
+
+  // The same loop continued from a state set from outside (orc_resume_*: another run's trees and loop scalars after
+  // `iter` iterations, tree_A of the next iteration `a_is_goal`); timed from here.
+  bool resume(bool a_is_goal) {
+    t0 = std::chrono::steady_clock::now();
+    return a_is_goal ? loop(&tb, &ta) : loop(&ta, &tb);
+  }
+
+  bool loop(Tree* A, Tree* B) {
+    for (;;) {
       double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
       if (P.max_checked > 0) {
         if (!(st.checked < P.max_checked)) break;
@@ -1747,6 +1765,126 @@ void orc_u01(uint64_t seed, uint32_t query, const uint32_t* ctr, int n, double* 
   for (int i = 0; i < n; ++i) out[i] = orc::u01(seed, query, ctr[4 * i], ctr[4 * i + 1], ctr[4 * i + 2], ctr[4 * i + 3]);
 }
 
+static int fill_result(orc_handle* h, bool ok, orc_result* res);
+
+static void set_params(orc::Planner& pl, const orc_params* p) {
+  pl.P.near_r = p->near_r; pl.P.step = p->step; pl.P.n_pts = p->n_pts; pl.P.max_near = p->max_near;
+  pl.P.opt_thresh = p->opt_thresh; pl.P.tree_opt = p->tree_opt; pl.P.informed = p->informed;
+  pl.P.env_x[0] = p->env_x[0]; pl.P.env_x[1] = p->env_x[1]; pl.P.env_y[0] = p->env_y[0]; pl.P.env_y[1] = p->env_y[1];
+  pl.P.self = p->self; pl.P.map = p->map; pl.P.seed = p->seed; pl.P.query = p->query;
+  pl.P.max_iter = p->max_iter; pl.P.max_time = p->max_time; pl.P.max_checked = p->max_checked;
+  pl.P.threads = p->threads;
+}
+
+// Continuing another run (test infrastructure: the GPU planner's state after some iterations, DESIGN.md "Large
+// trees"): begin = init_planner of the same query, then both trees and the loop scalars replace the fresh state, then
+// the loop runs on to the budget of `p` (max_iter counts from the run's start, as the GPU's budget).
+int orc_resume_begin(void* hp, const double* start, const double* goal, const orc_params* p) {
+  orc_handle* h = (orc_handle*)hp;
+  delete h->pl;
+  h->pl = new orc::Planner();
+  orc::Planner& pl = *h->pl;
+  pl.rb = h->rb;
+  pl.ck = &h->ck;
+  set_params(pl, p);
+  orc::Conf s, g;
+  for (int j = 0; j < 8; ++j) { s[j] = start[j]; g[j] = goal[j]; }
+  h->ck.calls = 0;
+  return pl.init(s, g);
+}
+
+// One tree: n nodes (parent id, configuration, costs, in-edge interpolation start / target) and every node's children
+// in the reference's out-edge order (child_ids[child_off[i] .. child_off[i + 1]]).
+void orc_resume_tree(void* hp, int which, int n, const int* parent, const double* q, const double* cost,
+                     const double* e_start, const double* e_target, const int* child_off, const int* child_ids,
+                     int num_edges, int num_rewire) {
+  orc_handle* h = (orc_handle*)hp;
+  orc::Planner& pl = *h->pl;
+  orc::Tree& t = which ? pl.tb : pl.ta;
+  t.nodes.assign(n, orc::Node());
+  for (int i = 0; i < n; ++i) {
+    orc::Node& nd = t.nodes[i];
+    nd.node_id = i;
+    nd.parent_id = parent[i];
+    for (int j = 0; j < 8; ++j) nd.q[j] = q[8 * (size_t)i + j];
+    nd.cost.total = cost[3 * (size_t)i]; nd.cost.rev = cost[3 * (size_t)i + 1]; nd.cost.prism = cost[3 * (size_t)i + 2];
+  }
+  for (int i = 0; i < n; ++i)
+    for (int k = child_off[i]; k < child_off[i + 1]; ++k) {
+      const int c = child_ids[k];
+      orc::Edge e;
+      e.root_node_id = i;
+      e.child_node_id = c;
+      // connectNodesInterpolation's trajectory from the child's in-edge (the arithmetic of connect_nodes)
+      double step[8];
+      for (int j = 0; j < 8; ++j) step[j] = (e_target[8 * (size_t)c + j] - e_start[8 * (size_t)c + j]) / double(pl.P.n_pts);
+      e.traj.resize(pl.P.n_pts + 1);
+      for (int inc = 0; inc <= pl.P.n_pts; ++inc)
+        for (int j = 0; j < 8; ++j) e.traj[inc][j] = e_start[8 * (size_t)c + j] + inc * step[j];
+      for (int j = 0; j < 8; ++j) { e.s[j] = e_start[8 * (size_t)c + j]; e.g[j] = e_target[8 * (size_t)c + j]; }
+      t.nodes[i].out.push_back(e);
+    }
+  t.num_nodes = n;
+  t.num_edges = num_edges;
+  t.num_rewire = num_rewire;
+}
+
+// The loop scalars (iv: iteration, checked, valid, first_iter, last_iter, have_sol, conn_start, tree_A of the next
+// iteration (1 = goal), nB id / parent, nA id / parent; dv: c_best[3], nB q[8] / cost[3], nA q[8] / cost[3]), then the
+// loop to the budget.
+int orc_resume_run(void* hp, const long long* iv, const double* dv, orc_result* res) {
+  orc_handle* h = (orc_handle*)hp;
+  orc::Planner& pl = *h->pl;
+  std::memset(res, 0, sizeof(*res));
+  pl.iter = iv[0];
+  pl.st.checked = iv[1]; pl.st.valid = iv[2]; pl.st.first_iter = iv[3]; pl.st.last_iter = iv[4];
+  pl.have_sol = iv[5] != 0;
+  pl.conn_start = iv[6] != 0;
+  pl.cbest = dv[0]; pl.cbest_rev = dv[1]; pl.cbest_prism = dv[2];
+  orc::Node* nb[2] = {&pl.nB, &pl.nA};
+  for (int k = 0; k < 2; ++k) {
+    nb[k]->node_id = (int)iv[8 + 2 * k];
+    nb[k]->parent_id = (int)iv[9 + 2 * k];
+    for (int j = 0; j < 8; ++j) nb[k]->q[j] = dv[3 + 11 * k + j];
+    nb[k]->cost.total = dv[11 + 11 * k]; nb[k]->cost.rev = dv[12 + 11 * k]; nb[k]->cost.prism = dv[13 + 11 * k];
+    nb[k]->out.clear();
+  }
+  return fill_result(h, pl.resume(iv[7] != 0), res);
+}
+
+// The state orc_resume_* takes, of this handle's last run: per tree the in-edge (interpolation start / target) of every
+// node and the children in out-edge order (child_off: n + 1 offsets; returns the total), then the loop scalars.
+int orc_export_tree(void* hp, int which, double* e_start, double* e_target, int* child_off, int* child_ids) {
+  orc_handle* h = (orc_handle*)hp;
+  const orc::Tree& t = which ? h->pl->tb : h->pl->ta;
+  int k = 0;
+  for (size_t i = 0; i < t.nodes.size(); ++i) {
+    if (child_off) child_off[i] = k;
+    for (const orc::Edge& e : t.nodes[i].out) {
+      if (child_ids) child_ids[k] = e.child_node_id;
+      if (e_start) std::memcpy(e_start + 8 * (size_t)e.child_node_id, e.s.data(), 8 * sizeof(double));
+      if (e_target) std::memcpy(e_target + 8 * (size_t)e.child_node_id, e.g.data(), 8 * sizeof(double));
+      ++k;
+    }
+  }
+  if (child_off) child_off[t.nodes.size()] = k;
+  return k;
+}
+
+void orc_export_state(void* hp, long long* iv, double* dv) {
+  const orc::Planner& pl = *((orc_handle*)hp)->pl;
+  iv[0] = pl.iter; iv[1] = pl.st.checked; iv[2] = pl.st.valid; iv[3] = pl.st.first_iter; iv[4] = pl.st.last_iter;
+  iv[5] = pl.have_sol; iv[6] = pl.conn_start; iv[7] = pl.iter & 1;  // tree_A alternates, starting with the start tree
+  const orc::Node* nb[2] = {&pl.nB, &pl.nA};
+  dv[0] = pl.cbest; dv[1] = pl.cbest_rev; dv[2] = pl.cbest_prism;
+  for (int k = 0; k < 2; ++k) {
+    iv[8 + 2 * k] = nb[k]->node_id;
+    iv[9 + 2 * k] = nb[k]->parent_id;
+    for (int j = 0; j < 8; ++j) dv[3 + 11 * k + j] = nb[k]->q[j];
+    dv[11 + 11 * k] = nb[k]->cost.total; dv[12 + 11 * k] = nb[k]->cost.rev; dv[13 + 11 * k] = nb[k]->cost.prism;
+  }
+}
+
 int orc_plan(void* hp, const double* start, const double* goal, const orc_params* p, orc_result* res) {
   orc_handle* h = (orc_handle*)hp;
   delete h->pl;
@@ -1754,19 +1892,18 @@ int orc_plan(void* hp, const double* start, const double* goal, const orc_params
   orc::Planner& pl = *h->pl;
   pl.rb = h->rb;
   pl.ck = &h->ck;
-  pl.P.near_r = p->near_r; pl.P.step = p->step; pl.P.n_pts = p->n_pts; pl.P.max_near = p->max_near;
-  pl.P.opt_thresh = p->opt_thresh; pl.P.tree_opt = p->tree_opt; pl.P.informed = p->informed;
-  pl.P.env_x[0] = p->env_x[0]; pl.P.env_x[1] = p->env_x[1]; pl.P.env_y[0] = p->env_y[0]; pl.P.env_y[1] = p->env_y[1];
-  pl.P.self = p->self; pl.P.map = p->map; pl.P.seed = p->seed; pl.P.query = p->query;
-  pl.P.max_iter = p->max_iter; pl.P.max_time = p->max_time; pl.P.max_checked = p->max_checked;
-  pl.P.threads = p->threads;
+  set_params(pl, p);
   orc::Conf s, g;
   for (int j = 0; j < 8; ++j) { s[j] = start[j]; g[j] = goal[j]; }
   std::memset(res, 0, sizeof(*res));
   h->ck.calls = 0;
   int st = pl.init(s, g);
   if (st) { res->status = st; return st; }
-  bool ok = pl.run();
+  return fill_result(h, pl.run(), res);
+}
+
+static int fill_result(orc_handle* h, bool ok, orc_result* res) {
+  orc::Planner& pl = *h->pl;
   h->path = pl.final_path();
   res->status = ok ? 0 : 1;
   res->iterations = pl.st.iterations; res->first_iter = pl.st.first_iter; res->last_iter = pl.st.last_iter;

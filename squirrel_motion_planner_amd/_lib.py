@@ -140,6 +140,8 @@ PROBES = [
                             ctypes.POINTER(ctypes.c_uint64), _pd]),
     ("smp_probe_check_latency", _i, [_p, _pd, _i64, _i, _i, _i, _i, _pd, ctypes.POINTER(ctypes.c_uint64), _pd]),
     ("smp_probe_check_shape", _i, [_p, _pd, _i64, _i, _i, _i, _i, _p]),
+    ("smp_probe_export_tree", _i, [_p, _i, _p, _p, _pd, _pd]),
+    ("smp_probe_export_state", _i, [_p, _p, _pd]),
     ("smp_probe_robot_dev", _i64, [_p, _p, _i64]),
     ("smp_probe_scene_slabs", _i64, [_p, _p, _p, _i64]),
 ]

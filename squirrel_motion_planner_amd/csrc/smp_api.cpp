@@ -963,7 +963,6 @@ static QueryDev make_qdev(QueryBuffers& b, size_t cap, long long rows) {
   d.ttff = nullptr;
   d.lfin = nullptr;
   d.lquota = 0;
-  d.end_on_sol = 0;
   // scans of trees of at least this many nodes are split over the helpers (DESIGN.md "Scans of large trees");
   // SMP_SCAN_MIN overrides it (experiments and tests; 0: never)
   d.scan_min = 12288;
@@ -1066,42 +1065,10 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
   // M configs/s; C5, 8 queries: 0.49 / 0.61 / 0.62 M)
   int rb_div = 4;
   if (const char* e = std::getenv("SMP_REBALANCE_DIV")) rb_div = std::max(1, std::atoi(e));
-  // A single query with automatic helpers and scouts ends its first launch once it has a solution and continues
-  // re-provisioned for the post-solution phase (DESIGN.md "Post-solution provisioning"): scouts 2 and 3 have retired
-  // and the leader's own jobs are rare, so the leader keeps SMP_POST_LEAD helpers and scouts 0 and 1 (every
-  // iteration's choose-parent and rewire jobs) share the rest, up to SMP_POST_CAP helpers in all.  SMP_POST=0 keeps
-  // the first launch's provisioning (experiments).
-  int post_mode = nq == 1 && nh_req == 0 && want_scout && p->params.scout == 1 ? 1 : 0;
-  if (const char* e = std::getenv("SMP_POST")) post_mode = post_mode && std::atoi(e) != 0;
-  int post_lead = 16, post_cap = 220;
-  if (const char* e = std::getenv("SMP_POST_LEAD")) post_lead = std::max(1, std::atoi(e));
-  if (const char* e = std::getenv("SMP_POST_CAP")) post_cap = std::max(8, std::atoi(e));
   int nh = 0, ns = 0;
-  auto provision_post = [&](int i) {
-    const int cpq = slots;
-    ns = 2;
-    nh = std::min(post_cap, std::max(0, cpq - 1 - ns));
-    const int h_lead = std::min(post_lead, std::max(1, nh / 4));
-    const int rest = nh - 1 - h_lead;  // minus the sampler
-    qdev[i].jb = p->qb[i].jb.p;
-    qdev[i].sampler = 1;
-    qdev[i].nworkers = 1 + h_lead;
-    qdev[i].nscouts = ns;
-    qdev[i].end_on_sol = 0;
-    for (int sct = 0; sct < ns; ++sct) {
-      qdev[i].sjbs[sct] = p->qb[i].sjb[sct].p;
-      qdev[i].scbs[sct] = p->qb[i].scb[sct].p;
-      qdev[i].svias[sct] = p->qb[i].svia[sct].p;
-      qdev[i].sworkers_s[sct] = 1 + (sct == 0 ? rest - rest / 2 : rest / 2);
-    }
-  };
   auto provision = [&](const std::vector<int>& act) {
     const int na = std::max(1, (int)act.size());
     const int cpq = std::max(1, slots / na);
-    if (post_mode && na == 1 && S[act[0]].have_sol) {
-      provision_post(act[0]);
-      return;
-    }
     nh = nh_req;
     ns = 0;
     if (nh == 0) {
@@ -1138,7 +1105,6 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
       qdev[i].nscouts = ns;
       qdev[i].pre_delay = pre_delay;
       qdev[i].pre_commit = pre_commit;
-      qdev[i].end_on_sol = post_mode && ns >= 2 && !S[i].have_sol;
       qdev[i].sampler_jb = p->qb[i].jb.p;
       for (int s = 0; s < ns; ++s) {
         qdev[i].sjbs[s] = p->qb[i].sjb[s].p;
@@ -1332,12 +1298,10 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
     for (int i : act)
       if (!(S[i].phase == 2 || S[i].status != 0)) still.push_back(i);
     const bool shrank = still.size() < act.size();
-    // the single query's first launch ended at its first solution: the post-solution provisioning
-    const bool to_post = post_mode && still.size() == 1 && qdev[still[0]].end_on_sol && S[still[0]].have_sol;
     act.swap(still);
     if (act.empty()) break;
-    if (shrank || to_post) {
-      if (rebalance || to_post) provision(act);
+    if (shrank) {
+      if (rebalance) provision(act);
       if (int st = upload_active()) return st;
     }
     if (chunk < 4096) chunk *= 2;
@@ -1515,6 +1479,52 @@ extern "C" void smp_result_free(smp_result* r) {
   r->waypoints = nullptr;
   r->cost_rows = nullptr;
   r->n_waypoints = r->n_cost_rows = 0;
+}
+
+// The last query's state in the oracle's terms (test infrastructure, DESIGN.md "Large trees": the oracle continues
+// the same run from it, orc_resume_*): per tree the child lists (first child, next sibling: the GPU inserts children
+// at the head, so the reference's out-edge order is the list reversed) and every node's in-edge (interpolation start
+// and target, n x 8 row-major); then the loop scalars (iv: iteration, checked, valid, first_iter, last_iter,
+// have_sol, conn_start, tree_A of the next iteration, nB id / parent, nA id / parent, edges / rewires of both trees;
+// dv: c_best[3], nB q[8] / cost[3], nA q[8] / cost[3]).
+extern "C" int smp_probe_export_tree(smp_planner* p, int which, int32_t* first_child, int32_t* next_sib,
+                                     double* e_start, double* e_target) {
+  if (!p || p->qb.empty() || which < 0 || which > 1) return SMP_ERR_ARG;
+  HIPCHK(hipSetDevice(p->device));
+  QueryBuffers& b = p->qb[0];
+  const size_t cap = b.cap;
+  const int n = p->last_n[which];
+  if (first_child) HIPCHK(hipMemcpy(first_child, b.first_child.p + which * cap, n * sizeof(int), hipMemcpyDeviceToHost));
+  if (next_sib) HIPCHK(hipMemcpy(next_sib, b.next_sib.p + which * cap, n * sizeof(int), hipMemcpyDeviceToHost));
+  std::vector<double> tmp((size_t)n);
+  double* const outs[2] = {e_start, e_target};
+  double* const srcs[2] = {b.e_start.p, b.e_target.p};
+  for (int o = 0; o < 2; ++o) {
+    if (!outs[o]) continue;
+    for (int j = 0; j < NJ; ++j) {
+      HIPCHK(hipMemcpy(tmp.data(), srcs[o] + which * cap * NJ + (size_t)j * cap, n * sizeof(double), hipMemcpyDeviceToHost));
+      for (int i = 0; i < n; ++i) outs[o][(size_t)i * NJ + j] = tmp[i];
+    }
+  }
+  return SMP_OK;
+}
+
+extern "C" int smp_probe_export_state(smp_planner* p, int64_t* iv, double* dv) {
+  if (!p || p->qb.empty() || !iv || !dv) return SMP_ERR_ARG;
+  HIPCHK(hipSetDevice(p->device));
+  QState S;
+  HIPCHK(hipMemcpy(&S, p->qb[0].st.p, sizeof(QState), hipMemcpyDeviceToHost));
+  iv[0] = S.iter; iv[1] = S.checked; iv[2] = S.valid; iv[3] = S.first_iter; iv[4] = S.last_iter;
+  iv[5] = S.have_sol; iv[6] = S.conn_start; iv[7] = S.A;
+  iv[8] = S.nB.id; iv[9] = S.nB.parent; iv[10] = S.nA.id; iv[11] = S.nA.parent;
+  iv[12] = S.edges[0]; iv[13] = S.edges[1]; iv[14] = S.rewires[0]; iv[15] = S.rewires[1];
+  dv[0] = S.cbest[0]; dv[1] = S.cbest[1]; dv[2] = S.cbest[2];
+  const NodeRef* nb[2] = {&S.nB, &S.nA};
+  for (int k = 0; k < 2; ++k) {
+    for (int j = 0; j < NJ; ++j) dv[3 + 11 * k + j] = nb[k]->q[j];
+    for (int c = 0; c < 3; ++c) dv[11 + 11 * k + c] = nb[k]->c[c];
+  }
+  return SMP_OK;
 }
 
 extern "C" int64_t smp_get_tree(smp_planner* p, int which, int32_t* parent, double* conf, double* cost) {

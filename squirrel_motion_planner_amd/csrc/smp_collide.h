@@ -874,39 +874,6 @@ __device__ __forceinline__ void collide_wide(const RobotDev* __restrict__ rb, co
     if (lane == 0) W.pcand = 0u;
     wave_sync();
     if (prof && threadIdx.x == 0) ta = wall_clock64();
-#ifdef SMP_WIDE_ROWB
-    // B: the chain product, one lane per row r = 0..2 of T carrying the whole row (fmul's three-term sums in KDL
-    // order, the same values as the element-per-lane form): no cross-lane broadcast on the dependent chain, the local
-    // frames read as LDS broadcasts one step ahead
-    if (lane < 3) {
-      const int r = lane;
-      double t0v = r == 0 ? 1.0 : 0.0, t1v = r == 1 ? 1.0 : 0.0, t2v = r == 2 ? 1.0 : 0.0, tp = r == 2 ? rb->root_z : 0.0;
-      double l[12];
-#pragma unroll
-      for (int i = 0; i < 12; ++i) l[i] = W.u.lf[0][i];
-      int bd = rb->ch_body[0];
-      for (int k = 0; k < nch; ++k) {
-        const int kn = k + 1 < nch ? k + 1 : k;
-        double ln[12];
-#pragma unroll
-        for (int i = 0; i < 12; ++i) ln[i] = W.u.lf[kn][i];
-        const int bdn = rb->ch_body[kn];
-        const double n0 = t0v * l[0] + t1v * l[3] + t2v * l[6];
-        const double n1 = t0v * l[1] + t1v * l[4] + t2v * l[7];
-        const double n2 = t0v * l[2] + t1v * l[5] + t2v * l[8];
-        const double m = t0v * l[9] + t1v * l[10] + t2v * l[11];
-        tp = m + tp;
-        t0v = n0; t1v = n1; t2v = n2;
-        if (bd >= 0) {
-          W.v.fr[bd][r * 3 + 0] = t0v; W.v.fr[bd][r * 3 + 1] = t1v; W.v.fr[bd][r * 3 + 2] = t2v;
-          W.v.fr[bd][9 + r] = tp;
-        }
-#pragma unroll
-        for (int i = 0; i < 12; ++i) l[i] = ln[i];
-        bd = bdn;
-      }
-    }
-#else
     // B: the chain product, one lane per element (rows r = 0..2 of four lanes: columns 0..2 of R, then p), as
     // collide_tile's stage B (fmul's three-term sums in KDL order; row r of T from the lane's quad by DPP broadcasts)
     if (lane < 12) {
@@ -930,7 +897,6 @@ __device__ __forceinline__ void collide_wide(const RobotDev* __restrict__ rb, co
         bd = bdn;
       }
     }
-#endif
     wave_sync();
     if (prof && threadIdx.x == 0) tb = wall_clock64();
     // centres of every sphere and frames of every primitive (the self pairs need them all); the prefilter loads of

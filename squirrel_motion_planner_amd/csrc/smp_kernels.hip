@@ -4571,7 +4571,6 @@ __global__ void __launch_bounds__(BLOCK) plan_kernel(const RobotDev* __restrict_
       if (uni(g_L.go_end)) break;
     }
     iteration(C);
-    if (C.Q.end_on_sol && uni(g_L.S.have_sol)) break;  // re-provisioned for the post-solution phase (resumable)
   }
   if (threadIdx.x == 0) {
     if (C.Q.lquota > 0 && (g_L.S.phase == 2 || g_L.S.status != 0))

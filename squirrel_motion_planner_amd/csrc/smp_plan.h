@@ -287,8 +287,6 @@ struct QueryDev {
   // finished queries to the others (DESIGN.md "Many queries")
   unsigned* lfin;
   int lquota;
-  int end_on_sol;              // 1: the leader ends the launch once it has a solution (the host re-provisions the CUs
-                               // for the post-solution phase: two scouts, the leader's helpers moved to them)
   unsigned* ttff;              // host-mapped word set to 1 when the first feasible path is committed (null: none)
   int scan_min;                // nodes in a scan's range from which it is split over the helpers (0: never)
   int scan_pnn, scan_pnear;    // participants (this workgroup + helpers) of a split nearest / near scan, <= SCAN_P

@@ -370,6 +370,39 @@ class GpuPlanner:
                            cost.ctypes.data_as(ctypes.c_void_p))
         return par, conf, cost
 
+    def export_state(self):
+        """The last query's state in the form oracle.Oracle.resume() takes (test infrastructure: the oracle continues
+        the GPU's run from it -- large-tree parity and the CPU timed at the GPU's tree sizes)."""
+        iv = np.zeros(16, np.int64)
+        dv = np.zeros(25)
+        check(lib().smp_probe_export_state(self.h, iv.ctypes.data_as(ctypes.c_void_p), dv.ctypes.data_as(_pd)),
+              "smp_probe_export_state")
+        st = {"iv": iv[:12].copy(), "dv": dv}
+        for which, name in ((0, "start"), (1, "goal")):
+            par, conf, cost = self.tree(which)
+            n = len(par)
+            fc, ns = np.zeros(n, np.int32), np.zeros(n, np.int32)
+            es, et = np.zeros((n, 8)), np.zeros((n, 8))
+            check(lib().smp_probe_export_tree(self.h, which, fc.ctypes.data_as(ctypes.c_void_p),
+                                              ns.ctypes.data_as(ctypes.c_void_p), es.ctypes.data_as(_pd),
+                                              et.ctypes.data_as(_pd)), "smp_probe_export_tree")
+            # the reference's out-edge order: the GPU's child lists (head insertion) reversed
+            off = np.zeros(n + 1, np.int32)
+            ids = []
+            for i in range(n):
+                off[i] = len(ids)
+                ch = []
+                c = int(fc[i])
+                while c >= 0:
+                    ch.append(c)
+                    c = int(ns[c])
+                ids.extend(reversed(ch))
+            off[n] = len(ids)
+            st[name] = {"parent": par, "conf": conf, "cost": cost, "e_start": es, "e_target": et, "child_off": off,
+                        "child_ids": np.array(ids, np.int32), "edges": int(iv[12 + which]),
+                        "rewires": int(iv[14 + which])}
+        return st
+
     def __del__(self):
         if getattr(self, "h", None):
             lib().smp_planner_destroy(self.h)

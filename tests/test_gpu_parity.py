@@ -594,3 +594,30 @@ def test_large_tree_run_matches_golden(robot):
         assert dig(conf) == str(g[name + "_conf_sha"]), name
         assert dig(cost) == str(g[name + "_cost_sha"]), name
     assert np.array_equal(r["path"], g["path"])
+
+
+@pytest.mark.parametrize("n1,n2", [(3000, 3600), (20000, 20300)])
+def test_oracle_continues_the_gpu_state(gp, orobot, n1, n2):
+    """The oracle continued from the GPU planner's state after n1 iterations (GpuPlanner.export_state ->
+    Oracle.resume: both trees with their child order and in-edges, the loop scalars) plans exactly the GPU's own run of
+    n2 iterations: the GPU's state is the reference loop's state at n1, and the large-tree CPU timing
+    (tools/large_tree_report.py) resumes the CPU from the GPU's trees."""
+    sc, gscene, osc = scene_pair("c2")
+    gp.set_scene(gscene)
+    gp.set_disabled_map_links([])
+    kw = dict(env_x=sc.env_x, env_y=sc.env_y, seed=7, opt_thresh=-math.inf)
+    gpl = GpuPlanner(path_optimality_threshold=-math.inf)
+    gpl.set_scene(gscene)
+    gpl.plan(GpuPlanner.make_query(sc.start, sc.goal, sc.env_x, sc.env_y, iterations=n1, seed=7))
+    st = gpl.export_state()
+    r = gpl.plan(GpuPlanner.make_query(sc.start, sc.goal, sc.env_x, sc.env_y, iterations=n2, seed=7))
+    o = O.Oracle(orobot, osc).resume(sc.start, sc.goal, st, max_iter=n2, **kw)
+    assert o["iterations"] == r["iterations"] == n2
+    assert o["checked"] == r["configs_checked"] and o["valid"] == r["configs_valid"]
+    assert o["n_start"] == r["nodes_start"] and o["n_goal"] == r["nodes_goal"]
+    assert o["cost"] == list(r["cost_best"])
+    for which, name in ((0, "start"), (1, "goal")):
+        par, conf, cost = gpl.tree(which)
+        assert np.array_equal(par, o[name + "_parent"])
+        assert np.array_equal(conf, o[name + "_conf"]) and np.array_equal(cost, o[name + "_cost"])
+    assert np.array_equal(r["path"], o["path"])

@@ -216,3 +216,24 @@ def test_openmp_scans_plan_the_same_trees(orobot):
     assert a["cost"] == b["cost"]
     assert np.array_equal(a["start_parent"], b["start_parent"]) and np.array_equal(a["goal_conf"], b["goal_conf"])
     assert np.array_equal(a["path"], b["path"])
+
+
+def test_oracle_resume_equals_one_run(orobot):
+    """orc_resume_*: the oracle continued from its own state after 700 iterations plans exactly the run of 1500
+    iterations (trees, counters, costs, path) -- the mechanism the large-tree parity and timing use on GPU states."""
+    import math
+    from squirrel_motion_planner_amd import scenes
+    sc = scenes.box_room()
+    kw = dict(env_x=sc.env_x, env_y=sc.env_y, seed=1, opt_thresh=-math.inf)
+    o1 = O.Oracle(orobot, O.OracleScene(sc.keys, sc.res))
+    st = o1.export_state(o1.plan(sc.start, sc.goal, max_iter=700, **kw))
+    r2 = O.Oracle(orobot, O.OracleScene(sc.keys, sc.res)).resume(sc.start, sc.goal, st, max_iter=1500, **kw)
+    r3 = O.Oracle(orobot, O.OracleScene(sc.keys, sc.res)).plan(sc.start, sc.goal, max_iter=1500, **kw)
+    for k in ("iterations", "checked", "valid", "first_iter", "last_iter", "n_start", "n_goal", "edges_start",
+              "edges_goal", "rewires_start", "rewires_goal", "conn_b", "conn_a", "conn_start", "status"):
+        assert r2[k] == r3[k], k
+    assert r2["cost"] == r3["cost"]
+    for n in ("start", "goal"):
+        for f in ("parent", "conf", "cost"):
+            assert np.array_equal(r2[n + "_" + f], r3[n + "_" + f])
+    assert np.array_equal(r2["path"], r3["path"])

@@ -2,11 +2,8 @@
 set -e
 OUT=gpurun_out
 mkdir -p $OUT
-timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 200 --timeout-method thread -k "planner_parity or large_tree or relaunch" > $OUT/t_post.log 2>&1
-for v in "SMP_POST=0" "SMP_POST=1" "SMP_POST_LEAD=8" "SMP_POST_LEAD=32" "SMP_POST_CAP=200" "SMP_POST_CAP=240"; do
-  echo "== $v" >> $OUT/post_sweep.txt
-  env $v timeout -k 10 120 python -u tools/perf_probe.py 4000 >> $OUT/post_sweep.txt 2>&1
-done
-SMP_SETS=expand-edges,connect-edges SMP_TILES=8,-1 timeout -k 10 200 python -u tools/tile_probe.py > $OUT/tile_probe.txt 2>&1
-SMP_LIB=squirrel_motion_planner_amd/lib/libsmp_gpu_rowb.so SMP_SETS=expand-edges SMP_TILES=8,-1 timeout -k 10 200 python -u tools/tile_probe.py > $OUT/tile_probe_rowb.txt 2>&1
-SMP_LIB=squirrel_motion_planner_amd/lib/libsmp_gpu_rowb.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 200 --timeout-method thread -k "job_tile_shapes" > $OUT/t_rowb.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1
+timeout -k 10 400 python bench.py --steps 20 --warmup 2 > $OUT/bench_c2_20.json 2> $OUT/bench_c2_20.err
+timeout -k 10 300 python bench.py --workload c5 --steps 1 --warmup 1 > $OUT/c5_q8.json 2> $OUT/c5_q8.err
+timeout -k 10 300 python bench.py --workload c3 --steps 1 --warmup 1 > $OUT/c3_q8.json 2> $OUT/c3_q8.err
+timeout -k 10 300 python tools/ik_report.py $OUT/ik_report.json > $OUT/ik.log 2>&1

@@ -52,7 +52,7 @@ def main():
     rep = {"scene": "C2 box scene (10x10x2 m @5 cm, 20 boxes), robot at its start pose", "cpu": cpu_name(),
            "cpu_threads": 1, "goal_search": [], "batch": []}
     gp.find_goal_pose(goals(sc, 1, 0)[0], cur, 20.0)  # warm-up (module load, first launch)
-    for disc in (20.0, 5.0):
+    for disc in (20.0, 10.0, 5.0):  # 10 deg: the node's setting (parameters.yaml:33)
         rows = []
         for ee in goals(sc, 16, 1):
             t0 = time.perf_counter()
