@@ -1057,6 +1057,8 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
   // commits"); SMP_PRE_DELAY overrides it for experiments (0: at the request)
   int pre_delay = 3;
   if (const char* e = std::getenv("SMP_PRE_DELAY")) pre_delay = std::atoi(e);
+  int early_ask = 0;  // SMP_EARLY_ASK=1: after the first solution, iteration k + 2 is asked for before k's rewires (DESIGN.md "Early asks")
+  if (const char* e = std::getenv("SMP_EARLY_ASK")) early_ask = std::atoi(e);
   int pre_commit = 1;  // SMP_PRE_COMMIT=0: every iteration runs the full path (experiments)
   if (const char* e = std::getenv("SMP_PRE_COMMIT")) pre_commit = std::atoi(e);
   int rebalance = nh_req == 0 ? 1 : 0;  // SMP_REBALANCE=0: keep the first launch's provisioning (experiments)
@@ -1105,6 +1107,7 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
       qdev[i].nscouts = ns;
       qdev[i].pre_delay = pre_delay;
       qdev[i].pre_commit = pre_commit;
+      qdev[i].early_ask = early_ask;
       qdev[i].sampler_jb = p->qb[i].jb.p;
       for (int s = 0; s < ns; ++s) {
         qdev[i].sjbs[s] = p->qb[i].sjb[s].p;

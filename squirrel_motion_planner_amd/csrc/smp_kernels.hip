@@ -391,6 +391,12 @@ struct PlanLds {
   int asked_pre[SCOUT_SLOTS];   // leader: asked before the first solution (a pre-solution record)
   int conn_rec;                 // leader: connect of this iteration takes its scans from the record (g_L.sr.cc)
   int two_scouts;               // scout: two scouts share the iterations (post-solution records get SC_CONN)
+  unsigned sc_mod;              // scout: rewire commits of its pass's tree when the pass read it (stage granules carry it)
+  unsigned rw_at0;              // leader: rewire commits of tree_A at the start of the iteration (records must match)
+  int n_at0;                    // leader: nodes of tree_A at the start of the iteration (early asks' snapshot)
+  int sc_t, sc_rerun;           // scout: the pass's tree; 1 = the tree was rewired under the pass (rebuild it)
+  int rb_go[2];                 // scout: decision words of the rebuild wait (double-buffered like sp_go)
+  long long sc_k;               // scout: the pass's iteration
   int eg_hit[MAXE];
   int eg_rec[MAXE];             // leader: record edge (index into sr.e) equal to batch edge e, -1 = none
   int rec_grp;                  // leader: the record stage eg_rec was matched against (-1 = not matched)
@@ -1068,36 +1074,80 @@ __device__ void near_set(const Ctx& C, int t, const double* q, int excl, bool sp
   const int lane = lane_id(), wave = wave_id();
   TR();
   if (spec && spec_stage(C, SC_NEAR)) {
-    // the scout's near set of the same configuration over the tree's first X nodes is the answer if none of the
-    // nodes appended since is near (else the full scan below)
+    // the scout's near set of the same configuration over the tree's first X nodes, with the near nodes appended since
+    // (at most 64: else the full scan below) merged in exactly: the costs of the first X nodes are those the record
+    // saw (no rewire of this tree in between), so the K lowest / highest (cost, id) entries of the whole set are among
+    // the record's low / high lists and the appended near nodes
     const ScoutNear& R = g_L.sr.nr;
-    if (uni(R.ok && R.t == t && R.X <= n && same8(q, R.q))) {
-      bool any = false;
-      for (int i = R.X + (int)threadIdx.x; i < n; i += BLOCK) {
-        double sb = 0.0;
-        for (int j = 0; j < NJ; ++j) {
-          double d = q[j] - (tq + (size_t)j * cap)[(unsigned)i];
-          sb += d * d;
+    if (uni(R.ok && R.t == t && R.X <= n && n - R.X <= 64 && same8(q, R.q))) {
+      const int X = uni(R.X);
+      if (threadIdx.x < 64) {
+        const int i = X + lane;
+        bool nr = false;
+        unsigned long long key = 0;
+        if (i < n) {
+          double sb = 0.0;
+          for (int j = 0; j < NJ; ++j) {
+            const double d = q[j] - (tq + (size_t)j * cap)[(unsigned)i];
+            sb += d * d;
+          }
+          bool amb;
+          nr = near_radius(i != excl, sb, r, r2lo, r2hi, amb);
+          if (amb) nr = sqrt(sb) < r;
+          if (nr) key = (unsigned long long)__double_as_longlong(tc[(unsigned)i]);
         }
-        bool amb;
-        bool nr = near_radius(i != excl, sb, r, r2lo, r2hi, amb);
-        if (amb) nr = sqrt(sb) < r;
-        any |= nr;
+        const unsigned long long mk = __ballot(nr);
+        if (nr) {
+          const int s = __popcll(mk & ((1ull << lane) - 1));
+          g_L.nh.ck[0][s] = key;
+          g_L.nh.ci[0][s] = i;
+        }
+        if (lane == 0) g_L.nh.cnt[0] = __popcll(mk);
       }
-      if (!__syncthreads_or(any)) {
+      __syncthreads();
+      const int m = uni(g_L.nh.cnt[0]);
+      const int take = min(K, R.nk + m);
+      if (m == 0) {
         if (threadIdx.x < K) {
           g_L.lo_i[threadIdx.x] = R.lo_i[threadIdx.x]; g_L.lo_c[threadIdx.x] = R.lo_c[threadIdx.x];
           g_L.hi_i[threadIdx.x] = R.hi_i[threadIdx.x]; g_L.hi_c[threadIdx.x] = R.hi_c[threadIdx.x];
         }
-        if (threadIdx.x == 0) {
-          g_L.nk = R.nk; g_L.n_lo = R.n_lo; g_L.n_hi = R.n_hi;
-          g_L.S.near_nodes += n;
-          g_L.S.sc_near++;
+      } else if (threadIdx.x < 128) {
+        // wave 0 ranks the low side (the record's low list + the appended), wave 1 the high side; entries c = lane,
+        // lane + 64 of N <= K + 64, each ranked against all N as near_set's merge does
+        const int e = threadIdx.x >> 6;
+        const int nl = e == 0 ? R.n_lo : R.n_hi, N = nl + m;
+        for (int c = lane; c < N; c += 64) {
+          unsigned long long ck;
+          int ci;
+          if (c < nl) {
+            ck = (unsigned long long)__double_as_longlong(e == 0 ? R.lo_c[c] : R.hi_c[c]);
+            ci = e == 0 ? R.lo_i[c] : R.hi_i[c];
+          } else {
+            ck = g_L.nh.ck[0][c - nl];
+            ci = g_L.nh.ci[0][c - nl];
+          }
+          int rank = 0;
+          for (int o = 0; o < N; ++o) {
+            const unsigned long long ok = o < nl ? (unsigned long long)__double_as_longlong(e == 0 ? R.lo_c[o] : R.hi_c[o])
+                                                 : g_L.nh.ck[0][o - nl];
+            const int oi = o < nl ? (e == 0 ? R.lo_i[o] : R.hi_i[o]) : g_L.nh.ci[0][o - nl];
+            rank += e == 0 ? ki_less(ok, oi, ck, ci) : ki_less(ck, ci, ok, oi);
+          }
+          if (rank < take) {
+            if (e == 0) { g_L.lo_c[rank] = __longlong_as_double((long long)ck); g_L.lo_i[rank] = ci; }
+            else { g_L.hi_c[take - 1 - rank] = __longlong_as_double((long long)ck); g_L.hi_i[take - 1 - rank] = ci; }
+          }
         }
-        __syncthreads();
-        TR();
-        return;
       }
+      if (threadIdx.x == 0) {
+        g_L.nk = R.nk + m; g_L.n_lo = m == 0 ? R.n_lo : take; g_L.n_hi = m == 0 ? R.n_hi : take;
+        g_L.S.near_nodes += n;
+        g_L.S.sc_near++;
+      }
+      __syncthreads();
+      TR();
+      return;
     }
   }
   if (K == SCAN_K && scan_split(C, n)) {
@@ -2123,9 +2173,12 @@ __device__ bool spec_stage(const Ctx& C, int s, unsigned long long wait) {
   for (int k = 0;; k ^= 1) {
     if (threadIdx.x == 0) {
       const unsigned long long v = ld_agent(&sb->stage[par]);
+      const unsigned lo = (unsigned)v;
+      // a stage counts only if the scout built it on the tree as this iteration found it (its rewire commits)
+      const bool cur = ((lo >> 8) & 0xfffu) == (g_L.rw_at0 & 0xfffu);
       int go = 0;
       if ((unsigned)(v >> 32) != tag) go = -1;           // the scout is not on this iteration
-      else if ((int)(unsigned)v >= s) go = 1 + (int)(unsigned)v;
+      else if (cur && (int)(lo & 0xffu) >= s) go = 1 + (int)(lo & 0xffu);
       else if (wall_clock64() - t0 > wait) go = -1;
       g_L.sp_go[k] = go;
     }
@@ -2204,7 +2257,7 @@ __device__ void spec_copy(const ScoutBoard* sb, int par, int have, int st) {
 // for (asked[j % 4]); every scout also gets the leader's current iteration (its staleness test).
 // Thread 0: asks a scout for iteration k (expanding `tree`, whose first n[tree] nodes are final for it): before the
 // first solution scout k mod nscouts, after it scout k mod 2 (scouts 0 and 1).
-__device__ void scout_ask(const Ctx& C, long long k, int tree, bool pre, bool& fenced) {
+__device__ void scout_ask(const Ctx& C, long long k, int tree, bool pre, bool& fenced, int x_snap = -1) {
   const QState& S = g_L.S;
   const int ns = C.Q.nscouts;
   int which = 1 + (int)(pre ? k % ns : (ns >= 2 ? (k & 1) : 0));
@@ -2236,9 +2289,10 @@ __device__ void scout_ask(const Ctx& C, long long k, int tree, bool pre, bool& f
     fenced = true;
   }
   const unsigned tag = (unsigned)(k + 1);
-  const unsigned w0 = (unsigned)S.n[tree] | (unsigned)tree << 28 | (unsigned)(!pre) << 29;
+  const unsigned w0 = (unsigned)(x_snap >= 0 ? x_snap : S.n[tree]) | (unsigned)tree << 28 | (unsigned)(!pre) << 29;
   st_agent(&sb->req[2], granule(tag, (unsigned)S.n[1 - tree]));
-  st_agent(&sb->req[1], granule(tag, (unsigned)g_L.smp_ver));
+  // the sampler version (low 20 bits; the ring tags use 8) and the rewire commits of the tree the record expands
+  st_agent(&sb->req[1], granule(tag, ((unsigned)g_L.smp_ver & 0xfffffu) | ((unsigned)S.rewires[tree] & 0xfffu) << 20));
   st_agent(&sb->req[0], granule(tag, w0));
   g_L.asked[k & (SCOUT_SLOTS - 1)] = which;
   g_L.asked_conn[k & (SCOUT_SLOTS - 1)] = !pre && ns >= 2;
@@ -2256,9 +2310,29 @@ __device__ void scout_ask(const Ctx& C, long long k, int tree, bool pre, bool& f
 // covers the last iteration's stores): the leader's iteration for every scout, before the first solution the tree
 // sizes for the scouts' late snapshots, and the requests for the coming iterations not yet asked for (their snapshots
 // include the nodes the last iteration appended).
+// Early ask (after the first solution, two scouts on this XCD): iteration j + 2 is asked for as soon as its scout
+// (the one of iteration j) has finished record j's main pass -- before iteration j's inserts and rewire commits, not
+// after them.  The record reads tree_A(j) as it is then: nodes appended later are patched in by the leader as usual, and
+// a rewire commit on that tree makes the scout rebuild the pass (ScoutBoard::rwb / rwe; stage granules carry the count
+// of rewire commits the record was built on, and the leader takes only a record of the tree as it found it).  Thread 0.
+__device__ void scout_ask_early(const Ctx& C, int stage_j) {
+  const QState& S = g_L.S;
+  if (!C.Q.early_ask || C.Q.nscouts < 2 || !(S.tree_opt && S.have_sol) || stage_j < SC_DONE) return;
+  const long long k = S.iter + 2;
+  if (g_L.asked[k & (SCOUT_SLOTS - 1)]) return;
+  const int w = (int)(k & 1);
+  if (g_L.sc_same[w] != 1 || ((g_L.sc_dead >> w) & 1u)) return;
+  bool fenced = true;  // same XCD: no write-back needed
+  // the snapshot is tree_A as the iteration found it (those nodes' stores were drained by sample_read's round); the
+  // nodes this iteration inserts count as appended, as j + 1's connect nodes do
+  scout_ask(C, k, S.A, false, fenced, g_L.n_at0);
+}
+
 __device__ void scout_slots() {
   const QState& S = g_L.S;
   const long long j = S.iter;
+  g_L.rw_at0 = (unsigned)S.rewires[S.A];
+  g_L.n_at0 = S.n[S.A];
   g_L.asked[(j - 1) & (SCOUT_SLOTS - 1)] = 0;
   g_L.asked_conn[(j - 1) & (SCOUT_SLOTS - 1)] = 0;
   // a record asked for before the first solution (found in iteration f) is exact only while the tree it expands has
@@ -2866,7 +2940,9 @@ __device__ void sample_read(const Ctx& C) {
     int st = -1;
     if (pre && !prerec) {
       const unsigned long long v = ld_agent(&sb->stage[par]);
-      if ((unsigned)(v >> 32) == (unsigned)(S.iter + 1)) st = (int)(unsigned)v;
+      const unsigned lo = (unsigned)v;
+      if ((unsigned)(v >> 32) == (unsigned)(S.iter + 1) && ((lo >> 8) & 0xfffu) == (g_L.rw_at0 & 0xfffu))
+        st = (int)(lo & 0xffu);
     }
     g_L.sp_go[0] = st;
   }
@@ -2894,7 +2970,10 @@ __device__ void sample_read(const Ctx& C) {
     g_L.prer_ok = prer_ok;
     if (prer_ok) g_L.sc_seen |= 1u << (sw - 1);
     sample_publish(C);
-    if (C.Q.nscouts > 0) scout_asks(C, 1 - g_L.S.A);
+    if (C.Q.nscouts > 0) {
+      scout_asks(C, 1 - g_L.S.A);
+      scout_ask_early(C, g_L.sp_go[0]);  // record j's stage as this round found it
+    }
   }
   const int st = uni(g_L.sp_go[0]);
   __syncthreads();
@@ -3053,6 +3132,7 @@ __device__ void rewire(const Ctx& C, int t) {
   __syncthreads();
   if (C.Q.jb && rec_match(C, cnt, SC_DONE)) edge_costs_rec(cnt);
   else edge_costs(C, cnt);
+  if (threadIdx.x == 0 && g_L.sp_on) scout_ask_early(C, g_L.sp_stage);  // before this iteration's commits
   if (threadIdx.x < cnt) {
     int e = threadIdx.x, v = g_L.eg_near[e];
     // costs only decrease during the loop, so a candidate failing against the current cost never passes
@@ -3105,6 +3185,15 @@ __device__ void rewire(const Ctx& C, int t) {
         const int v = g_L.eg_near[e];
         double red[3];
         for (int k = 0; k < 3; ++k) red[k] = g_L.eg_cost[e][k] - g_L.rw_cost[e][k];
+        // early asks: every scout learns that tree t changes before any of this commit's stores can be seen
+        const bool pub = C.Q.nscouts >= 2;
+        if (pub) {
+          // (the iteration's earlier stores, its `cur` for the scouts among them, are performed first: a scout that
+          // sees the commit also sees that the leader is at this iteration, whose own commits need no rebuild)
+          drain();
+          for (int s2 = 0; s2 < 2; ++s2) st_agent(reinterpret_cast<int*>(&C.Q.scbs[s2]->rwb[t]), S.rewires[t] + 1);
+          drain();
+        }
         // unlink from the old parent (the reference erases the outgoing edge, birrt_star.cpp:5124-5169)
         const int p = g_L.rw_par[e];
         const int pv = T.prev_sib[v], nx = T.next_sib[v];
@@ -3132,6 +3221,10 @@ __device__ void rewire(const Ctx& C, int t) {
         DETAIL_END(_dc, 29);
         S.edges[t]++;
         S.rewires[t]++;
+        if (pub) {
+          drain();  // the commit's tree stores are performed (a same-XCD scout reads them through the shared L2)
+          for (int s2 = 0; s2 < 2; ++s2) st_agent(reinterpret_cast<int*>(&C.Q.scbs[s2]->rwe[t]), S.rewires[t]);
+        }
         next = e + 1;
         break;
       }
@@ -3805,7 +3898,7 @@ __device__ void sc_publish(const Ctx& C, int par, unsigned tag, int stage) {
   drain();
   __syncthreads();
   if (threadIdx.x == 0) {
-    st_agent(&C.Q.scb->stage[par], granule(tag, (unsigned)stage));
+    st_agent(&C.Q.scb->stage[par], granule(tag, (unsigned)stage | (g_L.sc_mod & 0xfffu) << 8));
     g_L.S.prof[29] += pclk() - t0;
   }
   __syncthreads();
@@ -3819,6 +3912,19 @@ __device__ bool sc_stale(const Ctx& C, unsigned tag) {
   const int s = uni(g_L.sp_go[0]);
   __syncthreads();
   return s != 0;
+}
+
+// True (block-uniform) if the leader began a rewire commit on the pass's tree since the pass read it (early asks): the
+// pass stops and scout_main rebuilds it on the tree as it is now.
+__device__ bool sc_moved(const Ctx& C) {
+  // (once the leader is at the pass's iteration, the commits are its own, after it took the record's stages)
+  if (threadIdx.x == 0)
+    g_L.sc_rerun = (ld_agent(&C.Q.scb->rwb[g_L.sc_t]) & 0xfffu) != g_L.sc_mod &&
+                   (long long)ld_agent(&C.Q.scb->cur) < g_L.sc_k;
+  __syncthreads();
+  const int r = uni(g_L.sc_rerun);
+  __syncthreads();
+  return r != 0;
 }
 
 // Scout, after its record's rewire stage (two scouts, after the first solution): waits until the leader reports
@@ -4079,6 +4185,7 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
     return;
   }
   // nearest + expand edge (iteration())
+  if (opt && sc_moved(C)) return;
   const int nid = nearest(C, t, g_L.xr);
   if (threadIdx.x == 0) {
     load_node(C, t, nid, &g_L.nn);
@@ -4102,6 +4209,7 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
   }
   SC_PHASE(1);
   TR();
+  if (opt && sc_moved(C)) return;
   edge_costs(C, 1);
   if (threadIdx.x == 0) {  // the expand edge's interpolation data, for the leader (published with SC_EXPAND)
     for (int j = 0; j < NJ; ++j) { R.ex.ext[j] = g_L.eg_target[0][j]; R.ex.step[j] = g_L.eg_step[0][j]; R.ex.end[j] = g_L.eg_end[0][j]; }
@@ -4200,6 +4308,7 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
   sc_publish(C, par, tag, SC_EXPAND);
   SC_PHASE(2);
   TR();
+  if (sc_moved(C)) return;
   // near set of x_new (the leader's, before choose_parent)
   if (!(uni(g_L.ext_nn) && take_spec(OV_NEAR_EXPAND))) near_set<20>(C, t, g_L.xn.q, X);
   if (threadIdx.x < 20) {
@@ -4216,6 +4325,7 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
   sc_publish(C, par, tag, SC_NEAR);
   SC_PHASE(3);
   TR();
+  if (sc_moved(C)) return;
   // choose_parent's candidate edges (all needed ones checked: the job computes every tile)
   if (threadIdx.x == 0) {
     int E = 0;
@@ -4288,6 +4398,7 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
   SC_PHASE(5);
   TR();
   if (!uni(g_L.ext_nn || g_L.ext_bp)) { sc_end(C, par, tag, opt); return; }
+  if (sc_moved(C)) return;
   // rewire's candidate edges (rewire())
   const TreeDev& T = C.Q.tr[t];
   rewire_count(T);
@@ -4325,6 +4436,7 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
   sc_publish(C, par, tag, SC_DONE);
   SC_PHASE(6);
   TR();
+  if (sc_moved(C)) return;
   if (uni(g_L.two_scouts)) scout_connect(C, it, t, par, tag);
   TR();
 }
@@ -4384,6 +4496,11 @@ __device__ __forceinline__ void scout_main(Ctx& C, int which) {
 #else
   const bool retired = which >= 2 && uni(g_L.S.tree_opt && g_L.S.have_sol);
 #endif
+  // the last pass's request: a post-solution pass is rebuilt when the leader rewires its tree after asking for it
+  // (early asks, ScoutBoard::rwb / rwe) and the leader has not yet moved past the iteration
+  unsigned l_w0 = 0, l_ver = 0;
+  int l_X = 0, l_XB = 0;
+  if (threadIdx.x == 0) { g_L.sc_mod = 0; g_L.sc_t = 0; g_L.sc_rerun = 0; }
   for (int k = 0; !retired; k ^= 1) {
     if (threadIdx.x == 0) {
       int go = 0;
@@ -4396,9 +4513,13 @@ __device__ __forceinline__ void scout_main(Ctx& C, int which) {
         if (tag > last && (unsigned)(r1 >> 32) == tag && (unsigned)(r2 >> 32) == tag) {
           go = 1;
           g_L.cnt = (int)(unsigned)r0;        // X | t << 28 | opt << 29
-          g_L.nn_t = (int)(unsigned)r1;       // sampler parameter version
+          g_L.nn_t = (int)(unsigned)r1;       // sampler parameter version | rewire commits of tree t << 20
           g_L.found = (int)(unsigned)r2;      // XB
           g_L.tree_expand = (int)tag;
+        } else if (last && ((l_w0 >> 29) & 1u) &&
+                   (ld_agent(&C.Q.scb->rwb[(l_w0 >> 28) & 1u]) & 0xfffu) != g_L.sc_mod &&
+                   (long long)ld_agent(&C.Q.scb->cur) < (long long)last - 1) {
+          go = 2;  // the last record's tree was rewired after it was built: rebuild it
         } else if (wall_clock64() - t_last > 200000000ull) {
           go = -1;  // 2 s idle
         }
@@ -4412,12 +4533,23 @@ __device__ __forceinline__ void scout_main(Ctx& C, int which) {
       __builtin_amdgcn_s_sleep(2);
       continue;
     }
-    const unsigned w0 = (unsigned)uni(g_L.cnt), ver = (unsigned)uni(g_L.nn_t), tag = (unsigned)uni(g_L.tree_expand);
-    int XB = uni(g_L.found);
-    int X = (int)(w0 & ((1u << 28) - 1));
+    unsigned w0, ver, tag;
+    int X, XB;
+    if (go == 1) {
+      const unsigned r1w = (unsigned)uni(g_L.nn_t);
+      w0 = (unsigned)uni(g_L.cnt);
+      ver = r1w & 0xfffffu;
+      tag = (unsigned)uni(g_L.tree_expand);
+      XB = uni(g_L.found);
+      X = (int)(w0 & ((1u << 28) - 1));
+      __syncthreads();
+      if (threadIdx.x == 0) g_L.sc_mod = (r1w >> 20) & 0xfffu;
+    } else {
+      w0 = l_w0; ver = l_ver; tag = last; X = l_X; XB = l_XB;
+    }
     const int t = (int)(w0 >> 28) & 1, opt = (int)(w0 >> 29) & 1;
     __syncthreads();
-    if (!opt && C.Q.pre_delay > 0) {
+    if (go == 1 && !opt && C.Q.pre_delay > 0) {
       // before the first solution: start once the leader is pre_delay iterations from this one, on the tree sizes
       // it published after its latest drain (trees only grow until the first solution, so they are at least the
       // request's): fewer nodes appended between the snapshot and the record's use, fewer records a newer node beats
@@ -4442,14 +4574,42 @@ __device__ __forceinline__ void scout_main(Ctx& C, int which) {
       XB = uni(g_L.found);
       __syncthreads();
     }
-    // tree words stored by the leader since this CU / XCD last cached them: drop stale copies (the invalidate completes
-    // asynchronously: every wave waits for it before its first plain load, MI355X_MICROARCH.md consumer form)
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    drain();
-    __syncthreads();
+    l_w0 = w0; l_ver = ver; l_X = X; l_XB = XB;
     const unsigned long long tb = wall_clock64();
     if (threadIdx.x == 0) g_L.S.prof[28] += tb - t_last;  // idle: waiting for a request
-    scout_iteration(C, (long long)tag - 1, t, X, opt, ver, XB);
+    for (;;) {  // the pass, rebuilt while the leader rewires its tree under it
+      if (opt) {
+        // the tree as the leader left it: a begun rewire commit is waited for until its words are stored
+        int st = 0;
+        for (int r = 0;; r ^= 1) {
+          if (threadIdx.x == 0) {
+            const unsigned b = ld_agent(&C.Q.scb->rwb[t]);
+            int v;
+            if ((b & 0xfffu) == g_L.sc_mod) v = 1;
+            else if (ld_agent(&C.Q.scb->stop) || (long long)ld_agent(&C.Q.scb->cur) > (long long)tag - 1) v = -1;
+            else if (ld_agent(&C.Q.scb->rwe[t]) == b) { v = 1; g_L.sc_mod = b & 0xfffu; }
+            else v = 0;
+            g_L.rb_go[r] = v;
+          }
+          __syncthreads();
+          st = uni(g_L.rb_go[r]);
+          if (st != 0) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+        __syncthreads();  // every wave has read rb_go before it is written again
+        if (st < 0) break;
+      }
+      if (threadIdx.x == 0) { g_L.sc_t = t; g_L.sc_rerun = 0; g_L.sc_k = (long long)tag - 1; }
+      // tree words stored by the leader since this CU / XCD last cached them: drop stale copies (the invalidate
+      // completes asynchronously: every wave waits for it before its first plain load, MI355X_MICROARCH.md consumer
+      // form)
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      drain();
+      __syncthreads();
+      scout_iteration(C, (long long)tag - 1, t, X, opt, ver, XB);
+      if (!opt || !uni(g_L.sc_rerun)) break;
+      __syncthreads();
+    }
     last = tag;
     t_last = wall_clock64();
     if (threadIdx.x == 0) g_L.S.prof[31] += t_last - tb;
@@ -4511,6 +4671,13 @@ __global__ void __launch_bounds__(BLOCK) plan_kernel(const RobotDev* __restrict_
     g_L.near_blo = ~0ull;
     g_L.near_bhi = 0;
     g_L.smp_ver = 0;
+    // the scouts' rewire-commit counters start at the trees' counts (the boards were zeroed for this launch)
+    for (int s = 0; s < C.Q.nscouts && s < 2; ++s)
+      for (int t = 0; t < 2; ++t) {
+        st_agent(reinterpret_cast<int*>(&C.Q.scbs[s]->rwb[t]), g_L.S.rewires[t]);
+        st_agent(reinterpret_cast<int*>(&C.Q.scbs[s]->rwe[t]), g_L.S.rewires[t]);
+      }
+    drain();  // before any request reaches a scout
 #ifdef SMP_TRACE
     g_L.trole = 0;
     g_L.tit = -1;

@@ -247,7 +247,11 @@ struct ScoutBoard {
   unsigned long long req[3];
   int stop;                    // the leader left the launch
   int xcc;                     // the scout's XCD (XCC_ID) + 1, 0 = not yet known
-  int pad0[8];
+  // leader -> scout, after the first solution: rewire commits on tree t begun (rwb) and finished (rwe), counted in
+  // QState::rewires.  A record asked for before its tree's last rewires (early asks) is rebuilt by the scout when rwb
+  // moves; both counters equal again = the tree's words are stored (DESIGN.md "Early asks")
+  unsigned rwb[2], rwe[2];
+  int pad0[4];
   unsigned long long cur;      // leader -> scout: the leader's current iteration (a record of an earlier one is stale)
   // leader -> scout, before the first solution: (iteration & 0xffffff) << 40 | n[0] << 20 | n[1], stored after the
   // iteration's drain, so both trees' first n nodes are visible (a scout binds its snapshot to it late)
@@ -272,6 +276,7 @@ struct QueryDev {
   int nscouts;
   int pre_delay;               // before the first solution a scout starts record k once the leader is at k - pre_delay
   int pre_commit;              // 1: pre-solution iterations are committed from complete scout records
+  int early_ask;               // 1: after the first solution, iteration k + 2 is asked for as soon as its scout is free
   ScoutBoard* scbs[MAX_SCOUTS];
   JobBoard* sjbs[MAX_SCOUTS];
   ViaNode* svias[MAX_SCOUTS];
