@@ -279,6 +279,82 @@ __device__ __forceinline__ int sphere_bricks(const SceneDev& sc, const double* c
 
 constexpr int MAP_STAGE_W = 96;  // brick words staged per configuration (its dead body-frame rows, TileLds::fr)
 
+constexpr int MAP_LIST = 256;  // occupied cells of one sphere's reach listed at once (sweep_occupied)
+
+// Exact map test of a sphere (centre cc, radius r, reach lo..hi, its brick box b0 / nbx of nbs <= 64 bricks, lane b
+// holding brick b's occupancy word) over the occupied cells of its reach only: each word masked to the reach, bricks
+// farther than r + 1e-9 from the centre dropped (every cell of them fails the exact test), the remaining occupied cells
+// listed in LDS (`list`, MAP_LIST entries) and tested 64 at a time.  A reach of a 2 cm scene holds up to 12^3 cells,
+// mostly free: cell-by-cell passes take up to 27 rounds where the list takes one or two.  Returns 1 hit, 0 free,
+// 2 = more than MAP_LIST occupied cells (the caller sweeps cell by cell).
+__device__ __forceinline__ int sweep_occupied(const SceneDev& sc, const double* cc, double r, const int* lo, const int* hi,
+                                              const int* b0, const int* nbx, int nbs, uint64_t w, uint16_t* list,
+                                              int lane) {
+  const double r2 = r * r;
+  if (lane < nbs && w) {
+    const int bi = lane % nbx[0], t = lane / nbx[0];
+    const int bj = t % nbx[1], bk = t / nbx[1];
+    const int gi = b0[0] + bi, gj = b0[1] + bj, gk = b0[2] + bk;
+    const int il = max(lo[0] - 4 * gi, 0), ih = min(hi[0] - 4 * gi, 3);
+    const int jl = max(lo[1] - 4 * gj, 0), jh = min(hi[1] - 4 * gj, 3);
+    const int kl = max(lo[2] - 4 * gk, 0), kh = min(hi[2] - 4 * gk, 3);
+    const uint32_t xm = ((2u << ih) - 1u) & ~((1u << il) - 1u);
+    uint32_t row = 0;
+    for (int jj = jl; jj <= jh; ++jj) row |= xm << (4 * jj);
+    uint64_t m = 0;
+    for (int kk = kl; kk <= kh; ++kk) m |= (uint64_t)row << (16 * kk);
+    w &= m;
+    if (w) {
+      const double x0 = sc.ox + (double)(4 * gi + il) * sc.res, x1 = sc.ox + (double)(4 * gi + ih + 1) * sc.res;
+      const double y0 = sc.oy + (double)(4 * gj + jl) * sc.res, y1 = sc.oy + (double)(4 * gj + jh + 1) * sc.res;
+      const double z0 = sc.oz + (double)(4 * gk + kl) * sc.res, z1 = sc.oz + (double)(4 * gk + kh + 1) * sc.res;
+      const double dx = cc[0] < x0 ? x0 - cc[0] : (cc[0] > x1 ? cc[0] - x1 : 0.0);
+      const double dy = cc[1] < y0 ? y0 - cc[1] : (cc[1] > y1 ? cc[1] - y1 : 0.0);
+      const double dz = cc[2] < z0 ? z0 - cc[2] : (cc[2] > z1 ? cc[2] - z1 : 0.0);
+      const double re = r + 1e-9;
+      if (dx * dx + dy * dy + dz * dz > re * re) w = 0;
+    }
+  } else {
+    w = 0;
+  }
+  const int cnt = __popcll(w);
+  int inc = cnt;
+  for (int d = 1; d < 64; d <<= 1) {
+    const int v = __shfl_up(inc, d);
+    if (lane >= d) inc += v;
+  }
+  const int T = __shfl(inc, 63);
+  if (T > MAP_LIST) return 2;
+  for (int pos = inc - cnt; w; ++pos) {
+    const int bit = __builtin_ctzll(w);
+    w &= w - 1;
+    list[pos] = (uint16_t)(lane << 6 | bit);
+  }
+  wave_sync();
+  int res = 0;
+  for (int t0 = 0; t0 < T; t0 += 64) {
+    const int t = t0 + lane;
+    bool hit = false;
+    if (t < T) {
+      const int code = list[t], bb = code >> 6, bit = code & 63;
+      const int bi = bb % nbx[0], tt = bb / nbx[0];
+      const int bj = tt % nbx[1], bk = tt / nbx[1];
+      const int i = 4 * (b0[0] + bi) + (bit & 3), j = 4 * (b0[1] + bj) + ((bit >> 2) & 3);
+      const int k = 4 * (b0[2] + bk) + (bit >> 4);
+      const double xlo = sc.ox + (double)i * sc.res, xhi = sc.ox + (double)(i + 1) * sc.res;
+      const double ylo = sc.oy + (double)j * sc.res, yhi = sc.oy + (double)(j + 1) * sc.res;
+      const double zlo = sc.oz + (double)k * sc.res, zhi = sc.oz + (double)(k + 1) * sc.res;
+      const double dx = cc[0] < xlo ? xlo - cc[0] : (cc[0] > xhi ? cc[0] - xhi : 0.0);
+      const double dy = cc[1] < ylo ? ylo - cc[1] : (cc[1] > yhi ? cc[1] - yhi : 0.0);
+      const double dz = cc[2] < zlo ? zlo - cc[2] : (cc[2] > zhi ? cc[2] - zhi : 0.0);
+      hit = dx * dx + dy * dy + dz * dz <= r2;
+    }
+    if (__ballot(hit)) { res = 1; break; }
+  }
+  wave_sync();  // the list is rewritten by the next sphere
+  return res;
+}
+
 // Exact map tests of all candidate spheres of one configuration by one wavefront, their brick words fetched in ONE
 // memory round trip: lanes over spheres give each candidate (<= 64 bricks) its slot range of the staging buffer `buf`
 // (MAP_STAGE_W words, in sphere order; owner[w] = the sphere of word w, off[s] = its first slot), lanes over slots
@@ -288,7 +364,7 @@ constexpr int MAP_STAGE_W = 96;  // brick words staged per configuration (its de
 // after the other; wave_sphere_map pays one load round trip per candidate.
 __device__ __forceinline__ bool wave_map_staged(const RobotDev* __restrict__ rb, const SceneDev& sc, const double (*wc)[3],
                                                 const uint32_t* cand, int nsph, uint64_t* buf, uint8_t* owner,
-                                                uint8_t* off, int lane) {
+                                                uint8_t* off, int lane, uint16_t* list = nullptr) {
   // slots: sphere s = g * 64 + lane of group g.  Staged are the candidates (of at most 64 bricks) whose inclusive
   // prefix of brick counts still ends within the buffer: a prefix of them in sphere order, so the words [0, base)
   // all have an owner; off[s] = first slot of a staged candidate, else 255
@@ -347,9 +423,14 @@ __device__ __forceinline__ bool wave_map_staged(const RobotDev* __restrict__ rb,
       const double cc[3] = {wc[s][0], wc[s][1], wc[s][2]};
       const double r = rb->sph_r[s], r2 = r * r;
       int lo[3], hi[3], b0[3], nbx[3];
-      sphere_bricks(sc, cc, r, lo, hi, b0, nbx);
+      const int nbs = sphere_bricks(sc, cc, r, lo, hi, b0, nbx);
       const int ni = hi[0] - lo[0] + 1, nj = hi[1] - lo[1] + 1, nk = hi[2] - lo[2] + 1;
       const int nv = ni * nj * nk;
+      if (list) {
+        const int h = sweep_occupied(sc, cc, r, lo, hi, b0, nbx, nbs, lane < nbs ? buf[o + lane] : 0ull, list, lane);
+        if (h == 1) return true;
+        if (h == 0) continue;
+      }
       for (int v0 = 0; v0 < nv; v0 += 64) {
         const int vv = v0 + lane;
         bool hit = false;
@@ -380,6 +461,21 @@ __device__ __forceinline__ bool wave_map_staged(const RobotDev* __restrict__ rb,
       const int s = g * 64 + __builtin_ctzll(m);
       m &= m - 1;
       const double cc[3] = {wc[s][0], wc[s][1], wc[s][2]};
+      if (list) {  // its brick words one per lane (one round trip), then the occupied cells only
+        int lo[3], hi[3], b0[3], nbx[3];
+        const int nbs = sphere_bricks(sc, cc, rb->sph_r[s], lo, hi, b0, nbx);
+        if (nbs <= 64) {
+          uint64_t w = 0;
+          if (lane < nbs) {
+            const int bi = lane % nbx[0], t = lane / nbx[0];
+            const int bj = t % nbx[1], bk = t / nbx[1];
+            w = sc.bricks[((size_t)(b0[2] + bk) * sc.bny + (b0[1] + bj)) * sc.bnx + (b0[0] + bi)];
+          }
+          const int h = sweep_occupied(sc, cc, rb->sph_r[s], lo, hi, b0, nbx, nbs, w, list, lane);
+          if (h == 1) return true;
+          if (h == 0) continue;
+        }
+      }
       if (wave_sphere_map(sc, cc, rb->sph_r[s], lane)) return true;
     }
   }
@@ -826,6 +922,7 @@ struct WideWave {
   uint32_t cand[(MAX_SPH + 31) / 32];       // this wavefront's candidate spheres (map sweep)
   uint32_t pcand;                           // this wavefront's candidate primitives
   uint8_t owner[MAP_STAGE_W], off[MAX_SPH];  // wave_map_staged: slot owners, first slot per sphere
+  uint16_t list[MAP_LIST];                  // wave_map_staged: the occupied cells of one candidate's reach
 };
 static_assert(sizeof(WideWave::v) == MAP_STAGE_W * sizeof(uint64_t), "staging buffer = the body-frame rows");
 struct WideLds {
@@ -960,7 +1057,7 @@ __device__ __forceinline__ void collide_wide(const RobotDev* __restrict__ rb, co
     for (int wd = 0; wd < (MAX_SPH + 31) / 32; ++wd) any |= W.cand[wd];
     if (!hit && __builtin_amdgcn_readfirstlane((int)(any != 0)) &&
         !__builtin_amdgcn_readfirstlane(__hip_atomic_load(&L.coll[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))
-      hit = wave_map_staged(rb, sc, W.u.c.wc, W.cand, nsph, W.v.stage, W.owner, W.off, lane);
+      hit = wave_map_staged(rb, sc, W.u.c.wc, W.cand, nsph, W.v.stage, W.owner, W.off, lane, W.list);
     if (prof2 && threadIdx.x == 0) tp2 = wall_clock64();
     // self: this wavefront's 64-pair chunks of the sphere pairs, then of the (primitive, sphere) pairs
     if (self && !hit &&

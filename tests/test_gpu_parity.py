@@ -43,7 +43,8 @@ def scene_pair(name):
                               (0, 0), (0, 0))
             sc.env_x, sc.env_y = sc.bounds()
         else:
-            sc = {"c1": scenes.empty_room, "c2": scenes.box_room, "c4": scenes.narrow_passage}[name]()
+            sc = {"c1": scenes.empty_room, "c2": scenes.box_room, "c4": scenes.narrow_passage,
+                  "c5": scenes.clutter_cloud}[name]()
         _SCENES[name] = (sc, Scene.from_keys(sc.keys, sc.res), O.OracleScene(sc.keys, sc.res))
     return _SCENES[name]
 
@@ -114,7 +115,7 @@ def test_check_configs_parity(gp, orobot, name, flags):
     assert 0.05 < v.mean() < 0.99
 
 
-@pytest.mark.parametrize("name", ["c2", "room3"])
+@pytest.mark.parametrize("name", ["c2", "room3", "c5"])
 @pytest.mark.parametrize("tile", [-1, -2, -4, -8, 8])
 def test_job_tile_shapes_parity(gp, orobot, name, tile):
     """The helpers' job tiles (collide_wide: ct = -tile configurations spread over the workgroup's 8 wavefronts, the map
