@@ -398,6 +398,12 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "limiter": "latency (sequential iteration chain of one query)",
+                         # the latency bound beside the bandwidth one: one query's iterations are a dependent chain
+                         # (each reads the trees the last one wrote); per query, the time of one iteration and the
+                         # collision-checked configurations it yields
+                         "latency": {"us_per_iteration_per_query": (elapsed * 1e6 * a.queries_per_gpu * world / iters)
+                                     if iters else None,
+                                     "configs_per_iteration": checked / iters if iters else None},
                          "kernel": "smp::plan_kernel", "kernel_ms_rank0": plan_ms_rank0,
                          "avg_launch_ms": plan_ms_rank0 / max(totals["launches"], 1),
                          "launches_rank0": totals["launches"],

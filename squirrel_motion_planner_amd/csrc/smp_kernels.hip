@@ -1398,9 +1398,18 @@ __device__ void edge_costs(const Ctx& C, int E) {
   }
   __syncthreads();
   if (threadIdx.x < E * 3) {
+    // the ordered sum (compute_edge_cost_interpolation's loop order) with every norm loaded up front: the adds are
+    // the only dependent chain (np is uniform, so the early exit is a scalar branch)
     int e = threadIdx.x / 3, k = threadIdx.x - e * 3;
+    double v[MAX_PTS];
+#pragma unroll
+    for (int s = 0; s < MAX_PTS; ++s) v[s] = s < np ? g_L.u.seg[e][s][k] : 0.0;
     double acc = 0.0;
-    for (int s = 0; s < np; ++s) acc += g_L.u.seg[e][s][k];
+#pragma unroll
+    for (int s = 0; s < MAX_PTS; ++s) {
+      if (s >= np) break;
+      acc += v[s];
+    }
     g_L.eg_acc[e][k] = acc;
     g_L.eg_cost[e][k] = g_L.eg_base[e][k] + acc;
   }

@@ -16,3 +16,4 @@ run c5 600 python bench.py --workload c5 --steps 1 --warmup 1 > $OUT/c5_q8.json 
 run c3 400 python bench.py --workload c3 --steps 1 --warmup 1 > $OUT/c3_q8.json 2> $OUT/c3_q8.err
 run ik 300 python tools/ik_report.py $OUT/ik_report.json > $OUT/ik.log 2>&1
 for v in 6 20; do run ttff$v 200 env SMP_PRE_HELPERS=$v python -u tools/ttff_seeds.py 3 $OUT/ttff_pre$v.json > $OUT/ttff_pre$v.txt 2>&1; done
+run trace 120 env SMP_TRACE_W0=16 SMP_TRACE_NW=4 SMP_LIB=squirrel_motion_planner_amd/lib/libsmp_gpu_trace.so python -u tools/trace_probe.py > $OUT/trace_r04.txt 2>&1
