@@ -280,6 +280,9 @@ __device__ __forceinline__ int sphere_bricks(const SceneDev& sc, const double* c
 constexpr int MAP_STAGE_W = 96;  // brick words staged per configuration (its dead body-frame rows, TileLds::fr)
 
 constexpr int MAP_LIST = 256;  // occupied cells of one sphere's reach listed at once (sweep_occupied)
+// reaches of at most this many cells are swept cell by cell (a 5 cm scene's spheres reach <= 216 cells: four passes
+// cost less than listing; a 2 cm scene's reach up to 1728)
+constexpr int MAP_LIST_MIN = 4 * 64;
 
 // Exact map test of a sphere (centre cc, radius r, reach lo..hi, its brick box b0 / nbx of nbs <= 64 bricks, lane b
 // holding brick b's occupancy word) over the occupied cells of its reach only: each word masked to the reach, bricks
@@ -426,7 +429,7 @@ __device__ __forceinline__ bool wave_map_staged(const RobotDev* __restrict__ rb,
       const int nbs = sphere_bricks(sc, cc, r, lo, hi, b0, nbx);
       const int ni = hi[0] - lo[0] + 1, nj = hi[1] - lo[1] + 1, nk = hi[2] - lo[2] + 1;
       const int nv = ni * nj * nk;
-      if (list) {
+      if (list && nv > MAP_LIST_MIN) {
         const int h = sweep_occupied(sc, cc, r, lo, hi, b0, nbx, nbs, lane < nbs ? buf[o + lane] : 0ull, list, lane);
         if (h == 1) return true;
         if (h == 0) continue;
@@ -464,7 +467,7 @@ __device__ __forceinline__ bool wave_map_staged(const RobotDev* __restrict__ rb,
       if (list) {  // its brick words one per lane (one round trip), then the occupied cells only
         int lo[3], hi[3], b0[3], nbx[3];
         const int nbs = sphere_bricks(sc, cc, rb->sph_r[s], lo, hi, b0, nbx);
-        if (nbs <= 64) {
+        if (nbs <= 64 && (hi[0] - lo[0] + 1) * (hi[1] - lo[1] + 1) * (hi[2] - lo[2] + 1) > MAP_LIST_MIN) {
           uint64_t w = 0;
           if (lane < nbs) {
             const int bi = lane % nbx[0], t = lane / nbx[0];

@@ -1398,18 +1398,9 @@ __device__ void edge_costs(const Ctx& C, int E) {
   }
   __syncthreads();
   if (threadIdx.x < E * 3) {
-    // the ordered sum (compute_edge_cost_interpolation's loop order) with every norm loaded up front: the adds are
-    // the only dependent chain (np is uniform, so the early exit is a scalar branch)
     int e = threadIdx.x / 3, k = threadIdx.x - e * 3;
-    double v[MAX_PTS];
-#pragma unroll
-    for (int s = 0; s < MAX_PTS; ++s) v[s] = s < np ? g_L.u.seg[e][s][k] : 0.0;
     double acc = 0.0;
-#pragma unroll
-    for (int s = 0; s < MAX_PTS; ++s) {
-      if (s >= np) break;
-      acc += v[s];
-    }
+    for (int s = 0; s < np; ++s) acc += g_L.u.seg[e][s][k];
     g_L.eg_acc[e][k] = acc;
     g_L.eg_cost[e][k] = g_L.eg_base[e][k] + acc;
   }
@@ -2029,29 +2020,40 @@ __device__ void near_set_dist(const Ctx& C, int t, const double* q, int excl) {
 #ifndef SMP_HELPER_SLEEP
 #define SMP_HELPER_SLEEP 2  // s_sleep units (64 clocks) between an idle helper's polls of its job board
 #endif
-// Helper workgroup w (1 .. W-1): wave 0 polls the first 64 payload granules of its query's board; a new job is
-// taken once every granule it needs carries the header's job number (jobs of one or two edges arrive within the
-// poll itself; longer payloads take one more read).  Then tiles w - 1, w - 1 + W, ... of the job, each result
-// stored as one granule.  Leaves on the stop flag, or after two idle seconds should the leader never start.
+#ifndef SMP_POLL_N
+#define SMP_POLL_N 128  // payload granules read by an idle helper's poll (64 per wave-0 load instruction)
+#endif
+// Helper workgroup w (1 .. W-1): wave 0 polls the first SMP_POLL_N payload granules of its query's board (two per
+// lane: a header and three edges, so the pre-solution scouts' expand + connect jobs arrive within the poll); a new job
+// is taken once every granule it needs carries the header's job number (longer payloads take one more read).  Then
+// tiles w - 1, w - 1 + W, ... of the job, each result stored as one granule.  Leaves on the stop flag, or after two
+// idle seconds should the leader never start.
 __device__ __forceinline__ void helper_main(const Ctx& C, int hidx, JobLds& J) {
   JobBoard* jb = C.Q.jb;
   const int w = 1 + hidx, W = C.Q.nworkers;
   int last = 0;
   unsigned long long t_last = wall_clock64();
+  constexpr int PU = SMP_POLL_N / 64;
+  static_assert(PU >= 1 && PU * 64 <= JOB_WORDS, "poll width");
   for (int k = 0;; k ^= 1) {
     // 0 = nothing new, > 0 = job number complete in J.words, -1 = leave, -2 = payload longer than the poll
     if (threadIdx.x < 64) {
-      const unsigned long long v = ld_agent(&jb->pay[threadIdx.x]);
-      const unsigned tag = (unsigned)(v >> 32);
-      const unsigned tag0 = __builtin_amdgcn_readfirstlane(tag);
-      const unsigned hdr = __builtin_amdgcn_readfirstlane((unsigned)v);
+      unsigned long long v[PU];
+#pragma unroll
+      for (int u = 0; u < PU; ++u) v[u] = ld_agent(&jb->pay[u * 64 + threadIdx.x]);
+      const unsigned tag0 = __builtin_amdgcn_readfirstlane((unsigned)(v[0] >> 32));
+      const unsigned hdr = __builtin_amdgcn_readfirstlane((unsigned)v[0]);
       int go = 0;
       if (tag0 != 0 && (int)tag0 != last) {
         const int nw = 1 + 32 * (int)(hdr & 255);
-        const bool mine = (int)threadIdx.x < nw;
-        if (!__ballot(mine && tag != tag0)) {
-          if (mine) J.words[threadIdx.x] = (unsigned)v;
-          go = nw <= 64 ? (int)tag0 : -2;
+        bool stale = false;
+#pragma unroll
+        for (int u = 0; u < PU; ++u) stale |= u * 64 + (int)threadIdx.x < nw && (unsigned)(v[u] >> 32) != tag0;
+        if (!__ballot(stale)) {
+#pragma unroll
+          for (int u = 0; u < PU; ++u)
+            if (u * 64 + (int)threadIdx.x < nw) J.words[u * 64 + threadIdx.x] = (unsigned)v[u];
+          go = nw <= PU * 64 ? (int)tag0 : -2;
         }
       }
       if (threadIdx.x == 0) {
@@ -2080,7 +2082,7 @@ __device__ __forceinline__ void helper_main(const Ctx& C, int hidx, JobLds& J) {
       // the rest of a long payload (one read; granules not yet current abandon the job to the next poll, which
       // sees it again since `last` is unchanged)
       int bad = 0;
-      for (int i = 64 + threadIdx.x; i < nw; i += BLOCK) {
+      for (int i = PU * 64 + threadIdx.x; i < nw; i += BLOCK) {
         const unsigned long long v = ld_agent(&jb->pay[i]);
         if ((int)(v >> 32) != seq) bad = 1;
         J.words[i] = (unsigned)v;

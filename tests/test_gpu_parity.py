@@ -138,7 +138,7 @@ def test_job_tile_shapes_parity(gp, orobot, name, tile):
         ov = orc.check_configs(q, *flags)
         mism = np.flatnonzero(v != ov)
         assert len(mism) == 0, "tile %d flags %s: mismatches at %s" % (tile, flags, mism[:10])
-        assert 0.05 < v.mean() < 0.99
+        assert 0.01 < v.mean() < 0.99  # both outcomes exercised (the 2 cm clutter leaves ~4 % of them free)
 
 
 def test_disabled_map_links(gp, orobot):

@@ -2,15 +2,12 @@
 # Every step has its own time limit; a fault, abort or time-out ends the session (no further GPU step).
 OUT=gpurun_out
 mkdir -p $OUT
+# heartbeat for long silent CPU legs (every step still has its own time limit)
+( while true; do date +%s >> $OUT/heartbeat.txt; sleep 30; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
 run() { local name=$1; shift; timeout -k 10 "$@"; local rc=$?; echo "$name rc=$rc" >> $OUT/status.txt
         case $rc in 124|134|137|139) exit $rc;; esac; }
-run tiles 400 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "job_tile_shapes or check_configs" > $OUT/t_tiles.log 2>&1
-run tests 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1
-for v in 0 1; do
-  run ea$v 120 env SMP_EARLY_ASK=$v python -u tools/perf_probe.py 4000 > $OUT/ea$v.txt 2>&1
-done
-run tprobe 200 env SMP_SETS=expand-edges,connect-edges,random SMP_TILES=8,-1 python -u tools/tile_probe.py > $OUT/tile_probe.txt 2>&1
-run tprobe5 300 env SMP_SCENE=c5 SMP_SETS=expand-edges,random SMP_TILES=8,-1 python -u tools/tile_probe.py > $OUT/tile_probe_c5.txt 2>&1
 run bench 500 python bench.py --steps 20 --warmup 2 > $OUT/bench_c2_20.json 2> $OUT/bench_c2_20.err
 run c5 600 python bench.py --workload c5 --steps 1 --warmup 1 > $OUT/c5_q8.json 2> $OUT/c5_q8.err
 run c3 400 python bench.py --workload c3 --steps 1 --warmup 1 > $OUT/c3_q8.json 2> $OUT/c3_q8.err

@@ -14,9 +14,12 @@ from squirrel_motion_planner_amd.planner import GpuPlanner, Scene  # noqa: E402
 
 # SMP_SCENE=c5: the 2 cm clutter scene (BASELINE configs[4]) instead of C2's box room
 sc = scenes.clutter_cloud() if os.environ.get("SMP_SCENE") == "c5" else scenes.box_room()
+print("scene %s: %d occupied keys" % (sc.name, len(sc.keys)), flush=True)
 gp = GpuPlanner(path_optimality_threshold=-math.inf)
 gp.set_scene(Scene.from_keys(sc.keys, sc.res))
+print("scene set", flush=True)
 r = gp.plan(GpuPlanner.make_query(sc.start, sc.goal, sc.env_x, sc.env_y, iterations=1500, seed=1))
+print("planned %d iterations" % r["iterations"], flush=True)
 qs = []
 for w in (0, 1):
     par, conf, _ = gp.tree(w)
