@@ -28,6 +28,7 @@ void launch_check(int ct, int grid, hipStream_t st, const RobotDev* rb, SceneDev
 __global__ void plan_kernel(const RobotDev* rb, SceneDev sc, const MapCfg* mc, QueryDev* qs, int nq, int scout_base,
                             int iters);
 __global__ void helper_kernel(const RobotDev* rb, SceneDev sc, const MapCfg* mc, QueryDev* qs, int nq);
+__global__ void helper2_kernel(const RobotDev* rb, SceneDev sc, const MapCfg* mc, QueryDev* qs, int nq);
 __global__ void path_kernel(QueryDev* qs, int* counts);
 __global__ void path_edges_kernel(const QueryDev* qs, int q, int ns, int ng, double* out);
 __global__ void boards_reset_kernel(const QueryDev* qs, int ns);
@@ -146,6 +147,7 @@ struct smp_planner {
   // last plan (query 0) bookkeeping for smp_get_tree
   int last_n[2] = {0, 0};
   int slots_cache = 0;  // resident_slots (occupancy queries) once per planner
+  int occ_twin = -1;    // helper2_kernel workgroups per CU (twin_occupancy)
   int slot_share = 1;   // planners planning on this planner's GPU at once (smp_plan_multi): its share of the slots
 };
 
@@ -163,6 +165,20 @@ static int resident_slots(smp_planner* p) {
   }
   p->slots_cache = p->num_cus * std::max(1, std::min(occ_plan, occ_help));
   return std::max(1, p->slots_cache / std::max(1, p->slot_share));
+}
+
+// Twin helpers (helper2_kernel) resident per CU beside nothing else: 2 when its registers and LDS allow.
+static int twin_occupancy(smp_planner* p) {
+  if (p->occ_twin < 0) {
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(&helper2_kernel), BLOCK, 0) !=
+        hipSuccess) {
+      (void)hipGetLastError();
+      occ = 1;
+    }
+    p->occ_twin = std::max(1, occ);
+  }
+  return p->occ_twin;
 }
 
 static int update_mapcfg(smp_planner* p) {
@@ -184,6 +200,9 @@ static int update_mapcfg(smp_planner* p) {
 }
 
 extern "C" int smp_debug_bounds(int* out);
+#ifdef SMP_RING_CHECK
+extern "C" void smp_ringchk_dump();
+#endif
 
 extern "C" {
 
@@ -386,7 +405,7 @@ int smp_planner_create(int device, const smp_robot* robot, const smp_params* par
     size_t need = 0;
     hipFuncAttributes fa;
     const void* ks[] = {reinterpret_cast<const void*>(&plan_kernel), reinterpret_cast<const void*>(&helper_kernel),
-                        reinterpret_cast<const void*>(&path_kernel)};
+                        reinterpret_cast<const void*>(&helper2_kernel), reinterpret_cast<const void*>(&path_kernel)};
     for (const void* k : ks)
       if (hipFuncGetAttributes(&fa, k) == hipSuccess) need = std::max(need, (size_t)fa.localSizeBytes);
     need = std::max(need, check_kernels_private_bytes());
@@ -1067,12 +1086,19 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
   // M configs/s; C5, 8 queries: 0.49 / 0.61 / 0.62 M)
   int rb_div = 4;
   if (const char* e = std::getenv("SMP_REBALANCE_DIV")) rb_div = std::max(1, std::atoi(e));
+  // twin helpers (helper2_kernel, two workgroups per CU; DESIGN.md "Twin helpers") when queries share the CUs:
+  // SMP_TWIN=0 / 1 forces them off / on
+  int twin_req = -1;
+  if (const char* e = std::getenv("SMP_TWIN")) twin_req = std::atoi(e) != 0 ? 1 : 0;
+  const int occ2 = twin_occupancy(p);
+  bool twin = false;
   int nh = 0, ns = 0;
   auto provision = [&](const std::vector<int>& act) {
     const int na = std::max(1, (int)act.size());
     const int cpq = std::max(1, slots / na);
     nh = nh_req;
     ns = 0;
+    twin = occ2 >= 2 && (twin_req == 1 || (twin_req < 0 && nh_req == 0 && cpq < 64));
     if (nh == 0) {
       if (want_scout) ns = cpq >= 64 ? 4 : cpq >= 18 ? 2 : cpq >= 6 ? 1 : 0;
       if (want_scout && p->params.scout > 1) ns = std::min(p->params.scout, MAX_SCOUTS);
@@ -1083,12 +1109,15 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
     if (want_scout && p->params.scout > 1) ns = std::min(p->params.scout, MAX_SCOUTS);  // explicit count
     if (nh < 0) nh = 0;
     if (nh < 4) ns = 0;
+    // twin helpers: occ2 per CU on the CUs the leaders and scouts leave (each of those fills a CU)
+    const int tcap = std::max(0, occ2 * (slots - na * (1 + ns)) / na);
+    if (twin && nh_req == 0) nh = want_scout ? std::min(cap_s, tcap) : std::min(63, tcap);
     // an explicit request larger than what can be resident is clamped to the automatic count: a helper that never
     // starts would leave its tiles to the leader's 8 us timeout on every job (helper sweeps: 250 helpers beside four
     // scouts no longer all start on 256 CUs and stall)
-    if (1 + ns + nh > cpq) {
-      nh = std::max(0, want_scout ? std::min(cap_s, cpq - 1 - ns) : std::min(63, cpq - 1));
-      if (nh < 4) { ns = 0; nh = std::max(0, std::min(nh, cpq - 1)); }
+    if (twin ? nh > tcap : 1 + ns + nh > cpq) {
+      nh = std::max(0, want_scout ? std::min(cap_s, twin ? tcap : cpq - 1 - ns) : std::min(63, twin ? tcap : cpq - 1));
+      if (nh < 4) { ns = 0; nh = std::max(0, std::min(nh, cpq - 1)); twin = false; }
     }
     // after the first solution scouts 0 and 1 check choose-parent / rewire candidate batches (many tiles); scouts 2
     // and 3 only work before it, one edge per job (3 tiles); the leader's own jobs (edges no record had) are rare
@@ -1223,8 +1252,12 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
     HIPCHK(hipEventRecord(p->ev1, p->stream));
     if (nh > 0) {  // the helpers on their own (high-priority, separate hardware queue) stream, after the board reset
       HIPCHK(hipStreamWaitEvent(p->hstream, p->ev_board, 0));
-      hipLaunchKernelGGL(helper_kernel, dim3(na * nh), dim3(BLOCK), 0, p->hstream, p->d_rb, p->sc, p->d_mc,
-                         p->d_qdev.p, na);
+      if (twin)
+        hipLaunchKernelGGL(helper2_kernel, dim3(na * nh), dim3(BLOCK), 0, p->hstream, p->d_rb, p->sc, p->d_mc,
+                           p->d_qdev.p, na);
+      else
+        hipLaunchKernelGGL(helper_kernel, dim3(na * nh), dim3(BLOCK), 0, p->hstream, p->d_rb, p->sc, p->d_mc,
+                           p->d_qdev.p, na);
       HIPCHK(hipGetLastError());
     }
     if (launches == 0) hstamp("kernels launched");
@@ -1310,6 +1343,9 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
     if (chunk < 4096) chunk *= 2;
   }
   hstamp("launch loop done");
+#ifdef SMP_RING_CHECK
+  smp_ringchk_dump();
+#endif
   // path extraction reads every query's record: the full array again
   HIPCHK(hipMemcpyAsync(p->d_qdev.p, qdev.data(), nq * sizeof(QueryDev), hipMemcpyHostToDevice, p->stream));
   nh = nh_first;

@@ -365,9 +365,12 @@ __device__ __forceinline__ int sweep_occupied(const SceneDev& sc, const double* 
 // wave_sphere_map).  A candidate that does not fit (more than 64 bricks, or the buffer full) is swept by
 // wave_sphere_map itself.  The outcome (any candidate touching an occupied cell) is the same as sweeping them one
 // after the other; wave_sphere_map pays one load round trip per candidate.
+template <int CAP = MAP_STAGE_W, typename OffT = uint8_t>
 __device__ __forceinline__ bool wave_map_staged(const RobotDev* __restrict__ rb, const SceneDev& sc, const double (*wc)[3],
                                                 const uint32_t* cand, int nsph, uint64_t* buf, uint8_t* owner,
-                                                uint8_t* off, int lane, uint16_t* list = nullptr) {
+                                                OffT* off, int lane, uint16_t* list = nullptr) {
+  constexpr OffT NONE = (OffT)~(OffT)0;
+  static_assert(CAP < (int)NONE, "slot offsets");
   // slots: sphere s = g * 64 + lane of group g.  Staged are the candidates (of at most 64 bricks) whose inclusive
   // prefix of brick counts still ends within the buffer: a prefix of them in sphere order, so the words [0, base)
   // all have an owner; off[s] = first slot of a staged candidate, else 255
@@ -387,9 +390,9 @@ __device__ __forceinline__ bool wave_map_staged(const RobotDev* __restrict__ rb,
       const int v = __shfl_up(inc, d);
       if (lane >= d) inc += v;
     }
-    const bool staged = nb > 0 && base + inc <= MAP_STAGE_W;
+    const bool staged = nb > 0 && base + inc <= CAP;
     const int start = base + inc - nb;
-    if (s < nsph) off[s] = staged ? (uint8_t)start : (uint8_t)255;
+    if (s < nsph) off[s] = staged ? (OffT)start : NONE;
     if (staged)
       for (int b = 0; b < nb; ++b) owner[start + b] = (uint8_t)s;
     spill[g] = __ballot(is_c && !staged);
@@ -398,9 +401,11 @@ __device__ __forceinline__ bool wave_map_staged(const RobotDev* __restrict__ rb,
   }
   wave_sync();
   // one round: every staged word loaded (two slots per lane), then stored
-  uint64_t v[2] = {0, 0};
+  constexpr int SU = (CAP + 63) / 64;
+  uint64_t v[SU];
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
+  for (int u = 0; u < SU; ++u) {
+    v[u] = 0;
     const int w = u * 64 + lane;
     if (w < base) {
       const int s = owner[w];
@@ -412,7 +417,7 @@ __device__ __forceinline__ bool wave_map_staged(const RobotDev* __restrict__ rb,
     }
   }
 #pragma unroll
-  for (int u = 0; u < 2; ++u)
+  for (int u = 0; u < SU; ++u)
     if (u * 64 + lane < base) buf[u * 64 + lane] = v[u];
   wave_sync();
   // sweeps of the staged candidates in sphere order (scalar loop over the candidate mask)
@@ -422,7 +427,7 @@ __device__ __forceinline__ bool wave_map_staged(const RobotDev* __restrict__ rb,
       const int s = wd * 32 + __builtin_ctz(m);
       m &= m - 1;
       const int o = off[s];
-      if (o == 255) continue;
+      if (o == (int)NONE) continue;
       const double cc[3] = {wc[s][0], wc[s][1], wc[s][2]};
       const double r = rb->sph_r[s], r2 = r * r;
       int lo[3], hi[3], b0[3], nbx[3];
@@ -909,6 +914,12 @@ __device__ __forceinline__ void collide_tile(const RobotDev* __restrict__ rb, co
 }
 
 // ------------------------------------------------------------------------------------------ job tiles (collide_wide)
+// brick words a wavefront of collide_wide stages for its candidate spheres in one round trip (a 2 cm sphere needs up to
+// 64: collide_tile's 96 held one of them)
+#ifndef SMP_WIDE_STAGE_W
+#define SMP_WIDE_STAGE_W 320
+#endif
+constexpr int WIDE_STAGE_W = SMP_WIDE_STAGE_W;
 // LDS of one wavefront of collide_wide: the configuration's kinematics, centres and staging, private to the wavefront.
 struct WideWave {
   union {
@@ -918,16 +929,16 @@ struct WideWave {
       double pw[MAX_PRIM][5];               // C: primitive centres and x axes
     } c;
   } u;
-  union {
+  struct {
     double fr[MAX_BODY][12];                // B -> centres: body frames (R row-major, p)
-    uint64_t stage[MAP_STAGE_W];            // map sweeps: the candidates' brick words (wave_map_staged)
   } v;
   uint32_t cand[(MAX_SPH + 31) / 32];       // this wavefront's candidate spheres (map sweep)
   uint32_t pcand;                           // this wavefront's candidate primitives
-  uint8_t owner[MAP_STAGE_W], off[MAX_SPH];  // wave_map_staged: slot owners, first slot per sphere
-  uint16_t list[MAP_LIST];                  // wave_map_staged: the occupied cells of one candidate's reach
+  uint64_t stage[WIDE_STAGE_W];             // map sweeps: the candidates' brick words (wave_map_staged)
+  uint16_t off[MAX_SPH];                    // wave_map_staged: first slot per sphere
+  uint8_t owner[WIDE_STAGE_W];              // wave_map_staged: slot owners
+  uint16_t list[MAP_LIST];                  // sweep_occupied: the occupied cells of one candidate's reach
 };
-static_assert(sizeof(WideWave::v) == MAP_STAGE_W * sizeof(uint64_t), "staging buffer = the body-frame rows");
 struct WideLds {
   WideWave w[NWAVE];
   int coll[NWAVE];                          // configuration c: 1 = in collision
@@ -1003,13 +1014,16 @@ __device__ __forceinline__ void collide_wide(const RobotDev* __restrict__ rb, co
     // this wavefront's share, all issued together
     const int nsph = rb->n_sph, npr = rb->n_prim;
     const bool do_map = map && mc->has_map;
-    long long cell[2];
-    bool pc[2];
+    // (the cells first, then every load -- box-gap bytes of the spheres, slab words of the primitives -- issued before
+    // any is used: in a 2 cm scene the 25 MB field lives in the Infinity Cache, and dependent rounds cost ~1 us each)
+    long long cell[2], pcell[2];
+    const uint16_t* pslab[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int it = u * 64 + lane;
       cell[u] = -1;
-      pc[u] = false;
+      pcell[u] = -1;
+      pslab[u] = nullptr;
       if (it < nsph) {
         const double* B = W.v.fr[rb->sph_body[it]];
         const double* p = &rb->sph_cb[it * 3];
@@ -1025,22 +1039,26 @@ __device__ __forceinline__ void collide_wide(const RobotDev* __restrict__ rb, co
         double pw[5];
         prim_world(rb, p, W.v.fr[rb->prim_body[p]], pw);
         for (int i = 0; i < 5; ++i) W.u.c.pw[p][i] = pw[i];
-        pc[u] = do_map && mc->p_map_on[p] && p % G == g && prim_candidate(sc, sc_in.slab[p], mc->pT[p], pw);
+        if (do_map && mc->p_map_on[p] && p % G == g) {  // prim_candidate: its centre's column, else free
+          const double fx = floor((pw[0] - sc.ox) * sc.inv_res), fy = floor((pw[1] - sc.oy) * sc.inv_res);
+          if (fx >= 0 && fx < sc.nx && fy >= 0 && fy < sc.ny) {
+            pcell[u] = (long long)(int)fy * sc.nx + (int)fx;
+            pslab[u] = sc_in.slab[p];
+          }
+        }
       }
     }
-    uint32_t dv[2];
-    if (sc.d2b) {
+    uint32_t dv[2], sv[2];
 #pragma unroll
-      for (int u = 0; u < 2; ++u) dv[u] = cell[u] >= 0 ? (uint32_t)sc.d2b[cell[u]] : 0xffffffffu;
-    } else {
-#pragma unroll
-      for (int u = 0; u < 2; ++u) dv[u] = cell[u] >= 0 ? (uint32_t)sc.d2[cell[u]] : 0xffffffffu;
+    for (int u = 0; u < 2; ++u) {
+      dv[u] = cell[u] < 0 ? 0xffffffffu : (sc.d2b ? (uint32_t)sc.d2b[cell[u]] : (uint32_t)sc.d2[cell[u]]);
+      sv[u] = pcell[u] < 0 ? 0xffffffffu : (uint32_t)pslab[u][pcell[u]];
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int it = u * 64 + lane;
       if (cell[u] >= 0 && dv[u] <= mc->T[it]) atomicOr(&W.cand[it >> 5], 1u << (it & 31));
-      if (pc[u]) atomicOr(&W.pcand, 1u << (it - nsph));
+      if (pcell[u] >= 0 && sv[u] <= mc->pT[it - nsph]) atomicOr(&W.pcand, 1u << (it - nsph));
     }
     wave_sync();
     if (prof && threadIdx.x == 0) tc = wall_clock64();
@@ -1060,7 +1078,8 @@ __device__ __forceinline__ void collide_wide(const RobotDev* __restrict__ rb, co
     for (int wd = 0; wd < (MAX_SPH + 31) / 32; ++wd) any |= W.cand[wd];
     if (!hit && __builtin_amdgcn_readfirstlane((int)(any != 0)) &&
         !__builtin_amdgcn_readfirstlane(__hip_atomic_load(&L.coll[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))
-      hit = wave_map_staged(rb, sc, W.u.c.wc, W.cand, nsph, W.v.stage, W.owner, W.off, lane, W.list);
+      hit = wave_map_staged<WIDE_STAGE_W, uint16_t>(rb, sc, W.u.c.wc, W.cand, nsph, W.stage, W.owner, W.off, lane,
+                                                    W.list);
     if (prof2 && threadIdx.x == 0) tp2 = wall_clock64();
     // self: this wavefront's 64-pair chunks of the sphere pairs, then of the (primitive, sphere) pairs
     if (self && !hit &&

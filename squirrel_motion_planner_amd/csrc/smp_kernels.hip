@@ -274,8 +274,15 @@ __device__ __forceinline__ unsigned long long merge_key(const MergeLds& M, int s
 }
 // LDS of job mode (leader and helper kernel): the published job + one job tile.
 struct JobLds {
-  ScanLds scan;                            // helper: its slice of a scan job
-  WideLds T;                               // one job tile (collide_wide)
+#ifdef SMP_NO_SCAN_UNION
+  ScanLds scan;
+  WideLds T;
+#else
+  union {
+    ScanLds scan;                          // helper: its slice of a scan job
+    WideLds T;                             // one job tile (collide_wide)
+  };
+#endif
   double tq[TILE_CT_MAX][NJ];
   double start[MAXE][NJ], step[MAXE][NJ];  // the job's edges (needed edges of the batch, compacted)
   unsigned words[JOB_WORDS];               // helper: the payload words as received
@@ -875,7 +882,7 @@ __device__ __noinline__ void near_set_stream(const Ctx& C, int t, const double* 
 // ------------------------------------------------------------------------------- slices of distributed scans
 // Nearest over the nodes [i0, i1): the first strict minimum as nearest_scan, reduced to (distance key, id) in X.wk[0],
 // X.wi[0] (key of 10000.0 and id INT_MAX if no node is below 10000).  All threads.
-__device__ void slice_nn(gcdptr tq, int cap, int i0, int i1, const double* q, ScanLds& X) {
+__device__ __forceinline__ void slice_nn_body(gcdptr tq, int cap, int i0, int i1, const double* q, ScanLds& X) {
   double qq[NJ];
   for (int j = 0; j < NJ; ++j) qq[j] = q[j];
   double best = 10000.0, best_s = 1e300;
@@ -924,12 +931,15 @@ __device__ void slice_nn(gcdptr tq, int cap, int i0, int i1, const double* q, Sc
   }
   __syncthreads();
 }
+__device__ void slice_nn(gcdptr tq, int cap, int i0, int i1, const double* q, ScanLds& X) {
+  slice_nn_body(tq, cap, i0, i1, q, X);
+}
 
 // Near set over the nodes [i0, i1) (find_near_vertices_interpolation's radius test, excluding `excl`): count X.cnt,
 // its SCAN_K lowest (cost, id) entries ascending in X.lk / X.li and SCAN_K highest descending in X.hk / X.hi (X.take
 // each).  near_set_stream's per-wave lists and rank merge over a range.  All threads.
-__device__ __noinline__ void slice_near(gcdptr tq, gcdptr tc, int cap, int i0, int i1, const double* q, int excl,
-                                        double r, ScanLds& X) {
+__device__ __forceinline__ void slice_near_body(gcdptr tq, gcdptr tc, int cap, int i0, int i1, const double* q,
+                                                int excl, double r, ScanLds& X) {
   constexpr int K = SCAN_K, NW = BLOCK / 64, NB = 4;
   const double r2 = r * r, r2lo = r2 * (1.0 - 1e-12), r2hi = r2 * (1.0 + 1e-12);
   const int lane = lane_id(), wave = wave_id();
@@ -1026,6 +1036,10 @@ __device__ __noinline__ void slice_near(gcdptr tq, gcdptr tc, int cap, int i0, i
   }
   if (threadIdx.x == 0) { X.cnt = tot; X.take = take; }
   __syncthreads();
+}
+__device__ __noinline__ void slice_near(gcdptr tq, gcdptr tc, int cap, int i0, int i1, const double* q, int excl,
+                                        double r, ScanLds& X) {
+  slice_near_body(tq, tc, cap, i0, i1, q, excl, r, X);
 }
 
 // find_near_vertices_interpolation (birrt_star.cpp:4272-4324): count k, the first K and the last K entries of
@@ -1573,7 +1587,11 @@ __device__ __forceinline__ void edge_validity_job(const Ctx& C, int E, int pslot
       J.ntiles = (ne * np1 + J.ct - 1) / J.ct;
       J.self = g_L.S.self; J.map = g_L.S.map;
       J.seq = ++g_L.job_seq;
+#ifdef SMP_NO_SKIP
+      J.skip = 0;
+#else
       J.skip = J.ntiles > W;  // more tiles than workers: later rounds skip what earlier ones decided
+#endif
       J.sfv = J.skip && sfv;
     }
   }
@@ -1755,18 +1773,26 @@ __device__ void scan_publish(const Ctx& C, int seq, int near, int t, const doubl
 }
 
 // Participant w's slice of a scan, its result as granules of sres[w] (helper) or into the merge area (workgroup).
+// (INL: the slice functions inlined, for the twin helpers)
+template <bool INL = false>
 __device__ void scan_slice(const Ctx& C, int near, int t, const double* q, int i0, int n, int excl, double r, int P, int w,
                            ScanLds& X) {
   const gcdptr tq = uni_gptr(C.Q.tr[t].q), tc = uni_gptr(C.Q.tr[t].cost);
   const int cap = uni(__hip_atomic_load(&C.Q.st->cap, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   int lo, hi;
   scan_range(i0, n, P, w, &lo, &hi);
-  if (near) slice_near(tq, tc, cap, lo, hi, q, excl, r, X);
-  else slice_nn(tq, cap, lo, hi, q, X);
+  if constexpr (INL) {
+    if (near) slice_near_body(tq, tc, cap, lo, hi, q, excl, r, X);
+    else slice_nn_body(tq, cap, lo, hi, q, X);
+  } else {
+    if (near) slice_near(tq, tc, cap, lo, hi, q, excl, r, X);
+    else slice_nn(tq, cap, lo, hi, q, X);
+  }
 }
 
 // Helper side of a scan job already in J.words (seq): its slice, then the result granules.
-__device__ __noinline__ void scan_helper(const Ctx& C, JobLds& J, int w, int seq) {
+template <bool INL>
+__device__ __forceinline__ void scan_helper_body(const Ctx& C, JobLds& J, int w, int seq) {
   const unsigned hdr = J.words[0];
   const int near = (hdr >> 19) & 1, t = (hdr >> 20) & 1;
   double q[NJ];
@@ -1782,7 +1808,7 @@ __device__ __noinline__ void scan_helper(const Ctx& C, JobLds& J, int w, int seq
   }
   __syncthreads();
   ScanLds& X = J.scan;
-  scan_slice(C, near, t, q, i0, n, excl, r, P, w, X);
+  scan_slice<INL>(C, near, t, q, i0, n, excl, r, P, w, X);
   unsigned long long* out = C.Q.jb->sres[w];
   if (!near) {
     if (threadIdx.x == 0) {
@@ -1807,6 +1833,7 @@ __device__ __noinline__ void scan_helper(const Ctx& C, JobLds& J, int w, int seq
   }
   __syncthreads();
 }
+__device__ __noinline__ void scan_helper(const Ctx& C, JobLds& J, int w, int seq) { scan_helper_body<false>(C, J, w, seq); }
 
 // Slot w of the merge area from a slice result in X (all threads).
 __device__ __forceinline__ void merge_put(MergeLds& M, const ScanLds& X, int near, int w) {
@@ -2028,6 +2055,8 @@ __device__ void near_set_dist(const Ctx& C, int t, const double* q, int excl) {
 // is taken once every granule it needs carries the header's job number (longer payloads take one more read).  Then
 // tiles w - 1, w - 1 + W, ... of the job, each result stored as one granule.  Leaves on the stop flag, or after two
 // idle seconds should the leader never start.
+// INL: the scan slice inlined (the twin helpers' kernel: a call would be compiled for the full register file).
+template <bool INL>
 __device__ __forceinline__ void helper_main(const Ctx& C, int hidx, JobLds& J) {
   JobBoard* jb = C.Q.jb;
   const int w = 1 + hidx, W = C.Q.nworkers;
@@ -2072,7 +2101,8 @@ __device__ __forceinline__ void helper_main(const Ctx& C, int hidx, JobLds& J) {
     const int seq = uni(J.seq);
     const unsigned hdr = J.words[0];
     if (uni((int)((hdr >> 18) & 1u))) {  // scan job: this helper's slice (the payload fits the first poll)
-      scan_helper(C, J, w, seq);
+      if constexpr (INL) scan_helper_body<true>(C, J, w, seq);
+      else scan_helper(C, J, w, seq);
       last = seq;
       t_last = wall_clock64();
       continue;
@@ -2760,6 +2790,23 @@ __device__ void insert_via(const Ctx& C, int t, const ViaNode* rec = nullptr, in
   TR();
 }
 
+#ifdef SMP_RING_CHECK
+__device__ unsigned long long g_ringchk[24];
+__device__ unsigned long long g_ringdbg[SMP_RING][8];  // sampler: parameters of the slot's sample
+extern "C" void smp_ringchk_dump() {
+  unsigned long long v[24];
+  if (hipMemcpyFromSymbol(v, HIP_SYMBOL(g_ringchk), sizeof(v)) == hipSuccess) {
+    std::fprintf(stderr, "[smp] ring check: uniform(it) %llu, it-1 %llu, it+1 %llu, other %llu\n", v[0], v[1], v[2], v[3]);
+    double d[24];
+    __builtin_memcpy(d, v, sizeof(d));
+    std::fprintf(stderr, "[smp] first mismatch it %llu: leader ver %llu have_sol %llu cbest %.17g %.17g %.17g\n", v[4], v[5],
+                 v[6], d[7], d[8], d[9]);
+    std::fprintf(stderr, "[smp]   sampler slot: it %llu ver %llu have_sol %llu cbest %.17g %.17g %.17g informed %llu\n",
+                 v[10], v[11], v[12], d[13], d[14], d[15], v[16]);
+    std::fprintf(stderr, "[smp]   ring xr0 %.17g leader xr0 %.17g ring xr1 %.17g leader xr1 %.17g\n", d[17], d[18], d[19], d[20]);
+  }
+}
+#endif
 // --------------------------------------------------------------------------------------- sampling
 // getRandomConf (control_laws.cpp:1120-1188) draw `inner` of outer attempt `outer` in iteration `it`; the
 // caller keeps the first draw with EE z >= 0.
@@ -2962,8 +3009,11 @@ __device__ void sample_read(const Ctx& C) {
     // the slot's 16 granules in one round; current iff every tag is this iteration's with the current version
     const unsigned want = ring_tag(it, (unsigned)__builtin_amdgcn_readfirstlane(g_L.smp_ver));
     unsigned long long v = 0;
-    if (threadIdx.x < 2 * NJ) v = ld_agent(&jb->ring[it % SMP_RING].g[threadIdx.x]);
-    const bool ok = threadIdx.x >= 2 * NJ || (unsigned)(v >> 32) == want;
+    if (threadIdx.x < RING_G) v = ld_agent(&jb->ring[it % SMP_RING].g[threadIdx.x]);
+    // current: every granule this iteration's at this version, and the parameters it was drawn with the leader's
+    const int pk = (int)threadIdx.x - 2 * NJ;
+    const bool ok = threadIdx.x >= RING_G ||
+                    ((unsigned)(v >> 32) == want && (pk < 0 || (unsigned)v == ring_param(pk, S.have_sol, S.cbest)));
     const unsigned hi = (unsigned)__shfl((int)(unsigned)v, (threadIdx.x | 1) & 63);
     if (threadIdx.x < 2 * NJ && !(threadIdx.x & 1))
       g_L.xr[threadIdx.x >> 1] = __longlong_as_double((long long)(((unsigned long long)hi << 32) | (unsigned)v));
@@ -3000,6 +3050,55 @@ __device__ void sample_read(const Ctx& C) {
     if (sample_conf(S, it, g_L.u.smp, g_L.xr) < 0 && threadIdx.x == 0) { S.status = -1; S.phase = 2; }
     __syncthreads();
   }
+#ifdef SMP_RING_CHECK  // debugging: a sample taken from the ring or a record, recomputed here and compared (prof[28..30])
+  else {
+    __shared__ double chk_xr[NJ];
+    __shared__ int chk_bad;
+    sample_conf(S, it, g_L.u.smp, chk_xr);
+    if (threadIdx.x == 0) {
+      int bad = 0;
+      for (int j = 0; j < NJ; ++j) bad |= __double_as_longlong(chk_xr[j]) != __double_as_longlong(g_L.xr[j]);
+      chk_bad = bad;
+      S.prof[30]++;
+      if (bad) { S.prof[28]++; if (!S.prof[29]) S.prof[29] = (unsigned long long)it + 1; }
+      if (bad && g_ringchk[21] == 0) {
+        g_ringchk[21] = 1;
+        g_ringchk[17] = (unsigned long long)__double_as_longlong(g_L.xr[0]);
+        g_ringchk[18] = (unsigned long long)__double_as_longlong(chk_xr[0]);
+        g_ringchk[19] = (unsigned long long)__double_as_longlong(g_L.xr[1]);
+        g_ringchk[20] = (unsigned long long)__double_as_longlong(chk_xr[1]);
+      }
+    }
+    __syncthreads();
+    if (uni(chk_bad)) {  // which sample the ring held: prof[20] the uniform one of this iteration, [21] iteration
+      // it - 1's, [22] it + 1's (current parameters), [23] none of them
+      int cls = 23;
+      for (int v = 0; v < 3 && cls == 23; ++v) {
+        if (v == 0) sample_uniform(S, it, g_L.u.smp, chk_xr);
+        else sample_conf(S, v == 1 ? it - 1 : it + 1, g_L.u.smp, chk_xr);
+        if (threadIdx.x == 0) {
+          int same = 1;
+          for (int j = 0; j < NJ; ++j) same &= __double_as_longlong(chk_xr[j]) == __double_as_longlong(g_L.xr[j]);
+          chk_bad = same;
+        }
+        __syncthreads();
+        if (uni(chk_bad)) cls = 20 + v;
+        __syncthreads();
+      }
+      if (threadIdx.x == 0) {
+        g_ringchk[cls - 20]++;
+        if (cls == 23 && g_ringchk[4] == 0) {
+          g_ringchk[4] = (unsigned long long)it;
+          g_ringchk[5] = g_L.smp_ver;
+          g_ringchk[6] = S.have_sol;
+          for (int k = 0; k < 3; ++k) g_ringchk[7 + k] = (unsigned long long)__double_as_longlong(S.cbest[k]);
+          for (int k = 0; k < 7; ++k) g_ringchk[10 + k] = ld_agent(&g_ringdbg[it % SMP_RING][k]);
+        }
+      }
+      __syncthreads();
+    }
+  }
+#endif
 }
 
 // --------------------------------------------------------------------------------------- tree updates
@@ -4788,7 +4887,7 @@ struct SamplerLds {
 // up to (published iteration) + SMP_RING - 1 only.  Leaves on the stop flag or after two idle seconds.
 // (not inlined into helper_kernel, like scan_helper: the tile helpers' loop is compiled without the sampler's and the
 // scan slices' registers live around it -- C2 73.1 -> 71.8 us per iteration, perf_probe.py with SMP_JOB_PROF, round 3)
-__device__ __noinline__ void sampler_main(const Ctx& C, SamplerLds& L) {
+__device__ __forceinline__ void sampler_body(const Ctx& C, SamplerLds& L) {
   JobBoard* jb = C.Q.jb;
   {
     const int* src = reinterpret_cast<const int*>(C.Q.st);
@@ -4826,9 +4925,23 @@ __device__ __noinline__ void sampler_main(const Ctx& C, SamplerLds& L) {
     }
     const long long it = L.next;
     const int st = sample_conf(L.S, (uint32_t)it, L.W, L.out);
-    if (st == 0 && threadIdx.x < 2 * NJ) {
-      const unsigned long long bits = (unsigned long long)__double_as_longlong(L.out[threadIdx.x >> 1]);
-      const unsigned w = (threadIdx.x & 1) ? (unsigned)(bits >> 32) : (unsigned)bits;
+#ifdef SMP_RING_CHECK
+    if (threadIdx.x == 0) {
+      unsigned long long* d = g_ringdbg[it % SMP_RING];
+      st_agent(&d[0], (unsigned long long)it); st_agent(&d[1], (unsigned long long)L.ver);
+      st_agent(&d[2], (unsigned long long)L.S.have_sol);
+      for (int k = 0; k < 3; ++k) st_agent(&d[3 + k], (unsigned long long)__double_as_longlong(L.S.cbest[k]));
+      st_agent(&d[6], (unsigned long long)L.S.informed);
+    }
+#endif
+    if (st == 0 && threadIdx.x < RING_G) {
+      unsigned w;
+      if (threadIdx.x < 2 * NJ) {
+        const unsigned long long bits = (unsigned long long)__double_as_longlong(L.out[threadIdx.x >> 1]);
+        w = (threadIdx.x & 1) ? (unsigned)(bits >> 32) : (unsigned)bits;
+      } else {
+        w = ring_param((int)threadIdx.x - 2 * NJ, L.S.have_sol, L.S.cbest);
+      }
       st_agent(&jb->ring[it % SMP_RING].g[threadIdx.x], granule((int)ring_tag(it, L.ver), w));
     }
     if (threadIdx.x == 0) L.next = it + 1;
@@ -4837,10 +4950,22 @@ __device__ __noinline__ void sampler_main(const Ctx& C, SamplerLds& L) {
   }
 }
 
-__global__ void __launch_bounds__(BLOCK) helper_kernel(const RobotDev* __restrict__ rb, SceneDev sc,
-                                                       const MapCfg* __restrict__ mc, QueryDev* qs, int nq) {
-  __shared__ JobLds J;
-  __shared__ SamplerLds SL;
+__device__ __noinline__ void sampler_main(const Ctx& C, SamplerLds& L) { sampler_body(C, L); }
+
+// The LDS of a helper workgroup: one role at a time.
+union HelperLds {
+  JobLds J;
+  SamplerLds S;
+};
+
+// OCC = 1: one helper workgroup per CU (the full register file: the lowest tile latency, for a query with helpers to
+// spare).  OCC = 2: twin helpers, two workgroups per CU (128 registers, LDS under half a CU's; every call inlined),
+// for many queries sharing the CUs: a tile is a chain of dependent loads, and the second workgroup's waves run in
+// the first's load shadows (DESIGN.md "Twin helpers").
+template <int OCC>
+__device__ __forceinline__ void helper_entry(const RobotDev* __restrict__ rb, SceneDev sc, const MapCfg* __restrict__ mc,
+                                             QueryDev* qs, int nq) {
+  __shared__ HelperLds H;
   // the block's context and role in LDS (see plan_kernel): -1 nothing to do, -2 run-ahead sampler, else tile helper h
   __shared__ Ctx g_ctx;
   __shared__ int g_role;
@@ -4872,10 +4997,63 @@ __global__ void __launch_bounds__(BLOCK) helper_kernel(const RobotDev* __restric
   const int role = uni(g_role);
   if (role == -1) return;
   if (role == -2) {
+    if constexpr (OCC == 2) sampler_body(g_ctx, H.S);
+    else sampler_main(g_ctx, H.S);
+    return;
+  }
+  helper_main<OCC == 2>(g_ctx, role, H.J);
+}
+
+#ifdef SMP_OLD_HELPER_KERNEL
+__global__ void __launch_bounds__(BLOCK) helper_kernel(const RobotDev* __restrict__ rb, SceneDev sc,
+                                                       const MapCfg* __restrict__ mc, QueryDev* qs, int nq) {
+  __shared__ JobLds J;
+  __shared__ SamplerLds SL;
+  __shared__ Ctx g_ctx;
+  __shared__ int g_role;
+  if (threadIdx.x == 0) {
+    Ctx c;
+    c.sc = sc;
+    c.Q = qs[blockIdx.x % nq];
+    const int hidx = (int)blockIdx.x / nq, nh = (int)gridDim.x / nq;
+    int role = hidx;
+    if (!c.Q.jb) {
+      role = -1;
+    } else if (c.Q.sampler && hidx == nh - 1) {
+      role = -2;
+    } else if (role >= c.Q.nworkers - 1) {
+      role -= c.Q.nworkers - 1;
+      int s = 0;
+      for (; s < c.Q.nscouts && role >= c.Q.sworkers_s[s] - 1; ++s) role -= c.Q.sworkers_s[s] - 1;
+      if (s >= c.Q.nscouts) {
+        role = -1;
+      } else {
+        c.Q.jb = c.Q.sjbs[s];
+        c.Q.nworkers = c.Q.sworkers_s[s];
+      }
+    }
+    g_ctx = c;
+    g_role = role;
+  }
+  stage_model(rb, mc, &g_rb, &g_mc);
+  const int role = uni(g_role);
+  if (role == -1) return;
+  if (role == -2) {
     sampler_main(g_ctx, SL);
     return;
   }
-  helper_main(g_ctx, role, J);
+  helper_main<false>(g_ctx, role, J);
+}
+#else
+__global__ void __launch_bounds__(BLOCK) helper_kernel(const RobotDev* __restrict__ rb, SceneDev sc,
+                                                       const MapCfg* __restrict__ mc, QueryDev* qs, int nq) {
+  helper_entry<1>(rb, sc, mc, qs, nq);
+}
+#endif
+// (launch bounds: BLOCK threads, 4 waves per SIMD = two workgroups per CU)
+__global__ void __launch_bounds__(BLOCK, 4) helper2_kernel(const RobotDev* __restrict__ rb, SceneDev sc,
+                                                           const MapCfg* __restrict__ mc, QueryDev* qs, int nq) {
+  helper_entry<2>(rb, sc, mc, qs, nq);
 }
 
 // Fresh job / scout boards for a launch (all zero: no granule carries a job number, no stop flag): block b clears

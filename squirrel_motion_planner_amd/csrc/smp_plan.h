@@ -106,6 +106,14 @@ constexpr int SCAN_W = 2 + 2 * 3 * MAX_NEAR;
 __host__ __device__ inline unsigned ring_tag(long long it, unsigned ver) {
   return ((unsigned)it & 0xffffffu) << 8 | (ver & 0xffu);
 }
+constexpr int RING_PARAMS = 5;               // ring slot: have_sol, cbest[1] (lo, hi), cbest[2] (lo, hi)
+constexpr int RING_G = 2 * NJ + RING_PARAMS;  // granules per ring slot
+// The parameter word k of a ring slot (sampler and leader).
+__device__ inline unsigned ring_param(int k, int have_sol, const double* cbest) {
+  if (k == 0) return (unsigned)have_sol;
+  const unsigned long long b = (unsigned long long)__double_as_longlong(cbest[1 + ((k - 1) >> 1)]);
+  return ((k - 1) & 1) ? (unsigned)(b >> 32) : (unsigned)b;
+}
 struct JobBoard {
   int stop;                    // 1 once the leader left the launch: helpers exit
   int pad0[7];
@@ -125,12 +133,14 @@ struct JobBoard {
   long long s_iter;
   unsigned long long s_cbest[3];  // fp64 bit patterns
   int pad6[22];
-  // sampler -> leader: the sample of iteration i in slot i % SMP_RING, tag = (i << 32) | version, stored after
-  // the drained configuration.
+  // sampler -> leader: the sample of iteration i in slot i % SMP_RING.
   // Each configuration value travels as two data-tagged granules (low, high 32 bits) whose tag is
-  // ring_tag(iteration, version), so one round of 16 loads both reads a slot and tells whether it is current.
+  // ring_tag(iteration, version), so one round of loads both reads a slot and tells whether it is current; then
+  // RING_PARAMS granules of the sampling parameters the sample was drawn with (have_sol, the halves of cbest[1] and
+  // cbest[2]: everything else it reads is a query constant), which the leader compares with its own -- a sample is
+  // taken only if drawn with exactly the leader's parameters, whatever the version bookkeeping did.
   struct {
-    unsigned long long g[2 * NJ];
+    unsigned long long g[RING_G];
   } ring[SMP_RING];
   unsigned long long sres[SCAN_P][SCAN_W];  // scan jobs: participant w's partial result (w >= 1)
 };

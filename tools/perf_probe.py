@@ -10,12 +10,19 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from squirrel_motion_planner_amd import scenes  # noqa: E402
 from squirrel_motion_planner_amd.planner import GpuPlanner, Scene  # noqa: E402
 
-sc = scenes.box_room()
-gp = GpuPlanner(path_optimality_threshold=-math.inf, helpers=int(os.environ.get("SMP_HELPERS", "0")))
+# SMP_SCENE=c5: the 2 cm clutter scene and one of C5's random queries (bench.py --workload c5, query SMP_C5Q)
+sc = scenes.clutter_cloud() if os.environ.get("SMP_SCENE") == "c5" else scenes.box_room()
+print("scene %s" % sc.name, flush=True)
+gp = GpuPlanner(path_optimality_threshold=-math.inf, helpers=int(os.environ.get("SMP_HELPERS", "0")),
+                scout=int(os.environ.get("SMP_SCOUT", "1")))
 gp.set_scene(Scene.from_keys(sc.keys, sc.res))
+start, goal = sc.start, sc.goal
+if os.environ.get("SMP_C5Q"):  # query k of the bench's random pairs (scenes.random_queries, seed 7)
+    k = int(os.environ["SMP_C5Q"])
+    start, goal = scenes.random_queries(sc, k + 1, seed=7, check=lambda q: bool(gp.check_configs([q])[0]))[k]
 for iters in [int(v) for v in (sys.argv[1:] or ["2000", "10000", "50000"])]:
     t = time.perf_counter()
-    r = gp.plan(GpuPlanner.make_query(sc.start, sc.goal, sc.env_x, sc.env_y, iterations=iters, seed=1))
+    r = gp.plan(GpuPlanner.make_query(start, goal, sc.env_x, sc.env_y, iterations=iters, seed=1))
     dt = time.perf_counter() - t
     _, pms, nl = gp.last_kernel_ms()
     print("iters %7d wall %.2fs kernel %.2fs launches %d  us/iter %.1f  checked %d (%.0f/s)  nodes %d/%d "
