@@ -1086,9 +1086,10 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
   // M configs/s; C5, 8 queries: 0.49 / 0.61 / 0.62 M)
   int rb_div = 4;
   if (const char* e = std::getenv("SMP_REBALANCE_DIV")) rb_div = std::max(1, std::atoi(e));
-  // twin helpers (helper2_kernel, two workgroups per CU; DESIGN.md "Twin helpers") when queries share the CUs:
-  // SMP_TWIN=0 / 1 forces them off / on
-  int twin_req = -1;
+  // twin helpers (helper2_kernel, two workgroups per CU; DESIGN.md "Twin helpers"): SMP_TWIN=1 (experiments; slower
+  // than one helper per CU where measured: C3 8 queries 7.93 -> 6.57, C5 0.664 -> 0.525 M configs/s, the 128-register
+  // tile loop spills)
+  int twin_req = 0;
   if (const char* e = std::getenv("SMP_TWIN")) twin_req = std::atoi(e) != 0 ? 1 : 0;
   const int occ2 = twin_occupancy(p);
   bool twin = false;

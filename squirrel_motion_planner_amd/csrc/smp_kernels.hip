@@ -2791,19 +2791,23 @@ __device__ void insert_via(const Ctx& C, int t, const ViaNode* rec = nullptr, in
 }
 
 #ifdef SMP_RING_CHECK
-__device__ unsigned long long g_ringchk[24];
-__device__ unsigned long long g_ringdbg[SMP_RING][8];  // sampler: parameters of the slot's sample
+__device__ unsigned long long g_ringchk[64];
+__device__ unsigned long long g_ringdbg[SMP_RING][16];  // sampler: parameters of the slot's sample
 extern "C" void smp_ringchk_dump() {
-  unsigned long long v[24];
+  unsigned long long v[64];
   if (hipMemcpyFromSymbol(v, HIP_SYMBOL(g_ringchk), sizeof(v)) == hipSuccess) {
-    std::fprintf(stderr, "[smp] ring check: uniform(it) %llu, it-1 %llu, it+1 %llu, other %llu\n", v[0], v[1], v[2], v[3]);
-    double d[24];
+    double d[64];
     __builtin_memcpy(d, v, sizeof(d));
-    std::fprintf(stderr, "[smp] first mismatch it %llu: leader ver %llu have_sol %llu cbest %.17g %.17g %.17g\n", v[4], v[5],
-                 v[6], d[7], d[8], d[9]);
-    std::fprintf(stderr, "[smp]   sampler slot: it %llu ver %llu have_sol %llu cbest %.17g %.17g %.17g informed %llu\n",
-                 v[10], v[11], v[12], d[13], d[14], d[15], v[16]);
-    std::fprintf(stderr, "[smp]   ring xr0 %.17g leader xr0 %.17g ring xr1 %.17g leader xr1 %.17g\n", d[17], d[18], d[19], d[20]);
+    std::fprintf(stderr, "[smp] ring check: uniform(it) %llu, it-1 %llu, it+1 %llu, other %llu; first mismatch it %llu\n",
+                 v[0], v[1], v[2], v[3], v[4]);
+    std::fprintf(stderr, "[smp]   ring  :");
+    for (int j = 0; j < 8; ++j) std::fprintf(stderr, " %.17g", d[24 + j]);
+    std::fprintf(stderr, "\n[smp]   leader:");
+    for (int j = 0; j < 8; ++j) std::fprintf(stderr, " %.17g", d[32 + j]);
+    std::fprintf(stderr, "\n[smp]   sampler h0 %.17g Crev0 %.17g Crev7 %.17g ctr0 %.17g qmin2 %.17g qmax2 %.17g rev %llx\n",
+                 d[40], d[41], d[42], d[43], d[44], d[45], v[46]);
+    std::fprintf(stderr, "[smp]   leader  h0 %.17g Crev0 %.17g Crev7 %.17g ctr0 %.17g qmin2 %.17g qmax2 %.17g rev %llx\n",
+                 d[48], d[49], d[50], d[51], d[52], d[53], v[54]);
   }
 }
 #endif
@@ -2891,9 +2895,23 @@ __device__ __forceinline__ int sample_ellipse(const QState& S, uint32_t it, SmpL
           if (0.0 <= ee_z(rb, q)) break;
         }
       }
-      double br[6], bp[2], sr = 0.0, sp = 0.0;
-      int ir = 0, ip = 0;
-      for (int j = 0; j < NJ; ++j) { if (rb->rev[j]) br[ir++] = q[j]; else bp[ip++] = q[j]; }
+      // the revolute / prismatic parts in joint order, through static indices only (packing them through running
+      // counters into private arrays came out shifted by one slot in the run-ahead sampler's build: samples of the
+      // wrong joints; tests/test_gpu_parity.py::test_c5_informed_samples_from_the_ring)
+      double br[6] = {}, bp[2] = {}, sr = 0.0, sp = 0.0;
+      {
+        int cr = 0, cp = 0;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const bool rv = rb->rev[j] != 0;
+#pragma unroll
+          for (int i = 0; i < 6; ++i) br[i] = rv && cr == i ? q[j] : br[i];
+#pragma unroll
+          for (int i = 0; i < 2; ++i) bp[i] = !rv && cp == i ? q[j] : bp[i];
+          cr += rv ? 1 : 0;
+          cp += rv ? 0 : 1;
+        }
+      }
       for (int i = 0; i < 6; ++i) sr += br[i] * br[i];
       for (int i = 0; i < 2; ++i) sp += bp[i] * bp[i];
       double nr = sqrt(sr), npn = sqrt(sp);
@@ -2906,7 +2924,6 @@ __device__ __forceinline__ int sample_ellipse(const QState& S, uint32_t it, SmpL
       for (int i = 0; i < 6; ++i) lr[i] = i == 0 ? S.cbest[1] / 2.0 : srev;
       for (int i = 0; i < 2; ++i) lp[i] = i == 0 ? S.cbest[2] / 2.0 : spr;
       double r[NJ];
-      ir = 0; ip = 0;
       double rr[6], rp[2];
       for (int i = 0; i < 6; ++i) {
         double s = 0.0;
@@ -2918,7 +2935,21 @@ __device__ __forceinline__ int sample_ellipse(const QState& S, uint32_t it, SmpL
         for (int k = 0; k < 2; ++k) s += (S.Cpr[i * 2 + k] * lp[k]) * bp[k];
         rp[i] = s + S.ctr_pr[i];
       }
-      for (int j = 0; j < NJ; ++j) r[j] = rb->rev[j] ? rr[ir++] : rp[ip++];
+      {
+        int cr = 0, cp = 0;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const bool rv = rb->rev[j] != 0;
+          double v = 0.0;
+#pragma unroll
+          for (int i = 0; i < 6; ++i) v = rv && cr == i ? rr[i] : v;
+#pragma unroll
+          for (int i = 0; i < 2; ++i) v = !rv && cp == i ? rp[i] : v;
+          r[j] = v;
+          cr += rv ? 1 : 0;
+          cp += rv ? 0 : 1;
+        }
+      }
       bool above = 0.0 <= ee_z(rb, r);
       bool inside = (r[0] < S.env_x[1] && r[0] > S.env_x[0] && r[1] < S.env_y[1] && r[1] > S.env_y[0]) || env0;
       unsigned long long m = __ballot(above && inside && lane < SE_OUT);
@@ -3062,11 +3093,19 @@ __device__ void sample_read(const Ctx& C) {
       S.prof[30]++;
       if (bad) { S.prof[28]++; if (!S.prof[29]) S.prof[29] = (unsigned long long)it + 1; }
       if (bad && g_ringchk[21] == 0) {
+        const RobotDev* rb = (&g_rb);
         g_ringchk[21] = 1;
-        g_ringchk[17] = (unsigned long long)__double_as_longlong(g_L.xr[0]);
-        g_ringchk[18] = (unsigned long long)__double_as_longlong(chk_xr[0]);
-        g_ringchk[19] = (unsigned long long)__double_as_longlong(g_L.xr[1]);
-        g_ringchk[20] = (unsigned long long)__double_as_longlong(chk_xr[1]);
+        g_ringchk[4] = (unsigned long long)it;
+        for (int j = 0; j < NJ; ++j) {
+          g_ringchk[24 + j] = (unsigned long long)__double_as_longlong(g_L.xr[j]);
+          g_ringchk[32 + j] = (unsigned long long)__double_as_longlong(chk_xr[j]);
+        }
+        for (int k = 0; k < 7; ++k) g_ringchk[40 + k] = ld_agent(&g_ringdbg[it % SMP_RING][8 + k]);
+        const double lv[6] = {S.h0[1], S.Crev[0], S.Crev[7], S.ctr_rev[0], rb->q_min[2], rb->q_max[2]};
+        for (int k = 0; k < 6; ++k) g_ringchk[48 + k] = (unsigned long long)__double_as_longlong(lv[k]);
+        unsigned long long rv = 0;
+        for (int j = 0; j < NJ; ++j) rv |= (unsigned long long)(rb->rev[j] != 0) << j;
+        g_ringchk[54] = rv;
       }
     }
     __syncthreads();
@@ -3087,13 +3126,6 @@ __device__ void sample_read(const Ctx& C) {
       }
       if (threadIdx.x == 0) {
         g_ringchk[cls - 20]++;
-        if (cls == 23 && g_ringchk[4] == 0) {
-          g_ringchk[4] = (unsigned long long)it;
-          g_ringchk[5] = g_L.smp_ver;
-          g_ringchk[6] = S.have_sol;
-          for (int k = 0; k < 3; ++k) g_ringchk[7 + k] = (unsigned long long)__double_as_longlong(S.cbest[k]);
-          for (int k = 0; k < 7; ++k) g_ringchk[10 + k] = ld_agent(&g_ringdbg[it % SMP_RING][k]);
-        }
       }
       __syncthreads();
     }
@@ -4932,6 +4964,12 @@ __device__ __forceinline__ void sampler_body(const Ctx& C, SamplerLds& L) {
       st_agent(&d[2], (unsigned long long)L.S.have_sol);
       for (int k = 0; k < 3; ++k) st_agent(&d[3 + k], (unsigned long long)__double_as_longlong(L.S.cbest[k]));
       st_agent(&d[6], (unsigned long long)L.S.informed);
+      const RobotDev* rb = (&g_rb);
+      const double lv[6] = {L.S.h0[1], L.S.Crev[0], L.S.Crev[7], L.S.ctr_rev[0], rb->q_min[2], rb->q_max[2]};
+      for (int k = 0; k < 6; ++k) st_agent(&d[8 + k], (unsigned long long)__double_as_longlong(lv[k]));
+      unsigned long long rv = 0;
+      for (int j = 0; j < NJ; ++j) rv |= (unsigned long long)(rb->rev[j] != 0) << j;
+      st_agent(&d[14], rv);
     }
 #endif
     if (st == 0 && threadIdx.x < RING_G) {

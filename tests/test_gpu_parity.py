@@ -437,6 +437,24 @@ def test_c5_clutter_2cm_check_and_plan(orobot, robot, c5_pair):
     assert_same_run(gp2, r, o)
 
 
+@pytest.mark.parametrize("helpers,scout", [(2, 0), (29, 2)])
+def test_c5_informed_samples_from_the_ring(orobot, robot, c5_pair, helpers, scout):
+    """C5 query 0 (first solution at iteration 2136) to 3000 iterations with the run-ahead sampler serving the
+    informed (post-solution) samples: helpers = 2 is one tile helper + the sampler, no scout.  A ring sample drawn with
+    another cost bound than the leader's once slipped in here (trees equal to the oracle's up to the solution, then
+    not); the leader now takes a slot only if its sampling parameters equal its own."""
+    sc, gscene, osc = c5_pair
+    gp2 = GpuPlanner(robot, path_optimality_threshold=-np.inf, helpers=helpers, scout=scout)
+    gp2.set_scene(gscene)
+    s, g = scenes.random_queries(sc, 1, seed=7, check=lambda q: bool(gp2.check_configs([q])[0]))[0]
+    r = gp2.plan(GpuPlanner.make_query(s, g, sc.env_x, sc.env_y, iterations=3000, seed=1, query_id=0))
+    assert r["samples_precomputed"] > 2000  # the ring served most iterations, before and after the solution
+    o = O.Oracle(orobot, osc).plan(s, g, env_x=sc.env_x, env_y=sc.env_y, max_iter=3000, seed=1, query=0,
+                                   opt_thresh=-np.inf)
+    assert o["first_iter"] < 2500
+    assert_same_run(gp2, r, o)
+
+
 def test_c5_bench_share_full_budget(orobot, robot, c5_pair):
     """bench.py --workload c5 step 0 at full size: 8 random queries on the 2 cm clutter scene (seed 7), 1e6
     collision-checked samples each, path_optimality_threshold = -inf; every query equals its oracle run."""

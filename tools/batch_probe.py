@@ -14,7 +14,7 @@ nq = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 samples = int(sys.argv[2]) if len(sys.argv) > 2 else 1_000_000
 sc = scenes.clutter_cloud() if os.environ.get("SMP_SCENE", "c5") == "c5" else scenes.box_room()
 print("scene %s, %d queries, %d samples each" % (sc.name, nq, samples), flush=True)
-gp = GpuPlanner(path_optimality_threshold=-math.inf)
+gp = GpuPlanner(path_optimality_threshold=-math.inf, scout=int(os.environ.get("SMP_SCOUT", "1")))
 gp.set_scene(Scene.from_keys(sc.keys, sc.res))
 pairs = scenes.random_queries(sc, nq, seed=7, check=lambda q: bool(gp.check_configs([q])[0]))
 
