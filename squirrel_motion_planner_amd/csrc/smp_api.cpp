@@ -1092,6 +1092,8 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
   int twin_req = 0;
   if (const char* e = std::getenv("SMP_TWIN")) twin_req = std::atoi(e) != 0 ? 1 : 0;
   const int occ2 = twin_occupancy(p);
+  int xcd_margin = 1;
+  if (const char* e = std::getenv("SMP_XCD_MARGIN")) xcd_margin = std::max(0, std::atoi(e));
   bool twin = false;
   int nh = 0, ns = 0;
   auto provision = [&](const std::vector<int>& act) {
@@ -1113,6 +1115,19 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
     // twin helpers: occ2 per CU on the CUs the leaders and scouts leave (each of those fills a CU)
     const int tcap = std::max(0, occ2 * (slots - na * (1 + ns)) / na);
     if (twin && nh_req == 0) nh = want_scout ? std::min(cap_s, tcap) : std::min(63, tcap);
+    // per XCD: the workgroups of a launch are dealt round-robin over the 8 XCDs (blocks b and b + 8 share one), and a
+    // workgroup dealt to a full XCD waits there -- a persistent helper that never starts leaves its tiles to the
+    // leader's timeout on every job.  plan_kernel puts query q's leader and scouts on XCD slot q % 8, so the fullest
+    // XCD holds (1 + ns) ceil(na / 8) of them; the helpers, dealt evenly, get what that XCD leaves, less
+    // SMP_XCD_MARGIN CUs (default 1: the two launches race for the CUs).  C5, 8 queries rebalanced to 6 and 4:
+    // 39 / 59 helpers each (some never resident) 0.65 M configs/s, 26 each 1.12 M.
+    if (!twin && p->num_cus >= 8) {
+      const int per_xcd = p->num_cus / 8 / std::max(1, p->slot_share);
+      const int plan_max = (1 + ns) * ((na + 7) / 8);
+      const int free_xcd = std::max(0, per_xcd - plan_max - xcd_margin);
+      const int hcap = 8 * free_xcd / na;
+      if (nh > hcap) nh = std::max(0, hcap);
+    }
     // an explicit request larger than what can be resident is clamped to the automatic count: a helper that never
     // starts would leave its tiles to the leader's 8 us timeout on every job (helper sweeps: 250 helpers beside four
     // scouts no longer all start on 256 CUs and stall)

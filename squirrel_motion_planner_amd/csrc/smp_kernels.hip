@@ -2068,8 +2068,23 @@ __device__ __forceinline__ void helper_main(const Ctx& C, int hidx, JobLds& J) {
     // 0 = nothing new, > 0 = job number complete in J.words, -1 = leave, -2 = payload longer than the poll
     if (threadIdx.x < 64) {
       unsigned long long v[PU];
+#ifdef SMP_POLL_HDR
+      // experiments: poll the header granule alone (one request per poll), then the payload in a second round
+      {
+        const unsigned long long h = ld_agent(&jb->pay[0]);
+        const unsigned t = __builtin_amdgcn_readfirstlane((unsigned)(h >> 32));
+        if (t != 0 && (int)t != last) {
+#pragma unroll
+          for (int u = 0; u < PU; ++u) v[u] = ld_agent(&jb->pay[u * 64 + threadIdx.x]);
+        } else {
+#pragma unroll
+          for (int u = 0; u < PU; ++u) v[u] = h;
+        }
+      }
+#else
 #pragma unroll
       for (int u = 0; u < PU; ++u) v[u] = ld_agent(&jb->pay[u * 64 + threadIdx.x]);
+#endif
       const unsigned tag0 = __builtin_amdgcn_readfirstlane((unsigned)(v[0] >> 32));
       const unsigned hdr = __builtin_amdgcn_readfirstlane((unsigned)v[0]);
       int go = 0;
