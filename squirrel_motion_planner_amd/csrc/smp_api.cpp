@@ -941,6 +941,7 @@ static hipError_t alloc_query(QueryBuffers& b, size_t cap, int via_cap, long lon
 
 static QueryDev make_qdev(QueryBuffers& b, size_t cap, long long rows) {
   QueryDev d;
+  std::memset(&d, 0, sizeof(d));
   d.st = b.st.p;
   for (int t = 0; t < 2; ++t) {
     TreeDev& T = d.tr[t];
@@ -1084,6 +1085,11 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
   if (const char* e = std::getenv("SMP_REBALANCE")) rebalance = rebalance && std::atoi(e) != 0;
   // SMP_REBALANCE_DIV: a launch ends once 1/rb_div of its queries finished (C3, 64 queries: 2 / 4 / 8 all 10.1-10.3
   // M configs/s; C5, 8 queries: 0.49 / 0.61 / 0.62 M)
+  // several queries run in time slices (SMP_SLICE_MS, default 50; 0: chunks of 256 .. 4096 iterations): a launch
+  // ends at its slice or when a quarter of its queries finished, never waiting for the slowest query's chunk --
+  // C5's queries differ 5x in iteration time (tools/batch_probe.py)
+  double slice_ms = 50.0;
+  if (const char* e = std::getenv("SMP_SLICE_MS")) slice_ms = std::max(0.0, std::atof(e));
   int rb_div = 4;
   if (const char* e = std::getenv("SMP_REBALANCE_DIV")) rb_div = std::max(1, std::atoi(e));
   // twin helpers (helper2_kernel, two workgroups per CU; DESIGN.md "Twin helpers"): SMP_TWIN=1 (experiments; slower
@@ -1095,7 +1101,9 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
   int xcd_margin = 1;
   if (const char* e = std::getenv("SMP_XCD_MARGIN")) xcd_margin = std::max(0, std::atoi(e));
   bool twin = false;
-  int nh = 0, ns = 0;
+  int nh = 0, ns = 0, ns_base = 0;
+  int pre_scouts = 1;
+  if (const char* e = std::getenv("SMP_PRE_SCOUTS")) pre_scouts = std::atoi(e);
   auto provision = [&](const std::vector<int>& act) {
     const int na = std::max(1, (int)act.size());
     const int cpq = std::max(1, slots / na);
@@ -1112,6 +1120,13 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
     if (want_scout && p->params.scout > 1) ns = std::min(p->params.scout, MAX_SCOUTS);  // explicit count
     if (nh < 0) nh = 0;
     if (nh < 4) ns = 0;
+    // per query: where the automatic count is two, a query still without a path takes four (scouts 2 and 3 take every
+    // other pre-solution iteration and retire at the first path; C5 query 1 alone, 59 helpers: 25.5 -> 14.0 us per
+    // iteration); ns is then the launch's largest count (grid, boards, XCD budget).  SMP_PRE_SCOUTS=0: uniform
+    ns_base = ns;
+    if (pre_scouts && nh_req == 0 && p->params.scout == 1 && ns == 2)
+      for (int i : act)
+        if (!S[i].have_sol) { ns = 4; break; }
     // twin helpers: occ2 per CU on the CUs the leaders and scouts leave (each of those fills a CU)
     const int tcap = std::max(0, occ2 * (slots - na * (1 + ns)) / na);
     if (twin && nh_req == 0) nh = want_scout ? std::min(cap_s, tcap) : std::min(63, tcap);
@@ -1137,19 +1152,31 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
     }
     // after the first solution scouts 0 and 1 check choose-parent / rewire candidate batches (many tiles); scouts 2
     // and 3 only work before it, one edge per job (3 tiles); the leader's own jobs (edges no record had) are rare
-    int h_lead = 0, h_s[MAX_SCOUTS] = {};
-    if (ns > 0) {
-      const int avail = nh - 1;  // minus the sampler
-      h_lead = ns >= 2 ? avail / lead_div : avail / 2;
-      int rest = avail - h_lead;
-      for (int s = 2; s < ns; ++s) { h_s[s] = std::min(pre_h, rest); rest -= h_s[s]; }
-      if (ns >= 2) { h_s[0] = rest - rest / 2; h_s[1] = rest / 2; } else { h_s[0] = rest; }
-    }
+    auto split = [&](int nsq, int& h_lead, int* h_s) {
+      h_lead = 0;
+      for (int s = 0; s < MAX_SCOUTS; ++s) h_s[s] = 0;
+      if (nsq > ns_base) {  // a query's pre-solution scouts: their records carry its iterations, one in four each
+        const int avail = nh - 1;
+        h_lead = avail / 5;
+        const int per = (avail - h_lead) / nsq;
+        for (int s = 0; s < nsq; ++s) h_s[s] = per;
+        h_s[0] += avail - h_lead - per * nsq;
+      } else if (nsq > 0) {
+        const int avail = nh - 1;  // minus the sampler
+        h_lead = nsq >= 2 ? avail / lead_div : avail / 2;
+        int rest = avail - h_lead;
+        for (int s = 2; s < nsq; ++s) { h_s[s] = std::min(pre_h, rest); rest -= h_s[s]; }
+        if (nsq >= 2) { h_s[0] = rest - rest / 2; h_s[1] = rest / 2; } else { h_s[0] = rest; }
+      }
+    };
     for (int i : act) {
+      const int nsq = ns > ns_base && S[i].have_sol ? ns_base : ns;
+      int h_lead = 0, h_s[MAX_SCOUTS];
+      split(nsq, h_lead, h_s);
       qdev[i].jb = nh > 0 ? p->qb[i].jb.p : nullptr;
       qdev[i].sampler = nh >= 2;              // with two or more helpers, the last one runs ahead sampling
-      qdev[i].nworkers = ns > 0 ? 1 + h_lead : (nh >= 2 ? nh : 1 + nh);
-      qdev[i].nscouts = ns;
+      qdev[i].nworkers = nsq > 0 ? 1 + h_lead : (nh >= 2 ? nh : 1 + nh);
+      qdev[i].nscouts = nsq;
       qdev[i].pre_delay = pre_delay;
       qdev[i].pre_commit = pre_commit;
       qdev[i].early_ask = early_ask;
@@ -1168,6 +1195,7 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
     if (S[i].phase != 2 && S[i].status == 0) act.push_back(i);
   std::vector<int> all(nq);
   for (int i = 0; i < nq; ++i) all[i] = i;
+  std::vector<int> sol_seen(nq, 0);
   provision(act.empty() ? all : act);
   const int nh_first = nh, ns_first = ns;
   static int* trace_host = nullptr;
@@ -1211,6 +1239,7 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
     for (int i : act) {
       qdev[i].lfin = p->d_lfin.p;
       qdev[i].lquota = quota;
+      qdev[i].lticks = act.size() >= 2 && slice_ms > 0 ? (long long)(slice_ms * 1e-3 * p->wall_rate_hz) : 0;
       qlaunch.push_back(qdev[i]);
     }
     // (qlaunch outlives the copy: it changes only after the next launch has completed)
@@ -1231,7 +1260,7 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
   // a single query runs its whole budget in one launch (the loop state is resumable, but a relaunch costs the host
   // round trip, the board reset and the scouts' restart: C2, 5 launches of 256 .. 4096 iterations, ~1 ms each);
   // several queries start at 256 iterations and double, so that finished ones free their CUs early (rebalance)
-  int chunk = nq == 1 ? (1 << 30) : 256;
+  int chunk = nq == 1 || slice_ms > 0 ? (1 << 30) : 256;
   if (const char* e = std::getenv("SMP_CHUNK0")) chunk = std::max(1, std::atoi(e));  // experiments
   std::vector<std::array<unsigned long long, 32>> scout_prof(nq);
   for (auto& a : scout_prof) a.fill(0);
@@ -1242,7 +1271,9 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
     if (qs[i].budget_kind != SMP_BUDGET_SECONDS) max_iters = std::max(max_iters, (long long)qs[i].budget);
   while (!act.empty()) {
     // no progress: never spin forever (a launch ended early by finished queries counts too)
-    if (tmax == 0 && launches > max_iters / 256 + 64 + 2 * nq) return SMP_ERR_HIP;
+    if (tmax == 0 && launches > max_iters / 256 + 64 + 2 * nq +
+                                    (slice_ms > 0 ? (long long)(total_ms / slice_ms) * 2 : 0))
+      return SMP_ERR_HIP;
     if (tmax > 0 && std::chrono::duration<double>(std::chrono::steady_clock::now() - t_begin).count() > tmax * 4 + 60)
       return SMP_ERR_HIP;
     const int na = (int)act.size();
@@ -1347,12 +1378,16 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
                    nh ? jbh.res[0] : 0ull);
     }
     std::vector<int> still;
+    int solved_before = 0, solved_now = 0;
+    for (int i : act) solved_before += sol_seen[i];
     for (int i : act)
       if (!(S[i].phase == 2 || S[i].status != 0)) still.push_back(i);
+    for (int i : act) { sol_seen[i] = S[i].have_sol ? 1 : 0; solved_now += sol_seen[i]; }
     const bool shrank = still.size() < act.size();
     act.swap(still);
     if (act.empty()) break;
-    if (shrank) {
+    // (a query that found its first path gives its pre-solution scouts back: re-provisioned too)
+    if (shrank || (ns > ns_base && solved_now != solved_before)) {
       if (rebalance) provision(act);
       if (int st = upload_active()) return st;
     }

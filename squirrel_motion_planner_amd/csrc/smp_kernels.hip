@@ -4887,10 +4887,14 @@ __global__ void __launch_bounds__(BLOCK) plan_kernel(const RobotDev* __restrict_
       g_L.S.phase = (g_L.S.have_sol || (g_L.S.max_checked && g_L.S.checked >= g_L.S.max_checked)) ? 2 : 1;
     __syncthreads();
   }
+  const unsigned long long t_launch = wall_clock64();
   for (int k = 0; k < iters; ++k) {
     if (uni(g_L.S.status != 0 || g_L.S.phase != 1)) break;
-    if (C.Q.lquota > 0 && (k & 7) == 7) {  // enough of the launch's queries finished: end it (resumable)
-      if (threadIdx.x == 0) g_L.go_end = ld_agent(C.Q.lfin) >= (unsigned)C.Q.lquota;
+    if ((C.Q.lquota > 0 || C.Q.lticks > 0) && (k & 7) == 7) {
+      // enough of the launch's queries finished, or its time slice is over: end it (resumable)
+      if (threadIdx.x == 0)
+        g_L.go_end = (C.Q.lquota > 0 && ld_agent(C.Q.lfin) >= (unsigned)C.Q.lquota) ||
+                     (C.Q.lticks > 0 && (long long)(wall_clock64() - t_launch) > C.Q.lticks);
       __syncthreads();
       if (uni(g_L.go_end)) break;
     }

@@ -302,6 +302,8 @@ struct QueryDev {
   // finished queries to the others (DESIGN.md "Many queries")
   unsigned* lfin;
   int lquota;
+  long long lticks;            // > 0: the launch ends this many device-clock ticks after it started (resumable), so
+                               // that the host re-provisions (DESIGN.md "Many queries")
   unsigned* ttff;              // host-mapped word set to 1 when the first feasible path is committed (null: none)
   int scan_min;                // nodes in a scan's range from which it is split over the helpers (0: never)
   int scan_pnn, scan_pnear;    // participants (this workgroup + helpers) of a split nearest / near scan, <= SCAN_P

@@ -7,10 +7,12 @@ HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
 run() { local name=$1; shift; timeout -k 10 "$@"; local rc=$?; echo "$name rc=$rc" >> $OUT/status.txt
         case $rc in 124|134|137|139) exit $rc;; esac; }
-run c5 200 python -u bench.py --workload c5 --steps 1 --warmup 1 --no-cpu > $OUT/c5.json 2> $OUT/c5.err
-run c5m0 200 env SMP_XCD_MARGIN=0 python -u bench.py --workload c5 --steps 1 --warmup 1 --no-cpu > $OUT/c5m0.json 2> $OUT/c5m0.err
-run c5m2 200 env SMP_XCD_MARGIN=2 python -u bench.py --workload c5 --steps 1 --warmup 1 --no-cpu > $OUT/c5m2.json 2> $OUT/c5m2.err
-run c3 200 python -u bench.py --workload c3 --steps 1 --warmup 1 --no-cpu > $OUT/c3.json 2> $OUT/c3.err
-run c3m0 200 env SMP_XCD_MARGIN=0 python -u bench.py --workload c3 --steps 1 --warmup 1 --no-cpu > $OUT/c3m0.json 2> $OUT/c3m0.err
-run c2 200 python -u bench.py --no-cpu > $OUT/c2.json 2> $OUT/c2.err
-run t 400 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "full_budget or batch or reprovisioned" > $OUT/t_batch.txt 2>&1
+B="python -u bench.py --steps 1 --warmup 1 --no-cpu"
+run c5 200 $B --workload c5 > $OUT/c5.json 2> $OUT/c5.err
+run c3 200 $B --workload c3 > $OUT/c3.json 2> $OUT/c3.err
+run c5s20 200 env SMP_SLICE_MS=20 $B --workload c5 > $OUT/c5s20.json 2> $OUT/c5s20.err
+run c5s100 200 env SMP_SLICE_MS=100 $B --workload c5 > $OUT/c5s100.json 2> $OUT/c5s100.err
+run c3s20 200 env SMP_SLICE_MS=20 $B --workload c3 > $OUT/c3s20.json 2> $OUT/c3s20.err
+run c5np 200 env SMP_PRE_SCOUTS=0 $B --workload c5 > $OUT/c5np.json 2> $OUT/c5np.err
+run c3np 200 env SMP_PRE_SCOUTS=0 $B --workload c3 > $OUT/c3np.json 2> $OUT/c3np.err
+run t 400 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "full_budget or batch or reprovisioned or relaunch" > $OUT/t_batch.txt 2>&1
