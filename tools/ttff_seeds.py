@@ -2,7 +2,7 @@
 """Time to first feasible path on C2 for the bench's 20 step seeds (1, 1001, ..., 19001): the GPU on the host clock
 from smp_plan entry (median of `reps` runs per seed) beside the CPU oracle's from run() entry (one thread, median of
 `reps` runs), per seed; how many seeds the GPU is earlier on.  Knobs of the provisioning come from the environment
-(SMP_PRE_HELPERS, SMP_LEAD_DIV, SMP_PRE_DELAY, ...).
+(SMP_PRE_HELPERS, SMP_LEAD_DIV, SMP_PRE_DELAY, ...; SMP_SCOUT: the scout count).
 
   python tools/ttff_seeds.py [reps] [out.json]
 """
@@ -22,7 +22,7 @@ from squirrel_motion_planner_amd.planner import GpuPlanner, Scene  # noqa: E402
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
 out = sys.argv[2] if len(sys.argv) > 2 else None
 sc = scenes.box_room()
-gp = GpuPlanner(path_optimality_threshold=-math.inf)
+gp = GpuPlanner(path_optimality_threshold=-math.inf, scout=int(os.environ.get("SMP_SCOUT", "1")))
 gp.set_scene(Scene.from_keys(sc.keys, sc.res))
 orc = O.Oracle(O.OracleRobot(os.path.join(ROOT, "squirrel_motion_planner_amd", "data", "robotino_model.json")),
                O.OracleScene(sc.keys, sc.res))
