@@ -1141,7 +1141,8 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
       const int plan_max = (1 + ns) * ((na + 7) / 8);
       const int free_xcd = std::max(0, per_xcd - plan_max - xcd_margin);
       const int hcap = 8 * free_xcd / na;
-      if (nh > hcap) nh = std::max(0, hcap);
+      // (an explicit request beyond it gets no more than the automatic count either)
+      if (nh > hcap) nh = std::max(0, nh_req > 0 ? std::min(hcap, cap_s) : hcap);
     }
     // an explicit request larger than what can be resident is clamped to the automatic count: a helper that never
     // starts would leave its tiles to the leader's 8 us timeout on every job (helper sweeps: 250 helpers beside four

@@ -1,9 +1,11 @@
 # Scratch GPU session of the current experiment (rewritten per experiment; run from the repo root through gpurun).
+# Every step has its own time limit; a fault, abort or time-out ends the session (no further GPU step).
 OUT=gpurun_out
 mkdir -p $OUT
 ( while true; do date +%s >> $OUT/heartbeat.txt; sleep 30; done ) &
 HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
-bash tools/profile_round.sh r04 c2 && echo c2 done >> $OUT/status.txt && \
-bash tools/profile_round.sh r04 c3 --workload c3 && echo c3 done >> $OUT/status.txt && \
-bash tools/profile_round.sh r04 c5 --workload c5 && echo c5 done >> $OUT/status.txt
+run() { local name=$1; shift; timeout -k 10 "$@"; local rc=$?; echo "$name rc=$rc" >> $OUT/status.txt
+        case $rc in 124|134|137|139) exit $rc;; esac; }
+run gpu 700 python -u -m pytest tests/ -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/gpu_tests.txt 2>&1
+run smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.txt 2>&1
