@@ -143,6 +143,8 @@ struct smp_planner {
   double wall_rate_hz = 1e8;
   int num_cus = 256;
   unsigned* h_ttff = nullptr;      // host-mapped first-solution flags, one per query (QueryDev::ttff)
+  QState* h_st = nullptr;          // pinned host copies of the queries' loop states (asynchronous uploads)
+  int n_st = 0;
   int n_ttff = 0;
   // last plan (query 0) bookkeeping for smp_get_tree
   int last_n[2] = {0, 0};
@@ -461,6 +463,7 @@ void smp_planner_destroy(smp_planner* p) {
   if (p->hstream) (void)hipStreamDestroy(p->hstream);
   if (p->ev_board) (void)hipEventDestroy(p->ev_board);
   if (p->h_ttff) (void)hipHostFree(p->h_ttff);
+  if (p->h_st) (void)hipHostFree(p->h_st);
   delete p;
 }
 
@@ -1022,7 +1025,17 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
   hstamp("arguments checked");
   if ((int)p->qb.size() < nq) p->qb.resize(nq);
   std::vector<QueryDev> qdev(nq);
-  std::vector<QState> S(nq);
+  // the loop states in pinned host memory: their uploads and read-backs are true asynchronous copies (a pageable
+  // source is staged synchronously: tens of microseconds before the first launch, inside the time to a first path)
+  if (p->n_st < nq) {
+    if (p->h_st) (void)hipHostFree(p->h_st);
+    p->h_st = nullptr;
+    p->n_st = 0;
+    HIPCHK(hipHostMalloc(&p->h_st, (size_t)nq * sizeof(QState), hipHostMallocDefault));
+    p->n_st = nq;
+  }
+  QState* S = p->h_st;
+  hstamp("host states");
   std::vector<long long> rows_cap(nq, 0);
   for (int i = 0; i < nq; ++i) {
     const smp_query& q = qs[i];
@@ -1040,8 +1053,10 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
     // three quarters of an explicit node_capacity usable.  A longer chain ends the run with SMP_ERR_CAPACITY.
     const int via_cap = (int)std::max<int64_t>(64, std::min<int64_t>(4096, cap / 8));
     HIPCHK(alloc_query(p->qb[i], (size_t)cap, via_cap, rows_cap[i]));
+    if (i == 0) hstamp("query 0 buffers");
     qdev[i] = make_qdev(p->qb[i], (size_t)cap, rows_cap[i]);
     init_qstate(p, q, cap, via_cap, &S[i]);
+    if (i == 0) hstamp("query 0 state");
     if (q.budget_kind == SMP_BUDGET_SECONDS) {
       // the budget counts from smp_plan entry (start / goal checks and first-call allocation included); the kernel
       // turns the rest into a deadline when it records the planning start

@@ -7,5 +7,4 @@ HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
 run() { local name=$1; shift; timeout -k 10 "$@"; local rc=$?; echo "$name rc=$rc" >> $OUT/status.txt
         case $rc in 124|134|137|139) exit $rc;; esac; }
-run gpu 700 python -u -m pytest tests/ -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/gpu_tests.txt 2>&1
-run smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.txt 2>&1
+run pp 100 env SMP_HOST_PROF=1 python -u tools/perf_probe.py 1 1 120 > $OUT/pp_small.txt 2>&1
