@@ -1118,6 +1118,8 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
   bool twin = false;
   int nh = 0, ns = 0, ns_base = 0;
   int pre_scouts = 1;
+  int pre_lead_div = 5;  // SMP_PRE_LEAD_DIV: the leader's share of a pre-solution query's helpers (1 / n)
+  if (const char* e = std::getenv("SMP_PRE_LEAD_DIV")) pre_lead_div = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("SMP_PRE_SCOUTS")) pre_scouts = std::atoi(e);
   auto provision = [&](const std::vector<int>& act) {
     const int na = std::max(1, (int)act.size());
@@ -1173,7 +1175,7 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
       for (int s = 0; s < MAX_SCOUTS; ++s) h_s[s] = 0;
       if (nsq > ns_base) {  // a query's pre-solution scouts: their records carry its iterations, one in four each
         const int avail = nh - 1;
-        h_lead = avail / 5;
+        h_lead = avail / pre_lead_div;
         const int per = (avail - h_lead) / nsq;
         for (int s = 0; s < nsq; ++s) h_s[s] = per;
         h_s[0] += avail - h_lead - per * nsq;
