@@ -7,8 +7,4 @@ HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
 run() { local name=$1; shift; timeout -k 10 "$@"; local rc=$?; echo "$name rc=$rc" >> $OUT/status.txt
         case $rc in 124|134|137|139) exit $rc;; esac; }
-B="python -u bench.py --steps 1 --warmup 1 --no-cpu --workload c5"
-run d5 200 $B > $OUT/d5.json 2> $OUT/d5.err
-run d3 200 env SMP_PRE_LEAD_DIV=3 $B > $OUT/d3.json 2> $OUT/d3.err
-run d8 200 env SMP_PRE_LEAD_DIV=8 $B > $OUT/d8.json 2> $OUT/d8.err
-run d12 200 env SMP_PRE_LEAD_DIV=12 $B > $OUT/d12.json 2> $OUT/d12.err
+run bench 400 python -u bench.py > $OUT/bench_final.json 2> $OUT/bench_final.err
