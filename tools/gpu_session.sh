@@ -7,4 +7,8 @@ HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
 run() { local name=$1; shift; timeout -k 10 "$@"; local rc=$?; echo "$name rc=$rc" >> $OUT/status.txt
         case $rc in 124|134|137|139) exit $rc;; esac; }
-run bench 400 python -u bench.py > $OUT/bench_final.json 2> $OUT/bench_final.err
+B="python -u bench.py --steps 2 --warmup 1 --no-cpu --workload c3"
+run s50 200 $B > $OUT/s50.json 2> $OUT/s50.err
+run s100 200 env SMP_SLICE_MS=100 $B > $OUT/s100.json 2> $OUT/s100.err
+run s200 200 env SMP_SLICE_MS=200 $B > $OUT/s200.json 2> $OUT/s200.err
+run s0 200 env SMP_SLICE_MS=0 $B > $OUT/s0.json 2> $OUT/s0.err
