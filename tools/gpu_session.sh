@@ -7,8 +7,5 @@ HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
 run() { local name=$1; shift; timeout -k 10 "$@"; local rc=$?; echo "$name rc=$rc" >> $OUT/status.txt
         case $rc in 124|134|137|139) exit $rc;; esac; }
-B="python -u bench.py --steps 2 --warmup 1 --no-cpu --workload c3"
-run s50 200 $B > $OUT/s50.json 2> $OUT/s50.err
-run s100 200 env SMP_SLICE_MS=100 $B > $OUT/s100.json 2> $OUT/s100.err
-run s200 200 env SMP_SLICE_MS=200 $B > $OUT/s200.json 2> $OUT/s200.err
-run s0 200 env SMP_SLICE_MS=0 $B > $OUT/s0.json 2> $OUT/s0.err
+run twin 700 env SMP_TWIN=1 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread > $OUT/twin_tests.txt 2>&1
+run slice0 700 env SMP_SLICE_MS=0 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "batch or queries or reprovisioned or full_budget" > $OUT/slice0_tests.txt 2>&1
