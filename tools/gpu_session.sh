@@ -7,5 +7,6 @@ HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
 run() { local name=$1; shift; timeout -k 10 "$@"; local rc=$?; echo "$name rc=$rc" >> $OUT/status.txt
         case $rc in 124|134|137|139) exit $rc;; esac; }
-run twin 700 env SMP_TWIN=1 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread > $OUT/twin_tests.txt 2>&1
-run slice0 700 env SMP_SLICE_MS=0 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "batch or queries or reprovisioned or full_budget" > $OUT/slice0_tests.txt 2>&1
+run q4 200 env SMP_QSEL=1,2,4,7 SMP_SCOUT=4 python -u tools/batch_probe.py > $OUT/q4s4.txt 2>&1
+run q6 200 env SMP_QSEL=1,2,4,7 SMP_SCOUT=6 python -u tools/batch_probe.py > $OUT/q4s6.txt 2>&1
+run q8 200 env SMP_QSEL=1,2,4,7 SMP_SCOUT=8 python -u tools/batch_probe.py > $OUT/q4s8.txt 2>&1
