@@ -28,7 +28,6 @@ void launch_check(int ct, int grid, hipStream_t st, const RobotDev* rb, SceneDev
 __global__ void plan_kernel(const RobotDev* rb, SceneDev sc, const MapCfg* mc, QueryDev* qs, int nq, int scout_base,
                             int iters);
 __global__ void helper_kernel(const RobotDev* rb, SceneDev sc, const MapCfg* mc, QueryDev* qs, int nq);
-__global__ void helper2_kernel(const RobotDev* rb, SceneDev sc, const MapCfg* mc, QueryDev* qs, int nq);
 __global__ void path_kernel(QueryDev* qs, int* counts);
 __global__ void path_edges_kernel(const QueryDev* qs, int q, int ns, int ng, double* out);
 __global__ void boards_reset_kernel(const QueryDev* qs, int ns);
@@ -142,6 +141,7 @@ struct smp_planner {
   int64_t last_plan_launches = 0;
   double wall_rate_hz = 1e8;
   int num_cus = 256;
+  int num_xcd = 8;                 // XCDs (hipDeviceAttributeNumberOfXccs): the per-XCD helper budget of provision()
   unsigned* h_ttff = nullptr;      // host-mapped first-solution flags, one per query (QueryDev::ttff)
   QState* h_st = nullptr;          // pinned host copies of the queries' loop states (asynchronous uploads)
   int n_st = 0;
@@ -149,9 +149,23 @@ struct smp_planner {
   // last plan (query 0) bookkeeping for smp_get_tree
   int last_n[2] = {0, 0};
   int slots_cache = 0;  // resident_slots (occupancy queries) once per planner
-  int occ_twin = -1;    // helper2_kernel workgroups per CU (twin_occupancy)
   int slot_share = 1;   // planners planning on this planner's GPU at once (smp_plan_multi): its share of the slots
+  // a planning call gave up (SMP_ERR_HIP) while its kernels may still run on these buffers: every later call that
+  // would touch them fails with SMP_ERR_HIP until both streams are idle again (busy_check), and destroy leaks them
+  // rather than freeing memory a live kernel uses
+  bool busy = false;
 };
+
+// SMP_OK once no kernel of an abandoned planning call runs any more (smp_planner::busy), else SMP_ERR_HIP.
+static int busy_check(smp_planner* p) {
+  if (!p->busy) return SMP_OK;
+  (void)hipSetDevice(p->device);
+  const hipError_t a = hipStreamQuery(p->stream), b = hipStreamQuery(p->hstream);
+  if (a == hipErrorNotReady || b == hipErrorNotReady) return SMP_ERR_HIP;
+  (void)hipGetLastError();
+  p->busy = false;
+  return SMP_OK;
+}
 
 // Workgroups of BLOCK threads that can be resident at once on the device, for the planner's kernels (leader / scout
 // plan_kernel and helper_kernel share the CUs): occupancy per CU (registers, LDS) x CUs.
@@ -167,20 +181,6 @@ static int resident_slots(smp_planner* p) {
   }
   p->slots_cache = p->num_cus * std::max(1, std::min(occ_plan, occ_help));
   return std::max(1, p->slots_cache / std::max(1, p->slot_share));
-}
-
-// Twin helpers (helper2_kernel) resident per CU beside nothing else: 2 when its registers and LDS allow.
-static int twin_occupancy(smp_planner* p) {
-  if (p->occ_twin < 0) {
-    int occ = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(&helper2_kernel), BLOCK, 0) !=
-        hipSuccess) {
-      (void)hipGetLastError();
-      occ = 1;
-    }
-    p->occ_twin = std::max(1, occ);
-  }
-  return p->occ_twin;
 }
 
 static int update_mapcfg(smp_planner* p) {
@@ -407,7 +407,7 @@ int smp_planner_create(int device, const smp_robot* robot, const smp_params* par
     size_t need = 0;
     hipFuncAttributes fa;
     const void* ks[] = {reinterpret_cast<const void*>(&plan_kernel), reinterpret_cast<const void*>(&helper_kernel),
-                        reinterpret_cast<const void*>(&helper2_kernel), reinterpret_cast<const void*>(&path_kernel)};
+                        reinterpret_cast<const void*>(&path_kernel)};
     for (const void* k : ks)
       if (hipFuncGetAttributes(&fa, k) == hipSuccess) need = std::max(need, (size_t)fa.localSizeBytes);
     need = std::max(need, check_kernels_private_bytes());
@@ -439,6 +439,9 @@ int smp_planner_create(int device, const smp_robot* robot, const smp_params* par
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
     p->num_cus = cus;
+  int xcc = 0;
+  if (hipDeviceGetAttribute(&xcc, hipDeviceAttributeNumberOfXccs, device) == hipSuccess && xcc > 0) p->num_xcd = xcc;
+  else (void)hipGetLastError();
   std::memset(&p->sc, 0, sizeof(p->sc));
   int st = update_mapcfg(p);
   if (st) { smp_planner_destroy(p); return st; }
@@ -449,6 +452,10 @@ int smp_planner_create(int device, const smp_robot* robot, const smp_params* par
 void smp_planner_destroy(smp_planner* p) {
   if (!p) return;
   (void)hipSetDevice(p->device);
+  if (busy_check(p) != SMP_OK) {  // a kernel still runs on the buffers: leak them rather than free them under it
+    fprintf(stderr, "smp_gpu: planner destroyed while a planning launch still runs; its device memory is leaked\n");
+    return;
+  }
   if (p->stream) (void)hipStreamSynchronize(p->stream);
   if (p->hstream) (void)hipStreamSynchronize(p->hstream);
   for (auto& q : p->qb) q.release();
@@ -495,6 +502,7 @@ static bool occupancy_clear_of_faces(const uint64_t* bricks, int nx, int ny, int
 
 int smp_planner_set_scene(smp_planner* p, const smp_scene* s) {
   if (!p || !s) return SMP_ERR_ARG;
+  if (int b_ = busy_check(const_cast<smp_planner*>(p))) return b_;
   if (!occupancy_clear_of_faces(s->h.bricks.data(), s->h.nx, s->h.ny, s->h.nz, s->h.res)) {
     fprintf(stderr, "smp_gpu: an occupied cell lies within %.2f m of the grid's faces (pad the grid)\n", GRID_REACH);
     return SMP_ERR_ARG;
@@ -562,6 +570,7 @@ static void scene_layout(const smp_planner* p, smp_scene_device* o) {
 
 int smp_planner_scene_device(const smp_planner* p, smp_scene_device* io) {
   if (!p || !io) return SMP_ERR_ARG;
+  if (int b_ = busy_check(const_cast<smp_planner*>(p))) return b_;
   if (!p->have_scene) return SMP_ERR_ARG;
   HIPCHK(hipSetDevice(p->device));
   uint64_t* bricks = io->bricks;
@@ -582,6 +591,7 @@ int smp_planner_scene_device(const smp_planner* p, smp_scene_device* io) {
 
 int smp_planner_set_scene_device(smp_planner* p, const smp_scene_device* in) {
   if (!p || !in || !in->bricks || !in->d2) return SMP_ERR_ARG;
+  if (int b_ = busy_check(const_cast<smp_planner*>(p))) return b_;
   const int nx = in->dims[0], ny = in->dims[1], nz = in->dims[2];
   if (nx <= 0 || ny <= 0 || nz <= 0 || !(in->resolution > 0)) return SMP_ERR_ARG;
   const RobotDev& d = p->robot.dev;
@@ -662,6 +672,7 @@ int smp_planners_share_scene(smp_planner* const* ps, int n, int src) {
 
 int smp_set_disabled_map_links(smp_planner* p, const char* const* names, int n) {
   if (!p || (n > 0 && !names)) return SMP_ERR_ARG;
+  if (int b_ = busy_check(const_cast<smp_planner*>(p))) return b_;
   HIPCHK(hipSetDevice(p->device));
   p->disabled.clear();
   for (int i = 0; i < n; ++i) if (names[i]) p->disabled.insert(names[i]);
@@ -670,6 +681,7 @@ int smp_set_disabled_map_links(smp_planner* p, const char* const* names, int n) 
 
 int smp_check_configs(smp_planner* p, const double* q_soa, int64_t n, int check_self, int check_map, uint8_t* valid) {
   if (!p || n < 0 || (n > 0 && (!q_soa || !valid))) return SMP_ERR_ARG;
+  if (int b_ = busy_check(const_cast<smp_planner*>(p))) return b_;
   if (n == 0) return SMP_OK;
   HIPCHK(hipSetDevice(p->device));
   HIPCHK(p->d_cq.reserve((size_t)n * NJ));
@@ -697,6 +709,7 @@ int smp_get_collisions(smp_planner* p, const double q[8], int32_t* self_pairs, i
   if (!p || !q || !n_self || !n_map || max_self < 0 || max_map < 0 || (max_self > 0 && !self_pairs) ||
       (max_map > 0 && !map_links))
     return SMP_ERR_ARG;
+  if (int b_ = busy_check(const_cast<smp_planner*>(p))) return b_;
   const RobotDev& d = p->robot.dev;
   HIPCHK(hipSetDevice(p->device));
   HIPCHK(p->d_cq.reserve(NJ));
@@ -731,6 +744,7 @@ int smp_get_collisions(smp_planner* p, const double q[8], int32_t* self_pairs, i
 int smp_check_sequence(smp_planner* p, const double* q_rows, int64_t n, int check_self, int check_map,
                        int64_t* first_invalid) {
   if (!p || !first_invalid || n < 0 || (n > 0 && !q_rows)) return SMP_ERR_ARG;
+  if (int b_ = busy_check(const_cast<smp_planner*>(p))) return b_;
   *first_invalid = -1;
   if (n == 0) return SMP_OK;
   std::vector<double> soa((size_t)n * NJ);
@@ -746,6 +760,7 @@ int smp_check_sequence(smp_planner* p, const double* q_rows, int64_t n, int chec
 
 int smp_is_config_valid(smp_planner* p, const double q[8], int check_self, int check_map, int* valid) {
   if (!p || !q || !valid) return SMP_ERR_ARG;
+  if (int b_ = busy_check(const_cast<smp_planner*>(p))) return b_;
   double soa[8];
   for (int j = 0; j < 8; ++j) soa[j] = q[j];
   uint8_t v = 0;
@@ -783,6 +798,7 @@ static int ik_run(smp_planner* p, const std::vector<IkTaskDev>& tasks, std::vect
 
 int smp_ik_solve(smp_planner* p, const smp_ik_request* reqs, int n, smp_ik_result* out) {
   if (!p || n < 0 || (n > 0 && (!reqs || !out))) return SMP_ERR_ARG;
+  if (int b_ = busy_check(const_cast<smp_planner*>(p))) return b_;
   if (n == 0) return SMP_OK;
   std::vector<IkTaskDev> tasks(n);
   for (int i = 0; i < n; ++i) {
@@ -816,6 +832,7 @@ int smp_find_goal_pose(smp_planner* p, const double ee_pose[6], const double pos
                        int check_self, int check_map, double pose_goal[8], int* result, smp_goal_search* info) {
   if (!p || !ee_pose || !pose_current || !pose_goal || !result || !(discretization_deg == discretization_deg))
     return SMP_ERR_ARG;
+  if (int b_ = busy_check(const_cast<smp_planner*>(p))) return b_;
   int n = 0;
   ik_goal_candidates(ee_pose, pose_current, discretization_deg, nullptr, 0, &n);
   std::vector<IkTaskDev> tasks(n);
@@ -991,13 +1008,14 @@ static QueryDev make_qdev(QueryBuffers& b, size_t cap, long long rows) {
   d.scan_min = 12288;
   if (const char* e = std::getenv("SMP_SCAN_MIN")) d.scan_min = std::max(0, std::atoi(e));
   // participants of one split scan: a nearest result is 3 granules, a near result 122, and the near merge ranks
-  // every list entry against the other lists -- fewer, longer slices for near (SMP_SCAN_PNN / SMP_SCAN_PNEAR)
+  // every list entry against the other lists -- fewer, longer slices for near: one per 4096 nodes, 8 to 32
+  // (SMP_SCAN_PNN / SMP_SCAN_PNEAR cap them)
   d.scan_pnn = 64;
-  d.scan_pnear = 8;
+  d.scan_pnear = SCAN_PNEAR;
   if (const char* e = std::getenv("SMP_SCAN_PNN")) d.scan_pnn = std::atoi(e);
   if (const char* e = std::getenv("SMP_SCAN_PNEAR")) d.scan_pnear = std::atoi(e);
   d.scan_pnn = std::min(SCAN_P, std::max(2, d.scan_pnn));
-  d.scan_pnear = std::min(SCAN_P, std::max(2, d.scan_pnear));
+  d.scan_pnear = std::min(SCAN_PNEAR, std::max(2, d.scan_pnear));
   return d;
 }
 
@@ -1107,15 +1125,8 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
   if (const char* e = std::getenv("SMP_SLICE_MS")) slice_ms = std::max(0.0, std::atof(e));
   int rb_div = 4;
   if (const char* e = std::getenv("SMP_REBALANCE_DIV")) rb_div = std::max(1, std::atoi(e));
-  // twin helpers (helper2_kernel, two workgroups per CU; DESIGN.md "Twin helpers"): SMP_TWIN=1 (experiments; slower
-  // than one helper per CU where measured: C3 8 queries 7.93 -> 6.57, C5 0.664 -> 0.525 M configs/s, the 128-register
-  // tile loop spills)
-  int twin_req = 0;
-  if (const char* e = std::getenv("SMP_TWIN")) twin_req = std::atoi(e) != 0 ? 1 : 0;
-  const int occ2 = twin_occupancy(p);
   int xcd_margin = 1;
   if (const char* e = std::getenv("SMP_XCD_MARGIN")) xcd_margin = std::max(0, std::atoi(e));
-  bool twin = false;
   int nh = 0, ns = 0, ns_base = 0;
   int pre_scouts = 1;
   int pre_lead_div = 5;  // SMP_PRE_LEAD_DIV: the leader's share of a pre-solution query's helpers (1 / n)
@@ -1126,7 +1137,6 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
     const int cpq = std::max(1, slots / na);
     nh = nh_req;
     ns = 0;
-    twin = occ2 >= 2 && (twin_req == 1 || (twin_req < 0 && nh_req == 0 && cpq < 64));
     if (nh == 0) {
       if (want_scout) ns = cpq >= 64 ? 4 : cpq >= 18 ? 2 : cpq >= 6 ? 1 : 0;
       if (want_scout && p->params.scout > 1) ns = std::min(p->params.scout, MAX_SCOUTS);
@@ -1144,35 +1154,37 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
     if (pre_scouts && nh_req == 0 && p->params.scout == 1 && ns == 2)
       for (int i : act)
         if (!S[i].have_sol) { ns = 4; break; }
-    // twin helpers: occ2 per CU on the CUs the leaders and scouts leave (each of those fills a CU)
-    const int tcap = std::max(0, occ2 * (slots - na * (1 + ns)) / na);
-    if (twin && nh_req == 0) nh = want_scout ? std::min(cap_s, tcap) : std::min(63, tcap);
     // per XCD: the workgroups of a launch are dealt round-robin over the 8 XCDs (blocks b and b + 8 share one), and a
     // workgroup dealt to a full XCD waits there -- a persistent helper that never starts leaves its tiles to the
     // leader's timeout on every job.  plan_kernel puts query q's leader and scouts on XCD slot q % 8, so the fullest
     // XCD holds (1 + ns) ceil(na / 8) of them; the helpers, dealt evenly, get what that XCD leaves, less
     // SMP_XCD_MARGIN CUs (default 1: the two launches race for the CUs).  C5, 8 queries rebalanced to 6 and 4:
     // 39 / 59 helpers each (some never resident) 0.65 M configs/s, 26 each 1.12 M.
-    if (!twin && p->num_cus >= 8) {
-      const int per_xcd = p->num_cus / 8 / std::max(1, p->slot_share);
-      const int plan_max = (1 + ns) * ((na + 7) / 8);
+    // (a device of one XCD has no such round-robin: no cap)
+    const int nx = p->num_xcd;
+    if (nx > 1 && p->num_cus >= nx) {
+      const int per_xcd = p->num_cus / nx / std::max(1, p->slot_share);
+      const int plan_max = (1 + ns) * ((na + nx - 1) / nx);
       const int free_xcd = std::max(0, per_xcd - plan_max - xcd_margin);
-      const int hcap = 8 * free_xcd / na;
+      const int hcap = nx * free_xcd / na;
       // (an explicit request beyond it gets no more than the automatic count either)
       if (nh > hcap) nh = std::max(0, nh_req > 0 ? std::min(hcap, cap_s) : hcap);
+      // scouts need helpers of their own (and the boards' reset needs nh > 0): below four, none (as above)
+      if (nh < 4) { ns = 0; ns_base = 0; }
     }
     // an explicit request larger than what can be resident is clamped to the automatic count: a helper that never
     // starts would leave its tiles to the leader's 8 us timeout on every job (helper sweeps: 250 helpers beside four
     // scouts no longer all start on 256 CUs and stall)
-    if (twin ? nh > tcap : 1 + ns + nh > cpq) {
-      nh = std::max(0, want_scout ? std::min(cap_s, twin ? tcap : cpq - 1 - ns) : std::min(63, twin ? tcap : cpq - 1));
-      if (nh < 4) { ns = 0; nh = std::max(0, std::min(nh, cpq - 1)); twin = false; }
+    if (1 + ns + nh > cpq) {
+      nh = std::max(0, want_scout ? std::min(cap_s, cpq - 1 - ns) : std::min(63, cpq - 1));
+      if (nh < 4) { ns = 0; ns_base = 0; nh = std::max(0, std::min(nh, cpq - 1)); }
     }
     // after the first solution scouts 0 and 1 check choose-parent / rewire candidate batches (many tiles); scouts 2
     // and 3 only work before it, one edge per job (3 tiles); the leader's own jobs (edges no record had) are rare
     auto split = [&](int nsq, int& h_lead, int* h_s) {
       h_lead = 0;
       for (int s = 0; s < MAX_SCOUTS; ++s) h_s[s] = 0;
+      if (nh < 1) return;  // (nh < 4 has no scouts: nothing to split)
       if (nsq > ns_base) {  // a query's pre-solution scouts: their records carry its iterations, one in four each
         const int avail = nh - 1;
         h_lead = avail / pre_lead_div;
@@ -1317,12 +1329,8 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
     HIPCHK(hipEventRecord(p->ev1, p->stream));
     if (nh > 0) {  // the helpers on their own (high-priority, separate hardware queue) stream, after the board reset
       HIPCHK(hipStreamWaitEvent(p->hstream, p->ev_board, 0));
-      if (twin)
-        hipLaunchKernelGGL(helper2_kernel, dim3(na * nh), dim3(BLOCK), 0, p->hstream, p->d_rb, p->sc, p->d_mc,
-                           p->d_qdev.p, na);
-      else
-        hipLaunchKernelGGL(helper_kernel, dim3(na * nh), dim3(BLOCK), 0, p->hstream, p->d_rb, p->sc, p->d_mc,
-                           p->d_qdev.p, na);
+      hipLaunchKernelGGL(helper_kernel, dim3(na * nh), dim3(BLOCK), 0, p->hstream, p->d_rb, p->sc, p->d_mc,
+                         p->d_qdev.p, na);
       HIPCHK(hipGetLastError());
     }
     if (launches == 0) hstamp("kernels launched");
@@ -1338,8 +1346,10 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
         for (int i : act) all = all && host_ttff[i] >= 0;
         if (all) std::this_thread::sleep_for(std::chrono::microseconds(50));
         else std::this_thread::yield();
-        if (tmax > 0 && std::chrono::duration<double>(std::chrono::steady_clock::now() - t_begin).count() > tmax * 4 + 60)
+        if (tmax > 0 && std::chrono::duration<double>(std::chrono::steady_clock::now() - t_begin).count() > tmax * 4 + 60) {
+          p->busy = true;  // the launch still runs on this planner's buffers
           return SMP_ERR_HIP;
+        }
       }
       if (qe != hipSuccess) HIPCHK(qe);
       poll_ttff();
@@ -1522,6 +1532,10 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
 extern "C" int smp_plan_batch(smp_planner* p, const smp_query* qs, int nq, smp_result* out) {
   if (!p || !qs || nq <= 0 || !out) return SMP_ERR_ARG;
   for (int i = 0; i < nq; ++i) std::memset(&out[i], 0, sizeof(smp_result));
+  if (int b_ = busy_check(p)) {
+    for (int i = 0; i < nq; ++i) out[i].status = b_;
+    return b_;
+  }
   std::vector<char> done(nq, 0);
   const int rc = plan_batch_impl(p, qs, nq, out, done);
   // the runtime's last-error slot still holds a failed call's error (e.g. an allocation): clear it, so the next
@@ -1598,6 +1612,7 @@ extern "C" void smp_result_free(smp_result* r) {
 extern "C" int smp_probe_export_tree(smp_planner* p, int which, int32_t* first_child, int32_t* next_sib,
                                      double* e_start, double* e_target) {
   if (!p || p->qb.empty() || which < 0 || which > 1) return SMP_ERR_ARG;
+  if (int b_ = busy_check(const_cast<smp_planner*>(p))) return b_;
   HIPCHK(hipSetDevice(p->device));
   QueryBuffers& b = p->qb[0];
   const size_t cap = b.cap;
@@ -1619,6 +1634,7 @@ extern "C" int smp_probe_export_tree(smp_planner* p, int which, int32_t* first_c
 
 extern "C" int smp_probe_export_state(smp_planner* p, int64_t* iv, double* dv) {
   if (!p || p->qb.empty() || !iv || !dv) return SMP_ERR_ARG;
+  if (int b_ = busy_check(const_cast<smp_planner*>(p))) return b_;
   HIPCHK(hipSetDevice(p->device));
   QState S;
   HIPCHK(hipMemcpy(&S, p->qb[0].st.p, sizeof(QState), hipMemcpyDeviceToHost));
@@ -1707,6 +1723,7 @@ extern "C" int smp_probe_u01(int device, uint64_t seed, uint32_t query, const ui
 
 extern "C" int smp_probe_fk(smp_planner* p, const double* q, int n, double* frames, double* eez) {
   if (!p) return SMP_ERR_ARG;
+  if (int b_ = busy_check(const_cast<smp_planner*>(p))) return b_;
   HIPCHK(hipSetDevice(p->device));
   int nb = p->robot.dev.n_body;
   double *dq, *df, *dz;
@@ -1730,6 +1747,7 @@ extern "C" int smp_probe_fk(smp_planner* p, const double* q, int n, double* fram
 extern "C" int smp_probe_check_latency(smp_planner* p, const double* q_soa, int64_t n, int check_self, int check_map,
                                        int grid, int tile, double* ms, unsigned long long* ticks, double* clock_hz) {
   if (!p || n <= 0 || !q_soa || grid <= 0) return SMP_ERR_ARG;
+  if (int b_ = busy_check(const_cast<smp_planner*>(p))) return b_;
   HIPCHK(hipSetDevice(p->device));
   HIPCHK(p->d_cq.reserve((size_t)n * NJ));
   HIPCHK(p->d_valid.reserve((size_t)n));
@@ -1758,6 +1776,7 @@ extern "C" int smp_probe_check_latency(smp_planner* p, const double* q_soa, int6
 extern "C" int smp_probe_check_shape(smp_planner* p, const double* q_soa, int64_t n, int check_self, int check_map,
                                      int tile, int grid, uint8_t* valid) {
   if (!p || n <= 0 || !q_soa || !valid || grid <= 0) return SMP_ERR_ARG;
+  if (int b_ = busy_check(const_cast<smp_planner*>(p))) return b_;
   if (!(tile == 8 || tile == 16 || tile == 32 || tile == -1 || tile == -2 || tile == -4 || tile == -8)) return SMP_ERR_ARG;
   HIPCHK(hipSetDevice(p->device));
   HIPCHK(p->d_cq.reserve((size_t)n * NJ));

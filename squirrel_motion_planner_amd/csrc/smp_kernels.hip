@@ -261,8 +261,8 @@ struct ScanLds {
   int wi[BLOCK / 64];
 };
 struct MergeLds {
-  unsigned kw[2][SCAN_P][SCAN_K][2];  // [0] lows ascending, [1] highs descending, per participant: key halves
-  int id[2][SCAN_P][SCAN_K];
+  unsigned kw[2][SCAN_PNEAR][SCAN_K][2];  // [0] lows ascending, [1] highs descending, per participant: key halves
+  int id[2][SCAN_PNEAR][SCAN_K];
   int len[SCAN_P], cnt[SCAN_P], done[SCAN_P], bad[SCAN_P];
   unsigned hv[SCAN_P][3];             // collection: near header (count, take) / nearest (key halves, id)
   unsigned long long nk[SCAN_P];      // nearest: per participant (distance key, id)
@@ -306,7 +306,7 @@ constexpr int NEAR_BINS = 256;   // near_set register path: cost histogram bins
 constexpr int NEAR_BUF = 128;    // near_set register path: candidate buffer entries per end
 constexpr int NEAR_NBK = 16;     // near_set register path: 64-node batches per wave held in registers
 #ifndef SMP_PLAN_CT
-#define SMP_PLAN_CT 32
+#define SMP_PLAN_CT 8  // (the local path of a query without helpers, and init_planner's start / goal check)
 #endif
 constexpr int PLAN_CT = SMP_PLAN_CT;  // configurations per collision tile of the planner
 constexpr int PATCH_K = 32;           // leader: recently appended nodes kept in LDS per tree (power of two)
@@ -320,25 +320,30 @@ struct PlanLds {
     JobLds job;  // job mode: the leader's LDS copy of its published job + one job tile
     double seg[MAXE][MAX_PTS][3];
     SmpLds smp;
-    struct {            // a distributed scan (never while a collision job holds u.job)
+  } u;
+  // scan scratch (outside the union u: a scan may run while a collision job holds u.job, overlap_work): a local near set's
+  // lists, or a distributed scan's own slice and merge area -- a scan is one or the other
+  union {
+    struct {
+      struct {  // near_set: per-wave sorted low / high ends of the near list
+        unsigned long long wlk[BLOCK / 64][MAX_NEAR], whk[BLOCK / 64][MAX_NEAR];
+        int wli[BLOCK / 64][MAX_NEAR], whi[BLOCK / 64][MAX_NEAR];
+        int wtot[BLOCK / 64];
+      } nr;
+      struct {  // near_set, register path: cost histogram and the two candidate buffers
+        unsigned hist[NEAR_BINS];
+        unsigned long long ck[2][NEAR_BUF];
+        int ci[2][NEAR_BUF];
+        unsigned long long wmin[BLOCK / 64], wmax[BLOCK / 64];
+        int wtot[BLOCK / 64];
+        int cnt[2], blo, bhi, fast;
+      } nh;
+    };
+    struct {  // a distributed scan (scan_run)
       ScanLds s;
       MergeLds m;
     } sc;
-  } u;
-  // near_set scratch (outside the union: a near set may be computed while a collision job holds u.job)
-  struct {  // near_set: per-wave sorted low / high ends of the near list
-    unsigned long long wlk[BLOCK / 64][MAX_NEAR], whk[BLOCK / 64][MAX_NEAR];
-    int wli[BLOCK / 64][MAX_NEAR], whi[BLOCK / 64][MAX_NEAR];
-    int wtot[BLOCK / 64];
-  } nr;
-  struct {  // near_set, register path: cost histogram and the two candidate buffers
-    unsigned hist[NEAR_BINS];
-    unsigned long long ck[2][NEAR_BUF];
-    int ci[2][NEAR_BUF];
-    unsigned long long wmin[BLOCK / 64], wmax[BLOCK / 64];
-    int wtot[BLOCK / 64];
-    int cnt[2], blo, bhi, fast;
-  } nh;
+  };
   // edge batch
   double eg_start[MAXE][NJ], eg_target[MAXE][NJ], eg_step[MAXE][NJ], eg_end[MAXE][NJ];
   double eg_base[MAXE][3], eg_cost[MAXE][3];
@@ -391,6 +396,9 @@ struct PlanLds {
   long long tit;                // iteration the records belong to
 #endif
   int sp_on, sp_stage, sp_go[2];
+#ifdef SMP_SCAN_PROF
+  unsigned long long spc_t;     // SMP_SCAN_PROF: end of the last scan's collection
+#endif
   int sc_same[MAX_SCOUTS];      // leader: scout s runs on this XCD (1), another (0), not yet known (-1)
   unsigned sc_seen, sc_dead;    // leader: scouts that delivered a pre-solution record / that never did and timed out
   int asked[SCOUT_SLOTS];       // leader: scout s + 1 asked for iteration k in slot k % SCOUT_SLOTS, 0 = none
@@ -557,11 +565,18 @@ __device__ void insert_node(const Ctx& C, int t, const double* e_start, const do
 // squared distance; the (correctly rounded) sqrt is taken only then and compared exactly as the reference does.
 __device__ bool spec_stage(const Ctx& C, int s, unsigned long long wait = 0);
 // Distributed scans (defined with the job protocol below): true if a scan of `nodes` nodes is split over the helpers.
-__device__ __forceinline__ int scan_parts(const Ctx& C, int near) {
-  return uni(min(min(C.Q.nworkers, SCAN_P), near ? C.Q.scan_pnear : C.Q.scan_pnn));
+// Participants of a distributed scan: this workgroup and up to SCAN_P - 1 helpers (SCAN_PNEAR for a near scan).  While a
+// collision job runs (overlap_work), its tiles hold workers 1 .. ntiles and participant p >= 1 is worker W - p: the scan
+// takes the helpers the job leaves free, at least 8 participants (a busy helper takes its slice after its tile).
+// A near scan takes one participant per 4096 nodes (at least 8): its merge and result collection grow with the
+// participants (122 granules each), a nearest result is 3 granules.
+__device__ __forceinline__ int scan_parts(const Ctx& C, int near, int nodes) {
+  int P = min(min(C.Q.nworkers, SCAN_P), near ? min(min(C.Q.scan_pnear, SCAN_PNEAR), max(8, nodes >> 12)) : C.Q.scan_pnn);
+  if (g_L.in_job) P = min(P, max(C.Q.nworkers - g_L.u.job.ntiles, 8));
+  return uni(P);
 }
 __device__ __forceinline__ bool scan_split(const Ctx& C, int nodes) {
-  return uni(C.Q.jb != nullptr && C.Q.scan_min > 0 && nodes >= C.Q.scan_min && C.Q.nworkers >= 8 && !g_L.in_job);
+  return uni(C.Q.jb != nullptr && C.Q.scan_min > 0 && nodes >= C.Q.scan_min && C.Q.nworkers >= 8);
 }
 __device__ int nearest_dist(const Ctx& C, int t, const double* q, int i0, int n, double* d_out);
 __device__ void near_set_dist(const Ctx& C, int t, const double* q, int excl);
@@ -1571,7 +1586,7 @@ __device__ __forceinline__ void edge_validity_job(const Ctx& C, int E, int pslot
   JobBoard* jb = C.Q.jb;
   auto& J = g_L.u.job;
   const int np1 = g_L.S.n_pts + 1;
-  const int W = C.Q.nworkers;
+  const int W = max(1, C.Q.nworkers);  // (a workgroup without helpers takes every tile itself)
   if (threadIdx.x < 64) {
     const int e = threadIdx.x;
     const bool need = e < E && g_L.eg_need[e] && g_L.eg_hit[e] < 0;  // edges the scout checked are not published
@@ -1735,6 +1750,17 @@ __device__ __forceinline__ void edge_validity_job(const Ctx& C, int E, int pslot
 // each slice's answer is its first strict minimum; the near lists take every entry whose rank over all slices' lists
 // is below SCAN_K (an entry beyond a slice's K-th cannot rank below K: K entries are ahead of it).
 constexpr unsigned SCAN_HDR = 1u | 1u << 18;  // edge-count field 1 (33 payload words), scan job bit
+// SMP_SCAN_PROF builds (tools/scan_probe.py): clocks of the distributed scans, summed over every scan of the leader and
+// the scouts, read by smp_debug_scanprof: [0] scans, [1] write-back + publication, [2] own slice, [3] collection,
+// [4] merge, [5] stolen slices, [6] collection rounds, [7] helper slices, [8] helper pickup (publication -> acquire),
+// [9] helper acquire, [10] helper slice, [11] publication -> helper result stored, [12] near scans, [13] their
+// collection, [14] participants, [15] nodes
+#ifdef SMP_SCAN_PROF
+__device__ unsigned long long g_scanprof[16];
+#define SCANPROF_ADD(k, v) atomicAdd(&g_scanprof[k], (unsigned long long)(v))
+#else
+#define SCANPROF_ADD(k, v)
+#endif
 constexpr unsigned long long SCAN_WAIT = 2000;  // device-clock ticks (20 us) without progress before stealing a slice
 
 __device__ __forceinline__ void scan_range(int i0, int n, int P, int w, int* lo, int* hi) {
@@ -1749,7 +1775,7 @@ __device__ void scan_publish(const Ctx& C, int seq, int near, int t, const doubl
                              int P) {
   JobBoard* jb = C.Q.jb;
   const int i = threadIdx.x;
-  if (i < 33) {
+  if (i < SCAN_WORDS) {
     unsigned w = 0;
     if (i == 0) {
       w = SCAN_HDR | (unsigned)near << 19 | (unsigned)t << 20;
@@ -1768,38 +1794,35 @@ __device__ void scan_publish(const Ctx& C, int seq, int near, int t, const doubl
     } else if (i == 22) {
       w = (unsigned)P;
     }
-    st_agent(&jb->pay[i], granule(seq, w));
+    st_agent(&jb->spay[i], granule(seq, w));
   }
 }
 
 // Participant w's slice of a scan, its result as granules of sres[w] (helper) or into the merge area (workgroup).
-// (INL: the slice functions inlined, for the twin helpers)
-template <bool INL = false>
 __device__ void scan_slice(const Ctx& C, int near, int t, const double* q, int i0, int n, int excl, double r, int P, int w,
                            ScanLds& X) {
   const gcdptr tq = uni_gptr(C.Q.tr[t].q), tc = uni_gptr(C.Q.tr[t].cost);
   const int cap = uni(__hip_atomic_load(&C.Q.st->cap, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   int lo, hi;
   scan_range(i0, n, P, w, &lo, &hi);
-  if constexpr (INL) {
-    if (near) slice_near_body(tq, tc, cap, lo, hi, q, excl, r, X);
-    else slice_nn_body(tq, cap, lo, hi, q, X);
-  } else {
-    if (near) slice_near(tq, tc, cap, lo, hi, q, excl, r, X);
-    else slice_nn(tq, cap, lo, hi, q, X);
-  }
+  if (near) slice_near(tq, tc, cap, lo, hi, q, excl, r, X);
+  else slice_nn(tq, cap, lo, hi, q, X);
 }
 
-// Helper side of a scan job already in J.words (seq): its slice, then the result granules.
-template <bool INL>
-__device__ __forceinline__ void scan_helper_body(const Ctx& C, JobLds& J, int w, int seq) {
+// Helper side of a scan job already in J.words (seq): worker w is participant W - w (smp_plan.h SCAN_P); its slice, then
+// the result granules.
+__device__ __noinline__ void scan_helper(const Ctx& C, JobLds& J, int worker, int seq) {
   const unsigned hdr = J.words[0];
   const int near = (hdr >> 19) & 1, t = (hdr >> 20) & 1;
   double q[NJ];
   for (int j = 0; j < NJ; ++j) q[j] = __hiloint2double((int)J.words[2 + 2 * j], (int)J.words[1 + 2 * j]);
   const int i0 = (int)J.words[17], n = (int)J.words[18], excl = (int)J.words[19], P = (int)J.words[22];
   const double r = __hiloint2double((int)J.words[21], (int)J.words[20]);
-  if (w >= P) return;
+  const int w = C.Q.nworkers - worker;
+  if (w < 1 || w >= P) return;
+#ifdef SMP_SCAN_PROF
+  const unsigned long long hp0 = wall_clock64();
+#endif
   // tree words stored by the leader since this CU last cached them: drop stale copies (consumer form: one acquire,
   // its wait, a barrier, then plain loads)
   if (threadIdx.x < 64) {
@@ -1807,8 +1830,18 @@ __device__ __forceinline__ void scan_helper_body(const Ctx& C, JobLds& J, int w,
     drain();
   }
   __syncthreads();
+#ifdef SMP_SCAN_PROF
+  const unsigned long long hp1 = wall_clock64();
+#endif
   ScanLds& X = J.scan;
-  scan_slice<INL>(C, near, t, q, i0, n, excl, r, P, w, X);
+  scan_slice(C, near, t, q, i0, n, excl, r, P, w, X);
+#ifdef SMP_SCAN_PROF
+  if (threadIdx.x == 0) {
+    const unsigned long long hp2 = wall_clock64(), pub = ld_agent(&C.Q.jb->dbg[8]);
+    SCANPROF_ADD(7, 1); SCANPROF_ADD(8, hp0 - pub); SCANPROF_ADD(9, hp1 - hp0); SCANPROF_ADD(10, hp2 - hp1);
+    SCANPROF_ADD(11, hp2 - pub);
+  }
+#endif
   unsigned long long* out = C.Q.jb->sres[w];
   if (!near) {
     if (threadIdx.x == 0) {
@@ -1833,7 +1866,6 @@ __device__ __forceinline__ void scan_helper_body(const Ctx& C, JobLds& J, int w,
   }
   __syncthreads();
 }
-__device__ __noinline__ void scan_helper(const Ctx& C, JobLds& J, int w, int seq) { scan_helper_body<false>(C, J, w, seq); }
 
 // Slot w of the merge area from a slice result in X (all threads).
 __device__ __forceinline__ void merge_put(MergeLds& M, const ScanLds& X, int near, int w) {
@@ -1854,15 +1886,18 @@ __device__ __forceinline__ void merge_put(MergeLds& M, const ScanLds& X, int nea
 }
 
 // Publishes a scan of [i0, n) over P participants, scans slice 0, collects (or steals) the other slices into
-// g_L.u.sc.m.  All threads.
+// g_L.sc.m.  All threads.
 __device__ void scan_run(const Ctx& C, int near, int t, const double* q, int i0, int n, int excl, double r, int P) {
-  MergeLds& M = g_L.u.sc.m;
-  ScanLds& X = g_L.u.sc.s;
+  MergeLds& M = g_L.sc.m;
+  ScanLds& X = g_L.sc.s;
   __syncthreads();
   const int seq = uni(g_L.job_seq) + 1;
   if (threadIdx.x < SCAN_P) { M.done[threadIdx.x] = 0; M.bad[threadIdx.x] = 0; }
   __syncthreads();
   if (threadIdx.x == 0) { g_L.job_seq = seq; M.ndone = 0; }
+#ifdef SMP_SCAN_PROF
+  const unsigned long long sp0 = wall_clock64();
+#endif
   // the helpers read the tree through their own CUs and XCDs: the tree stores (this workgroup's, or the leader's on
   // this XCD for a scout) are written back before the job is published (MI355X_MICROARCH.md producer form)
   drain();
@@ -1872,10 +1907,18 @@ __device__ void scan_run(const Ctx& C, int near, int t, const double* q, int i0,
     drain();
   }
   __syncthreads();
+#ifdef SMP_SCAN_PROF
+  const unsigned long long sp1 = wall_clock64();
+  if (threadIdx.x == 0) st_agent(&C.Q.jb->dbg[8], sp1);
+#endif
   scan_publish(C, seq, near, t, q, i0, n, excl, r, P);
   scan_slice(C, near, t, q, i0, n, excl, r, P, 0, X);
   merge_put(M, X, near, 0);
   __syncthreads();
+#ifdef SMP_SCAN_PROF
+  const unsigned long long sp2 = wall_clock64();
+  int sp_rounds = 0, sp_steals = 0;
+#endif
   const JobBoard* jb = C.Q.jb;
   unsigned long long t_prog = wall_clock64();
   int last_done = 0;
@@ -1968,29 +2011,47 @@ __device__ void scan_run(const Ctx& C, int near, int t, const double* q, int i0,
     }
     __syncthreads();
     const int go = uni(M.go[k]);
+#ifdef SMP_SCAN_PROF
+    ++sp_rounds;
+#endif
     if (go == 1) break;
     if (go == 2) {
       const int w = uni(M.steal);
       scan_slice(C, near, t, q, i0, n, excl, r, P, w, X);
       merge_put(M, X, near, w);
       if (threadIdx.x == 0) { M.ndone++; t_prog = wall_clock64(); }
+#ifdef SMP_SCAN_PROF
+      ++sp_steals;
+#endif
       __syncthreads();
       continue;
     }
     __builtin_amdgcn_s_sleep(1);
   }
   __syncthreads();
+#ifdef SMP_SCAN_PROF
+  if (threadIdx.x == 0) {
+    const unsigned long long sp3 = wall_clock64();
+    SCANPROF_ADD(0, 1); SCANPROF_ADD(1, sp1 - sp0); SCANPROF_ADD(2, sp2 - sp1); SCANPROF_ADD(3, sp3 - sp2);
+    SCANPROF_ADD(5, sp_steals); SCANPROF_ADD(6, sp_rounds); SCANPROF_ADD(14, P); SCANPROF_ADD(15, n - i0);
+    if (near) { SCANPROF_ADD(12, 1); SCANPROF_ADD(13, sp3 - sp2); }
+    g_L.spc_t = sp3;
+  }
+#endif
 }
 
 __device__ int nearest_dist(const Ctx& C, int t, const double* q, int i0, int n, double* d_out) {
-  const int P = scan_parts(C, 0);
+  const int P = scan_parts(C, 0, n - i0);
   scan_run(C, 0, t, q, i0, n, -1, 0.0, P);
-  const MergeLds& M = g_L.u.sc.m;
+  const MergeLds& M = g_L.sc.m;
   unsigned long long bk = M.nk[0];
   int bi = M.ni[0];
   for (int w = 1; w < P; ++w)
     if (M.nk[w] < bk || (M.nk[w] == bk && M.ni[w] < bi)) { bk = M.nk[w]; bi = M.ni[w]; }
   __syncthreads();
+#ifdef SMP_SCAN_PROF
+  if (threadIdx.x == 0) SCANPROF_ADD(4, wall_clock64() - g_L.spc_t);
+#endif
   *d_out = __longlong_as_double((long long)bk);
   return bi;
 }
@@ -2000,9 +2061,9 @@ __device__ int nearest_dist(const Ctx& C, int t, const double* q, int i0, int n,
 // search.  Threads [0, 256) the low lists, [256, 512) the high lists, candidates strided.
 __device__ void near_set_dist(const Ctx& C, int t, const double* q, int excl) {
   const int n = uni(g_L.S.n[t]);
-  const int P = scan_parts(C, 1);
+  const int P = scan_parts(C, 1, n);
   scan_run(C, 1, t, q, 0, n, excl, g_L.S.near_r, P);
-  const MergeLds& M = g_L.u.sc.m;
+  const MergeLds& M = g_L.sc.m;
   int tot = 0;
   for (int w = 0; w < P; ++w) tot += M.cnt[w];
   tot = uni(tot);
@@ -2042,6 +2103,9 @@ __device__ void near_set_dist(const Ctx& C, int t, const double* q, int excl) {
   }
   if (threadIdx.x == 0) { g_L.nk = tot; g_L.n_lo = take; g_L.n_hi = take; g_L.S.near_nodes += n; }
   __syncthreads();
+#ifdef SMP_SCAN_PROF
+  if (threadIdx.x == 0) SCANPROF_ADD(4, wall_clock64() - g_L.spc_t);
+#endif
 }
 
 #ifndef SMP_HELPER_SLEEP
@@ -2050,45 +2114,41 @@ __device__ void near_set_dist(const Ctx& C, int t, const double* q, int excl) {
 #ifndef SMP_POLL_N
 #define SMP_POLL_N 128  // payload granules read by an idle helper's poll (64 per wave-0 load instruction)
 #endif
-// Helper workgroup w (1 .. W-1): wave 0 polls the first SMP_POLL_N payload granules of its query's board (two per
-// lane: a header and three edges, so the pre-solution scouts' expand + connect jobs arrive within the poll); a new job
-// is taken once every granule it needs carries the header's job number (longer payloads take one more read).  Then
-// tiles w - 1, w - 1 + W, ... of the job, each result stored as one granule.  Leaves on the stop flag, or after two
-// idle seconds should the leader never start.
-// INL: the scan slice inlined (the twin helpers' kernel: a call would be compiled for the full register file).
-template <bool INL>
+// Helper workgroup w (1 .. W-1): wave 0 polls the first SMP_POLL_N payload granules of its board's collision job (two
+// per lane: a header and three edges, so the pre-solution scouts' expand + connect jobs arrive within the poll) and the
+// scan job's granules (one per lane); a job is taken once every granule it needs carries its header's job number (a
+// longer collision payload takes one more read).  A new scan job goes first -- its publisher collects the slices before
+// its collision job's tiles (overlap_work) -- and this helper scans its slice if it is a participant (scan_helper).  Then
+// tiles w - 1, w - 1 + W, ... of a collision job, each result stored as one granule.  Leaves on the stop flag, or after
+// two idle seconds should the leader never start.
 __device__ __forceinline__ void helper_main(const Ctx& C, int hidx, JobLds& J) {
   JobBoard* jb = C.Q.jb;
   const int w = 1 + hidx, W = C.Q.nworkers;
-  int last = 0;
+  int last = 0, last_scan = 0;
   unsigned long long t_last = wall_clock64();
   constexpr int PU = SMP_POLL_N / 64;
   static_assert(PU >= 1 && PU * 64 <= JOB_WORDS, "poll width");
+  static_assert(SCAN_WORDS <= 64, "a scan payload is one granule per lane");
   for (int k = 0;; k ^= 1) {
-    // 0 = nothing new, > 0 = job number complete in J.words, -1 = leave, -2 = payload longer than the poll
+    // 0 = nothing new, > 0 = collision job number complete in J.words, -1 = leave, -2 = collision payload longer than
+    // the poll, -3 = scan job complete in J.words
     if (threadIdx.x < 64) {
       unsigned long long v[PU];
-#ifdef SMP_POLL_HDR
-      // experiments: poll the header granule alone (one request per poll), then the payload in a second round
-      {
-        const unsigned long long h = ld_agent(&jb->pay[0]);
-        const unsigned t = __builtin_amdgcn_readfirstlane((unsigned)(h >> 32));
-        if (t != 0 && (int)t != last) {
-#pragma unroll
-          for (int u = 0; u < PU; ++u) v[u] = ld_agent(&jb->pay[u * 64 + threadIdx.x]);
-        } else {
-#pragma unroll
-          for (int u = 0; u < PU; ++u) v[u] = h;
-        }
-      }
-#else
 #pragma unroll
       for (int u = 0; u < PU; ++u) v[u] = ld_agent(&jb->pay[u * 64 + threadIdx.x]);
-#endif
+      const unsigned long long sv = ld_agent(&jb->spay[threadIdx.x]);
+      const unsigned stag = __builtin_amdgcn_readfirstlane((unsigned)(sv >> 32));
       const unsigned tag0 = __builtin_amdgcn_readfirstlane((unsigned)(v[0] >> 32));
       const unsigned hdr = __builtin_amdgcn_readfirstlane((unsigned)v[0]);
       int go = 0;
-      if (tag0 != 0 && (int)tag0 != last) {
+      if (stag != 0 && (int)stag != last_scan) {
+        const bool stale = (int)threadIdx.x < SCAN_WORDS && (unsigned)(sv >> 32) != stag;
+        if (!__ballot(stale)) {
+          if ((int)threadIdx.x < SCAN_WORDS) J.words[threadIdx.x] = (unsigned)sv;
+          go = -3;
+        }
+      }
+      if (go == 0 && tag0 != 0 && (int)tag0 != last) {
         const int nw = 1 + 32 * (int)(hdr & 255);
         bool stale = false;
 #pragma unroll
@@ -2103,7 +2163,7 @@ __device__ __forceinline__ void helper_main(const Ctx& C, int hidx, JobLds& J) {
       if (threadIdx.x == 0) {
         if (go == 0 && (ld_agent(&jb->stop) || wall_clock64() - t_last > 200000000ull)) go = -1;  // 2 s idle
         J.go[k] = go;
-        J.seq = (int)tag0;
+        J.seq = go == -3 ? (int)stag : (int)tag0;
       }
     }
     __syncthreads();
@@ -2114,14 +2174,13 @@ __device__ __forceinline__ void helper_main(const Ctx& C, int hidx, JobLds& J) {
       continue;
     }
     const int seq = uni(J.seq);
-    const unsigned hdr = J.words[0];
-    if (uni((int)((hdr >> 18) & 1u))) {  // scan job: this helper's slice (the payload fits the first poll)
-      if constexpr (INL) scan_helper_body<true>(C, J, w, seq);
-      else scan_helper(C, J, w, seq);
-      last = seq;
+    if (go == -3) {  // scan job: this helper's slice, if it is a participant
+      scan_helper(C, J, w, seq);
+      last_scan = seq;
       t_last = wall_clock64();
       continue;
     }
+    const unsigned hdr = J.words[0];
     const int ne = min((int)(hdr & 255), MAXE), nw = 1 + 32 * ne;
     if (go == -2) {
       // the rest of a long payload (one read; granules not yet current abandon the job to the next poll, which
@@ -3342,8 +3401,9 @@ __device__ void rewire(const Ctx& C, int t) {
         const int v = g_L.eg_near[e];
         double red[3];
         for (int k = 0; k < 3; ++k) red[k] = g_L.eg_cost[e][k] - g_L.rw_cost[e][k];
-        // early asks: every scout learns that tree t changes before any of this commit's stores can be seen
-        const bool pub = C.Q.nscouts >= 2;
+        // early asks: every scout learns that tree t changes before any of this commit's stores can be seen (without
+        // early asks no record is asked for before its tree's rewires are done: nothing to publish)
+        const bool pub = C.Q.early_ask && C.Q.nscouts >= 2;
         if (pub) {
           // (the iteration's earlier stores, its `cur` for the scouts among them, are performed first: a scout that
           // sees the commit also sees that the leader is at this iteration, whose own commits need no rebuild)
@@ -4074,7 +4134,9 @@ __device__ bool sc_stale(const Ctx& C, unsigned tag) {
 // True (block-uniform) if the leader began a rewire commit on the pass's tree since the pass read it (early asks): the
 // pass stops and scout_main rebuilds it on the tree as it is now.
 __device__ bool sc_moved(const Ctx& C) {
-  // (once the leader is at the pass's iteration, the commits are its own, after it took the record's stages)
+  // (once the leader is at the pass's iteration, the commits are its own, after it took the record's stages; without
+  // early asks the leader publishes no rewire commits: rwb / rwe keep their launch-start values)
+  if (!C.Q.early_ask) return false;
   if (threadIdx.x == 0)
     g_L.sc_rerun = (ld_agent(&C.Q.scb->rwb[g_L.sc_t]) & 0xfffu) != g_L.sc_mod &&
                    (long long)ld_agent(&C.Q.scb->cur) < g_L.sc_k;
@@ -4673,7 +4735,7 @@ __device__ __forceinline__ void scout_main(Ctx& C, int which) {
           g_L.nn_t = (int)(unsigned)r1;       // sampler parameter version | rewire commits of tree t << 20
           g_L.found = (int)(unsigned)r2;      // XB
           g_L.tree_expand = (int)tag;
-        } else if (last && ((l_w0 >> 29) & 1u) &&
+        } else if (last && C.Q.early_ask && ((l_w0 >> 29) & 1u) &&
                    (ld_agent(&C.Q.scb->rwb[(l_w0 >> 28) & 1u]) & 0xfffu) != g_L.sc_mod &&
                    (long long)ld_agent(&C.Q.scb->cur) < (long long)last - 1) {
           go = 2;  // the last record's tree was rewired after it was built: rebuild it
@@ -4735,7 +4797,7 @@ __device__ __forceinline__ void scout_main(Ctx& C, int which) {
     const unsigned long long tb = wall_clock64();
     if (threadIdx.x == 0) g_L.S.prof[28] += tb - t_last;  // idle: waiting for a request
     for (;;) {  // the pass, rebuilt while the leader rewires its tree under it
-      if (opt) {
+      if (opt && C.Q.early_ask) {
         // the tree as the leader left it: a begun rewire commit is waited for until its words are stored
         int st = 0;
         for (int r = 0;; r ^= 1) {
@@ -5015,13 +5077,10 @@ union HelperLds {
   SamplerLds S;
 };
 
-// OCC = 1: one helper workgroup per CU (the full register file: the lowest tile latency, for a query with helpers to
-// spare).  OCC = 2: twin helpers, two workgroups per CU (128 registers, LDS under half a CU's; every call inlined),
-// for many queries sharing the CUs: a tile is a chain of dependent loads, and the second workgroup's waves run in
-// the first's load shadows (DESIGN.md "Twin helpers").
-template <int OCC>
-__device__ __forceinline__ void helper_entry(const RobotDev* __restrict__ rb, SceneDev sc, const MapCfg* __restrict__ mc,
-                                             QueryDev* qs, int nq) {
+// Helper blocks (gridDim = nq * helpers): block b serves query b % nq -- the leader's tile helpers first, then each
+// scout's, the run-ahead sampler last; one helper workgroup per CU (the full register file: the lowest tile latency).
+__global__ void __launch_bounds__(BLOCK) helper_kernel(const RobotDev* __restrict__ rb, SceneDev sc,
+                                                       const MapCfg* __restrict__ mc, QueryDev* qs, int nq) {
   __shared__ HelperLds H;
   // the block's context and role in LDS (see plan_kernel): -1 nothing to do, -2 run-ahead sampler, else tile helper h
   __shared__ Ctx g_ctx;
@@ -5054,63 +5113,10 @@ __device__ __forceinline__ void helper_entry(const RobotDev* __restrict__ rb, Sc
   const int role = uni(g_role);
   if (role == -1) return;
   if (role == -2) {
-    if constexpr (OCC == 2) sampler_body(g_ctx, H.S);
-    else sampler_main(g_ctx, H.S);
+    sampler_main(g_ctx, H.S);
     return;
   }
-  helper_main<OCC == 2>(g_ctx, role, H.J);
-}
-
-#ifdef SMP_OLD_HELPER_KERNEL
-__global__ void __launch_bounds__(BLOCK) helper_kernel(const RobotDev* __restrict__ rb, SceneDev sc,
-                                                       const MapCfg* __restrict__ mc, QueryDev* qs, int nq) {
-  __shared__ JobLds J;
-  __shared__ SamplerLds SL;
-  __shared__ Ctx g_ctx;
-  __shared__ int g_role;
-  if (threadIdx.x == 0) {
-    Ctx c;
-    c.sc = sc;
-    c.Q = qs[blockIdx.x % nq];
-    const int hidx = (int)blockIdx.x / nq, nh = (int)gridDim.x / nq;
-    int role = hidx;
-    if (!c.Q.jb) {
-      role = -1;
-    } else if (c.Q.sampler && hidx == nh - 1) {
-      role = -2;
-    } else if (role >= c.Q.nworkers - 1) {
-      role -= c.Q.nworkers - 1;
-      int s = 0;
-      for (; s < c.Q.nscouts && role >= c.Q.sworkers_s[s] - 1; ++s) role -= c.Q.sworkers_s[s] - 1;
-      if (s >= c.Q.nscouts) {
-        role = -1;
-      } else {
-        c.Q.jb = c.Q.sjbs[s];
-        c.Q.nworkers = c.Q.sworkers_s[s];
-      }
-    }
-    g_ctx = c;
-    g_role = role;
-  }
-  stage_model(rb, mc, &g_rb, &g_mc);
-  const int role = uni(g_role);
-  if (role == -1) return;
-  if (role == -2) {
-    sampler_main(g_ctx, SL);
-    return;
-  }
-  helper_main<false>(g_ctx, role, J);
-}
-#else
-__global__ void __launch_bounds__(BLOCK) helper_kernel(const RobotDev* __restrict__ rb, SceneDev sc,
-                                                       const MapCfg* __restrict__ mc, QueryDev* qs, int nq) {
-  helper_entry<1>(rb, sc, mc, qs, nq);
-}
-#endif
-// (launch bounds: BLOCK threads, 4 waves per SIMD = two workgroups per CU)
-__global__ void __launch_bounds__(BLOCK, 4) helper2_kernel(const RobotDev* __restrict__ rb, SceneDev sc,
-                                                           const MapCfg* __restrict__ mc, QueryDev* qs, int nq) {
-  helper_entry<2>(rb, sc, mc, qs, nq);
+  helper_main(g_ctx, role, H.J);
 }
 
 // Fresh job / scout boards for a launch (all zero: no granule carries a job number, no stop flag): block b clears
@@ -5229,6 +5235,20 @@ extern "C" int smp_debug_tlog(unsigned long long* out, int cap, int reset) {
 }
 #else
 extern "C" int smp_debug_tlog(unsigned long long*, int, int) { return -1; }
+#endif
+
+#ifdef SMP_SCAN_PROF
+extern "C" int smp_debug_scanprof(unsigned long long* out, int reset) {
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(smp::g_scanprof), 16 * sizeof(unsigned long long)) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(smp::g_scanprof), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#else
+extern "C" int smp_debug_scanprof(unsigned long long*, int) { return -1; }
 #endif
 
 #ifdef SMP_PRE_VERIFY

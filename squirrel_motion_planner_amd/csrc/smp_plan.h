@@ -98,8 +98,13 @@ constexpr int SMP_RING = 16;                     // run-ahead sampler: samples k
 // over itself and up to SCAN_P - 1 of its helpers; participant w's partial result is SCAN_W granules of sres[w]:
 // nearest: key low / high half, id; near set: count, list lengths (lo | hi << 16), then per entry of the low and the
 // high list (key low half, key high half, id).
+// Participant p >= 1 of a scan is worker W - p (W = the workgroup's workers: the helpers from the top down), so that a scan
+// published while a collision job runs (the job's tiles go to workers 1, 2, ... from the bottom up) takes the helpers the
+// job leaves free.  A near scan has at most SCAN_PNEAR participants (its merge ranks every list entry).
 constexpr int SCAN_P = 64;
+constexpr int SCAN_PNEAR = 32;
 constexpr int SCAN_W = 2 + 2 * 3 * MAX_NEAR;
+constexpr int SCAN_WORDS = 33;  // payload granules of a scan job (JobBoard::spay)
 // Tag of the run-ahead sampler's ring granules: iteration (low 24 bits) and parameter version (low 8 bits).  A slot
 // holds only iteration i (mod SMP_RING) and the version changes at most once per iteration, so the short fields
 // cannot alias within a run of fewer than 2^24 iterations.
@@ -127,6 +132,10 @@ struct JobBoard {
   // helpers -> leader: tile t's collision mask (bit c = configuration c of the tile collides)
   unsigned long long res[JOB_TILES];
   int pad2[32 - (2 * JOB_TILES) % 32];
+  // leader -> helpers: a scan job (DESIGN.md "Scans of large trees"), in its own granules beside `pay`, so that a scan may
+  // run while a collision job holds `pay`: word 0 = header (scan bit << 18 | near << 19 | tree << 20), words 1-16 the
+  // query configuration's halves, 17 range start, 18 range end, 19 excluded id, 20-21 radius halves, 22 participants
+  unsigned long long spay[64];
   // run-ahead sampler (DESIGN.md "Sampler").  Leader -> sampler: its current iteration and the informed-
   // sampling parameters, versioned (payload stores drained before the version store).
   int s_ver, s_have_sol;

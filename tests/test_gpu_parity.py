@@ -512,9 +512,11 @@ def test_check_sequence_fold_keyframes(gp, orobot):
     gp.set_disabled_map_links([])
     orc = O.Oracle(orobot, O.OracleScene(keys, 0.05))
     # every keyframe, untrimmed.  The stowed end of the trajectory (the tuw file's first keyframes, arm_joint2 2.26 rad)
-    # rests the fingers inside the front shell's exact box (robotino_plan.urdf:323-329): in self-collision for the
-    # reference too -- its FCL box against the finger meshes of squirrel-hand.dae (tools/gen_robot_model.py validate
-    # counts the mesh vertices inside the box).  GPU and oracle agree pose by pose and name the same pairs.
+    # rests the fingers inside the front shell's exact box of robotino_plan.urdf (:323-329), so under this collision
+    # model (that URDF's primitives + the finger covers of squirrel-hand.dae) they are in self-collision.  Whether the
+    # reference agrees is UNPINNED: the deployed launch file does not load robotino_plan.urdf (planner.launch:14 is
+    # commented out), FCL is absent, and the reference ships no vectors for it.  What is asserted is GPU == oracle, pose
+    # by pose and pair by pair.
     poses0 = np.array([[0.0, 0.0, 0.0] + list(a) for a in arm])
     ok_self = orc.check_configs(poses0, True, False)
     assert ok_self[0] == 0 and ok_self[-1] == 1, ok_self
@@ -550,10 +552,12 @@ def test_check_sequence_fold_keyframes(gp, orobot):
 
 # ------------------------------------------------------------------------------------------ C1 as SURVEY specifies it
 def test_c1_survey_start_is_in_self_collision(gp, orobot):
-    """SURVEY C1's start -- the first tuw folding keyframe -- puts the fingers inside the front shell's exact box
-    (robotino_plan.urdf:323-329; the finger meshes of squirrel-hand.dae enter it too, tools/gen_robot_model.py
-    validate): init_planner refuses it (birrt_star.cpp:353-357) on the GPU and in the oracle alike, with the same
-    collision listing.  The planning C1 cases start from pose_folded_arm instead (scenes.empty_room)."""
+    """SURVEY C1's start -- the first tuw folding keyframe -- puts the fingers inside the front shell's exact box of
+    robotino_plan.urdf (:323-329; the finger meshes of squirrel-hand.dae enter it too, tools/gen_robot_model.py
+    validate): under this collision model init_planner refuses it (birrt_star.cpp:353-357) on the GPU and in the oracle
+    alike, with the same collision listing.  The reference's own behaviour for this start is UNPINNED: its deployed launch
+    file does not load robotino_plan.urdf (planner.launch:14 is commented out) and FCL is absent here.  The planning C1
+    cases start from pose_folded_arm instead (scenes.empty_room)."""
     sc = scenes.empty_room(stowed=True)
     gs = Scene.from_keys(sc.keys, sc.res)
     gp.set_scene(gs)

@@ -7,6 +7,6 @@ HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
 run() { local name=$1; shift; timeout -k 10 "$@"; local rc=$?; echo "$name rc=$rc" >> $OUT/status.txt
         case $rc in 124|134|137|139) exit $rc;; esac; }
-run q4 200 env SMP_QSEL=1,2,4,7 SMP_SCOUT=4 python -u tools/batch_probe.py > $OUT/q4s4.txt 2>&1
-run q6 200 env SMP_QSEL=1,2,4,7 SMP_SCOUT=6 python -u tools/batch_probe.py > $OUT/q4s6.txt 2>&1
-run q8 200 env SMP_QSEL=1,2,4,7 SMP_SCOUT=8 python -u tools/batch_probe.py > $OUT/q4s8.txt 2>&1
+run scans 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_tree_scans.py > $OUT/r05_t_scans.txt 2>&1
+run perf 300 python -u tools/perf_probe.py 4000 100000 200000 > $OUT/r05_perf_s1.txt 2>&1
+run gpu 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests > $OUT/r05_t_gpu.txt 2>&1
