@@ -219,11 +219,13 @@ def cpu_many_queries(a, pairs, seed, procs, gpu_results):
     busy = [sum(x[4] for x in part) for part in res]
     span = max(busy)
     checked = sum(x[1] for x in flat)
+    used = len(res)  # processes that planned something: min(procs, queries)
     same = all(x[1] == r["configs_checked"] and x[2] == r["iterations"] for x, r in zip(flat, gpu_results))
-    return {"value": checked / span, "unit": "configs/s", "cores": procs, "processes": procs,
+    return {"value": checked / span, "unit": "configs/s", "cores": used, "processes": used,
             "queries": len(flat), "checked": checked, "span_s": span,
-            "how": "%d independent oracle processes (one thread each), the %d queries dealt round-robin; value = all "
-                   "configurations checked / the busiest process's planning time" % (procs, len(flat)),
+            "how": "%d independent oracle processes (one thread each) of the %d cores available, the %d queries dealt "
+                   "round-robin; value = all configurations checked / the busiest process's planning time" % (
+                       used, procs, len(flat)),
             "same_results_as_gpu_step0": bool(same)}
 
 
@@ -251,6 +253,12 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
+        ndev = max(1, torch.cuda.device_count())
+        if ndev < world:
+            # more ranks than GPUs (a rehearsal on a one-GPU box): ranks share a GPU, each planner provisions its share
+            # of the device's co-resident workgroups (read when the planner is created)
+            os.environ["SMP_SLOT_SHARE"] = str((world + ndev - 1) // ndev)
+        local = local % ndev
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
@@ -297,45 +305,52 @@ def main():
     for w in range(a.warmup):
         gp.plan_batch(queries(-1 - w, a.warmup_samples or a.samples))
 
-    totals = dict(checked=0, valid=0, iters=0, nn=0, near=0, plan_ms=0.0, launches=0)
-    first_t, first_host = [], []
-    step0 = None
-    step0_all = None
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for step in range(a.steps):
-        rs = gp.plan_batch(queries(step, a.samples))
-        if step0 is None:
-            step0 = rs[0]
-            step0_all = rs
-        for r in rs:
-            if r["status"] not in (0, -4):
-                raise RuntimeError("plan failed with status %d" % r["status"])
-            totals["checked"] += r["configs_checked"]
-            totals["valid"] += r["configs_valid"]
-            totals["iters"] += r["iterations"]
-            totals["nn"] += r["nn_nodes_scanned"]
-            totals["near"] += r["near_nodes_scanned"]
-            if r["time_first_solution"] >= 0:
-                first_t.append(r["time_first_solution"])
-                first_host.append(r["time_first_solution_host"])
-        _, pms, nl = gp.last_kernel_ms()
-        totals["plan_ms"] += pms
-        totals["launches"] += nl
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    def timed_steps(sync_ranks=True):
+        """The timed region: exactly a.steps planning steps of this rank's queries, bracketed by a barrier (several
+        ranks; not for rank 0's run alone) and a device synchronisation on both sides."""
+        totals = dict(checked=0, valid=0, iters=0, nn=0, near=0, plan_ms=0.0, launches=0)
+        first_t, first_host, steps0 = [], [], []
+        if world > 1 and sync_ranks:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for step in range(a.steps):
+            rs = gp.plan_batch(queries(step, a.samples))
+            if not steps0:
+                steps0.append(rs)
+            for r in rs:
+                if r["status"] not in (0, -4):
+                    raise RuntimeError("plan failed with status %d" % r["status"])
+                totals["checked"] += r["configs_checked"]
+                totals["valid"] += r["configs_valid"]
+                totals["iters"] += r["iterations"]
+                totals["nn"] += r["nn_nodes_scanned"]
+                totals["near"] += r["near_nodes_scanned"]
+                if r["time_first_solution"] >= 0:
+                    first_t.append(r["time_first_solution"])
+                    first_host.append(r["time_first_solution_host"])
+            _, pms, nl = gp.last_kernel_ms()
+            totals["plan_ms"] += pms
+            totals["launches"] += nl
+        torch.cuda.synchronize()
+        if world > 1 and sync_ranks:
+            dist.barrier()
+        return time.perf_counter() - t0, totals, steps0[0], first_t, first_host
+
+    elapsed, totals, step0_all, first_t, first_host = timed_steps()
+    step0 = step0_all[0]
 
     local_vec = [elapsed, totals["checked"], totals["valid"], totals["iters"], totals["nn"], totals["near"],
                  totals["plan_ms"], totals["launches"]]
+    alone = None
     if world > 1:
         tsum, tmax = D.reduce_counters(local_vec, device="cuda")
         elapsed = tmax[0]
         checked, valid, iters, nn, near, plan_ms, launches = tsum[1:]
         plan_ms_rank0 = totals["plan_ms"]
+        # the same per-GPU share on rank 0's GPU alone (the other ranks at a barrier): the single-GPU rate of THIS
+        # workload, so that the line carries its own scaling efficiency (the N = 1 line of a scaling run is C2)
+        alone = D.single_rank_reference(lambda: timed_steps(sync_ranks=False), rank)
     else:
         checked, valid, iters, nn, near, plan_ms, launches = local_vec[1:]
         plan_ms_rank0 = plan_ms
@@ -409,6 +424,11 @@ def main():
                          "launches_rank0": totals["launches"],
                          "algorithmic_bytes_rank0": alg_bytes_rank0},
         }
+        if alone is not None:
+            out.update(D.scaling_fields(checked / elapsed, world, (alone[1]["checked"], alone[0])))
+            out["single_gpu_same_workload"]["how"] = (
+                "rank 0 planned its own per-GPU share (the same %d queries, seeds and budgets) again alone, the other "
+                "ranks waiting at a barrier" % len(mine))
         if not a.no_cpu and world == 1 and a.workload == "c2" and a.iterations and a.iterations > a.cpu_iterations:
             out["cpu_baseline"] = cpu_window(a, gp, sc, pairs[0], a.seed, step0)
         elif not a.no_cpu and world == 1:

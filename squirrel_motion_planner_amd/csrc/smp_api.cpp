@@ -150,6 +150,9 @@ struct smp_planner {
   int last_n[2] = {0, 0};
   int slots_cache = 0;  // resident_slots (occupancy queries) once per planner
   int slot_share = 1;   // planners planning on this planner's GPU at once (smp_plan_multi): its share of the slots
+  // processes planning on this GPU at once (SMP_SLOT_SHARE, e.g. several ranks of one job on a one-GPU box): every
+  // workgroup of a query must be co-resident, so each process provisions its share of the device
+  int proc_share = 1;
   // a planning call gave up (SMP_ERR_HIP) while its kernels may still run on these buffers: every later call that
   // would touch them fails with SMP_ERR_HIP until both streams are idle again (busy_check), and destroy leaks them
   // rather than freeing memory a live kernel uses
@@ -439,6 +442,8 @@ int smp_planner_create(int device, const smp_robot* robot, const smp_params* par
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
     p->num_cus = cus;
+  if (const char* e = std::getenv("SMP_SLOT_SHARE")) p->proc_share = std::max(1, std::atoi(e));
+  p->slot_share = p->proc_share;
   int xcc = 0;
   if (hipDeviceGetAttribute(&xcc, hipDeviceAttributeNumberOfXccs, device) == hipSuccess && xcc > 0) p->num_xcd = xcc;
   else (void)hipGetLastError();
@@ -1574,7 +1579,7 @@ extern "C" int smp_plan_multi(smp_planner* const* ps, int np, const smp_query* q
   for (int k = 0; k < used; ++k) {
     int same = 0;
     for (int j = 0; j < used; ++j) same += ps[j]->device == ps[k]->device;
-    ps[k]->slot_share = same;
+    ps[k]->slot_share = same * ps[k]->proc_share;
   }
   std::vector<std::thread> th;
   th.reserve(used);
@@ -1583,7 +1588,7 @@ extern "C" int smp_plan_multi(smp_planner* const* ps, int np, const smp_query* q
     th.emplace_back([&, k] { rcs[k] = smp_plan_batch(ps[k], part[k].data(), (int)part[k].size(), res[k].data()); });
   }
   for (auto& t : th) t.join();
-  for (int k = 0; k < used; ++k) ps[k]->slot_share = 1;
+  for (int k = 0; k < used; ++k) ps[k]->slot_share = ps[k]->proc_share;
   int rc = SMP_OK;
   for (int i = 0; i < nq; ++i) {
     out[i] = res[i % used][i / used];
@@ -1812,7 +1817,8 @@ extern "C" int smp_probe_sqrt_div(int device, const double* a, const double* b, 
 extern "C" int smp_probe_near(int device, const double* q_soa, const double* cost, int n, const double* queries,
                               const int* excl, int m, double r, int reps, int* nn, int* nk, int* lo, int* hi,
                               unsigned long long* ticks, double* clock_hz) {
-  if (n <= 0 || m <= 0 || reps <= 0 || !q_soa || !cost || !queries || !excl) return SMP_ERR_ARG;
+  // reps < 0: the distributed scans' slice functions over the whole tree (tools/slice_probe.py)
+  if (n <= 0 || m <= 0 || reps == 0 || !q_soa || !cost || !queries || !excl) return SMP_ERR_ARG;
   if (hipSetDevice(device) != hipSuccess) return SMP_ERR_NO_DEVICE;
   double *dq, *dc, *dqq;
   int *dx, *dnn, *dnk, *dlo, *dhi;

@@ -249,9 +249,23 @@ __global__ void sqrt_div_kernel(const double* a, const double* b, int n, double*
 // lists of the near scan, the slice's merged lists, the nearest reduction); MergeLds: every participant's partial
 // result as the leader collects and merges them.
 constexpr int SCAN_K = 20;  // near-list ends a scan keeps (near_set<20>; max_near_nodes <= 20)
+constexpr int NEAR_BINS = 256;   // near_set register path: cost histogram bins
+constexpr int NEAR_BUF = 128;    // near_set register path: candidate buffer entries per end
+constexpr int NEAR_NBK = 16;     // near_set register path: 64-node batches per wave held in registers
 struct ScanLds {
-  unsigned long long wlk[BLOCK / 64][SCAN_K], whk[BLOCK / 64][SCAN_K];
-  int wli[BLOCK / 64][SCAN_K], whi[BLOCK / 64][SCAN_K];
+  union {
+    struct {  // slice_near_body (per-wave sorted lists)
+      unsigned long long wlk[BLOCK / 64][SCAN_K], whk[BLOCK / 64][SCAN_K];
+      int wli[BLOCK / 64][SCAN_K], whi[BLOCK / 64][SCAN_K];
+    };
+    struct {  // slice_near_hist (near_set's register path): cost histogram and the two candidate buffers
+      unsigned hist[NEAR_BINS];
+      unsigned long long ck[2][NEAR_BUF];
+      int ci[2][NEAR_BUF];
+    };
+  };
+  unsigned long long hmin[BLOCK / 64], hmax[BLOCK / 64];
+  int hcnt[2], hblo, hbhi, fast;
   int wtot[BLOCK / 64];
   unsigned long long blo, bhi;                       // near_batch's block bounds
   unsigned long long lk[SCAN_K], hk[SCAN_K];        // the slice's lowest (ascending) / highest (descending) entries
@@ -302,9 +316,6 @@ struct SmpLds {
   int ok[64];
   int win;
 };
-constexpr int NEAR_BINS = 256;   // near_set register path: cost histogram bins
-constexpr int NEAR_BUF = 128;    // near_set register path: candidate buffer entries per end
-constexpr int NEAR_NBK = 16;     // near_set register path: 64-node batches per wave held in registers
 #ifndef SMP_PLAN_CT
 #define SMP_PLAN_CT 8  // (the local path of a query without helpers, and init_planner's start / goal check)
 #endif
@@ -493,6 +504,21 @@ __device__ __forceinline__ gcdptr uni_gptr(const double* p) {
   return (gcdptr)(((unsigned long long)hi << 32) | lo);
 }
 
+// A global pointer made wave-uniform (SGPR pair): a pointer argument of a non-inlined function arrives in VGPRs.
+__device__ __forceinline__ gcdptr uni_g(gcdptr p) {
+  const unsigned long long v = reinterpret_cast<unsigned long long>(p);
+  const unsigned lo = __builtin_amdgcn_readfirstlane((int)(unsigned)v);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((int)(unsigned)(v >> 32));
+  return (gcdptr)(((unsigned long long)hi << 32) | lo);
+}
+// The column bases of a tree's configurations ([NJ][cap]) as scalar pointers: a scan's loads then issue as global_load
+// with a scalar base and a 32-bit lane offset, unconditionally (the scans clamp the index of lanes past the range to its
+// last node and ignore their values) -- no address arithmetic in 64-bit vector registers, no branch per load.
+__device__ __forceinline__ void tree_cols(gcdptr tq, int cap, gcdptr* c) {
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) c[j] = uni_g(tq + (size_t)j * (unsigned)cap);
+}
+
 // Stores into the tree arrays that the scout reads (q, cost, parent).  Plain stores: the lines stay in this XCD's
 // L2, where a scout on the same XCD (the usual placement, plan_kernel) and the leader's own scans find them;
 // scout_request publishes them (drain, plus an agent release when the scout runs on another XCD).
@@ -587,6 +613,8 @@ __device__ int nearest_scan(const Ctx& C, int t, const double* q, int i_begin, d
   if (scan_split(C, uni(g_L.S.n[t]) - i_begin)) return nearest_dist(C, t, q, i_begin, uni(g_L.S.n[t]), d_out);
   const gcdptr tq = uni_gptr(C.Q.tr[t].q);
   const int n = uni(g_L.S.n[t]), cap = uni(g_L.S.cap);
+  gcdptr tqc[NJ];
+  tree_cols(tq, cap, tqc);
   double qq[NJ];
   for (int j = 0; j < NJ; ++j) qq[j] = q[j];
   double best = 10000.0, best_s = 1e300;
@@ -598,9 +626,9 @@ __device__ int nearest_scan(const Ctx& C, int t, const double* q, int i_begin, d
     double a[NPT][NJ];
 #pragma unroll
     for (int u = 0; u < NPT; ++u) {
-      const int i = i0 + u * BLOCK;
+      const unsigned ii = (unsigned)min(i0 + u * BLOCK, n - 1);
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) a[u][j] = i < n ? (tq + (size_t)j * cap)[(unsigned)i] : 0.0;
+      for (int j = 0; j < NJ; ++j) a[u][j] = tqc[j][ii];
     }
     double s[NPT];
 #pragma unroll
@@ -774,6 +802,11 @@ __device__ __forceinline__ void near_batch(bool near, unsigned long long key, in
   }
 }
 
+// Histogram bin of a near cost (monotone in the cost: bins order like costs; near_set's register path).
+__device__ __forceinline__ int near_bin(unsigned long long key, double cmin, double scale) {
+  return (int)((__longlong_as_double((long long)key) - cmin) * scale);
+}
+
 // Radius test sqrt(s) < r of the reference, decided on s against r^2 (1 -+ 1e-12); the (correctly rounded)
 // sqrt is only taken inside that band, where the two could disagree.
 __device__ __forceinline__ bool near_radius(bool valid, double s, double r, double r2lo, double r2hi, bool& amb) {
@@ -793,6 +826,8 @@ __device__ __noinline__ void near_set_stream(const Ctx& C, int t, const double* 
   constexpr int NW = BLOCK / 64, NB = 4;
   const gcdptr tq = uni_gptr(C.Q.tr[t].q), tc = uni_gptr(C.Q.tr[t].cost);
   const int n = uni(g_L.S.n[t]), cap = uni(g_L.S.cap);
+  gcdptr tqc[NJ];
+  tree_cols(tq, cap, tqc);
   const double r = g_L.S.near_r;
   const double r2 = r * r, r2lo = r2 * (1.0 - 1e-12), r2hi = r2 * (1.0 + 1e-12);
   const int lane = lane_id(), wave = wave_id();
@@ -809,10 +844,10 @@ __device__ __noinline__ void near_set_stream(const Ctx& C, int t, const double* 
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       const int i = base + b * BLOCK + lane;
-      const bool v = i < n;
+      const unsigned ii = (unsigned)min(i, n - 1);
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) x[b][j] = v ? (tq + (size_t)j * cap)[(unsigned)i] : 0.0;
-      key[b] = v ? (unsigned long long)__double_as_longlong(tc[(unsigned)i]) : 0ull;
+      for (int j = 0; j < NJ; ++j) x[b][j] = tqc[j][ii];
+      key[b] = i < n ? (unsigned long long)__double_as_longlong(tc[ii]) : 0ull;
     }
     bool nr[NB], amb[NB];
     bool any_amb = false;
@@ -898,6 +933,8 @@ __device__ __noinline__ void near_set_stream(const Ctx& C, int t, const double* 
 // Nearest over the nodes [i0, i1): the first strict minimum as nearest_scan, reduced to (distance key, id) in X.wk[0],
 // X.wi[0] (key of 10000.0 and id INT_MAX if no node is below 10000).  All threads.
 __device__ __forceinline__ void slice_nn_body(gcdptr tq, int cap, int i0, int i1, const double* q, ScanLds& X) {
+  gcdptr tqc[NJ];
+  tree_cols(tq, cap, tqc);
   double qq[NJ];
   for (int j = 0; j < NJ; ++j) qq[j] = q[j];
   double best = 10000.0, best_s = 1e300;
@@ -907,9 +944,9 @@ __device__ __forceinline__ void slice_nn_body(gcdptr tq, int cap, int i0, int i1
     double a[NPT][NJ];
 #pragma unroll
     for (int u = 0; u < NPT; ++u) {
-      const int i = b0 + u * BLOCK;
+      const unsigned ii = (unsigned)min(b0 + u * BLOCK, i1 - 1);
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) a[u][j] = i < i1 ? (tq + (size_t)j * cap)[(unsigned)i] : 0.0;
+      for (int j = 0; j < NJ; ++j) a[u][j] = tqc[j][ii];
     }
     double s[NPT];
 #pragma unroll
@@ -958,6 +995,9 @@ __device__ __forceinline__ void slice_near_body(gcdptr tq, gcdptr tc, int cap, i
   constexpr int K = SCAN_K, NW = BLOCK / 64, NB = 4;
   const double r2 = r * r, r2lo = r2 * (1.0 - 1e-12), r2hi = r2 * (1.0 + 1e-12);
   const int lane = lane_id(), wave = wave_id();
+  gcdptr tqc[NJ];
+  tree_cols(tq, cap, tqc);
+  tc = uni_g(tc);
   double qq[NJ];
   for (int j = 0; j < NJ; ++j) qq[j] = q[j];
   const unsigned long long KMAX = ~0ull;
@@ -972,10 +1012,10 @@ __device__ __forceinline__ void slice_near_body(gcdptr tq, gcdptr tc, int cap, i
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       const int i = base + b * BLOCK + lane;
-      const bool v = i < i1;
+      const unsigned ii = (unsigned)min(i, i1 - 1);
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) x[b][j] = v ? (tq + (size_t)j * cap)[(unsigned)i] : 0.0;
-      key[b] = v ? (unsigned long long)__double_as_longlong(tc[(unsigned)i]) : 0ull;
+      for (int j = 0; j < NJ; ++j) x[b][j] = tqc[j][ii];
+      key[b] = i < i1 ? (unsigned long long)__double_as_longlong(tc[ii]) : 0ull;
     }
     bool nr[NB], amb[NB];
     bool any_amb = false;
@@ -1052,8 +1092,228 @@ __device__ __forceinline__ void slice_near_body(gcdptr tq, gcdptr tc, int cap, i
   if (threadIdx.x == 0) { X.cnt = tot; X.take = take; }
   __syncthreads();
 }
+// The same outputs by near_set's register path (histogram of the chunk's near costs, candidates at or beyond the bins of
+// the K-th lowest / highest, ranked by counting), chunk by chunk with the running lists X.lk / X.hk: a slice of a few
+// thousand nodes is one chunk, one pass of barrier-separated steps, instead of a per-wave insertion per candidate.
+// Returns false (outputs undefined) if a chunk's histogram cannot split its costs (many equal costs): the caller then
+// runs slice_near_body.  All threads.
+__device__ bool slice_near_hist(gcdptr tq, gcdptr tc, int cap, int i0, int i1, const double* q, int excl, double r,
+                                ScanLds& X) {
+  constexpr int K = SCAN_K, NW = BLOCK / 64, CH = NEAR_NBK * BLOCK;
+  static_assert(K <= 64 && NEAR_BUF == 128 && NEAR_BINS == 4 * 64, "register path layout");
+  const double r2 = r * r, r2lo = r2 * (1.0 - 1e-12), r2hi = r2 * (1.0 + 1e-12);
+  const int lane = lane_id(), wave = wave_id();
+  gcdptr tqc[NJ];
+  tree_cols(tq, cap, tqc);
+  tc = uni_g(tc);
+  double qq[NJ];
+  for (int j = 0; j < NJ; ++j) qq[j] = q[j];
+  int tot_all = 0;  // near nodes of the chunks before this one (block-uniform)
+  if (threadIdx.x == 0) X.take = 0;
+  __syncthreads();
+  for (int c0 = i0; c0 < i1; c0 += CH) {
+    unsigned long long key[NEAR_NBK];
+    unsigned nmask = 0;
+    unsigned long long kmin = ~0ull, kmax = 0;
+    int wc = 0;
+#pragma unroll
+    for (int g = 0; g < NEAR_NBK; g += 4) {
+      key[g] = key[g + 1] = key[g + 2] = key[g + 3] = 0;
+      if (c0 + g * BLOCK + wave * 64 < i1) {
+        double x[4][NJ];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const int i = c0 + (g + b) * BLOCK + wave * 64 + lane;
+          const unsigned ii = (unsigned)min(i, i1 - 1);
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) x[b][j] = tqc[j][ii];
+          key[g + b] = i < i1 ? (unsigned long long)__double_as_longlong(tc[ii]) : 0ull;
+        }
+        bool nr[4], amb[4];
+        bool any_amb = false;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const int i = c0 + (g + b) * BLOCK + wave * 64 + lane;
+          double sb = 0.0;
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) {
+            double d = qq[j] - x[b][j];
+            sb += d * d;
+          }
+          nr[b] = near_radius(i < i1 && i != excl, sb, r, r2lo, r2hi, amb[b]);
+          x[b][0] = sb;
+          any_amb |= amb[b];
+        }
+        if (__ballot(any_amb)) {
+#pragma unroll
+          for (int b = 0; b < 4; ++b)
+            if (amb[b]) nr[b] = sqrt(x[b][0]) < r;
+        }
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          if (nr[b]) {
+            nmask |= 1u << (g + b);
+            kmin = min(kmin, key[g + b]);
+            kmax = max(kmax, key[g + b]);
+          }
+          wc += __popcll(__ballot(nr[b]));
+        }
+      }
+    }
+    kmin = __ockl_wfred_min_u64(kmin);
+    kmax = __ockl_wfred_max_u64(kmax);
+    if (lane == 0) { X.hmin[wave] = kmin; X.hmax[wave] = kmax; X.wtot[wave] = wc; }
+    if (threadIdx.x < NEAR_BINS) X.hist[threadIdx.x] = 0;
+    __syncthreads();
+    int tot = 0;
+    kmin = ~0ull; kmax = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      tot += X.wtot[w];
+      kmin = min(kmin, X.hmin[w]);
+      kmax = max(kmax, X.hmax[w]);
+    }
+    tot = uni(tot);
+    if (tot == 0) {  // nothing near in this chunk: lists unchanged (the barrier: every wave has read X.wtot / hmin / hmax)
+      __syncthreads();
+      continue;
+    }
+    const int take_c = min(K, tot);
+    const int prev = X.take;  // both running lists hold this many entries
+    const double cmin = __longlong_as_double((long long)kmin), cmax = __longlong_as_double((long long)kmax);
+    const double scale = cmax > cmin ? (NEAR_BINS * (1.0 - 1e-9)) / (cmax - cmin) : 0.0;
+    unsigned bins[NEAR_NBK / 4] = {};  // 8-bit bin of every near key
+#pragma unroll
+    for (int b = 0; b < NEAR_NBK; ++b)
+      if (nmask >> b & 1) {
+        const int bin = near_bin(key[b], cmin, scale);
+        bins[b >> 2] |= (unsigned)bin << (8 * (b & 3));
+        atomicAdd(&X.hist[bin], 1u);
+      }
+    __syncthreads();
+    if (wave == 0) {
+      // lane l owns bins 4l .. 4l+3: inclusive cumulative counts (near_set)
+      const unsigned h0 = X.hist[4 * lane], h1 = X.hist[4 * lane + 1];
+      const unsigned h2 = X.hist[4 * lane + 2], h3 = X.hist[4 * lane + 3];
+      int inc = h0 + h1 + h2 + h3;
+      for (int off = 1; off < 64; off <<= 1) {
+        const int o = __shfl_up(inc, off);
+        if (lane >= off) inc += o;
+      }
+      const int c3 = inc, c2 = c3 - (int)h3, c1 = c2 - (int)h2, c0b = c1 - (int)h1;
+      const int e0 = c0b - (int)h0;
+      const int flo = c0b >= take_c ? 0 : c1 >= take_c ? 1 : c2 >= take_c ? 2 : c3 >= take_c ? 3 : 4;
+      const int Llo = __builtin_ctzll(__ballot(flo < 4));
+      const int blo = 4 * Llo + __shfl(flo, Llo);
+      const int cnt_lo = __shfl(flo == 0 ? c0b : flo == 1 ? c1 : flo == 2 ? c2 : c3, Llo);
+      const int lim = tot - take_c;
+      const int fhi = c2 <= lim ? 3 : c1 <= lim ? 2 : c0b <= lim ? 1 : e0 <= lim ? 0 : -1;
+      const int Lhi = 63 - __builtin_clzll(__ballot(fhi >= 0));
+      const int fh = __shfl(fhi, Lhi);
+      const int bhi = 4 * Lhi + fh;
+      const int cnt_hi = tot - __shfl(fhi == 3 ? c2 : fhi == 2 ? c1 : fhi == 1 ? c0b : e0, Lhi);
+      if (lane == 0) {
+        X.hblo = blo;
+        X.hbhi = bhi;
+        X.fast = cnt_lo + prev <= NEAR_BUF && cnt_hi + prev <= NEAR_BUF;
+        X.hcnt[0] = prev;  // the running lists take the first buffer slots
+        X.hcnt[1] = prev;
+      }
+    }
+    if (threadIdx.x < prev) {
+      X.ck[0][threadIdx.x] = X.lk[threadIdx.x];
+      X.ci[0][threadIdx.x] = X.li[threadIdx.x];
+    }
+    if (threadIdx.x >= 64 && threadIdx.x < 64 + prev) {
+      X.ck[1][threadIdx.x - 64] = X.hk[threadIdx.x - 64];
+      X.ci[1][threadIdx.x - 64] = X.hi[threadIdx.x - 64];
+    }
+    __syncthreads();
+    if (!uni(X.fast)) {
+      __syncthreads();
+      return false;
+    }
+    const int blo = X.hblo, bhi = X.hbhi;
+    int nw_lo = 0, nw_hi = 0;
+#pragma unroll
+    for (int g = 0; g < NEAR_NBK; ++g) {
+      if (c0 + g * BLOCK + wave * 64 < i1) {
+        const bool nr = nmask >> g & 1;
+        const int bin = bins[g >> 2] >> (8 * (g & 3)) & 255;
+        nw_lo += __popcll(__ballot(nr && bin <= blo));
+        nw_hi += __popcll(__ballot(nr && bin >= bhi));
+      }
+    }
+    int base_lo = 0, base_hi = 0;
+    if (lane == 0 && nw_lo) base_lo = atomicAdd(&X.hcnt[0], nw_lo);
+    if (lane == 1 && nw_hi) base_hi = atomicAdd(&X.hcnt[1], nw_hi);
+    base_lo = __shfl(base_lo, 0);
+    base_hi = __shfl(base_hi, 1);
+    const unsigned long long below = (1ull << lane) - 1;
+#pragma unroll
+    for (int g = 0; g < NEAR_NBK; ++g) {
+      if (c0 + g * BLOCK + wave * 64 < i1) {
+        const bool nr = nmask >> g & 1;
+        const int bin = bins[g >> 2] >> (8 * (g & 3)) & 255;
+        const int i = c0 + g * BLOCK + wave * 64 + lane;
+        const bool pl = nr && bin <= blo, ph = nr && bin >= bhi;
+        const unsigned long long ml = __ballot(pl), mh = __ballot(ph);
+        if (pl) {
+          const int slot = base_lo + __popcll(ml & below);
+          X.ck[0][slot] = key[g];
+          X.ci[0][slot] = i;
+        }
+        if (ph) {
+          const int slot = base_hi + __popcll(mh & below);
+          X.ck[1][slot] = key[g];
+          X.ci[1][slot] = i;
+        }
+        base_lo += __popcll(ml);
+        base_hi += __popcll(mh);
+      }
+    }
+    __syncthreads();
+    const int take = min(K, tot_all + tot);
+    {
+      // rank: threads [0, 256) the low buffer, [256, 512) the high buffer; L lanes per entry; the low list ascending,
+      // the high list descending (its rank counts the entries above it)
+      const int e = threadIdx.x >= 256;
+      const int idx = threadIdx.x & 255;
+      const int m = X.hcnt[e];
+      const int L = m <= 64 ? 4 : 2;
+      const int c = L == 4 ? idx >> 2 : idx >> 1, sl = idx & (L - 1);
+      int rank = 0;
+      unsigned long long ck = 0;
+      int ci = 0;
+      if (c < m) {
+        ck = X.ck[e][c];
+        ci = X.ci[e][c];
+        for (int j = sl; j < m; j += L) {
+          const unsigned long long ok = X.ck[e][j];
+          const int oi = X.ci[e][j];
+          rank += e == 0 ? ki_less(ok, oi, ck, ci) : ki_less(ck, ci, ok, oi);
+        }
+      }
+      rank += __shfl_xor(rank, 1);
+      if (L == 4) rank += __shfl_xor(rank, 2);
+      if (c < m && sl == 0 && rank < take) {
+        if (e == 0) { X.lk[rank] = ck; X.li[rank] = ci; }
+        else { X.hk[rank] = ck; X.hi[rank] = ci; }
+      }
+    }
+    tot_all += tot;
+    __syncthreads();
+    if (threadIdx.x == 0) X.take = take;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) X.cnt = tot_all;
+  __syncthreads();
+  return true;
+}
+
 __device__ __noinline__ void slice_near(gcdptr tq, gcdptr tc, int cap, int i0, int i1, const double* q, int excl,
                                         double r, ScanLds& X) {
+  if (uni(slice_near_hist(tq, tc, cap, i0, i1, q, excl, r, X))) return;
   slice_near_body(tq, tc, cap, i0, i1, q, excl, r, X);
 }
 
@@ -1083,9 +1343,6 @@ __device__ __noinline__ void slice_near(gcdptr tq, gcdptr tc, int cap, int i0, i
 #define NEAR_CLOCK(k)
 #define NEAR_COUNT(k)
 #endif
-__device__ __forceinline__ int near_bin(unsigned long long key, double cmin, double scale) {
-  return (int)((__longlong_as_double((long long)key) - cmin) * scale);
-}
 
 template <int K>
 __device__ void near_set(const Ctx& C, int t, const double* q, int excl, bool spec = false) {
@@ -1098,6 +1355,8 @@ __device__ void near_set(const Ctx& C, int t, const double* q, int excl, bool sp
   const int n = uni(g_L.S.n[t]);
   const gcdptr tq = uni_gptr(C.Q.tr[t].q), tc = uni_gptr(C.Q.tr[t].cost);
   const int cap = uni(g_L.S.cap);
+  gcdptr tqc[NJ];
+  tree_cols(tq, cap, tqc);
   const double r = g_L.S.near_r;
   const double r2 = r * r, r2lo = r2 * (1.0 - 1e-12), r2hi = r2 * (1.0 + 1e-12);
   const int lane = lane_id(), wave = wave_id();
@@ -1202,10 +1461,10 @@ __device__ void near_set(const Ctx& C, int t, const double* q, int excl, bool sp
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
           const int i = c0 + (g + b) * BLOCK + wave * 64 + lane;
-          const bool v = i < n;
+          const unsigned ii = (unsigned)min(i, n - 1);
 #pragma unroll
-          for (int j = 0; j < NJ; ++j) x[b][j] = v ? (tq + (size_t)j * cap)[(unsigned)i] : 0.0;
-          key[g + b] = v ? (unsigned long long)__double_as_longlong(tc[(unsigned)i]) : 0ull;
+          for (int j = 0; j < NJ; ++j) x[b][j] = tqc[j][ii];
+          key[g + b] = i < n ? (unsigned long long)__double_as_longlong(tc[ii]) : 0ull;
         }
         bool nr[4], amb[4];
         bool any_amb = false;
@@ -1253,7 +1512,10 @@ __device__ void near_set(const Ctx& C, int t, const double* q, int excl, bool sp
       kmax = max(kmax, g_L.nh.wmax[w]);
     }
     tot = uni(tot);
-    if (tot == 0) continue;  // nothing near in this chunk: lists unchanged
+    if (tot == 0) {  // nothing near in this chunk: lists unchanged (the barrier: every wave has read wtot / wmin / wmax)
+      __syncthreads();
+      continue;
+    }
     const int take_c = min(K, tot);
     const int prev_lo = g_L.n_lo, prev_hi = g_L.n_hi;
     const double cmin = __longlong_as_double((long long)kmin), cmax = __longlong_as_double((long long)kmax);
@@ -1754,9 +2016,10 @@ constexpr unsigned SCAN_HDR = 1u | 1u << 18;  // edge-count field 1 (33 payload 
 // the scouts, read by smp_debug_scanprof: [0] scans, [1] write-back + publication, [2] own slice, [3] collection,
 // [4] merge, [5] stolen slices, [6] collection rounds, [7] helper slices, [8] helper pickup (publication -> acquire),
 // [9] helper acquire, [10] helper slice, [11] publication -> helper result stored, [12] near scans, [13] their
-// collection, [14] participants, [15] nodes
+// collection, [14] participants, [15] nodes, [16] near scans' own slice, [17] near merge, [18] near helper slices,
+// [19] their slice clocks
 #ifdef SMP_SCAN_PROF
-__device__ unsigned long long g_scanprof[16];
+__device__ unsigned long long g_scanprof[24];
 #define SCANPROF_ADD(k, v) atomicAdd(&g_scanprof[k], (unsigned long long)(v))
 #else
 #define SCANPROF_ADD(k, v)
@@ -1840,6 +2103,7 @@ __device__ __noinline__ void scan_helper(const Ctx& C, JobLds& J, int worker, in
     const unsigned long long hp2 = wall_clock64(), pub = ld_agent(&C.Q.jb->dbg[8]);
     SCANPROF_ADD(7, 1); SCANPROF_ADD(8, hp0 - pub); SCANPROF_ADD(9, hp1 - hp0); SCANPROF_ADD(10, hp2 - hp1);
     SCANPROF_ADD(11, hp2 - pub);
+    if (near) { SCANPROF_ADD(18, 1); SCANPROF_ADD(19, hp2 - hp1); }
   }
 #endif
   unsigned long long* out = C.Q.jb->sres[w];
@@ -2034,7 +2298,7 @@ __device__ void scan_run(const Ctx& C, int near, int t, const double* q, int i0,
     const unsigned long long sp3 = wall_clock64();
     SCANPROF_ADD(0, 1); SCANPROF_ADD(1, sp1 - sp0); SCANPROF_ADD(2, sp2 - sp1); SCANPROF_ADD(3, sp3 - sp2);
     SCANPROF_ADD(5, sp_steals); SCANPROF_ADD(6, sp_rounds); SCANPROF_ADD(14, P); SCANPROF_ADD(15, n - i0);
-    if (near) { SCANPROF_ADD(12, 1); SCANPROF_ADD(13, sp3 - sp2); }
+    if (near) { SCANPROF_ADD(12, 1); SCANPROF_ADD(13, sp3 - sp2); SCANPROF_ADD(16, sp2 - sp1); }
     g_L.spc_t = sp3;
   }
 #endif
@@ -2056,9 +2320,10 @@ __device__ int nearest_dist(const Ctx& C, int t, const double* q, int i0, int n,
   return bi;
 }
 
-// near_set's outputs (g_L.nk, n_lo, n_hi, lo_*, hi_*) from the merged slices: an entry of participant w's list at
-// position j ranks j + (entries of the other lists ahead of it); the lists are sorted, so each count is a binary
-// search.  Threads [0, 256) the low lists, [256, 512) the high lists, candidates strided.
+// near_set's outputs (g_L.nk, n_lo, n_hi, lo_*, hi_*) from the merged slices: the lowest SCAN_K (cost, id) entries of
+// the P ascending low lists and the highest SCAN_K of the P descending high lists, by a tournament -- wave 0 the low
+// side, wave 1 the high side, lane w the head of participant w's list; each round one wave minimum (maximum) of the
+// heads, whose lane advances.  The slices partition the range, so ids are distinct and every round has one winner.
 __device__ void near_set_dist(const Ctx& C, int t, const double* q, int excl) {
   const int n = uni(g_L.S.n[t]);
   const int P = scan_parts(C, 1, n);
@@ -2068,43 +2333,29 @@ __device__ void near_set_dist(const Ctx& C, int t, const double* q, int excl) {
   for (int w = 0; w < P; ++w) tot += M.cnt[w];
   tot = uni(tot);
   const int take = min(SCAN_K, tot);
-  const int side = threadIdx.x >= 256;
-  for (int c = threadIdx.x & 255; c < P * SCAN_K; c += 256) {
-    const int w = c / SCAN_K, j = c - w * SCAN_K;
-    if (j >= M.len[w]) continue;
-    const unsigned long long ck = merge_key(M, side, w, j);
-    const int ci = M.id[side][w][j];
-    int rank = j;
-    for (int o0 = 0; o0 < P && rank < take; o0 += 8) {
-      int lo[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) lo[u] = 0;
-#pragma unroll
-      for (int step = 16; step > 0; step >>= 1) {
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int o = o0 + u;
-          const int m = lo[u] + step - 1;
-          if (o < P && o != w && m < M.len[o]) {
-            const unsigned long long ok = merge_key(M, side, o, m);
-            const int oi = M.id[side][o][m];
-            const bool ahead = side ? ki_less(ck, ci, ok, oi) : ki_less(ok, oi, ck, ci);
-            if (ahead) lo[u] += step;
-          }
-        }
+  static_assert(SCAN_PNEAR <= 64, "one lane per list");
+  if (threadIdx.x < 128) {
+    const int side = (int)threadIdx.x >> 6, w = lane_id();
+    const int len = w < P ? M.len[w] : 0;
+    int p = 0;
+    unsigned long long k = side ? 0ull : ~0ull;
+    int id = side ? -1 : 0x7fffffff;
+    if (len > 0) { k = merge_key(M, side, w, 0); id = M.id[side][w][0]; }
+    for (int r = 0; r < take; ++r) {
+      const unsigned long long mk = side ? __ockl_wfred_max_u64(k) : __ockl_wfred_min_u64(k);
+      const int mi = side ? __ockl_wfred_max_i32(k == mk ? id : -1) : __ockl_wfred_min_i32(k == mk ? id : 0x7fffffff);
+      if (k == mk && id == mi) {
+        if (!side) { g_L.lo_c[r] = __longlong_as_double((long long)mk); g_L.lo_i[r] = mi; }
+        else { g_L.hi_c[take - 1 - r] = __longlong_as_double((long long)mk); g_L.hi_i[take - 1 - r] = mi; }
+        if (++p < len) { k = merge_key(M, side, w, p); id = M.id[side][w][p]; }
+        else { k = side ? 0ull : ~0ull; id = side ? -1 : 0x7fffffff; }
       }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) rank += lo[u];
-    }
-    if (rank < take) {
-      if (!side) { g_L.lo_c[rank] = __longlong_as_double((long long)ck); g_L.lo_i[rank] = ci; }
-      else { g_L.hi_c[take - 1 - rank] = __longlong_as_double((long long)ck); g_L.hi_i[take - 1 - rank] = ci; }
     }
   }
   if (threadIdx.x == 0) { g_L.nk = tot; g_L.n_lo = take; g_L.n_hi = take; g_L.S.near_nodes += n; }
   __syncthreads();
 #ifdef SMP_SCAN_PROF
-  if (threadIdx.x == 0) SCANPROF_ADD(4, wall_clock64() - g_L.spc_t);
+  if (threadIdx.x == 0) { SCANPROF_ADD(4, wall_clock64() - g_L.spc_t); SCANPROF_ADD(17, wall_clock64() - g_L.spc_t); }
 #endif
 }
 
@@ -3487,6 +3738,11 @@ __device__ void connect_graphs(const Ctx& C, int t) {
       // the scout checked this edge (before the first solution: no near set to overlap)
       if (threadIdx.x == 0) { g_L.eg_first[0] = g_L.sr.cn.e.first; g_L.S.sc_edge_hit++; }
       __syncthreads();
+    } else if (crec && uni(g_L.sr.cc.nfirst >= 0)) {
+      // after the first solution: the record's connect edges were checked with its scans (scout_connect); the direct
+      // edge is the record's nearest node -> x_new, the same configurations
+      if (threadIdx.x == 0) { g_L.eg_first[0] = g_L.sr.cc.first0; g_L.S.sc_edge_hit++; }
+      __syncthreads();
     } else {
       edge_validity(C, 1, false, P_XCONNECT, (g_L.S.have_sol && !crec) ? OV_NEAR_XN : OV_NONE, t);
     }
@@ -3561,7 +3817,16 @@ __device__ void connect_graphs(const Ctx& C, int t) {
       }
       for (int e = E + threadIdx.x; e < MAXE; e += BLOCK) g_L.eg_need[e] = 0;
       __syncthreads();
-      edge_validity(C, E, true, P_XCONNECT);
+      if (crec && uni(g_L.sr.cc.nfirst >= E)) {  // the record's candidates, checked to the end (scout_connect)
+        if (threadIdx.x < 64) {  // (E <= max_near <= 20: wave 0)
+          if ((int)threadIdx.x < E) g_L.eg_first[threadIdx.x] = g_L.sr.cc.first[threadIdx.x];
+          const int hits = __popcll(__ballot((int)threadIdx.x < E && g_L.eg_need[threadIdx.x]));
+          if (threadIdx.x == 0) g_L.S.sc_edge_hit += hits;
+        }
+        __syncthreads();
+      } else {
+        edge_validity(C, E, true, P_XCONNECT);
+      }
       DETAIL_BEGIN(_dn);
       // replay of the near loop (birrt_star.cpp:2820-3030).  An edge acts (connects: 1, extends: 2) only on
       // conditions of state that changes when an edge acts, so wave 0 evaluates every remaining edge against
@@ -4200,6 +4465,14 @@ __device__ void scout_connect(const Ctx& C, long long it, int t, int par, unsign
   }
   __syncthreads();
   edge_costs(C, 1 + E);
+  // the validity of every connect edge (the direct one and each near candidate's, checked to the end): one job, so that the
+  // leader's connect takes them instead of its own two jobs (direct edge, near loop)
+  if (threadIdx.x < MAXE) g_L.eg_need[threadIdx.x] = threadIdx.x < 1 + E;
+  if (threadIdx.x == 0) g_L.rec_grp = -1;
+  __syncthreads();
+  edge_validity(C, 1 + E, false, P_XCONNECT);
+  if (threadIdx.x < E) R.cc.first[threadIdx.x] = g_L.eg_first[1 + threadIdx.x];
+  if (threadIdx.x == 0) { R.cc.first0 = g_L.eg_first[0]; R.cc.nfirst = E; }
   if (threadIdx.x < MAX_NEAR) {
     R.cc.lo_i[threadIdx.x] = g_L.lo_i[threadIdx.x]; R.cc.lo_c[threadIdx.x] = g_L.lo_c[threadIdx.x];
     R.cc.hi_i[threadIdx.x] = g_L.hi_i[threadIdx.x]; R.cc.hi_c[threadIdx.x] = g_L.hi_c[threadIdx.x];
@@ -4362,7 +4635,7 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
     S.n[1 - t] = XB;
     R.cn.ok = 0;
     R.pre.ok = 0;
-    R.nn.ok = 0; R.ex.ok = 0; R.nr.ok = 0; R.n_choose = 0; R.n_rewire = 0; R.cc.ok = 0;
+    R.nn.ok = 0; R.ex.ok = 0; R.nr.ok = 0; R.n_choose = 0; R.n_rewire = 0; R.cc.ok = 0; R.cc.nfirst = -1;
   }
   if (opt) sc_publish(C, par, tag, SC_STARTED);  // (a pre-solution pass publishes its record once, at its end)
   // the sample: the sampler's ring slot for (it, ver), if it is there within ~20 us
@@ -5171,14 +5444,14 @@ __global__ void path_edges_kernel(const QueryDev* qs, int q, int ns, int ng, dou
 // near_set<20>() for m query configurations against one tree (SoA q [NJ][cap], total cost [cap]), `reps` times
 // each; out: nearest id, near count, the first / last 20 near ids; ticks[0] / ticks[1] = device-clock ticks of
 // all nearest / near_set calls.
-__global__ void __launch_bounds__(BLOCK) near_probe_kernel(const double* tq, const double* tcost, int cap, int n,
+__global__ void __launch_bounds__(BLOCK) near_probe_kernel(const double* tqv, const double* tcost, int cap, int n,
                                                            const double* queries, const int* excl, int m, double r,
                                                            int reps, int* nn, int* nk, int* lo, int* hi,
                                                            unsigned long long* ticks) {
   Ctx C;
   C.Q.jb = nullptr;  // single workgroup: no helpers, scans stay local
   C.Q.scan_min = 0;
-  C.Q.tr[0].q = const_cast<double*>(tq);
+  C.Q.tr[0].q = const_cast<double*>(tqv);
   C.Q.tr[0].cost = const_cast<double*>(tcost);
   if (threadIdx.x == 0) {
     g_L.in_job = 0;
@@ -5189,29 +5462,56 @@ __global__ void __launch_bounds__(BLOCK) near_probe_kernel(const double* tq, con
     g_L.near_bhi = 0;
     for (int k = 0; k < 32; ++k) g_L.S.prof[k] = 0;
   }
+  const unsigned long long m0 = __builtin_amdgcn_s_memtime(), w0 = wall_clock64();
   unsigned long long t_nn = 0, t_near = 0;
+  // reps < 0: the slice functions of distributed scans (slice_nn / slice_near over [0, n)) instead of nearest / near_set
+  const bool slice = reps < 0;
+  if (slice) reps = -reps;
+  const gcdptr tq = uni_gptr(tqv), tc = uni_gptr(tcost);
   for (int k = 0; k < m; ++k) {
     if (threadIdx.x < NJ) g_L.xr[threadIdx.x] = queries[(size_t)k * NJ + threadIdx.x];
     __syncthreads();
     int id = 0;
     unsigned long long t0 = wall_clock64();
-    for (int rep = 0; rep < reps; ++rep) id = nearest(C, 0, g_L.xr);
+    for (int rep = 0; rep < reps; ++rep) {
+      if (slice) {
+        slice_nn(tq, cap, 0, n, g_L.xr, g_L.sc.s);
+        id = __longlong_as_double((long long)g_L.sc.s.wk[0]) < 10000.0 ? g_L.sc.s.wi[0] : 0;
+      } else {
+        id = nearest(C, 0, g_L.xr);
+      }
+    }
     unsigned long long t1 = wall_clock64();
-    for (int rep = 0; rep < reps; ++rep) near_set<20>(C, 0, g_L.xr, excl[k]);
+    for (int rep = 0; rep < reps; ++rep) {
+      if (slice) slice_near(tq, tc, cap, 0, n, g_L.xr, excl[k], r, g_L.sc.s);
+      else near_set<20>(C, 0, g_L.xr, excl[k]);
+    }
     unsigned long long t2 = wall_clock64();
     t_nn += t1 - t0;
     t_near += t2 - t1;
-    if (threadIdx.x == 0) { nn[k] = id; nk[k] = g_L.nk; }
-    if (threadIdx.x < 20) {
-      lo[k * 20 + threadIdx.x] = threadIdx.x < g_L.n_lo ? g_L.lo_i[threadIdx.x] : -1;
-      hi[k * 20 + threadIdx.x] = threadIdx.x < g_L.n_hi ? g_L.hi_i[threadIdx.x] : -1;
+    if (slice) {
+      const ScanLds& X = g_L.sc.s;
+      if (threadIdx.x == 0) { nn[k] = id; nk[k] = X.cnt; }
+      if (threadIdx.x < 20) {
+        lo[k * 20 + threadIdx.x] = (int)threadIdx.x < X.take ? X.li[threadIdx.x] : -1;
+        hi[k * 20 + threadIdx.x] = (int)threadIdx.x < X.take ? X.hi[X.take - 1 - threadIdx.x] : -1;
+      }
+    } else {
+      if (threadIdx.x == 0) { nn[k] = id; nk[k] = g_L.nk; }
+      if (threadIdx.x < 20) {
+        lo[k * 20 + threadIdx.x] = threadIdx.x < g_L.n_lo ? g_L.lo_i[threadIdx.x] : -1;
+        hi[k * 20 + threadIdx.x] = threadIdx.x < g_L.n_hi ? g_L.hi_i[threadIdx.x] : -1;
+      }
     }
     __syncthreads();
   }
   if (threadIdx.x == 0) {
     ticks[0] = t_nn;
     ticks[1] = t_near;
-    for (int k = 0; k < 12; ++k) ticks[2 + k] = g_L.S.prof[20 + k];
+    for (int k = 0; k < 10; ++k) ticks[2 + k] = g_L.S.prof[20 + k];
+    // shader clock over the whole probe: s_memtime (shader cycles) and wall-clock ticks
+    ticks[12] = __builtin_amdgcn_s_memtime() - m0;
+    ticks[13] = wall_clock64() - w0;
   }
 }
 
@@ -5240,9 +5540,9 @@ extern "C" int smp_debug_tlog(unsigned long long*, int, int) { return -1; }
 #ifdef SMP_SCAN_PROF
 extern "C" int smp_debug_scanprof(unsigned long long* out, int reset) {
   if (hipDeviceSynchronize() != hipSuccess) return -1;
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(smp::g_scanprof), 16 * sizeof(unsigned long long)) != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(smp::g_scanprof), 24 * sizeof(unsigned long long)) != hipSuccess) return -1;
   if (reset) {
-    unsigned long long z[16] = {};
+    unsigned long long z[24] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(smp::g_scanprof), z, sizeof(z)) != hipSuccess) return -1;
   }
   return 0;

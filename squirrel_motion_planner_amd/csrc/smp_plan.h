@@ -221,6 +221,10 @@ struct ScoutConn {
   double acc0[3];              // direct edge nearest -> x_new
   double pad0;
   double acc[MAX_NEAR][3];     // near candidate lo_i[e] -> x_new (e < min(n_lo, max_near))
+  // first colliding point of the direct edge and of every near candidate's edge (as eg_first: n_pts + 1 = free), all
+  // checked to the end (a pure function of the two configurations): connect takes them instead of its two jobs
+  int first0, nfirst;          // nfirst: candidates checked (-1: none, the record carries no validity)
+  int first[MAX_NEAR];
 };
 // Pre-solution record (DESIGN.md "Pre-solution commits"): everything pre_commit needs, written by the scout at the
 // end of its pass as data-tagged granules (tag = iteration + 1 in the high 32 bits, one 32-bit half of the struct

@@ -109,3 +109,25 @@ def reduce_counters(values, device="cpu"):
     dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return t.tolist(), tmax.tolist()
+
+
+def single_rank_reference(run, rank, src=0):
+    """The same-workload single-GPU reference of a multi-rank measurement (bench.py with WORLD_SIZE > 1): after the
+    multi-rank timed region, rank `src` runs `run()` -- its own per-GPU share of the job again, timed -- while every
+    other rank waits at a barrier, so the GPU runs alone.  Returns run()'s result on `src`, None elsewhere."""
+    dist.barrier()
+    out = run() if rank == src else None
+    dist.barrier()
+    return out
+
+
+def scaling_fields(value_all, world, alone):
+    """The line's scaling fields: `alone` = (configurations checked, seconds) of one GPU planning the same per-GPU
+    share alone; scaling_efficiency = whole-job rate / (world x that single-GPU rate) (weak scaling: the per-GPU work
+    is the same)."""
+    checked, seconds = alone
+    single = checked / seconds if seconds > 0 else None
+    return {"single_gpu_same_workload": {"value": single, "unit": "configs/s", "configs_checked": checked,
+                                         "seconds": seconds},
+            "scaling_efficiency": value_all / (world * single) if single else None}
+

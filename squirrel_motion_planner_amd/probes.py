@@ -11,7 +11,7 @@ import numpy as np
 from . import _lib as L
 
 
-def tree_scan(q, cost, queries, excl, r, reps=1, device=0):
+def tree_scan(q, cost, queries, excl, r, reps=1, device=0, slices=False):
     """q (n, 8) node configurations, cost (n,) total costs, queries (m, 8), excl (m,) node id left out of the near
     set (-1: none).  Returns nearest ids, near counts, the first / last 20 near ids (ascending (cost, id); -1
     padded) and the device seconds of all nearest / near_set calls."""
@@ -28,7 +28,7 @@ def tree_scan(q, cost, queries, excl, r, reps=1, device=0):
     hz = ctypes.c_double()
     pd = ctypes.POINTER(ctypes.c_double)
     L.check(L.lib().smp_probe_near(device, q.ctypes.data_as(pd), cost.ctypes.data_as(pd), n, queries.ctypes.data_as(pd),
-                                   excl.ctypes.data_as(ctypes.c_void_p), m, float(r), reps,
+                                   excl.ctypes.data_as(ctypes.c_void_p), m, float(r), -reps if slices else reps,
                                    nn.ctypes.data_as(ctypes.c_void_p), nk.ctypes.data_as(ctypes.c_void_p),
                                    lo.ctypes.data_as(ctypes.c_void_p), hi.ctypes.data_as(ctypes.c_void_p), ticks,
                                    ctypes.byref(hz)), "smp_probe_near")

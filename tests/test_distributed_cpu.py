@@ -90,6 +90,63 @@ def test_bench_dealing_reduces_to_single_rank_totals(tmp_path, orobot):
     assert got[0][:3].tolist() == tot and tot[0] > 0
 
 
+def _scaling_worker(rank, world, port, out_dir):
+    """bench.py's multi-rank line with the oracle in place of the GPU: the timed region over every rank's C3 share, the
+    reduced rate, then rank 0's share again alone (D.single_rank_reference) and the scaling fields (D.scaling_fields)."""
+    import json
+    import math
+    import sys
+    import time
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import oracle as O
+    from squirrel_motion_planner_amd import distributed as D, scenes
+    sc = scenes.box_room()
+    orc = O.Oracle(O.OracleRobot(os.path.join(ROOT, "squirrel_motion_planner_amd", "data", "robotino_model.json")),
+                   O.OracleScene(sc.keys, sc.res))
+    pairs = scenes.random_queries(sc, 4, seed=7, check=lambda q: bool(orc.check_configs(np.array([q]))[0]))
+    mine = D.shard_queries(len(pairs), world, rank)
+
+    def timed(sync):
+        if sync:
+            dist.barrier()
+        t0, checked = time.perf_counter(), 0
+        for qid in mine:
+            r = orc.plan(pairs[qid][0], pairs[qid][1], env_x=sc.env_x, env_y=sc.env_y, seed=1, query=qid,
+                         opt_thresh=-math.inf, max_iter=30)
+            checked += r["checked"]
+        if sync:
+            dist.barrier()
+        return time.perf_counter() - t0, checked
+
+    el, ch = timed(True)
+    s, m = D.reduce_counters([el, float(ch)])
+    alone = D.single_rank_reference(lambda: timed(False), rank)
+    if rank == 0:
+        out = D.scaling_fields(s[1] / m[0], world, (alone[1], alone[0]))
+        out["value"] = s[1] / m[0]
+        out["rank0_checked"] = ch
+        json.dump(out, open(os.path.join(out_dir, "scaling.json"), "w"))
+    else:
+        assert alone is None
+    dist.destroy_process_group()
+
+
+def test_bench_scaling_fields_world2(tmp_path):
+    """With WORLD_SIZE > 1 the line carries single_gpu_same_workload (rank 0's share planned again alone, the same
+    configurations) and scaling_efficiency = value / (world x that rate)."""
+    import json
+    world, port = 2, _free_port()
+    mp.spawn(_scaling_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)
+    out = json.load(open(os.path.join(str(tmp_path), "scaling.json")))
+    single = out["single_gpu_same_workload"]
+    assert single["configs_checked"] == out["rank0_checked"] > 0
+    assert single["unit"] == "configs/s" and single["value"] == single["configs_checked"] / single["seconds"]
+    assert abs(out["scaling_efficiency"] - out["value"] / (world * single["value"])) < 1e-12
+
+
 def test_scene_broadcast_and_sharding_world2(tmp_path):
     world, port = 2, _free_port()
     mp.spawn(_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)

@@ -20,7 +20,7 @@ lib.smp_debug_scanprof.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int
 sc = scenes.box_room()
 gp = GpuPlanner(path_optimality_threshold=-math.inf)
 gp.set_scene(Scene.from_keys(sc.keys, sc.res))
-buf = (ctypes.c_uint64 * 16)()
+buf = (ctypes.c_uint64 * 24)()
 for iters in [int(v) for v in (sys.argv[1:] or ["100000"])]:
     lib.smp_debug_scanprof(buf, 1)  # reset
     r = gp.plan(GpuPlanner.make_query(sc.start, sc.goal, sc.env_x, sc.env_y, iterations=iters, seed=1))
@@ -38,3 +38,7 @@ for iters in [int(v) for v in (sys.argv[1:] or ["100000"])]:
                                         v[6] / n, v[5] / n), flush=True)
     print("   per helper slice (us): pickup %.2f, acquire %.2f, slice %.2f, publication->result %.2f (%d slices)" % (
         us(v[8], nh), us(v[9], nh), us(v[10], nh), us(v[11], nh), v[7]), flush=True)
+    nf = max(v[0] - v[12], 1)
+    print("   near scans: own slice %.2f, collection %.2f, merge %.2f, helper slice %.2f | nearest scans: own slice %.2f, "
+          "collection %.2f, merge %.2f" % (us(v[16], nn), us(v[13], nn), us(v[17], nn), us(v[19], max(v[18], 1)),
+                                           us(v[2] - v[16], nf), us(v[3] - v[13], nf), us(v[4] - v[17], nf)), flush=True)
