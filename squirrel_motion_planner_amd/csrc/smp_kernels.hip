@@ -279,6 +279,7 @@ struct MergeLds {
   int id[2][SCAN_PNEAR][SCAN_K];
   int len[SCAN_P], cnt[SCAN_P], done[SCAN_P], bad[SCAN_P];
   unsigned hv[SCAN_P][3];             // collection: near header (count, take) / nearest (key halves, id)
+  unsigned hn[SCAN_PNEAR][3];         // collection: a fused scan's nearest (key halves, id)
   unsigned long long nk[SCAN_P];      // nearest: per participant (distance key, id)
   int ni[SCAN_P];
   int ndone, go[2], steal;
@@ -407,6 +408,8 @@ struct PlanLds {
   long long tit;                // iteration the records belong to
 #endif
   int sp_on, sp_stage, sp_go[2];
+  double fnn_d;                 // near_set<K, true>: the nearest node of the same configuration (distance, id)
+  int fnn_id;
 #ifdef SMP_SCAN_PROF
   unsigned long long spc_t;     // SMP_SCAN_PROF: end of the last scan's collection
 #endif
@@ -605,7 +608,7 @@ __device__ __forceinline__ bool scan_split(const Ctx& C, int nodes) {
   return uni(C.Q.jb != nullptr && C.Q.scan_min > 0 && nodes >= C.Q.scan_min && C.Q.nworkers >= 8);
 }
 __device__ int nearest_dist(const Ctx& C, int t, const double* q, int i0, int n, double* d_out);
-__device__ void near_set_dist(const Ctx& C, int t, const double* q, int excl);
+__device__ void near_set_dist(const Ctx& C, int t, const double* q, int excl, bool nn);
 // Block argmin of the nodes [i_begin, n) of tree t: the first strict minimum (d, id) of the distances, d = 10000
 // if none is below it.  All threads; result in (g_L.wd[0], g_L.wi[0]) via nearest_scan's return.
 __device__ int nearest_scan(const Ctx& C, int t, const double* q, int i_begin, double* d_out) {
@@ -802,6 +805,14 @@ __device__ __forceinline__ void near_batch(bool near, unsigned long long key, in
   }
 }
 
+// One node's part of a nearest scan inside a near scan (NN): the first strict minimum of the Euclidean distance (DH:128-156)
+// from its squared distance, the sqrt taken only when it can win.
+__device__ __forceinline__ void nn_take(bool valid, double s, int i, double& best, double& best_s, int& bid) {
+  if (valid && s < best_s) {
+    const double dist = sqrt(s);
+    if (dist < best) { best = dist; bid = i; best_s = s; }
+  }
+}
 // Histogram bin of a near cost (monotone in the cost: bins order like costs; near_set's register path).
 __device__ __forceinline__ int near_bin(unsigned long long key, double cmin, double scale) {
   return (int)((__longlong_as_double((long long)key) - cmin) * scale);
@@ -820,9 +831,29 @@ __device__ __forceinline__ bool near_radius(bool valid, double s, double r, doub
 //      smallest and K largest (key, id) of its nodes (near_batch);
 //   2. rank merge: every wave entry finds its rank among all NW*K entries by binary searches in the other
 //      waves' sorted lists (advanced in lock-step) and is written to its place if the rank is below K.
-template <int K>
+// The nearest-node part of a fused near_set<K, true>: the threads' candidates -> g_L.fnn_d / fnn_id.  All threads.
+__device__ __forceinline__ void fnn_reduce(double best, int bid) {
+  const unsigned long long key = (unsigned long long)__double_as_longlong(best);
+  const unsigned long long wk = __ockl_wfred_min_u64(key);
+  const int wi = __ockl_wfred_min_i32(key == wk ? bid : 0x7fffffff);
+  if (lane_id() == 0) { g_L.wk[wave_id()] = wk; g_L.wi[wave_id()] = wi; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long bk = g_L.wk[0];
+    int bi = g_L.wi[0];
+    for (int w = 1; w < BLOCK / 64; ++w)
+      if (g_L.wk[w] < bk || (g_L.wk[w] == bk && g_L.wi[w] < bi)) { bk = g_L.wk[w]; bi = g_L.wi[w]; }
+    g_L.fnn_d = __longlong_as_double((long long)bk);
+    g_L.fnn_id = bi;
+  }
+  __syncthreads();
+}
+
+template <int K, bool NN>
 __device__ __noinline__ void near_set_stream(const Ctx& C, int t, const double* q, int excl) {
   static_assert(K <= 64, "lane-distributed lists");
+  double nb = 10000.0, nb_s = 1e300;  // NN: this thread's nearest candidate
+  int nbi = 0x7fffffff;
   constexpr int NW = BLOCK / 64, NB = 4;
   const gcdptr tq = uni_gptr(C.Q.tr[t].q), tc = uni_gptr(C.Q.tr[t].cost);
   const int n = uni(g_L.S.n[t]), cap = uni(g_L.S.cap);
@@ -861,6 +892,7 @@ __device__ __noinline__ void near_set_stream(const Ctx& C, int t, const double* 
         sb += d * d;
       }
       nr[b] = near_radius(i < n && i != excl, sb, r, r2lo, r2hi, amb[b]);
+      if (NN) nn_take(i < n, sb, i, nb, nb_s, nbi);
       x[b][0] = sb;
       any_amb |= amb[b];
     }
@@ -927,11 +959,31 @@ __device__ __noinline__ void near_set_stream(const Ctx& C, int t, const double* 
   }
   if (threadIdx.x == 0) { g_L.nk = tot; g_L.n_lo = take; g_L.n_hi = take; g_L.near_blo = KMAX; g_L.near_bhi = 0; }
   __syncthreads();
+  if (NN) fnn_reduce(nb, nbi);
 }
 
 // ------------------------------------------------------------------------------- slices of distributed scans
 // Nearest over the nodes [i0, i1): the first strict minimum as nearest_scan, reduced to (distance key, id) in X.wk[0],
 // X.wi[0] (key of 10000.0 and id INT_MAX if no node is below 10000).  All threads.
+// Block reduction of the threads' nearest candidates (distance, id; each thread's first strict minimum over its nodes in
+// increasing index order) to the (distance key, id) minimum in X.wk[0], X.wi[0].  All threads.
+__device__ __forceinline__ void slice_nn_reduce(double best, int bid, ScanLds& X) {
+  const unsigned long long key = (unsigned long long)__double_as_longlong(best);
+  const unsigned long long wk = __ockl_wfred_min_u64(key);
+  const int wi = __ockl_wfred_min_i32(key == wk ? bid : 0x7fffffff);
+  if (lane_id() == 0) { X.wk[wave_id()] = wk; X.wi[wave_id()] = wi; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long bk = X.wk[0];
+    int bi = X.wi[0];
+    for (int w = 1; w < BLOCK / 64; ++w)
+      if (X.wk[w] < bk || (X.wk[w] == bk && X.wi[w] < bi)) { bk = X.wk[w]; bi = X.wi[w]; }
+    X.wk[0] = bk;
+    X.wi[0] = bi;
+  }
+  __syncthreads();
+}
+
 __device__ __forceinline__ void slice_nn_body(gcdptr tq, int cap, int i0, int i1, const double* q, ScanLds& X) {
   gcdptr tqc[NJ];
   tree_cols(tq, cap, tqc);
@@ -960,28 +1012,9 @@ __device__ __forceinline__ void slice_nn_body(gcdptr tq, int cap, int i0, int i1
       }
     }
 #pragma unroll
-    for (int u = 0; u < NPT; ++u) {
-      const int i = b0 + u * BLOCK;
-      if (i < i1 && s[u] < best_s) {
-        const double dist = sqrt(s[u]);
-        if (dist < best) { best = dist; bid = i; best_s = s[u]; }
-      }
-    }
+    for (int u = 0; u < NPT; ++u) nn_take(b0 + u * BLOCK < i1, s[u], b0 + u * BLOCK, best, best_s, bid);
   }
-  const unsigned long long key = (unsigned long long)__double_as_longlong(best);
-  const unsigned long long wk = __ockl_wfred_min_u64(key);
-  const int wi = __ockl_wfred_min_i32(key == wk ? bid : 0x7fffffff);
-  if (lane_id() == 0) { X.wk[wave_id()] = wk; X.wi[wave_id()] = wi; }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned long long bk = X.wk[0];
-    int bi = X.wi[0];
-    for (int w = 1; w < BLOCK / 64; ++w)
-      if (X.wk[w] < bk || (X.wk[w] == bk && X.wi[w] < bi)) { bk = X.wk[w]; bi = X.wi[w]; }
-    X.wk[0] = bk;
-    X.wi[0] = bi;
-  }
-  __syncthreads();
+  slice_nn_reduce(best, bid, X);
 }
 __device__ void slice_nn(gcdptr tq, int cap, int i0, int i1, const double* q, ScanLds& X) {
   slice_nn_body(tq, cap, i0, i1, q, X);
@@ -990,9 +1023,14 @@ __device__ void slice_nn(gcdptr tq, int cap, int i0, int i1, const double* q, Sc
 // Near set over the nodes [i0, i1) (find_near_vertices_interpolation's radius test, excluding `excl`): count X.cnt,
 // its SCAN_K lowest (cost, id) entries ascending in X.lk / X.li and SCAN_K highest descending in X.hk / X.hi (X.take
 // each).  near_set_stream's per-wave lists and rank merge over a range.  All threads.
+// NN: also the nearest node of q over the range (no exclusion), in X.wk[0] / X.wi[0] as slice_nn (fused scans: connect's
+// nearest node and near set of the same configuration in one pass over the tree).
+template <bool NN>
 __device__ __forceinline__ void slice_near_body(gcdptr tq, gcdptr tc, int cap, int i0, int i1, const double* q,
                                                 int excl, double r, ScanLds& X) {
   constexpr int K = SCAN_K, NW = BLOCK / 64, NB = 4;
+  double nb = 10000.0, nb_s = 1e300;
+  int nbi = 0x7fffffff;
   const double r2 = r * r, r2lo = r2 * (1.0 - 1e-12), r2hi = r2 * (1.0 + 1e-12);
   const int lane = lane_id(), wave = wave_id();
   gcdptr tqc[NJ];
@@ -1029,6 +1067,7 @@ __device__ __forceinline__ void slice_near_body(gcdptr tq, gcdptr tc, int cap, i
         sb += d * d;
       }
       nr[b] = near_radius(i < i1 && i != excl, sb, r, r2lo, r2hi, amb[b]);
+      if (NN) nn_take(i < i1, sb, i, nb, nb_s, nbi);
       x[b][0] = sb;
       any_amb |= amb[b];
     }
@@ -1091,15 +1130,19 @@ __device__ __forceinline__ void slice_near_body(gcdptr tq, gcdptr tc, int cap, i
   }
   if (threadIdx.x == 0) { X.cnt = tot; X.take = take; }
   __syncthreads();
+  if (NN) slice_nn_reduce(nb, nbi, X);
 }
 // The same outputs by near_set's register path (histogram of the chunk's near costs, candidates at or beyond the bins of
 // the K-th lowest / highest, ranked by counting), chunk by chunk with the running lists X.lk / X.hk: a slice of a few
 // thousand nodes is one chunk, one pass of barrier-separated steps, instead of a per-wave insertion per candidate.
 // Returns false (outputs undefined) if a chunk's histogram cannot split its costs (many equal costs): the caller then
 // runs slice_near_body.  All threads.
+template <bool NN>
 __device__ bool slice_near_hist(gcdptr tq, gcdptr tc, int cap, int i0, int i1, const double* q, int excl, double r,
                                 ScanLds& X) {
   constexpr int K = SCAN_K, NW = BLOCK / 64, CH = NEAR_NBK * BLOCK;
+  double nb = 10000.0, nb_s = 1e300;  // NN: this thread's nearest candidate
+  int nbi = 0x7fffffff;
   static_assert(K <= 64 && NEAR_BUF == 128 && NEAR_BINS == 4 * 64, "register path layout");
   const double r2 = r * r, r2lo = r2 * (1.0 - 1e-12), r2hi = r2 * (1.0 + 1e-12);
   const int lane = lane_id(), wave = wave_id();
@@ -1141,6 +1184,7 @@ __device__ bool slice_near_hist(gcdptr tq, gcdptr tc, int cap, int i0, int i1, c
             sb += d * d;
           }
           nr[b] = near_radius(i < i1 && i != excl, sb, r, r2lo, r2hi, amb[b]);
+          if (NN) nn_take(i < i1, sb, i, nb, nb_s, nbi);
           x[b][0] = sb;
           any_amb |= amb[b];
         }
@@ -1308,13 +1352,15 @@ __device__ bool slice_near_hist(gcdptr tq, gcdptr tc, int cap, int i0, int i1, c
   }
   if (threadIdx.x == 0) X.cnt = tot_all;
   __syncthreads();
+  if (NN) slice_nn_reduce(nb, nbi, X);
   return true;
 }
 
+template <bool NN>
 __device__ __noinline__ void slice_near(gcdptr tq, gcdptr tc, int cap, int i0, int i1, const double* q, int excl,
                                         double r, ScanLds& X) {
-  if (uni(slice_near_hist(tq, tc, cap, i0, i1, q, excl, r, X))) return;
-  slice_near_body(tq, tc, cap, i0, i1, q, excl, r, X);
+  if (uni(slice_near_hist<NN>(tq, tc, cap, i0, i1, q, excl, r, X))) return;
+  slice_near_body<NN>(tq, tc, cap, i0, i1, q, excl, r, X);
 }
 
 // find_near_vertices_interpolation (birrt_star.cpp:4272-4324): count k, the first K and the last K entries of
@@ -1344,7 +1390,9 @@ __device__ __noinline__ void slice_near(gcdptr tq, gcdptr tc, int cap, int i0, i
 #define NEAR_COUNT(k)
 #endif
 
-template <int K>
+// NN: also the nearest node of q over the whole tree (no exclusion; nearest()'s answer) in g_L.fnn_d / fnn_id -- connect's
+// two scans of x_new in tree_B in one pass (no scout record then: spec must be false).
+template <int K, bool NN = false>
 __device__ void near_set(const Ctx& C, int t, const double* q, int excl, bool spec = false) {
 #ifdef SMP_NEAR_PROF
   unsigned long long _tn = 0;
@@ -1361,7 +1409,7 @@ __device__ void near_set(const Ctx& C, int t, const double* q, int excl, bool sp
   const double r2 = r * r, r2lo = r2 * (1.0 - 1e-12), r2hi = r2 * (1.0 + 1e-12);
   const int lane = lane_id(), wave = wave_id();
   TR();
-  if (spec && spec_stage(C, SC_NEAR)) {
+  if (!NN && spec && spec_stage(C, SC_NEAR)) {
     // the scout's near set of the same configuration over the tree's first X nodes, with the near nodes appended since
     // (at most 64: else the full scan below) merged in exactly: the costs of the first X nodes are those the record
     // saw (no rewire of this tree in between), so the K lowest / highest (cost, id) entries of the whole set are among
@@ -1439,10 +1487,12 @@ __device__ void near_set(const Ctx& C, int t, const double* q, int excl, bool sp
     }
   }
   if (K == SCAN_K && scan_split(C, n)) {
-    near_set_dist(C, t, q, excl);
+    near_set_dist(C, t, q, excl, NN);
     TR();
     return;
   }
+  double nb = 10000.0, nb_s = 1e300;  // NN: this thread's nearest candidate
+  int nbi = 0x7fffffff;
   double qq[NJ];
   for (int j = 0; j < NJ; ++j) qq[j] = q[j];
   int tot_all = 0;  // near nodes of the chunks before this one (block-uniform)
@@ -1478,6 +1528,7 @@ __device__ void near_set(const Ctx& C, int t, const double* q, int excl, bool sp
             sb += d * d;
           }
           nr[b] = near_radius(i < n && i != excl, sb, r, r2lo, r2hi, amb[b]);
+          if (NN) nn_take(i < n, sb, i, nb, nb_s, nbi);
           x[b][0] = sb;
           any_amb |= amb[b];
         }
@@ -1574,7 +1625,7 @@ __device__ void near_set(const Ctx& C, int t, const double* q, int excl, bool sp
     if (!uni(g_L.nh.fast)) {
       NEAR_COUNT(26);
       __syncthreads();
-      near_set_stream<K>(C, t, q, excl);
+      near_set_stream<K, NN>(C, t, q, excl);
       return;
     }
     const int blo = g_L.nh.blo, bhi = g_L.nh.bhi;
@@ -1654,6 +1705,7 @@ __device__ void near_set(const Ctx& C, int t, const double* q, int excl, bool sp
   }
   if (threadIdx.x == 0) { g_L.nk = tot_all; g_L.S.near_nodes += n; }
   __syncthreads();
+  if (NN) fnn_reduce(nb, nbi);
   TR();
 }
 
@@ -2041,7 +2093,7 @@ __device__ void scan_publish(const Ctx& C, int seq, int near, int t, const doubl
   if (i < SCAN_WORDS) {
     unsigned w = 0;
     if (i == 0) {
-      w = SCAN_HDR | (unsigned)near << 19 | (unsigned)t << 20;
+      w = SCAN_HDR | (unsigned)(near != 0) << 19 | (unsigned)t << 20 | (unsigned)(near == 2) << 21;
     } else if (i <= 16) {
       const unsigned long long b = (unsigned long long)__double_as_longlong(q[(i - 1) >> 1]);
       w = ((i - 1) & 1) ? (unsigned)(b >> 32) : (unsigned)b;
@@ -2068,7 +2120,8 @@ __device__ void scan_slice(const Ctx& C, int near, int t, const double* q, int i
   const int cap = uni(__hip_atomic_load(&C.Q.st->cap, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   int lo, hi;
   scan_range(i0, n, P, w, &lo, &hi);
-  if (near) slice_near(tq, tc, cap, lo, hi, q, excl, r, X);
+  if (near == 2) slice_near<true>(tq, tc, cap, lo, hi, q, excl, r, X);
+  else if (near) slice_near<false>(tq, tc, cap, lo, hi, q, excl, r, X);
   else slice_nn(tq, cap, lo, hi, q, X);
 }
 
@@ -2076,7 +2129,7 @@ __device__ void scan_slice(const Ctx& C, int near, int t, const double* q, int i
 // the result granules.
 __device__ __noinline__ void scan_helper(const Ctx& C, JobLds& J, int worker, int seq) {
   const unsigned hdr = J.words[0];
-  const int near = (hdr >> 19) & 1, t = (hdr >> 20) & 1;
+  const int near = ((hdr >> 21) & 1) ? 2 : (int)((hdr >> 19) & 1), t = (hdr >> 20) & 1;
   double q[NJ];
   for (int j = 0; j < NJ; ++j) q[j] = __hiloint2double((int)J.words[2 + 2 * j], (int)J.words[1 + 2 * j]);
   const int i0 = (int)J.words[17], n = (int)J.words[18], excl = (int)J.words[19], P = (int)J.words[22];
@@ -2127,15 +2180,22 @@ __device__ __noinline__ void scan_helper(const Ctx& C, JobLds& J, int worker, in
       const unsigned v = f == 0 ? (unsigned)k : f == 1 ? (unsigned)(k >> 32) : (unsigned)id;
       st_agent(&out[2 + 3 * side * SCAN_K + j], granule(seq, v));
     }
+    // a fused scan's nearest node after the near lists: key halves, id
+    if (near == 2 && i >= 256 && i < 259) {
+      const int f = i - 256;
+      const unsigned v = f == 0 ? (unsigned)X.wk[0] : f == 1 ? (unsigned)(X.wk[0] >> 32) : (unsigned)X.wi[0];
+      st_agent(&out[2 + 6 * SCAN_K + f], granule(seq, v));
+    }
   }
   __syncthreads();
 }
 
 // Slot w of the merge area from a slice result in X (all threads).
 __device__ __forceinline__ void merge_put(MergeLds& M, const ScanLds& X, int near, int w) {
-  if (!near) {
+  if (near != 1) {  // nearest, or a fused scan's nearest part
     if (threadIdx.x == 0) { M.nk[w] = X.wk[0]; M.ni[w] = X.wi[0]; }
-  } else {
+  }
+  if (near) {
     const int take = X.take;
     if (threadIdx.x < SCAN_K) {
       const int e = threadIdx.x;
@@ -2188,7 +2248,9 @@ __device__ void scan_run(const Ctx& C, int near, int t, const double* q, int i0,
   int last_done = 0;
   // One collection round loads every granule of every outstanding result at once (up to 4 per thread per pass:
   // independent loads, one round trip), then keeps the results whose needed granules all carry this job's number.
-  const int per = near ? 2 + 6 * SCAN_K : 3;
+  // (a fused scan's result: the near lists, then its nearest node's 3 granules)
+  constexpr int NG = 2 + 6 * SCAN_K;
+  const int per = near ? NG + (near == 2 ? 3 : 0) : 3;
   const int total = (P - 1) * per;
   for (int k = 0;; k ^= 1) {
     for (int base = 0; base < total; base += 4 * BLOCK) {
@@ -2217,6 +2279,10 @@ __device__ void scan_run(const Ctx& C, int near, int t, const double* q, int i0,
             M.hv[w][i] = val[u];
             if (!((okm >> u) & 1u)) M.bad[w] = 1;
           }
+          if (near == 2 && !M.done[w] && i >= NG) {
+            M.hn[w][i - NG] = val[u];
+            if (!((okm >> u) & 1u)) M.bad[w] = 1;
+          }
         }
       }
       if (near) {
@@ -2227,7 +2293,7 @@ __device__ void scan_run(const Ctx& C, int near, int t, const double* q, int i0,
           const int g = base + u * BLOCK + (int)threadIdx.x;
           if (g < total) {
             const int w = 1 + g / per, i = g - (w - 1) * per;
-            if (!M.done[w] && i >= 2) {
+            if (!M.done[w] && i >= 2 && i < NG) {
               const int j = i - 2, side = j >= 3 * SCAN_K ? 1 : 0, jj = j - side * 3 * SCAN_K, e = jj / 3, f = jj - 3 * e;
               if (e < min((int)M.hv[w][1], SCAN_K)) {
                 if (!((okm >> u) & 1u)) M.bad[w] = 1;
@@ -2250,6 +2316,10 @@ __device__ void scan_run(const Ctx& C, int near, int t, const double* q, int i0,
           } else {
             M.nk[w] = (unsigned long long)M.hv[w][1] << 32 | M.hv[w][0];
             M.ni[w] = (int)M.hv[w][2];
+          }
+          if (near == 2) {
+            M.nk[w] = (unsigned long long)M.hn[w][1] << 32 | M.hn[w][0];
+            M.ni[w] = (int)M.hn[w][2];
           }
           M.done[w] = 1;
           atomicAdd(&M.ndone, 1);
@@ -2324,10 +2394,10 @@ __device__ int nearest_dist(const Ctx& C, int t, const double* q, int i0, int n,
 // the P ascending low lists and the highest SCAN_K of the P descending high lists, by a tournament -- wave 0 the low
 // side, wave 1 the high side, lane w the head of participant w's list; each round one wave minimum (maximum) of the
 // heads, whose lane advances.  The slices partition the range, so ids are distinct and every round has one winner.
-__device__ void near_set_dist(const Ctx& C, int t, const double* q, int excl) {
+__device__ void near_set_dist(const Ctx& C, int t, const double* q, int excl, bool nn) {
   const int n = uni(g_L.S.n[t]);
   const int P = scan_parts(C, 1, n);
-  scan_run(C, 1, t, q, 0, n, excl, g_L.S.near_r, P);
+  scan_run(C, nn ? 2 : 1, t, q, 0, n, excl, g_L.S.near_r, P);
   const MergeLds& M = g_L.sc.m;
   int tot = 0;
   for (int w = 0; w < P; ++w) tot += M.cnt[w];
@@ -2352,7 +2422,17 @@ __device__ void near_set_dist(const Ctx& C, int t, const double* q, int excl) {
       }
     }
   }
-  if (threadIdx.x == 0) { g_L.nk = tot; g_L.n_lo = take; g_L.n_hi = take; g_L.S.near_nodes += n; }
+  if (threadIdx.x == 0) {
+    g_L.nk = tot; g_L.n_lo = take; g_L.n_hi = take; g_L.S.near_nodes += n;
+    if (nn) {  // the fused scan's nearest node: the (distance key, id) minimum of the slices
+      unsigned long long bk = M.nk[0];
+      int bi = M.ni[0];
+      for (int w = 1; w < P; ++w)
+        if (M.nk[w] < bk || (M.nk[w] == bk && M.ni[w] < bi)) { bk = M.nk[w]; bi = M.ni[w]; }
+      g_L.fnn_d = __longlong_as_double((long long)bk);
+      g_L.fnn_id = bi;
+    }
+  }
   __syncthreads();
 #ifdef SMP_SCAN_PROF
   if (threadIdx.x == 0) { SCANPROF_ADD(4, wall_clock64() - g_L.spc_t); SCANPROF_ADD(17, wall_clock64() - g_L.spc_t); }
@@ -4440,14 +4520,16 @@ __device__ void scout_connect(const Ctx& C, long long it, int t, int par, unsign
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   if (threadIdx.x == 0) g_L.S.n[tb] = g_L.cnt;
   __syncthreads();
-  double d;
-  int cid = nearest_scan(C, tb, g_L.xn.q, 0, &d);
+  // the near set of x_new and its nearest node (no exclusion) in one pass over tree_B
+  near_set<20, true>(C, tb, g_L.xn.q, g_L.xn.id);
   if (threadIdx.x == 0) {
+    double d = g_L.fnn_d;
+    int cid = g_L.fnn_id;
     if (!(d < 10000.0)) { cid = 0; d = 10000.0; }
     R.cc.d = d; R.cc.id = cid;
     load_node(C, tb, cid, &g_L.xc);
   }
-  near_set<20>(C, tb, g_L.xn.q, g_L.xn.id);
+  __syncthreads();
   if (threadIdx.x == 0) {
     const int E = min(g_L.n_lo, g_L.S.max_near);
     g_L.cnt = E;
@@ -5464,16 +5546,19 @@ __global__ void __launch_bounds__(BLOCK) near_probe_kernel(const double* tqv, co
   }
   const unsigned long long m0 = __builtin_amdgcn_s_memtime(), w0 = wall_clock64();
   unsigned long long t_nn = 0, t_near = 0;
-  // reps < 0: the slice functions of distributed scans (slice_nn / slice_near over [0, n)) instead of nearest / near_set
-  const bool slice = reps < 0;
-  if (slice) reps = -reps;
+  // reps < 0: -(reps + ((mode - 1) << 20)), mode 1 the slice functions of distributed scans (slice_nn / slice_near over
+  // [0, n)) instead of nearest / near_set, 2 the fused near_set<20, true>, 3 the fused slice_near<true> (nearest and near
+  // set in one pass: the near timing holds both, the nearest timing nothing)
+  int mode = 0;
+  if (reps < 0) { reps = -reps; mode = 1 + (reps >> 20); reps &= (1 << 20) - 1; }
+  const bool slice = mode == 1 || mode == 3;
   const gcdptr tq = uni_gptr(tqv), tc = uni_gptr(tcost);
   for (int k = 0; k < m; ++k) {
     if (threadIdx.x < NJ) g_L.xr[threadIdx.x] = queries[(size_t)k * NJ + threadIdx.x];
     __syncthreads();
     int id = 0;
     unsigned long long t0 = wall_clock64();
-    for (int rep = 0; rep < reps; ++rep) {
+    for (int rep = 0; rep < reps && mode < 2; ++rep) {
       if (slice) {
         slice_nn(tq, cap, 0, n, g_L.xr, g_L.sc.s);
         id = __longlong_as_double((long long)g_L.sc.s.wk[0]) < 10000.0 ? g_L.sc.s.wi[0] : 0;
@@ -5483,9 +5568,13 @@ __global__ void __launch_bounds__(BLOCK) near_probe_kernel(const double* tqv, co
     }
     unsigned long long t1 = wall_clock64();
     for (int rep = 0; rep < reps; ++rep) {
-      if (slice) slice_near(tq, tc, cap, 0, n, g_L.xr, excl[k], r, g_L.sc.s);
+      if (mode == 1) slice_near<false>(tq, tc, cap, 0, n, g_L.xr, excl[k], r, g_L.sc.s);
+      else if (mode == 3) slice_near<true>(tq, tc, cap, 0, n, g_L.xr, excl[k], r, g_L.sc.s);
+      else if (mode == 2) near_set<20, true>(C, 0, g_L.xr, excl[k]);
       else near_set<20>(C, 0, g_L.xr, excl[k]);
     }
+    if (mode == 2) id = g_L.fnn_d < 10000.0 ? g_L.fnn_id : 0;
+    if (mode == 3) id = __longlong_as_double((long long)g_L.sc.s.wk[0]) < 10000.0 ? g_L.sc.s.wi[0] : 0;
     unsigned long long t2 = wall_clock64();
     t_nn += t1 - t0;
     t_near += t2 - t1;
