@@ -1117,6 +1117,8 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
   if (const char* e = std::getenv("SMP_PRE_DELAY")) pre_delay = std::atoi(e);
   int early_ask = 0;  // SMP_EARLY_ASK=1: after the first solution, iteration k + 2 is asked for before k's rewires (DESIGN.md "Early asks")
   if (const char* e = std::getenv("SMP_EARLY_ASK")) early_ask = std::atoi(e);
+  int conn_check = 0;  // SMP_CONN_CHECK=1: connect's edges checked by the scouts with their SC_CONN scans (experiments)
+  if (const char* e = std::getenv("SMP_CONN_CHECK")) conn_check = std::atoi(e);
   int pre_commit = 1;  // SMP_PRE_COMMIT=0: every iteration runs the full path (experiments)
   if (const char* e = std::getenv("SMP_PRE_COMMIT")) pre_commit = std::atoi(e);
   int rebalance = nh_req == 0 ? 1 : 0;  // SMP_REBALANCE=0: keep the first launch's provisioning (experiments)
@@ -1215,6 +1217,7 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
       qdev[i].pre_delay = pre_delay;
       qdev[i].pre_commit = pre_commit;
       qdev[i].early_ask = early_ask;
+      qdev[i].conn_check = conn_check;
       qdev[i].sampler_jb = p->qb[i].jb.p;
       for (int s = 0; s < ns; ++s) {
         qdev[i].sjbs[s] = p->qb[i].sjb[s].p;

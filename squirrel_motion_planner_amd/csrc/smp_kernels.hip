@@ -1224,6 +1224,52 @@ __device__ bool slice_near_hist(gcdptr tq, gcdptr tc, int cap, int i0, int i1, c
     }
     const int take_c = min(K, tot);
     const int prev = X.take;  // both running lists hold this many entries
+    if (uni(tot <= NEAR_BUF && prev == 0)) {
+      // few near nodes and no running lists: every near node of the chunk into one buffer (wave w's at the wave prefix
+      // of the counts), each ranked by counting -- rank r below K is the r-th lowest entry, m - 1 - r below K the
+      // (m - 1 - r)-th highest: no histogram
+      int base = 0;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) base += w < wave ? X.wtot[w] : 0;
+      const unsigned long long below = (1ull << lane) - 1;
+#pragma unroll
+      for (int g = 0; g < NEAR_NBK; ++g) {
+        if (c0 + g * BLOCK + wave * 64 < i1) {
+          const bool nr = nmask >> g & 1;
+          const unsigned long long ml = __ballot(nr);
+          if (nr) {
+            const int slot = base + __popcll(ml & below);
+            X.ck[0][slot] = key[g];
+            X.ci[0][slot] = c0 + g * BLOCK + wave * 64 + lane;
+          }
+          base += __popcll(ml);
+        }
+      }
+      __syncthreads();
+      {
+        const int c = threadIdx.x >> 2, sl = threadIdx.x & 3;  // 4 lanes per entry (m <= 128)
+        int rank = 0;
+        unsigned long long ck = 0;
+        int ci = 0;
+        if (c < tot) {
+          ck = X.ck[0][c];
+          ci = X.ci[0][c];
+          for (int j = sl; j < tot; j += 4) rank += ki_less(X.ck[0][j], X.ci[0][j], ck, ci);
+        }
+        rank += __shfl_xor(rank, 1);
+        rank += __shfl_xor(rank, 2);
+        if (c < tot && sl == 0) {
+          if (rank < take_c) { X.lk[rank] = ck; X.li[rank] = ci; }
+          const int h = tot - 1 - rank;
+          if (h < take_c) { X.hk[h] = ck; X.hi[h] = ci; }
+        }
+      }
+      tot_all += tot;
+      __syncthreads();
+      if (threadIdx.x == 0) X.take = take_c;
+      __syncthreads();
+      continue;
+    }
     const double cmin = __longlong_as_double((long long)kmin), cmax = __longlong_as_double((long long)kmax);
     const double scale = cmax > cmin ? (NEAR_BINS * (1.0 - 1e-9)) / (cmax - cmin) : 0.0;
     unsigned bins[NEAR_NBK / 4] = {};  // 8-bit bin of every near key
@@ -1569,6 +1615,51 @@ __device__ void near_set(const Ctx& C, int t, const double* q, int excl, bool sp
     }
     const int take_c = min(K, tot);
     const int prev_lo = g_L.n_lo, prev_hi = g_L.n_hi;
+    if (uni(tot <= NEAR_BUF && prev_lo == 0 && prev_hi == 0)) {
+      // few near nodes and no running lists: one buffer, ranked by counting (slice_near_hist's direct path)
+      int base = 0;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) base += w < wave ? g_L.nh.wtot[w] : 0;
+      const unsigned long long below = (1ull << lane) - 1;
+#pragma unroll
+      for (int g = 0; g < NEAR_NBK; ++g) {
+        if (c0 + g * BLOCK + wave * 64 < n) {
+          const bool nr = nmask >> g & 1;
+          const unsigned long long ml = __ballot(nr);
+          if (nr) {
+            const int slot = base + __popcll(ml & below);
+            g_L.nh.ck[0][slot] = key[g];
+            g_L.nh.ci[0][slot] = c0 + g * BLOCK + wave * 64 + lane;
+          }
+          base += __popcll(ml);
+        }
+      }
+      __syncthreads();
+      {
+        const int c = threadIdx.x >> 2, sl = threadIdx.x & 3;  // 4 lanes per entry (m <= 128)
+        int rank = 0;
+        unsigned long long ck = 0;
+        int ci = 0;
+        if (c < tot) {
+          ck = g_L.nh.ck[0][c];
+          ci = g_L.nh.ci[0][c];
+          for (int j = sl; j < tot; j += 4) rank += ki_less(g_L.nh.ck[0][j], g_L.nh.ci[0][j], ck, ci);
+        }
+        rank += __shfl_xor(rank, 1);
+        rank += __shfl_xor(rank, 2);
+        if (c < tot && sl == 0) {
+          if (rank < take_c) { g_L.lo_c[rank] = __longlong_as_double((long long)ck); g_L.lo_i[rank] = ci; }
+          const int h = tot - 1 - rank;
+          if (h < take_c) { g_L.hi_c[take_c - 1 - h] = __longlong_as_double((long long)ck); g_L.hi_i[take_c - 1 - h] = ci; }
+        }
+      }
+      tot_all += tot;
+      __syncthreads();
+      if (threadIdx.x == 0) { g_L.n_lo = take_c; g_L.n_hi = take_c; }
+      __syncthreads();
+      NEAR_COUNT(27);
+      continue;
+    }
     const double cmin = __longlong_as_double((long long)kmin), cmax = __longlong_as_double((long long)kmax);
     const double scale = cmax > cmin ? (NEAR_BINS * (1.0 - 1e-9)) / (cmax - cmin) : 0.0;
     unsigned bins[NEAR_NBK / 4] = {};  // 8-bit bin of every near key
@@ -4547,14 +4638,18 @@ __device__ void scout_connect(const Ctx& C, long long it, int t, int par, unsign
   }
   __syncthreads();
   edge_costs(C, 1 + E);
-  // the validity of every connect edge (the direct one and each near candidate's, checked to the end): one job, so that the
-  // leader's connect takes them instead of its own two jobs (direct edge, near loop)
-  if (threadIdx.x < MAXE) g_L.eg_need[threadIdx.x] = threadIdx.x < 1 + E;
-  if (threadIdx.x == 0) g_L.rec_grp = -1;
-  __syncthreads();
-  edge_validity(C, 1 + E, false, P_XCONNECT);
-  if (threadIdx.x < E) R.cc.first[threadIdx.x] = g_L.eg_first[1 + threadIdx.x];
-  if (threadIdx.x == 0) { R.cc.first0 = g_L.eg_first[0]; R.cc.nfirst = E; }
+  // QueryDev::conn_check: the validity of every connect edge (the direct one and each near candidate's, checked to the
+  // end) in one more job, so that the leader's connect takes them instead of its own two jobs (direct edge, near loop).
+  // Off by default: it lengthens the scout's turn (C2: scout busy 106 -> 121 us per pass, 67.8 -> 71.9 us per leader
+  // iteration -- the two post-solution scouts, not the leader's connect, bound the iteration)
+  if (uni(C.Q.conn_check)) {
+    if (threadIdx.x < MAXE) g_L.eg_need[threadIdx.x] = threadIdx.x < 1 + E;
+    if (threadIdx.x == 0) g_L.rec_grp = -1;
+    __syncthreads();
+    edge_validity(C, 1 + E, false, P_XCONNECT);
+    if (threadIdx.x < E) R.cc.first[threadIdx.x] = g_L.eg_first[1 + threadIdx.x];
+    if (threadIdx.x == 0) { R.cc.first0 = g_L.eg_first[0]; R.cc.nfirst = E; }
+  }
   if (threadIdx.x < MAX_NEAR) {
     R.cc.lo_i[threadIdx.x] = g_L.lo_i[threadIdx.x]; R.cc.lo_c[threadIdx.x] = g_L.lo_c[threadIdx.x];
     R.cc.hi_i[threadIdx.x] = g_L.hi_i[threadIdx.x]; R.cc.hi_c[threadIdx.x] = g_L.hi_c[threadIdx.x];
@@ -5292,6 +5387,24 @@ __global__ void __launch_bounds__(BLOCK) plan_kernel(const RobotDev* __restrict_
     if (i >= 0) g_L.pc_q[t][i & (PATCH_K - 1)][j] = C.Q.tr[t].q[(size_t)j * g_L.S.cap + i];
   }
   __syncthreads();
+  if (uni(g_L.S.status == 0 && g_L.S.phase == 0 && C.Q.nscouts > 0 && C.Q.pre_commit && C.Q.sampler)) {
+    // first launch, before the pre-loop connection: the sampling parameters (version 1: the run-ahead sampler starts
+    // filling its ring now) and the first iterations' pre-solution records.  Until the first solution the trees only
+    // grow, so a record of the roots' snapshot stays exact up to the nodes appended since -- the connection's via nodes
+    // included -- which the leader patches in as for any record: the scouts work while the leader checks the direct
+    // connection, instead of starting with iteration 0.
+    drain();  // the roots' stores
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      sample_version(C);
+      sample_publish(C);
+      bool fenced = false;
+      const long long j = g_L.S.iter;
+      for (int ahead = 0; ahead < C.Q.nscouts; ++ahead)
+        scout_ask(C, j + ahead, (ahead & 1) ? 1 - g_L.S.A : g_L.S.A, true, fenced);
+    }
+    __syncthreads();
+  }
   if (uni(g_L.S.status == 0 && g_L.S.phase == 0)) {
     // pre-loop direct connection of the two roots (birrt_star.cpp:1072-1075)
     if (threadIdx.x == 0) {

@@ -300,6 +300,7 @@ struct QueryDev {
   int pre_delay;               // before the first solution a scout starts record k once the leader is at k - pre_delay
   int pre_commit;              // 1: pre-solution iterations are committed from complete scout records
   int early_ask;               // 1: after the first solution, iteration k + 2 is asked for as soon as its scout is free
+  int conn_check;              // 1: the scout's SC_CONN record carries the validity of connect's edges (scout_connect)
   ScoutBoard* scbs[MAX_SCOUTS];
   JobBoard* sjbs[MAX_SCOUTS];
   ViaNode* svias[MAX_SCOUTS];
