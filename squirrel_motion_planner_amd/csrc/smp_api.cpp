@@ -26,8 +26,7 @@ namespace smp {
 void launch_check(int ct, int grid, hipStream_t st, const RobotDev* rb, SceneDev sc, const MapCfg* mc, const double* q,
                   long long n, int self, int map, uint8_t* valid, unsigned long long* prof);
 __global__ void plan_kernel(const RobotDev* rb, SceneDev sc, const MapCfg* mc, QueryDev* qs, int nq, int scout_base,
-                            int iters);
-__global__ void helper_kernel(const RobotDev* rb, SceneDev sc, const MapCfg* mc, QueryDev* qs, int nq);
+                            int helper_base, int iters);
 __global__ void path_kernel(QueryDev* qs, int* counts);
 __global__ void path_edges_kernel(const QueryDev* qs, int q, int ns, int ng, double* out);
 __global__ void boards_reset_kernel(const QueryDev* qs, int ns);
@@ -111,8 +110,6 @@ struct QueryBuffers {
 struct smp_planner {
   int device = 0;
   hipStream_t stream = nullptr;
-  hipStream_t hstream = nullptr;   // helper_kernel (collision-job helpers), concurrent with plan_kernel
-  hipEvent_t ev_board = nullptr;
   RobotHost robot;
   smp_params params;
   RobotDev* d_rb = nullptr;
@@ -163,26 +160,23 @@ struct smp_planner {
 static int busy_check(smp_planner* p) {
   if (!p->busy) return SMP_OK;
   (void)hipSetDevice(p->device);
-  const hipError_t a = hipStreamQuery(p->stream), b = hipStreamQuery(p->hstream);
-  if (a == hipErrorNotReady || b == hipErrorNotReady) return SMP_ERR_HIP;
+  if (hipStreamQuery(p->stream) == hipErrorNotReady) return SMP_ERR_HIP;
   (void)hipGetLastError();
   p->busy = false;
   return SMP_OK;
 }
 
-// Workgroups of BLOCK threads that can be resident at once on the device, for the planner's kernels (leader / scout
-// plan_kernel and helper_kernel share the CUs): occupancy per CU (registers, LDS) x CUs.
+// Workgroups of BLOCK threads that can be resident at once on the device for plan_kernel (leaders, scouts and helpers
+// of a launch are its blocks): occupancy per CU (registers, LDS) x CUs.
 static int resident_slots(smp_planner* p) {
   if (p->slots_cache > 0) return std::max(1, p->slots_cache / std::max(1, p->slot_share));
-  int occ_plan = 0, occ_help = 0;
+  int occ_plan = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_plan, reinterpret_cast<const void*>(&plan_kernel), BLOCK, 0) !=
-          hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_help, reinterpret_cast<const void*>(&helper_kernel), BLOCK, 0) !=
-          hipSuccess) {
+      hipSuccess) {
     (void)hipGetLastError();
     return p->num_cus;
   }
-  p->slots_cache = p->num_cus * std::max(1, std::min(occ_plan, occ_help));
+  p->slots_cache = p->num_cus * std::max(1, occ_plan);
   return std::max(1, p->slots_cache / std::max(1, p->slot_share));
 }
 
@@ -409,8 +403,7 @@ int smp_planner_create(int device, const smp_robot* robot, const smp_params* par
   {
     size_t need = 0;
     hipFuncAttributes fa;
-    const void* ks[] = {reinterpret_cast<const void*>(&plan_kernel), reinterpret_cast<const void*>(&helper_kernel),
-                        reinterpret_cast<const void*>(&path_kernel)};
+    const void* ks[] = {reinterpret_cast<const void*>(&plan_kernel), reinterpret_cast<const void*>(&path_kernel)};
     for (const void* k : ks)
       if (hipFuncGetAttributes(&fa, k) == hipSuccess) need = std::max(need, (size_t)fa.localSizeBytes);
     need = std::max(need, check_kernels_private_bytes());
@@ -425,11 +418,7 @@ int smp_planner_create(int device, const smp_robot* robot, const smp_params* par
     }
   }
   // every failure from here on releases what was created so far (smp_planner_destroy skips null handles)
-  int prio_lo = 0, prio_hi = 0;
   if (hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess ||
-      hipStreamCreateWithPriority(&p->hstream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
-      hipEventCreateWithFlags(&p->ev_board, hipEventDisableTiming) != hipSuccess ||
       hipMalloc(&p->d_rb, sizeof(RobotDev)) != hipSuccess || hipMalloc(&p->d_mc, sizeof(MapCfg)) != hipSuccess ||
       hipMemcpy(p->d_rb, &p->robot.dev, sizeof(RobotDev), hipMemcpyHostToDevice) != hipSuccess ||
       hipEventCreate(&p->ev0) != hipSuccess || hipEventCreate(&p->ev1) != hipSuccess) {
@@ -462,7 +451,6 @@ void smp_planner_destroy(smp_planner* p) {
     return;
   }
   if (p->stream) (void)hipStreamSynchronize(p->stream);
-  if (p->hstream) (void)hipStreamSynchronize(p->hstream);
   for (auto& q : p->qb) q.release();
   p->d_qdev.release(); p->d_counts.release(); p->d_lfin.release(); p->d_cq.release(); p->d_valid.release();
   p->d_ik_tasks.release(); p->d_ik_out.release(); p->d_ik_best.release(); p->d_path_edges.release();
@@ -472,8 +460,6 @@ void smp_planner_destroy(smp_planner* p) {
   if (p->ev0) (void)hipEventDestroy(p->ev0);
   if (p->ev1) (void)hipEventDestroy(p->ev1);
   if (p->stream) (void)hipStreamDestroy(p->stream);
-  if (p->hstream) (void)hipStreamDestroy(p->hstream);
-  if (p->ev_board) (void)hipEventDestroy(p->ev_board);
   if (p->h_ttff) (void)hipHostFree(p->h_ttff);
   if (p->h_st) (void)hipHostFree(p->h_st);
   delete p;
@@ -1317,30 +1303,24 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
     const int na = (int)act.size();
     HIPCHK(hipMemsetAsync(p->d_lfin.p, 0, sizeof(unsigned), p->stream));
     if (nh > 0) {
-      // fresh boards, then the helpers on their own (high-priority, separate hardware queue) stream; they wait
-      // for the reset and leave when the leader signals stop
+      // fresh boards before the launch (its helpers poll them from their start and leave on the leader's stop)
       hipLaunchKernelGGL(boards_reset_kernel, dim3(na * (1 + 2 * ns)), dim3(BLOCK), 0, p->stream, p->d_qdev.p, ns);
       HIPCHK(hipGetLastError());
-      HIPCHK(hipEventRecord(p->ev_board, p->stream));
     }
     if (launches == 0) hstamp("boards reset issued");
     HIPCHK(hipEventRecord(p->ev0, p->stream));
-    // scout s of query q at block scout_base + s * round8(nq) + q, scout_base a multiple of 8: blocks b and b + 8
-    // are dealt to the same XCD (plan_kernel).  The leaders and scouts are queued before the helpers, so their
-    // workgroups find CUs first (a scout queued behind 200 helpers was seen to start only when they left).
+    // one dispatch for every workgroup of the launch (plan_kernel): leaders at blocks [0, na), scout s of query q at
+    // scout_base + s * round8(na) + q, helper h of query q at helper_base + h * na + q; scout_base and helper_base are
+    // multiples of 8, so blocks b and b + 8 are dealt to the same XCD (a query's leader and scouts share one).  The
+    // leaders and scouts come first in dispatch order, so their workgroups find CUs first.
     const int r8 = (na + 7) / 8 * 8;
     const int scout_base = ns > 0 ? r8 : 0;
-    const int grid = ns > 0 ? scout_base + (ns - 1) * r8 + na : na;
+    const int helper_base = nh > 0 ? (ns > 0 ? scout_base + ns * r8 : r8) : (1 << 30);
+    const int grid = nh > 0 ? helper_base + na * nh : (ns > 0 ? scout_base + (ns - 1) * r8 + na : na);
     hipLaunchKernelGGL(plan_kernel, dim3(grid), dim3(BLOCK), 0, p->stream, p->d_rb, p->sc,
-                       p->d_mc, p->d_qdev.p, na, scout_base, chunk);
+                       p->d_mc, p->d_qdev.p, na, scout_base, helper_base, chunk);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(p->ev1, p->stream));
-    if (nh > 0) {  // the helpers on their own (high-priority, separate hardware queue) stream, after the board reset
-      HIPCHK(hipStreamWaitEvent(p->hstream, p->ev_board, 0));
-      hipLaunchKernelGGL(helper_kernel, dim3(na * nh), dim3(BLOCK), 0, p->hstream, p->d_rb, p->sc, p->d_mc,
-                         p->d_qdev.p, na);
-      HIPCHK(hipGetLastError());
-    }
     if (launches == 0) hstamp("kernels launched");
     launches++;
     // time the first feasible path on the host: poll the flags while the launch runs -- spinning (with a yield) until
@@ -1394,7 +1374,6 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
         }
     }
     HIPCHK(hipStreamSynchronize(p->stream));
-    if (nh > 0) HIPCHK(hipStreamSynchronize(p->hstream));
     if (std::getenv("SMP_BOUNDS")) {
       int dbg[8];
       if (smp_debug_bounds(dbg) == 0 && dbg[0])

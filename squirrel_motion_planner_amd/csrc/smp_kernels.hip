@@ -317,6 +317,14 @@ struct SmpLds {
   int ok[64];
   int win;
 };
+// LDS of the run-ahead sampler workgroup.
+struct SamplerLds {
+  QState S;        // the query's constants, with have_sol / cbest of the version being served
+  SmpLds W;
+  double out[NJ];
+  long long next;  // next iteration to sample
+  int ver, go[2];
+};
 #ifndef SMP_PLAN_CT
 #define SMP_PLAN_CT 8  // (the local path of a query without helpers, and init_planner's start / goal check)
 #endif
@@ -332,6 +340,7 @@ struct PlanLds {
     JobLds job;  // job mode: the leader's LDS copy of its published job + one job tile
     double seg[MAXE][MAX_PTS][3];
     SmpLds smp;
+    SamplerLds smpl;  // a helper block of plan_kernel that runs the run-ahead sampler
   } u;
   // scan scratch (outside the union u: a scan may run while a collision job holds u.job, overlap_work): a local near set's
   // lists, or a distributed scan's own slice and merge area -- a scan is one or the other
@@ -2543,7 +2552,7 @@ __device__ void near_set_dist(const Ctx& C, int t, const double* q, int excl, bo
 // its collision job's tiles (overlap_work) -- and this helper scans its slice if it is a participant (scan_helper).  Then
 // tiles w - 1, w - 1 + W, ... of a collision job, each result stored as one granule.  Leaves on the stop flag, or after
 // two idle seconds should the leader never start.
-__device__ __forceinline__ void helper_main(const Ctx& C, int hidx, JobLds& J) {
+__device__ __noinline__ void helper_main(const Ctx& C, int hidx, JobLds& J) {
   JobBoard* jb = C.Q.jb;
   const int w = 1 + hidx, W = C.Q.nworkers;
   int last = 0, last_scan = 0;
@@ -5289,23 +5298,135 @@ __device__ __forceinline__ void scout_main(Ctx& C, int which) {
   }
 }
 
-// Advances every query (one workgroup each) by at most `iters` planner iterations.
-// One block per query: the planner loop.  Its collision jobs are shared with helper_kernel's blocks when the
-// query has a job board (DESIGN.md "Helpers").
+// Run-ahead sampler (DESIGN.md "Sampler"): keeps the samples of the leader's next SMP_RING - 1 iterations in
+// the ring, computed with the latest published parameters and tagged (iteration, version); a parameter change
+// restarts the window.  Never writes the slot of an iteration the leader may be reading: it fills iterations
+// up to (published iteration) + SMP_RING - 1 only.  Leaves on the stop flag or after two idle seconds.
+// (not inlined into helper_main, like scan_helper: the tile helpers' loop is compiled without the sampler's and the
+// scan slices' registers live around it -- C2 73.1 -> 71.8 us per iteration, perf_probe.py with SMP_JOB_PROF, round 3)
+__device__ __forceinline__ void sampler_body(const Ctx& C, SamplerLds& L) {
+  JobBoard* jb = C.Q.jb;
+  {
+    const int* src = reinterpret_cast<const int*>(C.Q.st);
+    int* dst = reinterpret_cast<int*>(&L.S);
+    for (int i = threadIdx.x; i < (int)(sizeof(QState) / sizeof(int)); i += BLOCK) dst[i] = src[i];
+  }
+  if (threadIdx.x == 0) { L.ver = 0; L.next = 0; }
+  __syncthreads();
+  unsigned long long t_last = wall_clock64();
+  for (int k = 0;; k ^= 1) {
+    if (threadIdx.x == 0) {
+      int go = 0;
+      if (ld_agent(&jb->stop)) {
+        go = -1;
+      } else {
+        const int ver = ld_agent(&jb->s_ver);
+        const long long cur = (long long)ld_agent(reinterpret_cast<const unsigned long long*>(&jb->s_iter));
+        if (ver != L.ver) {
+          L.S.have_sol = ld_agent(&jb->s_have_sol);
+          for (int c = 0; c < 3; ++c) L.S.cbest[c] = __longlong_as_double((long long)ld_agent(&jb->s_cbest[c]));
+          if (ld_agent(&jb->s_ver) == ver) { L.ver = ver; L.next = cur + 1; }  // else re-read next poll
+        }
+        if (L.next < cur + 1) L.next = cur + 1;
+        if (L.ver > 0 && ver == L.ver && L.next <= cur + SMP_RING - 1) go = 1;
+        else if (wall_clock64() - t_last > 200000000ull) go = -1;  // 2 s idle
+      }
+      L.go[k] = go;
+    }
+    __syncthreads();
+    const int go = uni(L.go[k]);
+    if (go < 0) break;
+    if (go == 0) {
+      __builtin_amdgcn_s_sleep(2);
+      continue;
+    }
+    const long long it = L.next;
+    const int st = sample_conf(L.S, (uint32_t)it, L.W, L.out);
+#ifdef SMP_RING_CHECK
+    if (threadIdx.x == 0) {
+      unsigned long long* d = g_ringdbg[it % SMP_RING];
+      st_agent(&d[0], (unsigned long long)it); st_agent(&d[1], (unsigned long long)L.ver);
+      st_agent(&d[2], (unsigned long long)L.S.have_sol);
+      for (int k = 0; k < 3; ++k) st_agent(&d[3 + k], (unsigned long long)__double_as_longlong(L.S.cbest[k]));
+      st_agent(&d[6], (unsigned long long)L.S.informed);
+      const RobotDev* rb = (&g_rb);
+      const double lv[6] = {L.S.h0[1], L.S.Crev[0], L.S.Crev[7], L.S.ctr_rev[0], rb->q_min[2], rb->q_max[2]};
+      for (int k = 0; k < 6; ++k) st_agent(&d[8 + k], (unsigned long long)__double_as_longlong(lv[k]));
+      unsigned long long rv = 0;
+      for (int j = 0; j < NJ; ++j) rv |= (unsigned long long)(rb->rev[j] != 0) << j;
+      st_agent(&d[14], rv);
+    }
+#endif
+    if (st == 0 && threadIdx.x < RING_G) {
+      unsigned w;
+      if (threadIdx.x < 2 * NJ) {
+        const unsigned long long bits = (unsigned long long)__double_as_longlong(L.out[threadIdx.x >> 1]);
+        w = (threadIdx.x & 1) ? (unsigned)(bits >> 32) : (unsigned)bits;
+      } else {
+        w = ring_param((int)threadIdx.x - 2 * NJ, L.S.have_sol, L.S.cbest);
+      }
+      st_agent(&jb->ring[it % SMP_RING].g[threadIdx.x], granule((int)ring_tag(it, L.ver), w));
+    }
+    if (threadIdx.x == 0) L.next = it + 1;
+    t_last = wall_clock64();
+    __syncthreads();
+  }
+}
+
+__device__ __noinline__ void sampler_main(const Ctx& C, SamplerLds& L) { sampler_body(C, L); }
+
+
+// Advances every query (one workgroup each) by at most `iters` planner iterations.  One launch holds every workgroup of
+// its queries (DESIGN.md "Execution model"): blocks [0, nq) are the leaders (the planner loop); scout s of query q is
+// block scout_base + s * r8 + q (scout_base and r8 = nq rounded up to 8 are multiples of 8, and blocks are dealt to the 8
+// XCDs round-robin: a query's leader and scouts share an XCD); from helper_base (a multiple of 8) block helper_base + h *
+// nq + q is helper h of query q -- the leader's tile helpers first, then each scout's, the run-ahead sampler last.  Every
+// role of a query runs in this one dispatch: the helpers are co-resident with the workgroups that publish their jobs,
+// and a kernel trace or a counter pass sees the whole query as one kernel.
 __global__ void __launch_bounds__(BLOCK) plan_kernel(const RobotDev* __restrict__ rb, SceneDev sc,
                                                      const MapCfg* __restrict__ mc, QueryDev* qs, int nq, int scout_base,
-                                                     int iters) {
-  // blocks [0, nq): leaders; scout s of query q at scout_base + s * r8 + q (scout_base and r8 = nq rounded up to 8
-  // are multiples of 8, and blocks are dealt to the 8 XCDs round-robin: a query's workgroups share an XCD); any
-  // other block has nothing to do
+                                                     int helper_base, int iters) {
   const int b = (int)blockIdx.x;
   const int r8 = (nq + 7) / 8 * 8;
-  const int so = b - scout_base, srole = scout_base > 0 && b >= scout_base ? so / r8 : -1;
+  const int so = b - scout_base, srole = scout_base > 0 && b >= scout_base && b < helper_base ? so / r8 : -1;
   const int sq = srole >= 0 ? so - srole * r8 : b;
-  if (b >= nq && (srole < 0 || sq >= nq)) return;
   // the block's context in LDS: every function takes it by reference, and a private copy would live in scratch (each
   // field read a scratch load, invalidated with the L1 by every acquire)
   __shared__ Ctx g_ctx;
+  __shared__ int g_role;
+  if (b >= helper_base) {
+    // helper block: -1 nothing to do, -2 run-ahead sampler, else tile helper h of the leader or of a scout
+    if (threadIdx.x == 0) {
+      Ctx c;
+      c.sc = sc;
+      c.Q = qs[(b - helper_base) % nq];
+      const int hidx = (b - helper_base) / nq, nh = ((int)gridDim.x - helper_base) / nq;
+      int role = hidx;
+      if (!c.Q.jb) {
+        role = -1;
+      } else if (c.Q.sampler && hidx == nh - 1) {
+        role = -2;
+      } else if (role >= c.Q.nworkers - 1) {  // the leader's tile helpers first, then each scout's
+        role -= c.Q.nworkers - 1;
+        int s = 0;
+        for (; s < c.Q.nscouts && role >= c.Q.sworkers_s[s] - 1; ++s) role -= c.Q.sworkers_s[s] - 1;
+        if (s >= c.Q.nscouts) {
+          role = -1;
+        } else {
+          c.Q.jb = c.Q.sjbs[s];
+          c.Q.nworkers = c.Q.sworkers_s[s];
+        }
+      }
+      g_ctx = c;
+      g_role = role;
+    }
+    stage_model(rb, mc, &g_rb, &g_mc);  // (ends with a barrier)
+    const int role = uni(g_role);
+    if (role == -2) sampler_main(g_ctx, g_L.u.smpl);
+    else if (role >= 0) helper_main(g_ctx, role, g_L.u.job);
+    return;
+  }
+  if (b >= nq && (srole < 0 || sq >= nq)) return;
   if (threadIdx.x == 0) {
     Ctx c;
     c.sc = sc;
@@ -5446,145 +5567,6 @@ __global__ void __launch_bounds__(BLOCK) plan_kernel(const RobotDev* __restrict_
     if (C.Q.jb) st_agent(&C.Q.jb->stop, 1);
     for (int s = 0; s < C.Q.nscouts; ++s) st_agent(&C.Q.scbs[s]->stop, 1);
   }
-}
-
-// computeFinalSolutionPathTrajectories (birrt_star.cpp:6173-6274): the node chains of both trees, root
-// first for the start tree and connection first for the goal tree.  out[0] = n_start, out[1] = n_goal.
-// Helper blocks (gridDim = nq * helpers): block b serves query b % nq -- waits for its leader's collision jobs
-// and takes tiles of them until the leader signals stop.  A separate kernel on its own stream, so its
-// resources stay small and a leader never depends on it being resident.
-// LDS of the run-ahead sampler workgroup.
-struct SamplerLds {
-  QState S;        // the query's constants, with have_sol / cbest of the version being served
-  SmpLds W;
-  double out[NJ];
-  long long next;  // next iteration to sample
-  int ver, go[2];
-};
-
-// Run-ahead sampler (DESIGN.md "Sampler"): keeps the samples of the leader's next SMP_RING - 1 iterations in
-// the ring, computed with the latest published parameters and tagged (iteration, version); a parameter change
-// restarts the window.  Never writes the slot of an iteration the leader may be reading: it fills iterations
-// up to (published iteration) + SMP_RING - 1 only.  Leaves on the stop flag or after two idle seconds.
-// (not inlined into helper_kernel, like scan_helper: the tile helpers' loop is compiled without the sampler's and the
-// scan slices' registers live around it -- C2 73.1 -> 71.8 us per iteration, perf_probe.py with SMP_JOB_PROF, round 3)
-__device__ __forceinline__ void sampler_body(const Ctx& C, SamplerLds& L) {
-  JobBoard* jb = C.Q.jb;
-  {
-    const int* src = reinterpret_cast<const int*>(C.Q.st);
-    int* dst = reinterpret_cast<int*>(&L.S);
-    for (int i = threadIdx.x; i < (int)(sizeof(QState) / sizeof(int)); i += BLOCK) dst[i] = src[i];
-  }
-  if (threadIdx.x == 0) { L.ver = 0; L.next = 0; }
-  __syncthreads();
-  unsigned long long t_last = wall_clock64();
-  for (int k = 0;; k ^= 1) {
-    if (threadIdx.x == 0) {
-      int go = 0;
-      if (ld_agent(&jb->stop)) {
-        go = -1;
-      } else {
-        const int ver = ld_agent(&jb->s_ver);
-        const long long cur = (long long)ld_agent(reinterpret_cast<const unsigned long long*>(&jb->s_iter));
-        if (ver != L.ver) {
-          L.S.have_sol = ld_agent(&jb->s_have_sol);
-          for (int c = 0; c < 3; ++c) L.S.cbest[c] = __longlong_as_double((long long)ld_agent(&jb->s_cbest[c]));
-          if (ld_agent(&jb->s_ver) == ver) { L.ver = ver; L.next = cur + 1; }  // else re-read next poll
-        }
-        if (L.next < cur + 1) L.next = cur + 1;
-        if (L.ver > 0 && ver == L.ver && L.next <= cur + SMP_RING - 1) go = 1;
-        else if (wall_clock64() - t_last > 200000000ull) go = -1;  // 2 s idle
-      }
-      L.go[k] = go;
-    }
-    __syncthreads();
-    const int go = uni(L.go[k]);
-    if (go < 0) break;
-    if (go == 0) {
-      __builtin_amdgcn_s_sleep(2);
-      continue;
-    }
-    const long long it = L.next;
-    const int st = sample_conf(L.S, (uint32_t)it, L.W, L.out);
-#ifdef SMP_RING_CHECK
-    if (threadIdx.x == 0) {
-      unsigned long long* d = g_ringdbg[it % SMP_RING];
-      st_agent(&d[0], (unsigned long long)it); st_agent(&d[1], (unsigned long long)L.ver);
-      st_agent(&d[2], (unsigned long long)L.S.have_sol);
-      for (int k = 0; k < 3; ++k) st_agent(&d[3 + k], (unsigned long long)__double_as_longlong(L.S.cbest[k]));
-      st_agent(&d[6], (unsigned long long)L.S.informed);
-      const RobotDev* rb = (&g_rb);
-      const double lv[6] = {L.S.h0[1], L.S.Crev[0], L.S.Crev[7], L.S.ctr_rev[0], rb->q_min[2], rb->q_max[2]};
-      for (int k = 0; k < 6; ++k) st_agent(&d[8 + k], (unsigned long long)__double_as_longlong(lv[k]));
-      unsigned long long rv = 0;
-      for (int j = 0; j < NJ; ++j) rv |= (unsigned long long)(rb->rev[j] != 0) << j;
-      st_agent(&d[14], rv);
-    }
-#endif
-    if (st == 0 && threadIdx.x < RING_G) {
-      unsigned w;
-      if (threadIdx.x < 2 * NJ) {
-        const unsigned long long bits = (unsigned long long)__double_as_longlong(L.out[threadIdx.x >> 1]);
-        w = (threadIdx.x & 1) ? (unsigned)(bits >> 32) : (unsigned)bits;
-      } else {
-        w = ring_param((int)threadIdx.x - 2 * NJ, L.S.have_sol, L.S.cbest);
-      }
-      st_agent(&jb->ring[it % SMP_RING].g[threadIdx.x], granule((int)ring_tag(it, L.ver), w));
-    }
-    if (threadIdx.x == 0) L.next = it + 1;
-    t_last = wall_clock64();
-    __syncthreads();
-  }
-}
-
-__device__ __noinline__ void sampler_main(const Ctx& C, SamplerLds& L) { sampler_body(C, L); }
-
-// The LDS of a helper workgroup: one role at a time.
-union HelperLds {
-  JobLds J;
-  SamplerLds S;
-};
-
-// Helper blocks (gridDim = nq * helpers): block b serves query b % nq -- the leader's tile helpers first, then each
-// scout's, the run-ahead sampler last; one helper workgroup per CU (the full register file: the lowest tile latency).
-__global__ void __launch_bounds__(BLOCK) helper_kernel(const RobotDev* __restrict__ rb, SceneDev sc,
-                                                       const MapCfg* __restrict__ mc, QueryDev* qs, int nq) {
-  __shared__ HelperLds H;
-  // the block's context and role in LDS (see plan_kernel): -1 nothing to do, -2 run-ahead sampler, else tile helper h
-  __shared__ Ctx g_ctx;
-  __shared__ int g_role;
-  if (threadIdx.x == 0) {
-    Ctx c;
-    c.sc = sc;
-    c.Q = qs[blockIdx.x % nq];
-    const int hidx = (int)blockIdx.x / nq, nh = (int)gridDim.x / nq;
-    int role = hidx;
-    if (!c.Q.jb) {
-      role = -1;
-    } else if (c.Q.sampler && hidx == nh - 1) {
-      role = -2;
-    } else if (role >= c.Q.nworkers - 1) {  // the leader's tile helpers first, then each scout's
-      role -= c.Q.nworkers - 1;
-      int s = 0;
-      for (; s < c.Q.nscouts && role >= c.Q.sworkers_s[s] - 1; ++s) role -= c.Q.sworkers_s[s] - 1;
-      if (s >= c.Q.nscouts) {
-        role = -1;
-      } else {
-        c.Q.jb = c.Q.sjbs[s];
-        c.Q.nworkers = c.Q.sworkers_s[s];
-      }
-    }
-    g_ctx = c;
-    g_role = role;
-  }
-  stage_model(rb, mc, &g_rb, &g_mc);  // (ends with a barrier)
-  const int role = uni(g_role);
-  if (role == -1) return;
-  if (role == -2) {
-    sampler_main(g_ctx, H.S);
-    return;
-  }
-  helper_main(g_ctx, role, H.J);
 }
 
 // Fresh job / scout boards for a launch (all zero: no granule carries a job number, no stop flag): block b clears
