@@ -360,19 +360,19 @@ def main():
         # per launch: algorithmic bytes of one launch / its average duration (HIP events on the planner stream)
         achieved = alg_bytes_rank0 / (plan_ms_rank0 * 1e-3) / 1e9 if plan_ms_rank0 > 0 else 0.0
         traffic, traffic_src = None, None
-        # HBM bytes per launch: not measurable inside this run (counter passes serialise dispatches and need
-        # rocprofv3); taken from the newest committed FETCH_SIZE + WRITE_SIZE passes of THIS workload
-        # (profiles/r*_pmc_<tag>.json, tools/profile_round.sh), else null.  Counter collection serialises the
-        # dispatches, so those passes run the same queries with --helpers -1 (all tiles in plan_kernel): the bytes are
-        # that configuration's, as traffic_source says.
+        # HBM bytes per launch: not measurable inside this run (counter passes need rocprofv3); taken from the newest
+        # committed FETCH_SIZE + WRITE_SIZE passes of THIS workload (profiles/r*_pmc_<tag>.json, tools/profile_round.sh),
+        # else null.  From round 5 on one plan_kernel dispatch holds the leader, its scouts and helpers, so those passes
+        # run the benched configuration (round 4's ran --helpers -1: counter collection serialised the helper kernel).
         import glob
         tag = a.workload + ("_iter%d" % a.iterations if a.iterations else "")
         pmcs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_%s.json" % tag)))
         if pmcs:
             try:
                 traffic = json.load(open(pmcs[-1])).get("hbm_bytes_per_launch")
-                traffic_src = ("profiles/" + os.path.basename(pmcs[-1]) +
-                               " (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this workload with --helpers -1)")
+                name = os.path.basename(pmcs[-1])
+                traffic_src = ("profiles/" + name + " (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this workload, " +
+                               ("with --helpers -1)" if name < "r05" else "the benched configuration: one dispatch)"))
             except (OSError, ValueError):
                 traffic = None
         out = {
