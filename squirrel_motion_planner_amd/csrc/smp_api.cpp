@@ -43,6 +43,9 @@ __global__ void sqrt_div_kernel(const double* a, const double* b, int n, double*
 __global__ void near_probe_kernel(const double* tq, const double* tcost, int cap, int n, const double* queries,
                                   const int* excl, int m, double r, int reps, int* nn, int* nk, int* lo, int* hi,
                                   unsigned long long* ticks);
+__global__ void near_probe_inl_kernel(const double* tq, const double* tcost, int cap, int n, const double* queries,
+                                      const int* excl, int m, double r, int reps, int* nn, int* nk, int* lo, int* hi,
+                                      unsigned long long* ticks);
 }  // namespace smp
 
 using namespace smp;
@@ -1818,8 +1821,11 @@ extern "C" int smp_probe_near(int device, const double* q_soa, const double* cos
   HIPCHK(hipMemcpy(dc, cost, (size_t)n * sizeof(double), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(dqq, queries, (size_t)m * NJ * sizeof(double), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(dx, excl, (size_t)m * sizeof(int), hipMemcpyHostToDevice));
-  hipLaunchKernelGGL(near_probe_kernel, dim3(1), dim3(BLOCK), 0, 0, dq, dc, n, n, dqq, dx, m, r, reps, dnn, dnk, dlo,
-                     dhi, dt);
+  // modes 4 / 5 (the helpers' inlined slice forms) run in a kernel of their own, so that neither kernel's register
+  // allocation carries the other's code
+  const bool inl = reps < 0 && 1 + ((-reps) >> 20) >= 4;
+  hipLaunchKernelGGL(inl ? near_probe_inl_kernel : near_probe_kernel, dim3(1), dim3(BLOCK), 0, 0, dq, dc, n, n, dqq, dx,
+                     m, r, reps, dnn, dnk, dlo, dhi, dt);
   HIPCHK(hipGetLastError());
   HIPCHK(hipDeviceSynchronize());
   HIPCHK(hipMemcpy(nn, dnn, (size_t)m * sizeof(int), hipMemcpyDeviceToHost));

@@ -530,6 +530,13 @@ __device__ __forceinline__ void tree_cols(gcdptr tq, int cap, gcdptr* c) {
 #pragma unroll
   for (int j = 0; j < NJ; ++j) c[j] = uni_g(tq + (size_t)j * (unsigned)cap);
 }
+// Wave-uniform test of a scan's load group: true if the wavefront's 64 nodes starting at node `first` (a wave-uniform
+// index) reach into the range [.., end).  A group wholly beyond the range skips its loads (a scalar branch): the clamped
+// loads of such a group all read the range's last node, but each still costs its wave-instruction's address and data
+// cycles in the CU's load pipeline -- 7 of a round's 8 groups on a 512-node tree.
+__device__ __forceinline__ bool wave_group_live(int first, int end) {
+  return __builtin_amdgcn_readfirstlane((int)(first < end)) != 0;
+}
 
 // Stores into the tree arrays that the scout reads (q, cost, parent).  Plain stores: the lines stay in this XCD's
 // L2, where a scout on the same XCD (the usual placement, plan_kernel) and the leader's own scans find them;
@@ -622,7 +629,11 @@ __device__ void near_set_dist(const Ctx& C, int t, const double* q, int excl, bo
 // if none is below it.  All threads; result in (g_L.wd[0], g_L.wi[0]) via nearest_scan's return.
 __device__ int nearest_scan(const Ctx& C, int t, const double* q, int i_begin, double* d_out) {
   TR();
-  if (scan_split(C, uni(g_L.S.n[t]) - i_begin)) return nearest_dist(C, t, q, i_begin, uni(g_L.S.n[t]), d_out);
+  if (scan_split(C, uni(g_L.S.n[t]) - i_begin)) {
+    int id;
+    [[clang::always_inline]] id = nearest_dist(C, t, q, i_begin, uni(g_L.S.n[t]), d_out);
+    return id;
+  }
   const gcdptr tq = uni_gptr(C.Q.tr[t].q);
   const int n = uni(g_L.S.n[t]), cap = uni(g_L.S.cap);
   gcdptr tqc[NJ];
@@ -638,9 +649,14 @@ __device__ int nearest_scan(const Ctx& C, int t, const double* q, int i_begin, d
     double a[NPT][NJ];
 #pragma unroll
     for (int u = 0; u < NPT; ++u) {
-      const unsigned ii = (unsigned)min(i0 + u * BLOCK, n - 1);
+      if (wave_group_live(i0 - lane_id() + u * BLOCK, n)) {
+        const unsigned ii = (unsigned)min(i0 + u * BLOCK, n - 1);
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) a[u][j] = tqc[j][ii];
+        for (int j = 0; j < NJ; ++j) a[u][j] = tqc[j][ii];
+      } else {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) a[u][j] = qq[j];
+      }
     }
     double s[NPT];
 #pragma unroll
@@ -884,10 +900,16 @@ __device__ __noinline__ void near_set_stream(const Ctx& C, int t, const double* 
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       const int i = base + b * BLOCK + lane;
-      const unsigned ii = (unsigned)min(i, n - 1);
+      if (wave_group_live(base + b * BLOCK, n)) {
+        const unsigned ii = (unsigned)min(i, n - 1);
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) x[b][j] = tqc[j][ii];
-      key[b] = i < n ? (unsigned long long)__double_as_longlong(tc[ii]) : 0ull;
+        for (int j = 0; j < NJ; ++j) x[b][j] = tqc[j][ii];
+        key[b] = i < n ? (unsigned long long)__double_as_longlong(tc[ii]) : 0ull;
+      } else {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) x[b][j] = qq[j];
+        key[b] = 0ull;
+      }
     }
     bool nr[NB], amb[NB];
     bool any_amb = false;
@@ -1005,9 +1027,14 @@ __device__ __forceinline__ void slice_nn_body(gcdptr tq, int cap, int i0, int i1
     double a[NPT][NJ];
 #pragma unroll
     for (int u = 0; u < NPT; ++u) {
-      const unsigned ii = (unsigned)min(b0 + u * BLOCK, i1 - 1);
+      if (wave_group_live(b0 - lane_id() + u * BLOCK, i1)) {
+        const unsigned ii = (unsigned)min(b0 + u * BLOCK, i1 - 1);
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) a[u][j] = tqc[j][ii];
+        for (int j = 0; j < NJ; ++j) a[u][j] = tqc[j][ii];
+      } else {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) a[u][j] = qq[j];
+      }
     }
     double s[NPT];
 #pragma unroll
@@ -1059,10 +1086,16 @@ __device__ __forceinline__ void slice_near_body(gcdptr tq, gcdptr tc, int cap, i
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       const int i = base + b * BLOCK + lane;
-      const unsigned ii = (unsigned)min(i, i1 - 1);
+      if (wave_group_live(base + b * BLOCK, i1)) {
+        const unsigned ii = (unsigned)min(i, i1 - 1);
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) x[b][j] = tqc[j][ii];
-      key[b] = i < i1 ? (unsigned long long)__double_as_longlong(tc[ii]) : 0ull;
+        for (int j = 0; j < NJ; ++j) x[b][j] = tqc[j][ii];
+        key[b] = i < i1 ? (unsigned long long)__double_as_longlong(tc[ii]) : 0ull;
+      } else {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) x[b][j] = qq[j];
+        key[b] = 0ull;
+      }
     }
     bool nr[NB], amb[NB];
     bool any_amb = false;
@@ -1147,8 +1180,8 @@ __device__ __forceinline__ void slice_near_body(gcdptr tq, gcdptr tc, int cap, i
 // Returns false (outputs undefined) if a chunk's histogram cannot split its costs (many equal costs): the caller then
 // runs slice_near_body.  All threads.
 template <bool NN>
-__device__ bool slice_near_hist(gcdptr tq, gcdptr tc, int cap, int i0, int i1, const double* q, int excl, double r,
-                                ScanLds& X) {
+__device__ __forceinline__ bool slice_near_hist(gcdptr tq, gcdptr tc, int cap, int i0, int i1, const double* q, int excl,
+                                                double r, ScanLds& X) {
   constexpr int K = SCAN_K, NW = BLOCK / 64, CH = NEAR_NBK * BLOCK;
   double nb = 10000.0, nb_s = 1e300;  // NN: this thread's nearest candidate
   int nbi = 0x7fffffff;
@@ -1176,10 +1209,15 @@ __device__ bool slice_near_hist(gcdptr tq, gcdptr tc, int cap, int i0, int i1, c
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
           const int i = c0 + (g + b) * BLOCK + wave * 64 + lane;
-          const unsigned ii = (unsigned)min(i, i1 - 1);
+          if (wave_group_live(c0 + (g + b) * BLOCK + wave * 64, i1)) {
+            const unsigned ii = (unsigned)min(i, i1 - 1);
 #pragma unroll
-          for (int j = 0; j < NJ; ++j) x[b][j] = tqc[j][ii];
-          key[g + b] = i < i1 ? (unsigned long long)__double_as_longlong(tc[ii]) : 0ull;
+            for (int j = 0; j < NJ; ++j) x[b][j] = tqc[j][ii];
+            key[g + b] = i < i1 ? (unsigned long long)__double_as_longlong(tc[ii]) : 0ull;
+          } else {
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) x[b][j] = qq[j];
+          }
         }
         bool nr[4], amb[4];
         bool any_amb = false;
@@ -1417,6 +1455,20 @@ __device__ __noinline__ void slice_near(gcdptr tq, gcdptr tc, int cap, int i0, i
   if (uni(slice_near_hist<NN>(tq, tc, cap, i0, i1, q, excl, r, X))) return;
   slice_near_body<NN>(tq, tc, cap, i0, i1, q, excl, r, X);
 }
+template <bool NN>
+__device__ __noinline__ void slice_near_slow(gcdptr tq, gcdptr tc, int cap, int i0, int i1, const double* q, int excl,
+                                             double r, ScanLds& X) {
+  slice_near_body<NN>(tq, tc, cap, i0, i1, q, excl, r, X);
+}
+// The helpers' form of slice_near: the register path inlined into the helper loop, so that a scan job costs no call --
+// a non-inlined callee at 512 threads saves and restores every callee-saved VGPR it uses, ~100 of them here (≈200 KB
+// of scratch stores and loads per call through the CU's load pipeline, and most of a large tree's write traffic).
+template <bool NN>
+__device__ __forceinline__ void slice_near_inl(gcdptr tq, gcdptr tc, int cap, int i0, int i1, const double* q, int excl,
+                                               double r, ScanLds& X) {
+  if (uni(slice_near_hist<NN>(tq, tc, cap, i0, i1, q, excl, r, X))) return;
+  slice_near_slow<NN>(tq, tc, cap, i0, i1, q, excl, r, X);
+}
 
 // find_near_vertices_interpolation (birrt_star.cpp:4272-4324): count k, the first K and the last K entries of
 // the (cost,id)-sorted near list.  The tree is taken in chunks of NEAR_NBK * BLOCK nodes; the radius test leaves
@@ -1542,7 +1594,7 @@ __device__ void near_set(const Ctx& C, int t, const double* q, int excl, bool sp
     }
   }
   if (K == SCAN_K && scan_split(C, n)) {
-    near_set_dist(C, t, q, excl, NN);
+    [[clang::always_inline]] near_set_dist(C, t, q, excl, NN);
     TR();
     return;
   }
@@ -1566,10 +1618,15 @@ __device__ void near_set(const Ctx& C, int t, const double* q, int excl, bool sp
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
           const int i = c0 + (g + b) * BLOCK + wave * 64 + lane;
-          const unsigned ii = (unsigned)min(i, n - 1);
+          if (wave_group_live(c0 + (g + b) * BLOCK + wave * 64, n)) {
+            const unsigned ii = (unsigned)min(i, n - 1);
 #pragma unroll
-          for (int j = 0; j < NJ; ++j) x[b][j] = tqc[j][ii];
-          key[g + b] = i < n ? (unsigned long long)__double_as_longlong(tc[ii]) : 0ull;
+            for (int j = 0; j < NJ; ++j) x[b][j] = tqc[j][ii];
+            key[g + b] = i < n ? (unsigned long long)__double_as_longlong(tc[ii]) : 0ull;
+          } else {
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) x[b][j] = qq[j];
+          }
         }
         bool nr[4], amb[4];
         bool any_amb = false;
@@ -2214,12 +2271,20 @@ __device__ void scan_publish(const Ctx& C, int seq, int near, int t, const doubl
 }
 
 // Participant w's slice of a scan, its result as granules of sres[w] (helper) or into the merge area (workgroup).
+// INL: the helpers' form (slices inlined, scan_helper).
+template <bool INL = false>
 __device__ void scan_slice(const Ctx& C, int near, int t, const double* q, int i0, int n, int excl, double r, int P, int w,
                            ScanLds& X) {
   const gcdptr tq = uni_gptr(C.Q.tr[t].q), tc = uni_gptr(C.Q.tr[t].cost);
   const int cap = uni(__hip_atomic_load(&C.Q.st->cap, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   int lo, hi;
   scan_range(i0, n, P, w, &lo, &hi);
+  if (INL) {
+    if (near == 2) slice_near_inl<true>(tq, tc, cap, lo, hi, q, excl, r, X);
+    else if (near) slice_near_inl<false>(tq, tc, cap, lo, hi, q, excl, r, X);
+    else slice_nn_body(tq, cap, lo, hi, q, X);
+    return;
+  }
   if (near == 2) slice_near<true>(tq, tc, cap, lo, hi, q, excl, r, X);
   else if (near) slice_near<false>(tq, tc, cap, lo, hi, q, excl, r, X);
   else slice_nn(tq, cap, lo, hi, q, X);
@@ -2227,7 +2292,7 @@ __device__ void scan_slice(const Ctx& C, int near, int t, const double* q, int i
 
 // Helper side of a scan job already in J.words (seq): worker w is participant W - w (smp_plan.h SCAN_P); its slice, then
 // the result granules.
-__device__ __noinline__ void scan_helper(const Ctx& C, JobLds& J, int worker, int seq) {
+__device__ __forceinline__ void scan_helper(const Ctx& C, JobLds& J, int worker, int seq) {
   const unsigned hdr = J.words[0];
   const int near = ((hdr >> 21) & 1) ? 2 : (int)((hdr >> 19) & 1), t = (hdr >> 20) & 1;
   double q[NJ];
@@ -2250,7 +2315,7 @@ __device__ __noinline__ void scan_helper(const Ctx& C, JobLds& J, int worker, in
   const unsigned long long hp1 = wall_clock64();
 #endif
   ScanLds& X = J.scan;
-  scan_slice(C, near, t, q, i0, n, excl, r, P, w, X);
+  scan_slice<true>(C, near, t, q, i0, n, excl, r, P, w, X);
 #ifdef SMP_SCAN_PROF
   if (threadIdx.x == 0) {
     const unsigned long long hp2 = wall_clock64(), pub = ld_agent(&C.Q.jb->dbg[8]);
@@ -2336,7 +2401,7 @@ __device__ void scan_run(const Ctx& C, int near, int t, const double* q, int i0,
   if (threadIdx.x == 0) st_agent(&C.Q.jb->dbg[8], sp1);
 #endif
   scan_publish(C, seq, near, t, q, i0, n, excl, r, P);
-  scan_slice(C, near, t, q, i0, n, excl, r, P, 0, X);
+  scan_slice<true>(C, near, t, q, i0, n, excl, r, P, 0, X);
   merge_put(M, X, near, 0);
   __syncthreads();
 #ifdef SMP_SCAN_PROF
@@ -2451,7 +2516,7 @@ __device__ void scan_run(const Ctx& C, int near, int t, const double* q, int i0,
     if (go == 1) break;
     if (go == 2) {
       const int w = uni(M.steal);
-      scan_slice(C, near, t, q, i0, n, excl, r, P, w, X);
+      scan_slice<true>(C, near, t, q, i0, n, excl, r, P, w, X);
       merge_put(M, X, near, w);
       if (threadIdx.x == 0) { M.ndone++; t_prog = wall_clock64(); }
 #ifdef SMP_SCAN_PROF
@@ -4621,7 +4686,7 @@ __device__ void scout_connect(const Ctx& C, long long it, int t, int par, unsign
   if (threadIdx.x == 0) g_L.S.n[tb] = g_L.cnt;
   __syncthreads();
   // the near set of x_new and its nearest node (no exclusion) in one pass over tree_B
-  near_set<20, true>(C, tb, g_L.xn.q, g_L.xn.id);
+  [[clang::always_inline]] near_set<20, true>(C, tb, g_L.xn.q, g_L.xn.id);
   if (threadIdx.x == 0) {
     double d = g_L.fnn_d;
     int cid = g_L.fnn_id;
@@ -4655,7 +4720,7 @@ __device__ void scout_connect(const Ctx& C, long long it, int t, int par, unsign
     if (threadIdx.x < MAXE) g_L.eg_need[threadIdx.x] = threadIdx.x < 1 + E;
     if (threadIdx.x == 0) g_L.rec_grp = -1;
     __syncthreads();
-    edge_validity(C, 1 + E, false, P_XCONNECT);
+    [[clang::always_inline]] edge_validity(C, 1 + E, false, P_XCONNECT);
     if (threadIdx.x < E) R.cc.first[threadIdx.x] = g_L.eg_first[1 + threadIdx.x];
     if (threadIdx.x == 0) { R.cc.first0 = g_L.eg_first[0]; R.cc.nfirst = E; }
   }
@@ -4864,7 +4929,8 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
   }
   // nearest + expand edge (iteration())
   if (opt && sc_moved(C)) return;
-  const int nid = nearest(C, t, g_L.xr);
+  int nid;
+  [[clang::always_inline]] nid = nearest(C, t, g_L.xr);
   if (threadIdx.x == 0) {
     load_node(C, t, nid, &g_L.nn);
     double s = 0.0;
@@ -4903,7 +4969,7 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
   int cid_s = 0;
   if (spec_conn) {
     const int tb = 1 - t;
-    cid_s = nearest(C, tb, g_L.eg_end[0]);
+    [[clang::always_inline]] cid_s = nearest(C, tb, g_L.eg_end[0]);
     if (threadIdx.x == 0) {
       load_node(C, tb, cid_s, &g_L.xc);
       for (int j = 0; j < NJ; ++j) { g_L.eg_start[1][j] = g_L.xc.q[j]; g_L.eg_target[1][j] = g_L.eg_end[0][j]; }
@@ -4913,9 +4979,9 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
     for (int e = 2 + threadIdx.x; e < MAXE; e += BLOCK) g_L.eg_need[e] = 0;
     __syncthreads();
     edge_costs(C, 2);
-    edge_validity(C, 2, false, P_XEXPAND, OV_NONE, t);
+    [[clang::always_inline]] edge_validity(C, 2, false, P_XEXPAND, OV_NONE, t);
   } else {
-    edge_validity(C, 1, false, P_XEXPAND, opt ? OV_NEAR_EXPAND : OV_NONE, t);
+    [[clang::always_inline]] edge_validity(C, 1, false, P_XEXPAND, opt ? OV_NEAR_EXPAND : OV_NONE, t);
   }
   if (threadIdx.x == 0) {
     for (int j = 0; j < NJ; ++j) { R.e[0].s[j] = g_L.eg_start[0][j]; R.e[0].g[j] = g_L.eg_target[0][j]; }
@@ -4988,7 +5054,9 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
   TR();
   if (sc_moved(C)) return;
   // near set of x_new (the leader's, before choose_parent)
-  if (!(uni(g_L.ext_nn) && take_spec(OV_NEAR_EXPAND))) near_set<20>(C, t, g_L.xn.q, X);
+  if (!(uni(g_L.ext_nn) && take_spec(OV_NEAR_EXPAND))) {
+    [[clang::always_inline]] near_set<20>(C, t, g_L.xn.q, X);
+  }
   if (threadIdx.x < 20) {
     R.nr.lo_i[threadIdx.x] = g_L.lo_i[threadIdx.x]; R.nr.lo_c[threadIdx.x] = g_L.lo_c[threadIdx.x];
     R.nr.hi_i[threadIdx.x] = g_L.hi_i[threadIdx.x]; R.nr.hi_c[threadIdx.x] = g_L.hi_c[threadIdx.x];
@@ -5033,7 +5101,7 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
     if (threadIdx.x < E) g_L.eg_need[threadIdx.x] = g_L.eg_cost[threadIdx.x][0] <= g_L.xn.c[0];
     for (int e = E + threadIdx.x; e < MAXE; e += BLOCK) g_L.eg_need[e] = 0;
     __syncthreads();
-    edge_validity(C, E, false, P_XCHOOSE);
+    [[clang::always_inline]] edge_validity(C, E, false, P_XCHOOSE);
     if (threadIdx.x < E) {
       const int e = threadIdx.x;
       ScoutEdge& w = R.e[SCOUT_CHOOSE0 + e];
@@ -5098,7 +5166,7 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
     }
     for (int e = cnt + threadIdx.x; e < MAXE; e += BLOCK) g_L.eg_need[e] = 0;
     __syncthreads();
-    edge_validity(C, cnt, false, P_XREWIRE);
+    [[clang::always_inline]] edge_validity(C, cnt, false, P_XREWIRE);
     if (threadIdx.x < cnt) {
       const int e = threadIdx.x;
       ScoutEdge& w = R.e[SCOUT_REWIRE0 + e];
@@ -5115,7 +5183,9 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
   SC_PHASE(6);
   TR();
   if (sc_moved(C)) return;
-  if (uni(g_L.two_scouts)) scout_connect(C, it, t, par, tag);
+  if (uni(g_L.two_scouts)) {
+    [[clang::always_inline]] scout_connect(C, it, t, par, tag);
+  }
   TR();
 }
 #undef SC_PHASE
@@ -5138,7 +5208,7 @@ __device__ __forceinline__ void scout_ctx(Ctx& C, int which) {
   C.Q.ttff = nullptr;
 }
 
-__device__ __forceinline__ void scout_main(Ctx& C, int which) {
+__device__ __noinline__ void scout_main(Ctx& C, int which) {
   {
     const int* src = reinterpret_cast<const int*>(C.Q.st);
     int* dst = reinterpret_cast<int*>(&g_L.S);
@@ -5284,7 +5354,7 @@ __device__ __forceinline__ void scout_main(Ctx& C, int which) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       drain();
       __syncthreads();
-      scout_iteration(C, (long long)tag - 1, t, X, opt, ver, XB);
+      [[clang::always_inline]] scout_iteration(C, (long long)tag - 1, t, X, opt, ver, XB);
       if (!opt || !uni(g_L.sc_rerun)) break;
       __syncthreads();
     }
@@ -5621,10 +5691,10 @@ __global__ void path_edges_kernel(const QueryDev* qs, int q, int ns, int ng, dou
 // near_set<20>() for m query configurations against one tree (SoA q [NJ][cap], total cost [cap]), `reps` times
 // each; out: nearest id, near count, the first / last 20 near ids; ticks[0] / ticks[1] = device-clock ticks of
 // all nearest / near_set calls.
-__global__ void __launch_bounds__(BLOCK) near_probe_kernel(const double* tqv, const double* tcost, int cap, int n,
-                                                           const double* queries, const int* excl, int m, double r,
-                                                           int reps, int* nn, int* nk, int* lo, int* hi,
-                                                           unsigned long long* ticks) {
+template <bool INL>
+__device__ __forceinline__ void near_probe_body(const double* tqv, const double* tcost, int cap, int n,
+                                                const double* queries, const int* excl, int m, double r, int reps, int* nn,
+                                                int* nk, int* lo, int* hi, unsigned long long* ticks) {
   Ctx C;
   C.Q.jb = nullptr;  // single workgroup: no helpers, scans stay local
   C.Q.scan_min = 0;
@@ -5643,33 +5713,44 @@ __global__ void __launch_bounds__(BLOCK) near_probe_kernel(const double* tqv, co
   unsigned long long t_nn = 0, t_near = 0;
   // reps < 0: -(reps + ((mode - 1) << 20)), mode 1 the slice functions of distributed scans (slice_nn / slice_near over
   // [0, n)) instead of nearest / near_set, 2 the fused near_set<20, true>, 3 the fused slice_near<true> (nearest and near
-  // set in one pass: the near timing holds both, the nearest timing nothing)
+  // set in one pass: the near timing holds both, the nearest timing nothing), 4 / 5 the helpers' inlined forms of modes 1
+  // / 3 (slice_near_inl: no call)
   int mode = 0;
   if (reps < 0) { reps = -reps; mode = 1 + (reps >> 20); reps &= (1 << 20) - 1; }
-  const bool slice = mode == 1 || mode == 3;
+  const bool slice = mode == 1 || mode == 3 || mode == 4 || mode == 5;
   const gcdptr tq = uni_gptr(tqv), tc = uni_gptr(tcost);
   for (int k = 0; k < m; ++k) {
     if (threadIdx.x < NJ) g_L.xr[threadIdx.x] = queries[(size_t)k * NJ + threadIdx.x];
     __syncthreads();
     int id = 0;
     unsigned long long t0 = wall_clock64();
-    for (int rep = 0; rep < reps && mode < 2; ++rep) {
-      if (slice) {
-        slice_nn(tq, cap, 0, n, g_L.xr, g_L.sc.s);
+    for (int rep = 0; rep < reps && (mode < 2 || mode == 4); ++rep) {
+      if constexpr (INL) {
+        slice_nn_body(tq, cap, 0, n, g_L.xr, g_L.sc.s);
         id = __longlong_as_double((long long)g_L.sc.s.wk[0]) < 10000.0 ? g_L.sc.s.wi[0] : 0;
       } else {
-        id = nearest(C, 0, g_L.xr);
+        if (slice) {
+          slice_nn(tq, cap, 0, n, g_L.xr, g_L.sc.s);
+          id = __longlong_as_double((long long)g_L.sc.s.wk[0]) < 10000.0 ? g_L.sc.s.wi[0] : 0;
+        } else {
+          id = nearest(C, 0, g_L.xr);
+        }
       }
     }
     unsigned long long t1 = wall_clock64();
     for (int rep = 0; rep < reps; ++rep) {
-      if (mode == 1) slice_near<false>(tq, tc, cap, 0, n, g_L.xr, excl[k], r, g_L.sc.s);
-      else if (mode == 3) slice_near<true>(tq, tc, cap, 0, n, g_L.xr, excl[k], r, g_L.sc.s);
-      else if (mode == 2) near_set<20, true>(C, 0, g_L.xr, excl[k]);
-      else near_set<20>(C, 0, g_L.xr, excl[k]);
+      if constexpr (INL) {
+        if (mode == 4) slice_near_inl<false>(tq, tc, cap, 0, n, g_L.xr, excl[k], r, g_L.sc.s);
+        else slice_near_inl<true>(tq, tc, cap, 0, n, g_L.xr, excl[k], r, g_L.sc.s);
+      } else {
+        if (mode == 1) slice_near<false>(tq, tc, cap, 0, n, g_L.xr, excl[k], r, g_L.sc.s);
+        else if (mode == 3) slice_near<true>(tq, tc, cap, 0, n, g_L.xr, excl[k], r, g_L.sc.s);
+        else if (mode == 2) near_set<20, true>(C, 0, g_L.xr, excl[k]);
+        else near_set<20>(C, 0, g_L.xr, excl[k]);
+      }
     }
     if (mode == 2) id = g_L.fnn_d < 10000.0 ? g_L.fnn_id : 0;
-    if (mode == 3) id = __longlong_as_double((long long)g_L.sc.s.wk[0]) < 10000.0 ? g_L.sc.s.wi[0] : 0;
+    if (mode == 3 || mode == 5) id = __longlong_as_double((long long)g_L.sc.s.wk[0]) < 10000.0 ? g_L.sc.s.wi[0] : 0;
     unsigned long long t2 = wall_clock64();
     t_nn += t1 - t0;
     t_near += t2 - t1;
@@ -5697,6 +5778,19 @@ __global__ void __launch_bounds__(BLOCK) near_probe_kernel(const double* tqv, co
     ticks[12] = __builtin_amdgcn_s_memtime() - m0;
     ticks[13] = wall_clock64() - w0;
   }
+}
+__global__ void __launch_bounds__(BLOCK) near_probe_kernel(const double* tqv, const double* tcost, int cap, int n,
+                                                           const double* queries, const int* excl, int m, double r,
+                                                           int reps, int* nn, int* nk, int* lo, int* hi,
+                                                           unsigned long long* ticks) {
+  near_probe_body<false>(tqv, tcost, cap, n, queries, excl, m, r, reps, nn, nk, lo, hi, ticks);
+}
+// Modes 4 / 5 only (the helpers' inlined slice forms), in a kernel of their own.
+__global__ void __launch_bounds__(BLOCK) near_probe_inl_kernel(const double* tqv, const double* tcost, int cap, int n,
+                                                               const double* queries, const int* excl, int m, double r,
+                                                               int reps, int* nn, int* nk, int* lo, int* hi,
+                                                               unsigned long long* ticks) {
+  near_probe_body<true>(tqv, tcost, cap, n, queries, excl, m, r, reps, nn, nk, lo, hi, ticks);
 }
 
 }  // namespace smp

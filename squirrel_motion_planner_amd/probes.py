@@ -11,14 +11,15 @@ import numpy as np
 from . import _lib as L
 
 
-def _reps_code(reps, slices, fused):
+def _reps_code(reps, slices, fused, inline=False):
     """near_probe_kernel's mode in the sign and high bits of its repetition count: 0 nearest + near_set, 1 the slice
-    functions, 2 the fused near_set<20, true>, 3 the fused slice_near<true>."""
-    mode = (1 if slices else 0) + (2 if fused else 0)
+    functions, 2 the fused near_set<20, true>, 3 the fused slice_near<true>, 4 / 5 the helpers' inlined slice forms of
+    1 / 3."""
+    mode = (4 if fused else 3) + 1 if (slices and inline) else (1 if slices else 0) + (2 if fused else 0)
     return reps if mode == 0 else -(reps + ((mode - 1) << 20))
 
 
-def tree_scan(q, cost, queries, excl, r, reps=1, device=0, slices=False, fused=False):
+def tree_scan(q, cost, queries, excl, r, reps=1, device=0, slices=False, fused=False, inline=False):
     """q (n, 8) node configurations, cost (n,) total costs, queries (m, 8), excl (m,) node id left out of the near
     set (-1: none).  Returns nearest ids, near counts, the first / last 20 near ids (ascending (cost, id); -1
     padded) and the device seconds of all nearest / near_set calls."""
@@ -35,7 +36,7 @@ def tree_scan(q, cost, queries, excl, r, reps=1, device=0, slices=False, fused=F
     hz = ctypes.c_double()
     pd = ctypes.POINTER(ctypes.c_double)
     L.check(L.lib().smp_probe_near(device, q.ctypes.data_as(pd), cost.ctypes.data_as(pd), n, queries.ctypes.data_as(pd),
-                                   excl.ctypes.data_as(ctypes.c_void_p), m, float(r), _reps_code(reps, slices, fused),
+                                   excl.ctypes.data_as(ctypes.c_void_p), m, float(r), _reps_code(reps, slices, fused, inline),
                                    nn.ctypes.data_as(ctypes.c_void_p), nk.ctypes.data_as(ctypes.c_void_p),
                                    lo.ctypes.data_as(ctypes.c_void_p), hi.ctypes.data_as(ctypes.c_void_p), ticks,
                                    ctypes.byref(hz)), "smp_probe_near")

@@ -5,7 +5,8 @@ with many ties, constant / ascending / descending costs, and nodes placed on the
 four forms the planner uses: the workgroup's own scans (nearest, near_set), a distributed scan's slice functions over the
 whole range (slice_nn, slice_near), and the fused nearest + near set of connect (near_set<20, true>, slice_near<true>)."""
 
-MODES = {"local": {}, "slice": {"slices": True}, "fused": {"fused": True}, "fused_slice": {"slices": True, "fused": True}}
+MODES = {"local": {}, "slice": {"slices": True}, "fused": {"fused": True}, "fused_slice": {"slices": True, "fused": True},
+         "slice_inl": {"slices": True, "inline": True}, "fused_slice_inl": {"slices": True, "fused": True, "inline": True}}
 import numpy as np
 import pytest
 

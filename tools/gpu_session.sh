@@ -1,7 +1,8 @@
-# Scratch GPU session of the current experiment (rewritten per experiment; run from the repo root through gpurun).
-OUT=gpurun_out
+# scratch driver of one gpurun call (edited per call): heartbeat + the steps below, each under its own time limit
+OUT=$PWD/gpurun_out
 mkdir -p $OUT
 ( while true; do date +%s >> $OUT/heartbeat.txt; sleep 30; done ) &
 HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
-bash tools/profile_round.sh r05 c2 && echo "profile rc=0" >> $OUT/status.txt
+timeout -k 10 300 python -u tools/perf_probe.py 4000 100000 > $OUT/r05_perf_inl1.txt 2>&1 &&
+timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests > $OUT/r05_t_gpu_inl1.txt 2>&1

@@ -20,13 +20,17 @@ for n in [int(v) for v in (sys.argv[1:] or ["1024", "2048", "4096", "8192", "163
     excl = rng.integers(0, n, m).astype(np.int32)
     a = probes.tree_scan(q, cost, queries, excl, 4.0, reps=reps)
     b = probes.tree_scan(q, cost, queries, excl, 4.0, reps=reps, slices=True)
+    c = probes.tree_scan(q, cost, queries, excl, 4.0, reps=reps, slices=True, inline=True)
     same = (np.array_equal(a["nearest"], b["nearest"]) and np.array_equal(a["k"], b["k"]) and
-            np.array_equal(a["lo"], b["lo"]) and np.array_equal(a["hi"], b["hi"]))
+            np.array_equal(a["lo"], b["lo"]) and np.array_equal(a["hi"], b["hi"]) and
+            all(np.array_equal(a[f], c[f]) for f in ("nearest", "k", "lo", "hi")))
     calls = m * reps
     sclk = a["prof"][10] / (a["prof"][11] / a["clock_hz"]) / 1e9
-    print("n %6d (shader clock %.2f GHz, mean near %6.0f): nearest %.2f / slice_nn %.2f us, near_set %.2f / slice_near %.2f us, same %s" % (
-        n, sclk, a["k"].mean(), a["t_nearest"] / calls * 1e6, b["t_nearest"] / calls * 1e6, a["t_near"] / calls * 1e6,
-        b["t_near"] / calls * 1e6, same), flush=True)
+    print("n %6d (shader clock %.2f GHz, mean near %6.0f): nearest %.2f / slice_nn %.2f / inlined %.2f us, near_set %.2f / "
+          "slice_near %.2f / inlined %.2f us, same %s" % (
+              n, sclk, a["k"].mean(), a["t_nearest"] / calls * 1e6, b["t_nearest"] / calls * 1e6,
+              c["t_nearest"] / calls * 1e6, a["t_near"] / calls * 1e6, b["t_near"] / calls * 1e6,
+              c["t_near"] / calls * 1e6, same), flush=True)
     pf = a["prof"]
     if pf[6] + pf[7] > 0:  # SMP_NEAR_PROF build: near_set's barrier-separated steps (register path)
         fast = max(pf[7], 1)
