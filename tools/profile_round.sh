@@ -16,13 +16,20 @@ OUT=$R/gpurun_out
 P=$OUT/${ROUND}_${TAG}
 mkdir -p $OUT
 export TMPDIR=/tmp
-cd /tmp
-timeout -k 10 1000 rocprofv3 --pmc FETCH_SIZE -d ${P}_prof_pmc -o pmc -- python3 $R/bench.py --no-cpu --steps 1 --warmup 0 "$@" > ${P}_pmc.log 2>&1
-timeout -k 10 1000 rocprofv3 --pmc WRITE_SIZE -d ${P}_prof_pmcw -o pmcw -- python3 $R/bench.py --no-cpu --steps 1 --warmup 0 "$@" > ${P}_pmcw.log 2>&1
-cd $R
-python3 tools/rocpd_summary.py pmc plan_kernel $R/profiles/${ROUND}_pmc_${TAG}.json ${P}_prof_pmc/pmc_results.db ${P}_prof_pmcw/pmcw_results.db > ${P}_pmc_summary.txt
-cp $R/profiles/${ROUND}_pmc_${TAG}.json ${P}_pmc.json
-timeout -k 10 ${BENCH_LIMIT:-600} python bench.py "$@" > ${P}_bench.json 2> ${P}_bench.err
-cd /tmp
-timeout -k 10 ${KT_LIMIT:-400} rocprofv3 --kernel-trace --stats -d ${P}_prof_kt -o kt -- python3 $R/bench.py --no-cpu --steps 3 --warmup 1 "$@" > ${P}_kt.log 2>&1
-cd $R
+# SKIP_PMC / SKIP_BENCH / SKIP_KT=1 leave a step out (a long run's steps can go to separate calls)
+if [ -z "$SKIP_PMC" ]; then
+  cd /tmp
+  timeout -k 10 ${PMC_LIMIT:-1000} rocprofv3 --pmc FETCH_SIZE -d ${P}_prof_pmc -o pmc -- python3 $R/bench.py --no-cpu --steps 1 --warmup 0 "$@" > ${P}_pmc.log 2>&1
+  timeout -k 10 ${PMC_LIMIT:-1000} rocprofv3 --pmc WRITE_SIZE -d ${P}_prof_pmcw -o pmcw -- python3 $R/bench.py --no-cpu --steps 1 --warmup 0 "$@" > ${P}_pmcw.log 2>&1
+  cd $R
+  python3 tools/rocpd_summary.py pmc plan_kernel $R/profiles/${ROUND}_pmc_${TAG}.json ${P}_prof_pmc/pmc_results.db ${P}_prof_pmcw/pmcw_results.db > ${P}_pmc_summary.txt
+  cp $R/profiles/${ROUND}_pmc_${TAG}.json ${P}_pmc.json
+fi
+if [ -z "$SKIP_BENCH" ]; then
+  timeout -k 10 ${BENCH_LIMIT:-600} python bench.py "$@" > ${P}_bench.json 2> ${P}_bench.err
+fi
+if [ -z "$SKIP_KT" ]; then
+  cd /tmp
+  timeout -k 10 ${KT_LIMIT:-400} rocprofv3 --kernel-trace --stats -d ${P}_prof_kt -o kt -- python3 $R/bench.py --no-cpu --steps 3 --warmup 1 "$@" > ${P}_kt.log 2>&1
+  cd $R
+fi
