@@ -252,15 +252,21 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = "nccl"
     if world > 1:
         ndev = max(1, torch.cuda.device_count())
         if ndev < world:
             # more ranks than GPUs (a rehearsal on a one-GPU box): ranks share a GPU, each planner provisions its share
-            # of the device's co-resident workgroups (read when the planner is created)
+            # of the device's co-resident workgroups (read when the planner is created); RCCL refuses two ranks on one
+            # device, so the rehearsal's few collectives (scene broadcast, barriers, counter reductions) go over gloo
             os.environ["SMP_SLOT_SHARE"] = str((world + ndev - 1) // ndev)
+            backend = "gloo"
         local = local % ndev
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
 
     from squirrel_motion_planner_amd import distributed as D, scenes
     from squirrel_motion_planner_amd.planner import GpuPlanner, Scene
@@ -344,7 +350,7 @@ def main():
                  totals["plan_ms"], totals["launches"]]
     alone = None
     if world > 1:
-        tsum, tmax = D.reduce_counters(local_vec, device="cuda")
+        tsum, tmax = D.reduce_counters(local_vec, device="cuda" if backend == "nccl" else "cpu")
         elapsed = tmax[0]
         checked, valid, iters, nn, near, plan_ms, launches = tsum[1:]
         plan_ms_rank0 = totals["plan_ms"]
@@ -397,7 +403,8 @@ def main():
                        # the queries; with a scout, split between the leader's and the scout's tiles + the sampler)
                        "helpers_per_query": int(step0["helpers"]), "scout": int(step0["scout"]),
                        "parallelism": "one leader workgroup per query + helper workgroups sharing its collision "
-                       "tiles; queries sharded over ranks, scene broadcast once"},
+                       "tiles; queries sharded over ranks, scene broadcast once",
+                       "backend": backend if world > 1 else None},
             "valid_configs_per_s": valid / elapsed,
             "iterations_per_s": iters / elapsed,
             # time to the first feasible path on the host's clock from smp_plan entry (start / goal checks, uploads,
