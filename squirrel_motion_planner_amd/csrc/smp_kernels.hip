@@ -5540,7 +5540,7 @@ __global__ void __launch_bounds__(BLOCK) plan_kernel(const RobotDev* __restrict_
     drain();  // before any request reaches a scout
 #ifdef SMP_TRACE
     g_L.trole = 0;
-    g_L.tit = -1;
+    g_L.tit = 0;  // the pre-loop's records go with iteration 0's
     g_L.tn = g_tlog_n[0];
 #endif
   }

@@ -43,6 +43,11 @@ for iters in [int(v) for v in (sys.argv[1:] or ["2000", "10000", "50000"])]:
               " | publish %.1f busy %.1f idle %.1f | edge_costs %.1f tiles(job) %.1f" % (
                   ns, *[sp[k] * 1e6 / ns for k in (0, 1, 2, 3, 4, 5, 6, 29, 31, 28, 9, 7)]), flush=True)
     raw = r["phase_raw"]
+    if r["first_solution_iter"] < 0 or r["first_solution_iter"] > 0:
+        # the leader's pre_commit outcomes (plain builds: prof[28..31]): record committed / no usable record / a node
+        # appended since the record's snapshot is nearer / connect redone in full
+        print("   pre_commit outcomes: committed %d, no record %d, newer nearest %d, connect redone %d" % tuple(
+            int(v) for v in raw[28:32]), flush=True)
     nj = max(raw[15] * 1e8, 1)
     print("   jobs %d: publish %.1f us, own %.1f us, wait %.1f us per job" % (
         raw[15] * 1e8, raw[12] * 1e6 / nj, raw[13] * 1e6 / nj, raw[14] * 1e6 / nj), flush=True)
