@@ -42,10 +42,10 @@ __global__ void fk_kernel(const RobotDev* rb, const double* q, int n, double* fr
 __global__ void sqrt_div_kernel(const double* a, const double* b, int n, double* sq, double* dv);
 __global__ void near_probe_kernel(const double* tq, const double* tcost, int cap, int n, const double* queries,
                                   const int* excl, int m, double r, int reps, int* nn, int* nk, int* lo, int* hi,
-                                  unsigned long long* ticks);
+                                  unsigned long long* ticks, const float* tqf);
 __global__ void near_probe_inl_kernel(const double* tq, const double* tcost, int cap, int n, const double* queries,
                                       const int* excl, int m, double r, int reps, int* nn, int* nk, int* lo, int* hi,
-                                      unsigned long long* ticks);
+                                      unsigned long long* ticks, const float* tqf);
 }  // namespace smp
 
 using namespace smp;
@@ -92,6 +92,7 @@ struct DBuf {  // device buffer that only grows
 struct QueryBuffers {
   DBuf<QState> st;
   DBuf<double> q, cost, e_start, e_target, rows;
+  DBuf<float> qf;
   DBuf<int> parent, first_child, next_sib, prev_sib, stack, path_nodes;
   DBuf<ViaNode> via;
   DBuf<JobBoard> jb;               // the leader's collision-job board
@@ -100,7 +101,7 @@ struct QueryBuffers {
   DBuf<ViaNode> svia[MAX_SCOUTS];
   size_t cap = 0;
   void release() {
-    st.release(); q.release(); cost.release(); e_start.release(); e_target.release(); rows.release();
+    st.release(); q.release(); qf.release(); cost.release(); e_start.release(); e_target.release(); rows.release();
     parent.release(); first_child.release(); next_sib.release(); prev_sib.release(); stack.release();
     path_nodes.release(); via.release(); jb.release();
     for (int s = 0; s < MAX_SCOUTS; ++s) { sjb[s].release(); scb[s].release(); svia[s].release(); }
@@ -932,6 +933,7 @@ static hipError_t alloc_query(QueryBuffers& b, size_t cap, int via_cap, long lon
   hipError_t e;
   if ((e = b.st.reserve(1))) return e;
   if ((e = b.q.reserve(cap * NJ * 2))) return e;
+  if ((e = b.qf.reserve(cap * NJ * 2))) return e;
   if ((e = b.cost.reserve(cap * 3 * 2))) return e;
   if ((e = b.e_start.reserve(cap * NJ * 2))) return e;
   if ((e = b.e_target.reserve(cap * NJ * 2))) return e;
@@ -960,6 +962,7 @@ static QueryDev make_qdev(QueryBuffers& b, size_t cap, long long rows) {
   for (int t = 0; t < 2; ++t) {
     TreeDev& T = d.tr[t];
     T.q = b.q.p + (size_t)t * cap * NJ;
+    T.qf = b.qf.p + (size_t)t * cap * NJ;
     T.cost = b.cost.p + (size_t)t * cap * 3;
     T.e_start = b.e_start.p + (size_t)t * cap * NJ;
     T.e_target = b.e_target.p + (size_t)t * cap * NJ;
@@ -1001,13 +1004,15 @@ static QueryDev make_qdev(QueryBuffers& b, size_t cap, long long rows) {
   // SMP_SCAN_MIN overrides it (experiments and tests; 0: never)
   d.scan_min = 12288;
   if (const char* e = std::getenv("SMP_SCAN_MIN")) d.scan_min = std::max(0, std::atoi(e));
-  // participants of one split scan: a nearest result is 3 granules, a near result 122, and the near merge ranks
-  // every list entry against the other lists -- fewer, longer slices for near: one per 4096 nodes, 8 to 32
-  // (SMP_SCAN_PNN / SMP_SCAN_PNEAR cap them)
+  // participants of one split scan: a nearest result is 3 granules, a near result 122 -- fewer, longer slices for
+  // near: one per 2^scan_nshift nodes (4096), 8 to 32 (SMP_SCAN_PNN / SMP_SCAN_PNEAR cap them, SMP_SCAN_NSHIFT sets
+  // the shift)
   d.scan_pnn = 64;
   d.scan_pnear = SCAN_PNEAR;
   if (const char* e = std::getenv("SMP_SCAN_PNN")) d.scan_pnn = std::atoi(e);
   if (const char* e = std::getenv("SMP_SCAN_PNEAR")) d.scan_pnear = std::atoi(e);
+  d.scan_nshift = 12;
+  if (const char* e = std::getenv("SMP_SCAN_NSHIFT")) d.scan_nshift = std::min(20, std::max(6, std::atoi(e)));
   d.scan_pnn = std::min(SCAN_P, std::max(2, d.scan_pnn));
   d.scan_pnear = std::min(SCAN_PNEAR, std::max(2, d.scan_pnear));
   return d;
@@ -1821,11 +1826,17 @@ extern "C" int smp_probe_near(int device, const double* q_soa, const double* cos
   HIPCHK(hipMemcpy(dc, cost, (size_t)n * sizeof(double), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(dqq, queries, (size_t)m * NJ * sizeof(double), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(dx, excl, (size_t)m * sizeof(int), hipMemcpyHostToDevice));
+  // the tree's fp32 copy (TreeDev::qf: the planner writes it with every node)
+  std::vector<float> qf((size_t)n * NJ);
+  for (size_t k = 0; k < qf.size(); ++k) qf[k] = (float)q_soa[k];
+  float* dqf;
+  HIPCHK(hipMalloc(&dqf, qf.size() * sizeof(float)));
+  HIPCHK(hipMemcpy(dqf, qf.data(), qf.size() * sizeof(float), hipMemcpyHostToDevice));
   // modes 4 / 5 (the helpers' inlined slice forms) run in a kernel of their own, so that neither kernel's register
   // allocation carries the other's code
   const bool inl = reps < 0 && 1 + ((-reps) >> 20) >= 4;
   hipLaunchKernelGGL(inl ? near_probe_inl_kernel : near_probe_kernel, dim3(1), dim3(BLOCK), 0, 0, dq, dc, n, n, dqq, dx,
-                     m, r, reps, dnn, dnk, dlo, dhi, dt);
+                     m, r, reps, dnn, dnk, dlo, dhi, dt, (const float*)dqf);
   HIPCHK(hipGetLastError());
   HIPCHK(hipDeviceSynchronize());
   HIPCHK(hipMemcpy(nn, dnn, (size_t)m * sizeof(int), hipMemcpyDeviceToHost));
@@ -1834,7 +1845,7 @@ extern "C" int smp_probe_near(int device, const double* q_soa, const double* cos
   HIPCHK(hipMemcpy(hi, dhi, (size_t)m * 20 * sizeof(int), hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(ticks, dt, 14 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   (void)hipFree(dq); (void)hipFree(dc); (void)hipFree(dqq); (void)hipFree(dx); (void)hipFree(dnn);
-  (void)hipFree(dnk); (void)hipFree(dlo); (void)hipFree(dhi); (void)hipFree(dt);
+  (void)hipFree(dnk); (void)hipFree(dlo); (void)hipFree(dhi); (void)hipFree(dt); (void)hipFree(dqf);
   int dev_clock_khz = 0;
   HIPCHK(hipDeviceGetAttribute(&dev_clock_khz, hipDeviceAttributeWallClockRate, device));
   *clock_hz = dev_clock_khz * 1000.0;

@@ -543,6 +543,12 @@ __device__ __forceinline__ bool wave_group_live(int first, int end) {
 // scout_request publishes them (drain, plus an agent release when the scout runs on another XCD).
 __device__ __forceinline__ void st_tree(double* p, double v) { *p = v; }
 __device__ __forceinline__ void st_tree(int* p, int v) { *p = v; }
+__device__ __forceinline__ void st_tree(float* p, float v) { *p = v; }
+// Node coordinate j of node i of tree T: the fp64 value and its fp32 copy (the distributed scans' prefilter, TreeDev::qf).
+__device__ __forceinline__ void st_coord(const TreeDev& T, int cap, int j, int i, double v) {
+  st_tree(&T.q[(size_t)j * cap + i], v);
+  st_tree(&T.qf[(size_t)j * cap + i], (float)v);
+}
 // XCD of this workgroup (HW_REG_XCC_ID): placement knowledge for speed only.
 __device__ __forceinline__ int xcc_id() { return __builtin_amdgcn_s_getreg((3 << 11) | 20); }
 // Bitwise equality of two configurations (cache keys of the scout's records).
@@ -586,7 +592,7 @@ __device__ void insert_node(const Ctx& C, int t, const double* e_start, const do
   const TreeDev& T = C.Q.tr[t];
   int cap = S.cap;
   for (int j = 0; j < NJ; ++j) {
-    st_tree(&T.q[(size_t)j * cap + i], x.q[j]);
+    st_coord(T, cap, j, i, x.q[j]);
     T.e_start[(size_t)j * cap + i] = e_start[j];
     T.e_target[(size_t)j * cap + i] = e_target[j];
     g_L.pc_q[t][i & (PATCH_K - 1)][j] = x.q[j];
@@ -613,10 +619,10 @@ __device__ bool spec_stage(const Ctx& C, int s, unsigned long long wait = 0);
 // Participants of a distributed scan: this workgroup and up to SCAN_P - 1 helpers (SCAN_PNEAR for a near scan).  While a
 // collision job runs (overlap_work), its tiles hold workers 1 .. ntiles and participant p >= 1 is worker W - p: the scan
 // takes the helpers the job leaves free, at least 8 participants (a busy helper takes its slice after its tile).
-// A near scan takes one participant per 4096 nodes (at least 8): its merge and result collection grow with the
-// participants (122 granules each), a nearest result is 3 granules.
+// A near scan takes one participant per 2^scan_nshift nodes (4096 by default, at least 8): its result collection grows
+// with the participants (122 granules each), a nearest result is 3 granules.
 __device__ __forceinline__ int scan_parts(const Ctx& C, int near, int nodes) {
-  int P = min(min(C.Q.nworkers, SCAN_P), near ? min(min(C.Q.scan_pnear, SCAN_PNEAR), max(8, nodes >> 12)) : C.Q.scan_pnn);
+  int P = min(min(C.Q.nworkers, SCAN_P), near ? min(min(C.Q.scan_pnear, SCAN_PNEAR), max(8, nodes >> C.Q.scan_nshift)) : C.Q.scan_pnn);
   if (g_L.in_job) P = min(P, max(C.Q.nworkers - g_L.u.job.ntiles, 8));
   return uni(P);
 }
@@ -1052,6 +1058,125 @@ __device__ __forceinline__ void slice_nn_body(gcdptr tq, int cap, int i0, int i1
   }
   slice_nn_reduce(best, bid, X);
 }
+// ---- fp32 prefilter of the distributed scans (DESIGN.md "Scans of large trees").  A slice reads the tree's fp32 copy
+// (TreeDev::qf, 32 B per node instead of 64) and decides in fp64 only where fp32 cannot.  With u = 2^-24 and c = 6u *
+// max(|q_j|, |x_j|) (4u M bounds the error of one fp32 difference, M the largest magnitude; x1.5 margin), the fp32
+// squared distance s32 of a node differs from the fp64 one s by at most E(s) = 4 (2 sqrt(8) c sqrt(s) + 8 c^2 + 9 u s)
+// (the cross terms by Cauchy-Schwarz, the squares' and the eight-term sum's roundings; x4 margin).  Near test: a node
+// with s32 + E < r2lo is near, one with s32 - E > r2hi is not (E taken at s = 2 r2hi, which covers every node that can
+// fall between), the rest are decided from their fp64 coordinates exactly as before.  Nearest: a node can tie or beat
+// the minimum only if its s32 is within 2 E(2 m) of the smallest s32 m; each thread keeps its smallest and second
+// smallest s32, so the candidates are the threads' smallest nodes, and a thread whose second smallest is also within
+// the margin rescans its nodes in fp64 -- the first strict minimum in fp64, as the reference, decides.
+typedef const float __attribute__((address_space(1)))* gcfptr;
+__device__ __forceinline__ gcfptr uni_gf(const float* p) {
+  const unsigned long long v = reinterpret_cast<unsigned long long>(p);
+  const unsigned lo = __builtin_amdgcn_readfirstlane((int)(unsigned)v);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((int)(unsigned)(v >> 32));
+  return (gcfptr)(((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ void tree_cols_f(const float* tqf, int cap, gcfptr* c) {
+  const gcfptr b = uni_gf(tqf);
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) c[j] = b + (size_t)j * (unsigned)cap;
+}
+constexpr double F32_U = 0x1p-24;
+__device__ __forceinline__ double s32_err(double s, double c) {
+  return 4.0 * (5.6568543 * c * sqrt(s) + 8.0 * c * c + 9.0 * F32_U * s);
+}
+// One node's fp32 squared distance and its coordinates' largest magnitude.
+__device__ __forceinline__ float s32_of(const float* qf, const float* xf, float& xm) {
+  float s = 0.0f;
+  xm = 0.0f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const float d = qf[j] - xf[j];
+    s += d * d;
+    xm = fmaxf(xm, fabsf(xf[j]));
+  }
+  return s;
+}
+// The thread's two smallest s32 (b1 with its node, b2) and the largest magnitude seen.
+__device__ __forceinline__ void nn32_track(bool valid, float s, int i, float xm, float& b1, float& b2, int& bi1,
+                                           float& cm) {
+  if (valid) {
+    if (s < b1) { b2 = b1; b1 = s; bi1 = i; }
+    else if (s < b2) b2 = s;
+    cm = fmaxf(cm, xm);
+  }
+}
+// Exact finish of a prefiltered nearest scan over the nodes i0 + threadIdx.x + k * BLOCK of [i0, i1) (every thread's node
+// set in both slice forms): the candidates in fp64, the (distance key, id) minimum in X.wk[0], X.wi[0] (slice_nn_reduce).
+__device__ __forceinline__ void nn32_finish(const gcdptr* tqc, int i0, int i1, const double* qq, float qm, float b1,
+                                            float b2, int bi1, float cm, ScanLds& X) {
+  const unsigned mb = __ockl_wfred_min_u32(__float_as_uint(b1));  // non-negative floats order like their bits
+  const unsigned cb = __ockl_wfred_max_u32(__float_as_uint(cm));
+  if (lane_id() == 0) { X.wi[wave_id()] = (int)mb; X.wk[wave_id()] = cb; }
+  __syncthreads();
+  unsigned m = (unsigned)X.wi[0], c = (unsigned)X.wk[0];
+#pragma unroll
+  for (int w = 1; w < BLOCK / 64; ++w) { m = min(m, (unsigned)X.wi[w]); c = max(c, (unsigned)X.wk[w]); }
+  __syncthreads();  // (slice_nn_reduce writes X.wk / X.wi next)
+  const double md = (double)__uint_as_float(m);
+  const double th = md + 2.0 * s32_err(2.0 * md + 1e-300, 6.0 * F32_U * (double)fmaxf(__uint_as_float(c), qm));
+  double best = 10000.0, best_s = 1e300;
+  int bid = 0x7fffffff;
+  if ((double)b2 <= th) {
+    for (int i = i0 + (int)threadIdx.x; i < i1; i += BLOCK) {
+      double sd = 0.0;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const double d = qq[j] - tqc[j][(unsigned)i];
+        sd += d * d;
+      }
+      nn_take(true, sd, i, best, best_s, bid);
+    }
+  } else if ((double)b1 <= th) {
+    double sd = 0.0;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const double d = qq[j] - tqc[j][(unsigned)bi1];
+      sd += d * d;
+    }
+    nn_take(true, sd, bi1, best, best_s, bid);
+  }
+  slice_nn_reduce(best, bid, X);
+}
+// slice_nn over the fp32 copy (tqf), exact through nn32_finish.
+__device__ __forceinline__ void slice_nn_body32(gcdptr tq, const float* tqf, int cap, int i0, int i1, const double* q,
+                                                ScanLds& X) {
+  gcdptr tqc[NJ];
+  tree_cols(tq, cap, tqc);
+  gcfptr tfc[NJ];
+  tree_cols_f(tqf, cap, tfc);
+  double qq[NJ];
+  float qf[NJ], qm = 0.0f;
+  for (int j = 0; j < NJ; ++j) { qq[j] = q[j]; qf[j] = (float)q[j]; qm = fmaxf(qm, fabsf(qf[j])); }
+  float b1 = __builtin_inff(), b2 = __builtin_inff(), cm = 0.0f;
+  int bi1 = 0x7fffffff;
+  constexpr int NPT = 8;
+  for (int b0 = i0 + (int)threadIdx.x; b0 < i1; b0 += NPT * BLOCK) {
+    float a[NPT][NJ];
+#pragma unroll
+    for (int u = 0; u < NPT; ++u) {
+      if (wave_group_live(b0 - lane_id() + u * BLOCK, i1)) {
+        const unsigned ii = (unsigned)min(b0 + u * BLOCK, i1 - 1);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) a[u][j] = tfc[j][ii];
+      } else {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) a[u][j] = qf[j];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < NPT; ++u) {
+      float xm;
+      const float sv = s32_of(qf, a[u], xm);
+      nn32_track(b0 + u * BLOCK < i1, sv, b0 + u * BLOCK, xm, b1, b2, bi1, cm);
+    }
+  }
+  nn32_finish(tqc, i0, i1, qq, qm, b1, b2, bi1, cm, X);
+}
 __device__ void slice_nn(gcdptr tq, int cap, int i0, int i1, const double* q, ScanLds& X) {
   slice_nn_body(tq, cap, i0, i1, q, X);
 }
@@ -1179,20 +1304,29 @@ __device__ __forceinline__ void slice_near_body(gcdptr tq, gcdptr tc, int cap, i
 // thousand nodes is one chunk, one pass of barrier-separated steps, instead of a per-wave insertion per candidate.
 // Returns false (outputs undefined) if a chunk's histogram cannot split its costs (many equal costs): the caller then
 // runs slice_near_body.  All threads.
-template <bool NN>
+// F32: the radius test and the nearest node from the tree's fp32 copy tqf (the prefilter above), fp64 where it cannot
+// decide.
+template <bool NN, bool F32 = false>
 __device__ __forceinline__ bool slice_near_hist(gcdptr tq, gcdptr tc, int cap, int i0, int i1, const double* q, int excl,
-                                                double r, ScanLds& X) {
+                                                double r, ScanLds& X, const float* tqf = nullptr) {
   constexpr int K = SCAN_K, NW = BLOCK / 64, CH = NEAR_NBK * BLOCK;
   double nb = 10000.0, nb_s = 1e300;  // NN: this thread's nearest candidate
   int nbi = 0x7fffffff;
+  float b1 = __builtin_inff(), b2 = __builtin_inff(), cm = 0.0f;  // NN with F32: nn32_track's state
+  int bi1 = 0x7fffffff;
   static_assert(K <= 64 && NEAR_BUF == 128 && NEAR_BINS == 4 * 64, "register path layout");
   const double r2 = r * r, r2lo = r2 * (1.0 - 1e-12), r2hi = r2 * (1.0 + 1e-12);
   const int lane = lane_id(), wave = wave_id();
   gcdptr tqc[NJ];
   tree_cols(tq, cap, tqc);
+  gcfptr tfc[NJ];
+  if (F32) tree_cols_f(tqf, cap, tfc);
   tc = uni_g(tc);
   double qq[NJ];
-  for (int j = 0; j < NJ; ++j) qq[j] = q[j];
+  float qf[NJ], qm = 0.0f;
+  for (int j = 0; j < NJ; ++j) { qq[j] = q[j]; qf[j] = (float)q[j]; qm = fmaxf(qm, fabsf(qf[j])); }
+  // F32: E(2 r2hi) = c K1 + 32 c^2 + K2 for a node's c (s32_err at s = 2 r2hi)
+  const double K1 = 4.0 * 5.6568543 * sqrt(2.0 * r2hi), K2 = 4.0 * 9.0 * F32_U * 2.0 * r2hi;
   int tot_all = 0;  // near nodes of the chunks before this one (block-uniform)
   if (threadIdx.x == 0) X.take = 0;
   __syncthreads();
@@ -1204,7 +1338,62 @@ __device__ __forceinline__ bool slice_near_hist(gcdptr tq, gcdptr tc, int cap, i
 #pragma unroll
     for (int g = 0; g < NEAR_NBK; g += 4) {
       key[g] = key[g + 1] = key[g + 2] = key[g + 3] = 0;
-      if (c0 + g * BLOCK + wave * 64 < i1) {
+      if (F32 && c0 + g * BLOCK + wave * 64 < i1) {
+        float xf[4][NJ];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const int i = c0 + (g + b) * BLOCK + wave * 64 + lane;
+          if (wave_group_live(c0 + (g + b) * BLOCK + wave * 64, i1)) {
+            const unsigned ii = (unsigned)min(i, i1 - 1);
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) xf[b][j] = tfc[j][ii];
+            key[g + b] = i < i1 ? (unsigned long long)__double_as_longlong(tc[ii]) : 0ull;
+          } else {
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) xf[b][j] = qf[j];
+          }
+        }
+        bool nr[4], und[4];
+        bool any_und = false;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const int i = c0 + (g + b) * BLOCK + wave * 64 + lane;
+          const bool valid = i < i1 && i != excl;
+          float xm;
+          const float sv = s32_of(qf, xf[b], xm);
+          const double c = 6.0 * F32_U * (double)fmaxf(xm, qm), E = c * K1 + 32.0 * c * c + K2, sd = (double)sv;
+          nr[b] = valid && sd + E < r2lo;
+          und[b] = valid && !nr[b] && !(sd - E > r2hi);
+          if (NN) nn32_track(i < i1, sv, i, xm, b1, b2, bi1, cm);
+          any_und |= und[b];
+        }
+        if (__ballot(any_und)) {
+          // nodes the fp32 test cannot decide: their fp64 coordinates, near_set's test
+#pragma unroll
+          for (int b = 0; b < 4; ++b)
+            if (und[b]) {
+              const unsigned ii = (unsigned)(c0 + (g + b) * BLOCK + wave * 64 + lane);
+              double sb = 0.0;
+#pragma unroll
+              for (int j = 0; j < NJ; ++j) {
+                const double d = qq[j] - tqc[j][ii];
+                sb += d * d;
+              }
+              bool amb;
+              nr[b] = near_radius(true, sb, r, r2lo, r2hi, amb);
+              if (amb) nr[b] = sqrt(sb) < r;
+            }
+        }
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          if (nr[b]) {
+            nmask |= 1u << (g + b);
+            kmin = min(kmin, key[g + b]);
+            kmax = max(kmax, key[g + b]);
+          }
+          wc += __popcll(__ballot(nr[b]));
+        }
+      } else if (!F32 && c0 + g * BLOCK + wave * 64 < i1) {
         double x[4][NJ];
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
@@ -1445,7 +1634,8 @@ __device__ __forceinline__ bool slice_near_hist(gcdptr tq, gcdptr tc, int cap, i
   }
   if (threadIdx.x == 0) X.cnt = tot_all;
   __syncthreads();
-  if (NN) slice_nn_reduce(nb, nbi, X);
+  if (NN && F32) nn32_finish(tqc, i0, i1, qq, qm, b1, b2, bi1, cm, X);
+  else if (NN) slice_nn_reduce(nb, nbi, X);
   return true;
 }
 
@@ -1463,10 +1653,10 @@ __device__ __noinline__ void slice_near_slow(gcdptr tq, gcdptr tc, int cap, int 
 // The helpers' form of slice_near: the register path inlined into the helper loop, so that a scan job costs no call --
 // a non-inlined callee at 512 threads saves and restores every callee-saved VGPR it uses, ~100 of them here (≈200 KB
 // of scratch stores and loads per call through the CU's load pipeline, and most of a large tree's write traffic).
-template <bool NN>
+template <bool NN, bool F32 = false>
 __device__ __forceinline__ void slice_near_inl(gcdptr tq, gcdptr tc, int cap, int i0, int i1, const double* q, int excl,
-                                               double r, ScanLds& X) {
-  if (uni(slice_near_hist<NN>(tq, tc, cap, i0, i1, q, excl, r, X))) return;
+                                               double r, ScanLds& X, const float* tqf = nullptr) {
+  if (uni(slice_near_hist<NN, F32>(tq, tc, cap, i0, i1, q, excl, r, X, tqf))) return;
   slice_near_slow<NN>(tq, tc, cap, i0, i1, q, excl, r, X);
 }
 
@@ -2280,9 +2470,11 @@ __device__ void scan_slice(const Ctx& C, int near, int t, const double* q, int i
   int lo, hi;
   scan_range(i0, n, P, w, &lo, &hi);
   if (INL) {
-    if (near == 2) slice_near_inl<true>(tq, tc, cap, lo, hi, q, excl, r, X);
-    else if (near) slice_near_inl<false>(tq, tc, cap, lo, hi, q, excl, r, X);
-    else slice_nn_body(tq, cap, lo, hi, q, X);
+    // the fp32 prefilter (the tree's qf copy): half the bytes per node
+    const float* tqf = C.Q.tr[t].qf;
+    if (near == 2) slice_near_inl<true, true>(tq, tc, cap, lo, hi, q, excl, r, X, tqf);
+    else if (near) slice_near_inl<false, true>(tq, tc, cap, lo, hi, q, excl, r, X, tqf);
+    else slice_nn_body32(tq, tqf, cap, lo, hi, q, X);
     return;
   }
   if (near == 2) slice_near<true>(tq, tc, cap, lo, hi, q, excl, r, X);
@@ -3326,7 +3518,7 @@ __device__ void insert_via(const Ctx& C, int t, const ViaNode* rec = nullptr, in
         if (wid != i || (k > 0 && wpar != i - 1)) S.status = -7;  // not the chain insert_node expects
         for (int j = 0; j < NJ; ++j) {
           const double qj = ldd(&w.q[j]);
-          st_tree(&T.q[(size_t)j * cap + i], qj);
+          st_coord(T, cap, j, i, qj);
           g_L.pc_q[t][i & (PATCH_K - 1)][j] = qj;
           T.e_start[(size_t)j * cap + i] = ldd(&w.e_start[j]);
           T.e_target[(size_t)j * cap + i] = ldd(&w.e_target[j]);
@@ -3920,7 +4112,7 @@ __device__ void rewire(const Ctx& C, int t) {
           else if (v == S.nA.id && !connected) S.nA.parent = g_L.xn.id;
         }
         for (int j = 0; j < NJ; ++j) {
-          st_tree(&T.q[(size_t)j * cap + v], g_L.eg_end[e][j]);
+          st_coord(T, cap, j, v, g_L.eg_end[e][j]);
           T.e_start[(size_t)j * cap + v] = g_L.eg_start[e][j];
           T.e_target[(size_t)j * cap + v] = g_L.eg_target[e][j];
         }
@@ -5563,7 +5755,7 @@ __global__ void __launch_bounds__(BLOCK) plan_kernel(const RobotDev* __restrict_
     // first launch: the two roots (init_planner, birrt_star.cpp:386-443) from the query's start / goal
     const int t = threadIdx.x, cap = g_L.S.cap;
     const TreeDev& T = C.Q.tr[t];
-    for (int j = 0; j < NJ; ++j) T.q[(size_t)j * cap] = t == 0 ? g_L.S.qs[j] : g_L.S.qg[j];
+    for (int j = 0; j < NJ; ++j) st_coord(T, cap, j, 0, t == 0 ? g_L.S.qs[j] : g_L.S.qg[j]);
     for (int k = 0; k < 3; ++k) T.cost[(size_t)k * cap] = 0.0;
     T.parent[0] = 0;
     T.first_child[0] = -1;
@@ -5694,7 +5886,7 @@ __global__ void path_edges_kernel(const QueryDev* qs, int q, int ns, int ng, dou
 template <bool INL>
 __device__ __forceinline__ void near_probe_body(const double* tqv, const double* tcost, int cap, int n,
                                                 const double* queries, const int* excl, int m, double r, int reps, int* nn,
-                                                int* nk, int* lo, int* hi, unsigned long long* ticks) {
+                                                int* nk, int* lo, int* hi, unsigned long long* ticks, const float* tqf) {
   Ctx C;
   C.Q.jb = nullptr;  // single workgroup: no helpers, scans stay local
   C.Q.scan_min = 0;
@@ -5726,7 +5918,7 @@ __device__ __forceinline__ void near_probe_body(const double* tqv, const double*
     unsigned long long t0 = wall_clock64();
     for (int rep = 0; rep < reps && (mode < 2 || mode == 4); ++rep) {
       if constexpr (INL) {
-        slice_nn_body(tq, cap, 0, n, g_L.xr, g_L.sc.s);
+        slice_nn_body32(tq, tqf, cap, 0, n, g_L.xr, g_L.sc.s);
         id = __longlong_as_double((long long)g_L.sc.s.wk[0]) < 10000.0 ? g_L.sc.s.wi[0] : 0;
       } else {
         if (slice) {
@@ -5740,8 +5932,8 @@ __device__ __forceinline__ void near_probe_body(const double* tqv, const double*
     unsigned long long t1 = wall_clock64();
     for (int rep = 0; rep < reps; ++rep) {
       if constexpr (INL) {
-        if (mode == 4) slice_near_inl<false>(tq, tc, cap, 0, n, g_L.xr, excl[k], r, g_L.sc.s);
-        else slice_near_inl<true>(tq, tc, cap, 0, n, g_L.xr, excl[k], r, g_L.sc.s);
+        if (mode == 4) slice_near_inl<false, true>(tq, tc, cap, 0, n, g_L.xr, excl[k], r, g_L.sc.s, tqf);
+        else slice_near_inl<true, true>(tq, tc, cap, 0, n, g_L.xr, excl[k], r, g_L.sc.s, tqf);
       } else {
         if (mode == 1) slice_near<false>(tq, tc, cap, 0, n, g_L.xr, excl[k], r, g_L.sc.s);
         else if (mode == 3) slice_near<true>(tq, tc, cap, 0, n, g_L.xr, excl[k], r, g_L.sc.s);
@@ -5782,15 +5974,15 @@ __device__ __forceinline__ void near_probe_body(const double* tqv, const double*
 __global__ void __launch_bounds__(BLOCK) near_probe_kernel(const double* tqv, const double* tcost, int cap, int n,
                                                            const double* queries, const int* excl, int m, double r,
                                                            int reps, int* nn, int* nk, int* lo, int* hi,
-                                                           unsigned long long* ticks) {
-  near_probe_body<false>(tqv, tcost, cap, n, queries, excl, m, r, reps, nn, nk, lo, hi, ticks);
+                                                           unsigned long long* ticks, const float* tqf) {
+  near_probe_body<false>(tqv, tcost, cap, n, queries, excl, m, r, reps, nn, nk, lo, hi, ticks, tqf);
 }
-// Modes 4 / 5 only (the helpers' inlined slice forms), in a kernel of their own.
+// Modes 4 / 5 only (the helpers' inlined slice forms, over the fp32 copy tqf as in the planner), in a kernel of their own.
 __global__ void __launch_bounds__(BLOCK) near_probe_inl_kernel(const double* tqv, const double* tcost, int cap, int n,
                                                                const double* queries, const int* excl, int m, double r,
                                                                int reps, int* nn, int* nk, int* lo, int* hi,
-                                                               unsigned long long* ticks) {
-  near_probe_body<true>(tqv, tcost, cap, n, queries, excl, m, r, reps, nn, nk, lo, hi, ticks);
+                                                               unsigned long long* ticks, const float* tqf) {
+  near_probe_body<true>(tqv, tcost, cap, n, queries, excl, m, r, reps, nn, nk, lo, hi, ticks, tqf);
 }
 
 }  // namespace smp

@@ -29,6 +29,8 @@ struct TreeDev {               // SoA node arrays of one tree; capacity `cap`
   int* prev_sib;
   double* e_start;             // [NJ][cap] in-edge: interpolation start (parent config at creation)
   double* e_target;            // [NJ][cap] in-edge: interpolation target
+  float* qf;                   // [NJ][cap] q rounded to fp32: the distributed scans' prefilter (DESIGN.md "Scans of
+                               // large trees"), written with q
 };
 
 struct QState {                // per query, persisted in global memory across launches
@@ -321,6 +323,7 @@ struct QueryDev {
   unsigned* ttff;              // host-mapped word set to 1 when the first feasible path is committed (null: none)
   int scan_min;                // nodes in a scan's range from which it is split over the helpers (0: never)
   int scan_pnn, scan_pnear;    // participants (this workgroup + helpers) of a split nearest / near scan, <= SCAN_P
+  int scan_nshift;             // a split near scan takes one participant per 2^scan_nshift nodes (at least 8)
   int nworkers;                // leader + tile helper workgroups (tile w, w + nworkers, ... is worker w's)
   int tile_ct;                 // configurations per job tile: 0 = by job size (job_tile_ct), else 1 / 2 / 4 / 8
   int sampler;                 // 1: the last helper workgroup is the run-ahead sampler
