@@ -2592,8 +2592,10 @@ __device__ void scan_run(const Ctx& C, int near, int t, const double* q, int i0,
   const unsigned long long sp1 = wall_clock64();
   if (threadIdx.x == 0) st_agent(&C.Q.jb->dbg[8], sp1);
 #endif
+  TR();
   scan_publish(C, seq, near, t, q, i0, n, excl, r, P);
   scan_slice<true>(C, near, t, q, i0, n, excl, r, P, 0, X);
+  TR();
   merge_put(M, X, near, 0);
   __syncthreads();
 #ifdef SMP_SCAN_PROF
@@ -2706,6 +2708,7 @@ __device__ void scan_run(const Ctx& C, int near, int t, const double* q, int i0,
     ++sp_rounds;
 #endif
     if (go == 1) break;
+    TR();
     if (go == 2) {
       const int w = uni(M.steal);
       scan_slice<true>(C, near, t, q, i0, n, excl, r, P, w, X);
@@ -2755,6 +2758,7 @@ __device__ void near_set_dist(const Ctx& C, int t, const double* q, int excl, bo
   const int n = uni(g_L.S.n[t]);
   const int P = scan_parts(C, 1, n);
   scan_run(C, nn ? 2 : 1, t, q, 0, n, excl, g_L.S.near_r, P);
+  TR();
   const MergeLds& M = g_L.sc.m;
   int tot = 0;
   for (int w = 0; w < P; ++w) tot += M.cnt[w];
@@ -2762,23 +2766,40 @@ __device__ void near_set_dist(const Ctx& C, int t, const double* q, int excl, bo
   const int take = min(SCAN_K, tot);
   static_assert(SCAN_PNEAR <= 64, "one lane per list");
   if (threadIdx.x < 128) {
+    // per round: the extreme head by two 32-bit wave reductions (high word, then the low word among the lanes holding
+    // that high word: DPP min / max steps on 32 bits, cheaper than one 64-bit reduction), the id reduction only when
+    // two heads hold equal keys; each lane has its list's next entry loaded ahead, so a winning lane's new head is in
+    // registers when the next round starts
     const int side = (int)threadIdx.x >> 6, w = lane_id();
     const int len = w < P ? M.len[w] : 0;
+    const unsigned long long KN = side ? 0ull : ~0ull;
+    const int IN = side ? -1 : 0x7fffffff;
     int p = 0;
-    unsigned long long k = side ? 0ull : ~0ull;
-    int id = side ? -1 : 0x7fffffff;
-    if (len > 0) { k = merge_key(M, side, w, 0); id = M.id[side][w][0]; }
+    unsigned long long k = len > 0 ? merge_key(M, side, w, 0) : KN;
+    int id = len > 0 ? M.id[side][w][0] : IN;
+    unsigned long long kn = len > 1 ? merge_key(M, side, w, 1) : KN;
+    int idn = len > 1 ? M.id[side][w][1] : IN;
     for (int r = 0; r < take; ++r) {
-      const unsigned long long mk = side ? __ockl_wfred_max_u64(k) : __ockl_wfred_min_u64(k);
-      const int mi = side ? __ockl_wfred_max_i32(k == mk ? id : -1) : __ockl_wfred_min_i32(k == mk ? id : 0x7fffffff);
+      const unsigned kh = (unsigned)(k >> 32), kl = (unsigned)k;
+      unsigned mh, ml;
+      if (side) { mh = __ockl_wfred_max_u32(kh); ml = __ockl_wfred_max_u32(kh == mh ? kl : 0u); }
+      else { mh = __ockl_wfred_min_u32(kh); ml = __ockl_wfred_min_u32(kh == mh ? kl : ~0u); }
+      const unsigned long long mk = (unsigned long long)mh << 32 | ml;
+      const unsigned long long tie = __ballot(k == mk);
+      int mi = id;
+      if (__popcll(tie) > 1)
+        mi = side ? __ockl_wfred_max_i32(k == mk ? id : -1) : __ockl_wfred_min_i32(k == mk ? id : 0x7fffffff);
       if (k == mk && id == mi) {
         if (!side) { g_L.lo_c[r] = __longlong_as_double((long long)mk); g_L.lo_i[r] = mi; }
         else { g_L.hi_c[take - 1 - r] = __longlong_as_double((long long)mk); g_L.hi_i[take - 1 - r] = mi; }
-        if (++p < len) { k = merge_key(M, side, w, p); id = M.id[side][w][p]; }
-        else { k = side ? 0ull : ~0ull; id = side ? -1 : 0x7fffffff; }
+        ++p;
+        k = kn; id = idn;
+        if (p + 1 < len) { kn = merge_key(M, side, w, p + 1); idn = M.id[side][w][p + 1]; }
+        else { kn = KN; idn = IN; }
       }
     }
   }
+  TR();
   if (threadIdx.x == 0) {
     g_L.nk = tot; g_L.n_lo = take; g_L.n_hi = take; g_L.S.near_nodes += n;
     if (nn) {  // the fused scan's nearest node: the (distance key, id) minimum of the slices

@@ -4,7 +4,6 @@ mkdir -p $OUT
 ( while true; do date +%s >> $OUT/heartbeat.txt; sleep 30; done ) &
 HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_tree_scans.py > $OUT/r05_t_scans_f32.txt 2>&1 &&
-timeout -k 10 120 python -u tools/slice_probe.py 2048 16384 65536 > $OUT/r05_slice_probe_f32.txt 2>&1 &&
-timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests > $OUT/r05_t_gpu_f32.txt 2>&1 &&
-timeout -k 10 200 python -u tools/perf_probe.py 100000 > $OUT/r05_perf_f32.txt 2>&1
+timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests > $OUT/r05_t_gpu_m32.txt 2>&1 || exit 1
+timeout -k 10 200 python -u tools/perf_probe.py 4000 100000 > $OUT/r05_perf_m32.txt 2>&1 || exit 1
+timeout -k 10 200 env SMP_LIB=squirrel_motion_planner_amd/lib/libsmp_gpu_trace15.so SMP_TRACE_W0=20 python -u tools/trace_probe.py 100000 > $OUT/r05_trace_1e5e.txt 2>&1
