@@ -1013,6 +1013,8 @@ static QueryDev make_qdev(QueryBuffers& b, size_t cap, long long rows) {
   if (const char* e = std::getenv("SMP_SCAN_PNEAR")) d.scan_pnear = std::atoi(e);
   d.scan_nshift = 12;
   if (const char* e = std::getenv("SMP_SCAN_NSHIFT")) d.scan_nshift = std::min(20, std::max(6, std::atoi(e)));
+  d.scan_ps0 = 0;
+  if (const char* e = std::getenv("SMP_SCAN_PS0")) d.scan_ps0 = std::min(4, std::max(0, std::atoi(e)));
   d.scan_pnn = std::min(SCAN_P, std::max(2, d.scan_pnn));
   d.scan_pnear = std::min(SCAN_PNEAR, std::max(2, d.scan_pnear));
   return d;

@@ -2425,11 +2425,17 @@ __device__ unsigned long long g_scanprof[24];
 #endif
 constexpr unsigned long long SCAN_WAIT = 2000;  // device-clock ticks (20 us) without progress before stealing a slice
 
-__device__ __forceinline__ void scan_range(int i0, int n, int P, int w, int* lo, int* hi) {
-  int chunk = (n - i0 + P - 1) / P;
+// Slice w of [i0, n) over P participants, in index order, 64-node multiples.  The publisher's slice 0 is a fraction
+// 1 / 2^ps0 of a helper's (QueryDev::scan_ps0): it publishes first and collects and merges after its slice, so equal
+// slices would make it the last to finish.
+__device__ __forceinline__ void scan_range(int i0, int n, int P, int w, int ps0, int* lo, int* hi) {
+  const int m = n - i0;
+  // helpers' chunk c with c / 2^ps0 + (P - 1) c >= m
+  int chunk = (int)(((long long)m << ps0) / (((long long)(P - 1) << ps0) + 1)) + 1;
   chunk = (chunk + 63) & ~63;
-  *lo = min(n, i0 + w * chunk);
-  *hi = min(n, *lo + chunk);
+  const int c0 = ((chunk >> ps0) + 63) & ~63;
+  *lo = w == 0 ? i0 : min(n, i0 + c0 + (w - 1) * chunk);
+  *hi = w == 0 ? min(n, i0 + c0) : min(n, *lo + chunk);
 }
 
 // Publishes scan job `seq` (all threads).
@@ -2468,7 +2474,7 @@ __device__ void scan_slice(const Ctx& C, int near, int t, const double* q, int i
   const gcdptr tq = uni_gptr(C.Q.tr[t].q), tc = uni_gptr(C.Q.tr[t].cost);
   const int cap = uni(__hip_atomic_load(&C.Q.st->cap, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   int lo, hi;
-  scan_range(i0, n, P, w, &lo, &hi);
+  scan_range(i0, n, P, w, C.Q.scan_ps0, &lo, &hi);
   if (INL) {
     // the fp32 prefilter (the tree's qf copy): half the bytes per node
     const float* tqf = C.Q.tr[t].qf;

@@ -324,6 +324,7 @@ struct QueryDev {
   int scan_min;                // nodes in a scan's range from which it is split over the helpers (0: never)
   int scan_pnn, scan_pnear;    // participants (this workgroup + helpers) of a split nearest / near scan, <= SCAN_P
   int scan_nshift;             // a split near scan takes one participant per 2^scan_nshift nodes (at least 8)
+  int scan_ps0;                // the publisher's slice is 1 / 2^scan_ps0 of a helper's
   int nworkers;                // leader + tile helper workgroups (tile w, w + nworkers, ... is worker w's)
   int tile_ct;                 // configurations per job tile: 0 = by job size (job_tile_ct), else 1 / 2 / 4 / 8
   int sampler;                 // 1: the last helper workgroup is the run-ahead sampler
