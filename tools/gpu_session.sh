@@ -4,6 +4,7 @@ mkdir -p $OUT
 ( while true; do date +%s >> $OUT/heartbeat.txt; sleep 30; done ) &
 HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
-timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests > $OUT/r05_t_gpu_m32.txt 2>&1 || exit 1
-timeout -k 10 200 python -u tools/perf_probe.py 4000 100000 > $OUT/r05_perf_m32.txt 2>&1 || exit 1
-timeout -k 10 200 env SMP_LIB=squirrel_motion_planner_amd/lib/libsmp_gpu_trace15.so SMP_TRACE_W0=20 python -u tools/trace_probe.py 100000 > $OUT/r05_trace_1e5e.txt 2>&1
+PMC_LIMIT=200 BENCH_LIMIT=300 KT_LIMIT=200 bash tools/profile_round.sh r05 c2 && echo "c2 rc=0" >> $OUT/status.txt &&
+PMC_LIMIT=300 BENCH_LIMIT=500 KT_LIMIT=200 bash tools/profile_round.sh r05 c2_iter300000 --iterations 300000 --steps 1 --warmup 0 &&
+echo "iter3e5 rc=0" >> $OUT/status.txt
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_provision.py > $OUT/r05_t_prov.txt 2>&1
