@@ -2222,6 +2222,12 @@ __device__ __forceinline__ unsigned job_tile_mask(const Ctx& C, JobLds& J, int t
   return m;
 }
 
+// job_tile_mask as a call, for the publisher's own and stolen tiles (rare while it has helpers): the collision tile's
+// registers and code stay out of edge_validity and of the workgroups that inline it (the scouts).
+__device__ __noinline__ unsigned job_tile_mask_out(const Ctx& C, JobLds& J, int t, int seq) {
+  return job_tile_mask(C, J, t, nullptr, seq);
+}
+
 // Work the leader does while a collision job's tiles are checked by the helpers (see edge_validity).
 enum { OV_NONE = 0, OV_NEAR_EXPAND = 1, OV_NN = 2, OV_NEAR_XN = 3 };
 __device__ void overlap_work(const Ctx& C, int ov, int t);
@@ -2316,7 +2322,7 @@ __device__ __forceinline__ void edge_validity_job(const Ctx& C, int E, int pslot
   // the leader's own tiles (in skip mode published too: the helpers' skip decisions read every earlier tile)
   const bool skip = uni(J.skip) != 0;
   for (int t = W - 1; t < nt; t += W) {
-    const unsigned m = job_tile_mask(C, J, t, nullptr, skip ? seq : -1);
+    const unsigned m = job_tile_mask_out(C, J, t, skip ? seq : -1);
     if (threadIdx.x == 0) {
       J.rmask[t] = m;
       J.rdone[t] = 1;
@@ -2369,7 +2375,7 @@ __device__ __forceinline__ void edge_validity_job(const Ctx& C, int E, int pslot
       __syncthreads();
       const int t = uni(J.steal);
       if (t >= 0) {
-        const unsigned m = job_tile_mask(C, J, t);
+        const unsigned m = job_tile_mask_out(C, J, t, -1);
         if (threadIdx.x == 0) { J.rmask[t] = m; J.rdone[t] = 1; }
       }
       if (threadIdx.x == 0) t_prog = wall_clock64();
@@ -3272,6 +3278,14 @@ __device__ void edge_costs_rec(int E) {
   __syncthreads();
 }
 
+// One local collision tile of edge_validity's path without helpers (a call: the tile's registers stay out of the
+// callers that inline edge_validity).
+__device__ __noinline__ void local_tile(const Ctx& C, int nc) {
+  const TileOrder order{g_L.tile_e, g_L.tile_i, g_L.eg_first, false};
+  collide_tile<PLAN_CT>((&g_rb), C.sc, (&g_mc), nc, g_L.u.tile.tq, g_L.S.self, g_L.S.map, g_L.u.tile.T, &order,
+                        &g_L.S.prof[P_TFK]);
+}
+
 // Validity of the batch's needed edges -> eg_first.  `ov` (OV_*, tree `ovt`): scan work whose inputs are final
 // before the check, done while a collision job runs (after the check without helpers); overlap_work records it
 // in g_L.spec for the caller.
@@ -3279,7 +3293,7 @@ __device__ void edge_costs_rec(int E) {
 // (SC_EXPAND: the expand edge, SC_CHOOSE: choose-parent candidates, SC_DONE: rewire candidates).  A needed edge
 // whose start and target equal a checked record edge bit for bit takes that edge's first collision (a pure
 // function of the two configurations) and is left out of the job.
-__device__ void edge_validity(const Ctx& C, int E, bool stop_first_valid, int pslot, int ov = 0, int ovt = 0,
+__device__ __forceinline__ void edge_validity(const Ctx& C, int E, bool stop_first_valid, int pslot, int ov = 0, int ovt = 0,
                               int sgrp = -1) {
   const int np1 = g_L.S.n_pts + 1;
   if (threadIdx.x == 0) g_L.count_slot = pslot + 4;
@@ -3363,9 +3377,7 @@ __device__ void edge_validity(const Ctx& C, int E, bool stop_first_valid, int ps
     }
     __syncthreads();
     PROF_BEGIN();
-    const TileOrder order{g_L.tile_e, g_L.tile_i, g_L.eg_first, false};
-    collide_tile<PLAN_CT>((&g_rb), C.sc, (&g_mc), nc, g_L.u.tile.tq, g_L.S.self, g_L.S.map, g_L.u.tile.T, &order,
-                     &g_L.S.prof[P_TFK]);
+    local_tile(C, nc);
     PROF_END(P_TILES);
     if (threadIdx.x == 0) {
       g_L.S.prof[pslot] += pclk() - _pt;
