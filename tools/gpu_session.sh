@@ -6,5 +6,5 @@ HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
 PMC_LIMIT=200 BENCH_LIMIT=300 KT_LIMIT=200 bash tools/profile_round.sh r05 c2 && echo "c2 rc=0" >> $OUT/status.txt &&
 PMC_LIMIT=300 BENCH_LIMIT=500 KT_LIMIT=200 bash tools/profile_round.sh r05 c2_iter300000 --iterations 300000 --steps 1 --warmup 0 &&
-echo "iter3e5 rc=0" >> $OUT/status.txt
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_provision.py > $OUT/r05_t_prov.txt 2>&1
+echo "iter3e5 rc=0" >> $OUT/status.txt &&
+timeout -k 10 300 python -u tools/ttff_seeds.py 1 $OUT/r05_ttff_final.json > $OUT/r05_ttff_final.txt 2>&1 && echo "ttff rc=0" >> $OUT/status.txt
