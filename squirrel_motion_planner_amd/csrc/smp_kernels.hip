@@ -633,7 +633,7 @@ __device__ int nearest_dist(const Ctx& C, int t, const double* q, int i0, int n,
 __device__ void near_set_dist(const Ctx& C, int t, const double* q, int excl, bool nn);
 // Block argmin of the nodes [i_begin, n) of tree t: the first strict minimum (d, id) of the distances, d = 10000
 // if none is below it.  All threads; result in (g_L.wd[0], g_L.wi[0]) via nearest_scan's return.
-__device__ int nearest_scan(const Ctx& C, int t, const double* q, int i_begin, double* d_out) {
+__device__ __forceinline__ int nearest_scan(const Ctx& C, int t, const double* q, int i_begin, double* d_out) {
   TR();
   if (scan_split(C, uni(g_L.S.n[t]) - i_begin)) {
     int id;
@@ -759,6 +759,63 @@ __device__ int nearest(const Ctx& C, int t, const double* q, bool spec = false) 
   }
   double bd;
   const int bi = nearest_scan(C, t, q, 0, &bd);
+  return bd < 10000.0 ? bi : 0;
+}
+
+// The leader's nearest with a record (iteration): the record's path inline -- at most 64 appended nodes scanned by one
+// wave from global memory (tail_scan) -- and a full scan only as a call, so that the scan's registers are saved only
+// when it runs (a call that saves ~50 VGPRs at 512 threads costs ~1.5 us).  Same answer as nearest(C, t, q, true).
+__device__ __noinline__ int nearest_scan_call(const Ctx& C, int t, const double* q, int i_begin, double* d_out) {
+  return nearest_scan(C, t, q, i_begin, d_out);
+}
+// nearest_scan over at most 64 nodes [i0, n) of tree t: wave 0, one node per lane, the (distance, id) minimum as
+// nearest_scan's (patch_scan's from global memory: after the first solution rewires may leave the LDS copy stale).
+// All threads; returns the id, *d_out = its distance (10000 if none is below it).
+__device__ int tail_scan(const Ctx& C, int t, const double* q, int i0, int n, double* d_out) {
+  if (threadIdx.x < 64) {
+    const int i = i0 + (int)threadIdx.x;
+    double best = 10000.0;
+    int bid = 0x7fffffff;
+    if (i < n) {
+      const double* x = C.Q.tr[t].q;
+      const int cap = g_L.S.cap;
+      double s = 0.0;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const double d = q[j] - x[(size_t)j * cap + i];
+        s += d * d;
+      }
+      const double dist = sqrt(s);
+      if (dist < best) { best = dist; bid = i; }
+    }
+    const unsigned long long key = (unsigned long long)__double_as_longlong(best);
+    const unsigned long long wk = __ockl_wfred_min_u64(key);
+    const int wi = __ockl_wfred_min_i32(key == wk ? bid : 0x7fffffff);
+    if (threadIdx.x == 0) { g_L.wk[0] = wk; g_L.wi[0] = wi; }
+  }
+  __syncthreads();
+  *d_out = __longlong_as_double((long long)g_L.wk[0]);
+  const int id = g_L.wi[0];
+  __syncthreads();
+  return id;
+}
+__device__ __forceinline__ int nearest_leader(const Ctx& C, int t, const double* q) {
+  const int n = uni(g_L.S.n[t]);
+  if (threadIdx.x == 0) g_L.S.nn_nodes += n;
+  if (spec_stage(C, SC_NN)) {
+    const ScoutNN& R = g_L.sr.nn;
+    if (uni(R.ok && R.t == t && R.X <= n && same8(q, R.q))) {
+      if (threadIdx.x == 0) g_L.S.sc_nn++;
+      if (uni(R.X < n)) {
+        double dp;
+        const int ip = uni(n - R.X <= 64) ? tail_scan(C, t, q, R.X, n, &dp) : nearest_scan_call(C, t, q, R.X, &dp);
+        if (dp < R.d) return ip;
+      }
+      return R.d < 10000.0 ? R.id : 0;
+    }
+  }
+  double bd;
+  const int bi = nearest_scan_call(C, t, q, 0, &bd);
   return bd < 10000.0 ? bi : 0;
 }
 
@@ -1689,6 +1746,95 @@ __device__ __forceinline__ void slice_near_inl(gcdptr tq, gcdptr tc, int cap, in
 
 // NN: also the nearest node of q over the whole tree (no exclusion; nearest()'s answer) in g_L.fnn_d / fnn_id -- connect's
 // two scans of x_new in tree_B in one pass (no scout record then: spec must be false).
+// near_set's record path: the scout's near set of the same configuration, merged with the near nodes appended since its
+// snapshot (at most 64), if the record applies (returns false otherwise).  No tree scan: light enough to inline.
+template <int K>
+__device__ __forceinline__ bool near_set_rec(const Ctx& C, int t, const double* q, int excl) {
+  if (!spec_stage(C, SC_NEAR)) return false;
+  const int n = uni(g_L.S.n[t]);
+  const gcdptr tq = uni_gptr(C.Q.tr[t].q), tc = uni_gptr(C.Q.tr[t].cost);
+  const int cap = uni(g_L.S.cap);
+  const double r = g_L.S.near_r;
+  const double r2 = r * r, r2lo = r2 * (1.0 - 1e-12), r2hi = r2 * (1.0 + 1e-12);
+  const int lane = lane_id();
+  // the scout's near set of the same configuration over the tree's first X nodes, with the near nodes appended since
+  // (at most 64: else the full scan below) merged in exactly: the costs of the first X nodes are those the record
+  // saw (no rewire of this tree in between), so the K lowest / highest (cost, id) entries of the whole set are among
+  // the record's low / high lists and the appended near nodes
+  const ScoutNear& R = g_L.sr.nr;
+  if (uni(R.ok && R.t == t && R.X <= n && n - R.X <= 64 && same8(q, R.q))) {
+    const int X = uni(R.X);
+    if (threadIdx.x < 64) {
+      const int i = X + lane;
+      bool nr = false;
+      unsigned long long key = 0;
+      if (i < n) {
+        double sb = 0.0;
+        for (int j = 0; j < NJ; ++j) {
+          const double d = q[j] - (tq + (size_t)j * cap)[(unsigned)i];
+          sb += d * d;
+        }
+        bool amb;
+        nr = near_radius(i != excl, sb, r, r2lo, r2hi, amb);
+        if (amb) nr = sqrt(sb) < r;
+        if (nr) key = (unsigned long long)__double_as_longlong(tc[(unsigned)i]);
+      }
+      const unsigned long long mk = __ballot(nr);
+      if (nr) {
+        const int s = __popcll(mk & ((1ull << lane) - 1));
+        g_L.nh.ck[0][s] = key;
+        g_L.nh.ci[0][s] = i;
+      }
+      if (lane == 0) g_L.nh.cnt[0] = __popcll(mk);
+    }
+    __syncthreads();
+    const int m = uni(g_L.nh.cnt[0]);
+    const int take = min(K, R.nk + m);
+    if (m == 0) {
+      if (threadIdx.x < K) {
+        g_L.lo_i[threadIdx.x] = R.lo_i[threadIdx.x]; g_L.lo_c[threadIdx.x] = R.lo_c[threadIdx.x];
+        g_L.hi_i[threadIdx.x] = R.hi_i[threadIdx.x]; g_L.hi_c[threadIdx.x] = R.hi_c[threadIdx.x];
+      }
+    } else if (threadIdx.x < 128) {
+      // wave 0 ranks the low side (the record's low list + the appended), wave 1 the high side; entries c = lane,
+      // lane + 64 of N <= K + 64, each ranked against all N as near_set's merge does
+      const int e = threadIdx.x >> 6;
+      const int nl = e == 0 ? R.n_lo : R.n_hi, N = nl + m;
+      for (int c = lane; c < N; c += 64) {
+        unsigned long long ck;
+        int ci;
+        if (c < nl) {
+          ck = (unsigned long long)__double_as_longlong(e == 0 ? R.lo_c[c] : R.hi_c[c]);
+          ci = e == 0 ? R.lo_i[c] : R.hi_i[c];
+        } else {
+          ck = g_L.nh.ck[0][c - nl];
+          ci = g_L.nh.ci[0][c - nl];
+        }
+        int rank = 0;
+        for (int o = 0; o < N; ++o) {
+          const unsigned long long ok = o < nl ? (unsigned long long)__double_as_longlong(e == 0 ? R.lo_c[o] : R.hi_c[o])
+                                               : g_L.nh.ck[0][o - nl];
+          const int oi = o < nl ? (e == 0 ? R.lo_i[o] : R.hi_i[o]) : g_L.nh.ci[0][o - nl];
+          rank += e == 0 ? ki_less(ok, oi, ck, ci) : ki_less(ck, ci, ok, oi);
+        }
+        if (rank < take) {
+          if (e == 0) { g_L.lo_c[rank] = __longlong_as_double((long long)ck); g_L.lo_i[rank] = ci; }
+          else { g_L.hi_c[take - 1 - rank] = __longlong_as_double((long long)ck); g_L.hi_i[take - 1 - rank] = ci; }
+        }
+      }
+    }
+    if (threadIdx.x == 0) {
+      g_L.nk = R.nk + m; g_L.n_lo = m == 0 ? R.n_lo : take; g_L.n_hi = m == 0 ? R.n_hi : take;
+      g_L.S.near_nodes += n;
+      g_L.S.sc_near++;
+    }
+    __syncthreads();
+    TR();
+    return true;
+  }
+  return false;
+}
+
 template <int K, bool NN = false>
 __device__ void near_set(const Ctx& C, int t, const double* q, int excl, bool spec = false) {
 #ifdef SMP_NEAR_PROF
@@ -1706,83 +1852,7 @@ __device__ void near_set(const Ctx& C, int t, const double* q, int excl, bool sp
   const double r2 = r * r, r2lo = r2 * (1.0 - 1e-12), r2hi = r2 * (1.0 + 1e-12);
   const int lane = lane_id(), wave = wave_id();
   TR();
-  if (!NN && spec && spec_stage(C, SC_NEAR)) {
-    // the scout's near set of the same configuration over the tree's first X nodes, with the near nodes appended since
-    // (at most 64: else the full scan below) merged in exactly: the costs of the first X nodes are those the record
-    // saw (no rewire of this tree in between), so the K lowest / highest (cost, id) entries of the whole set are among
-    // the record's low / high lists and the appended near nodes
-    const ScoutNear& R = g_L.sr.nr;
-    if (uni(R.ok && R.t == t && R.X <= n && n - R.X <= 64 && same8(q, R.q))) {
-      const int X = uni(R.X);
-      if (threadIdx.x < 64) {
-        const int i = X + lane;
-        bool nr = false;
-        unsigned long long key = 0;
-        if (i < n) {
-          double sb = 0.0;
-          for (int j = 0; j < NJ; ++j) {
-            const double d = q[j] - (tq + (size_t)j * cap)[(unsigned)i];
-            sb += d * d;
-          }
-          bool amb;
-          nr = near_radius(i != excl, sb, r, r2lo, r2hi, amb);
-          if (amb) nr = sqrt(sb) < r;
-          if (nr) key = (unsigned long long)__double_as_longlong(tc[(unsigned)i]);
-        }
-        const unsigned long long mk = __ballot(nr);
-        if (nr) {
-          const int s = __popcll(mk & ((1ull << lane) - 1));
-          g_L.nh.ck[0][s] = key;
-          g_L.nh.ci[0][s] = i;
-        }
-        if (lane == 0) g_L.nh.cnt[0] = __popcll(mk);
-      }
-      __syncthreads();
-      const int m = uni(g_L.nh.cnt[0]);
-      const int take = min(K, R.nk + m);
-      if (m == 0) {
-        if (threadIdx.x < K) {
-          g_L.lo_i[threadIdx.x] = R.lo_i[threadIdx.x]; g_L.lo_c[threadIdx.x] = R.lo_c[threadIdx.x];
-          g_L.hi_i[threadIdx.x] = R.hi_i[threadIdx.x]; g_L.hi_c[threadIdx.x] = R.hi_c[threadIdx.x];
-        }
-      } else if (threadIdx.x < 128) {
-        // wave 0 ranks the low side (the record's low list + the appended), wave 1 the high side; entries c = lane,
-        // lane + 64 of N <= K + 64, each ranked against all N as near_set's merge does
-        const int e = threadIdx.x >> 6;
-        const int nl = e == 0 ? R.n_lo : R.n_hi, N = nl + m;
-        for (int c = lane; c < N; c += 64) {
-          unsigned long long ck;
-          int ci;
-          if (c < nl) {
-            ck = (unsigned long long)__double_as_longlong(e == 0 ? R.lo_c[c] : R.hi_c[c]);
-            ci = e == 0 ? R.lo_i[c] : R.hi_i[c];
-          } else {
-            ck = g_L.nh.ck[0][c - nl];
-            ci = g_L.nh.ci[0][c - nl];
-          }
-          int rank = 0;
-          for (int o = 0; o < N; ++o) {
-            const unsigned long long ok = o < nl ? (unsigned long long)__double_as_longlong(e == 0 ? R.lo_c[o] : R.hi_c[o])
-                                                 : g_L.nh.ck[0][o - nl];
-            const int oi = o < nl ? (e == 0 ? R.lo_i[o] : R.hi_i[o]) : g_L.nh.ci[0][o - nl];
-            rank += e == 0 ? ki_less(ok, oi, ck, ci) : ki_less(ck, ci, ok, oi);
-          }
-          if (rank < take) {
-            if (e == 0) { g_L.lo_c[rank] = __longlong_as_double((long long)ck); g_L.lo_i[rank] = ci; }
-            else { g_L.hi_c[take - 1 - rank] = __longlong_as_double((long long)ck); g_L.hi_i[take - 1 - rank] = ci; }
-          }
-        }
-      }
-      if (threadIdx.x == 0) {
-        g_L.nk = R.nk + m; g_L.n_lo = m == 0 ? R.n_lo : take; g_L.n_hi = m == 0 ? R.n_hi : take;
-        g_L.S.near_nodes += n;
-        g_L.S.sc_near++;
-      }
-      __syncthreads();
-      TR();
-      return;
-    }
-  }
+  if (!NN && spec && near_set_rec<K>(C, t, q, excl)) return;
   if (K == SCAN_K && scan_split(C, n)) {
     [[clang::always_inline]] near_set_dist(C, t, q, excl, NN);
     TR();
@@ -2054,6 +2124,12 @@ __device__ void near_set(const Ctx& C, int t, const double* q, int excl, bool sp
   __syncthreads();
   if (NN) fnn_reduce(nb, nbi);
   TR();
+}
+
+// near_set without a record, as a call (the leader: the record's path, near_set_rec, runs inline before it).
+template <int K, bool NN>
+__device__ __noinline__ void near_set_scan(const Ctx& C, int t, const double* q, int excl) {
+  [[clang::always_inline]] near_set<K, NN>(C, t, q, excl, false);
 }
 
 // --------------------------------------------------------------------------------------- edges
@@ -3813,7 +3889,7 @@ __device__ __forceinline__ bool pre_read_round(const ScoutBoard* sb, int par, un
   return (unsigned)(v >> 32) == tag;
 }
 
-__device__ void sample_read(const Ctx& C) {
+__device__ __forceinline__ void sample_read(const Ctx& C) {
   TR();
   QState& S = g_L.S;
   const uint32_t it = (uint32_t)S.iter;
@@ -4586,7 +4662,7 @@ __device__ void pre_verify_connect(const Ctx& C, int B, int cid) {
 }
 #endif
 
-__device__ bool pre_commit(const Ctx& C, int A, int B) {
+__device__ __forceinline__ bool pre_commit(const Ctx& C, int A, int B) {
   if (!uni(g_L.sp_on) || !pre_wait(C)) { PRE_COUNT(1); return false; }
   const PreRec& P = g_L.prer;
   const int nA = uni(g_L.S.n[A]);
@@ -4711,7 +4787,7 @@ __device__ __forceinline__ void iteration(const Ctx& C) {
   if (C.Q.pre_commit && C.Q.nscouts > 0 && !uni(g_L.S.have_sol) && pre_commit(C, A, B)) {
     PHASE(P_CONNECT);
   } else {
-  int nid = nearest(C, A, g_L.xr, true);
+  int nid = nearest_leader(C, A, g_L.xr);
   TR();
   PHASE(P_NN);
   if (threadIdx.x == 0) {
@@ -4770,7 +4846,8 @@ __device__ __forceinline__ void iteration(const Ctx& C) {
   if (opt) {
     // x_new is the expand edge's end exactly when the edge is valid: then its near set was computed during the job
     TR();
-    if (!(uni(g_L.ext_nn) && take_spec(OV_NEAR_EXPAND))) near_set<20>(C, A, g_L.xn.q, g_L.xn.id, true);
+    if (!(uni(g_L.ext_nn) && take_spec(OV_NEAR_EXPAND)) && !near_set_rec<20>(C, A, g_L.xn.q, g_L.xn.id))
+      near_set_scan<20, false>(C, A, g_L.xn.q, g_L.xn.id);
     TR();
     PHASE(P_NEAR);
     choose_parent(C, A);
