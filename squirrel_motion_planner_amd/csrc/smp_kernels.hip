@@ -631,6 +631,11 @@ __device__ __forceinline__ bool scan_split(const Ctx& C, int nodes) {
 }
 __device__ int nearest_dist(const Ctx& C, int t, const double* q, int i0, int n, double* d_out);
 __device__ void near_set_dist(const Ctx& C, int t, const double* q, int excl, bool nn);
+// A local scan of at least this many nodes reads the tree's fp32 copy (the distributed slices' prefilter, exact).
+constexpr int LOCAL_F32_MIN = 2048;
+struct ScanLds;
+__device__ __forceinline__ void slice_nn_body32(gcdptr tq, const float* tqf, int cap, int i0, int i1, const double* q,
+                                                ScanLds& X);
 // Block argmin of the nodes [i_begin, n) of tree t: the first strict minimum (d, id) of the distances, d = 10000
 // if none is below it.  All threads; result in (g_L.wd[0], g_L.wi[0]) via nearest_scan's return.
 __device__ __forceinline__ int nearest_scan(const Ctx& C, int t, const double* q, int i_begin, double* d_out) {
@@ -642,6 +647,13 @@ __device__ __forceinline__ int nearest_scan(const Ctx& C, int t, const double* q
   }
   const gcdptr tq = uni_gptr(C.Q.tr[t].q);
   const int n = uni(g_L.S.n[t]), cap = uni(g_L.S.cap);
+  if (n - i_begin >= LOCAL_F32_MIN) {
+    slice_nn_body32(tq, C.Q.tr[t].qf, cap, i_begin, n, q, g_L.sc.s);
+    *d_out = __longlong_as_double((long long)g_L.sc.s.wk[0]);
+    const int id = g_L.sc.s.wi[0];
+    __syncthreads();
+    return id;
+  }
   gcdptr tqc[NJ];
   tree_cols(tq, cap, tqc);
   double qq[NJ];
@@ -1855,6 +1867,24 @@ __device__ void near_set(const Ctx& C, int t, const double* q, int excl, bool sp
   if (!NN && spec && near_set_rec<K>(C, t, q, excl)) return;
   if (K == SCAN_K && scan_split(C, n)) {
     [[clang::always_inline]] near_set_dist(C, t, q, excl, NN);
+    TR();
+    return;
+  }
+  if (K == SCAN_K && n >= LOCAL_F32_MIN) {
+    // the slice form over the whole tree with the fp32 prefilter (exact): its lists into near_set's outputs
+    ScanLds& X = g_L.sc.s;
+    slice_near_inl<NN, true>(tq, tc, cap, 0, n, q, excl, r, X, C.Q.tr[t].qf);
+    const int take = X.take;
+    if (threadIdx.x < take) {
+      const int e = threadIdx.x;
+      g_L.lo_c[e] = __longlong_as_double((long long)X.lk[e]); g_L.lo_i[e] = X.li[e];
+      g_L.hi_c[take - 1 - e] = __longlong_as_double((long long)X.hk[e]); g_L.hi_i[take - 1 - e] = X.hi[e];
+    }
+    if (threadIdx.x == 0) {
+      g_L.nk = X.cnt; g_L.n_lo = take; g_L.n_hi = take; g_L.S.near_nodes += n;
+      if (NN) { g_L.fnn_d = __longlong_as_double((long long)X.wk[0]); g_L.fnn_id = X.wi[0]; }
+    }
+    __syncthreads();
     TR();
     return;
   }
@@ -6007,6 +6037,7 @@ __device__ __forceinline__ void near_probe_body(const double* tqv, const double*
   C.Q.jb = nullptr;  // single workgroup: no helpers, scans stay local
   C.Q.scan_min = 0;
   C.Q.tr[0].q = const_cast<double*>(tqv);
+  C.Q.tr[0].qf = const_cast<float*>(tqf);
   C.Q.tr[0].cost = const_cast<double*>(tcost);
   if (threadIdx.x == 0) {
     g_L.in_job = 0;

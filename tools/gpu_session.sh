@@ -4,6 +4,7 @@ mkdir -p $OUT
 ( while true; do date +%s >> $OUT/heartbeat.txt; sleep 30; done ) &
 HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
-timeout -k 10 200 python -u tools/perf_probe.py 100 4000 100000 > $OUT/r05_perf_ld.txt 2>&1 &&
-timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests > $OUT/r05_t_gpu_ld.txt 2>&1 &&
-timeout -k 10 300 python -u tools/ttff_seeds.py 1 $OUT/r05_ttff_ld.json > $OUT/r05_ttff_ld.txt 2>&1
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_tree_scans.py > $OUT/r05_t_scans_lf.txt 2>&1 &&
+timeout -k 10 120 python -u tools/slice_probe.py 2048 4096 16384 > $OUT/r05_slice_probe_lf.txt 2>&1 &&
+timeout -k 10 200 python -u tools/perf_probe.py 100 4000 100000 > $OUT/r05_perf_lf.txt 2>&1 &&
+timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests > $OUT/r05_t_gpu_lf.txt 2>&1
