@@ -4,7 +4,5 @@ mkdir -p $OUT
 ( while true; do date +%s >> $OUT/heartbeat.txt; sleep 30; done ) &
 HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
-PMC_LIMIT=200 BENCH_LIMIT=300 KT_LIMIT=200 bash tools/profile_round.sh r05 c2 && echo "c2 rc=0" >> $OUT/status.txt &&
-PMC_LIMIT=200 BENCH_LIMIT=300 KT_LIMIT=200 bash tools/profile_round.sh r05 c3 --workload c3 --queries-per-gpu 8 && echo "c3 rc=0" >> $OUT/status.txt &&
-PMC_LIMIT=200 BENCH_LIMIT=300 KT_LIMIT=200 bash tools/profile_round.sh r05 c5 --workload c5 --queries-per-gpu 8 && echo "c5 rc=0" >> $OUT/status.txt &&
-timeout -k 10 300 python -u tools/ttff_seeds.py 1 $OUT/r05_ttff_final.json > $OUT/r05_ttff_final.txt 2>&1 && echo "ttff rc=0" >> $OUT/status.txt
+PMC_LIMIT=300 BENCH_LIMIT=500 KT_LIMIT=200 bash tools/profile_round.sh r05 c2_iter300000 --iterations 300000 --steps 1 --warmup 0 && echo "3e5 rc=0" >> $OUT/status.txt &&
+SKIP_PMC=1 SKIP_BENCH=1 KT_LIMIT=400 bash tools/profile_round.sh r05 c2_iter1000000 --iterations 1000000 --steps 1 --warmup 0 && echo "1e6kt rc=0" >> $OUT/status.txt
