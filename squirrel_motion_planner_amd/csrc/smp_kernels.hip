@@ -3891,7 +3891,9 @@ __device__ void sample_version(const Ctx& C) {
     g_L.smp_pub = 1;
   }
 }
-__device__ void sample_publish(const Ctx& C) {
+// before_read: published ahead of this iteration's own sample read (the first launch, before the pre-loop connection):
+// the iteration is announced as the one before, so the run-ahead sampler starts with this iteration's sample.
+__device__ void sample_publish(const Ctx& C, bool before_read = false) {
   if (!C.Q.sampler) return;
   const QState& S = g_L.S;
   JobBoard* jb = C.Q.jb;
@@ -3901,7 +3903,7 @@ __device__ void sample_publish(const Ctx& C) {
     drain();  // payload before the version
     st_agent(&jb->s_ver, g_L.smp_ver);
   }
-  st_agent(reinterpret_cast<unsigned long long*>(&jb->s_iter), (unsigned long long)S.iter);
+  st_agent(reinterpret_cast<unsigned long long*>(&jb->s_iter), (unsigned long long)(S.iter - (before_read ? 1 : 0)));
 }
 
 // Second part: the sample from the ring (one round of tagged granules, wave 0) -- and, in the same round (wave 1),
@@ -5926,7 +5928,7 @@ __global__ void __launch_bounds__(BLOCK) plan_kernel(const RobotDev* __restrict_
     __syncthreads();
     if (threadIdx.x == 0) {
       sample_version(C);
-      sample_publish(C);
+      sample_publish(C, true);
       bool fenced = false;
       const long long j = g_L.S.iter;
       for (int ahead = 0; ahead < C.Q.nscouts; ++ahead)

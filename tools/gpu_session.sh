@@ -4,5 +4,7 @@ mkdir -p $OUT
 ( while true; do date +%s >> $OUT/heartbeat.txt; sleep 30; done ) &
 HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
-PMC_LIMIT=300 BENCH_LIMIT=500 KT_LIMIT=200 bash tools/profile_round.sh r05 c2_iter300000 --iterations 300000 --steps 1 --warmup 0 && echo "3e5 rc=0" >> $OUT/status.txt &&
-SKIP_PMC=1 SKIP_BENCH=1 KT_LIMIT=400 bash tools/profile_round.sh r05 c2_iter1000000 --iterations 1000000 --steps 1 --warmup 0 && echo "1e6kt rc=0" >> $OUT/status.txt
+timeout -k 10 120 python -u tools/startup_probe.py > $OUT/r05_startup4.txt 2>&1 &&
+timeout -k 10 200 python -u tools/perf_probe.py 100 > $OUT/r05_perf_s0.txt 2>&1 &&
+timeout -k 10 300 python -u tools/ttff_seeds.py 1 $OUT/r05_ttff_s0.json > $OUT/r05_ttff_s0.txt 2>&1 &&
+timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests > $OUT/r05_t_gpu_s0.txt 2>&1
