@@ -5885,6 +5885,7 @@ __global__ void __launch_bounds__(BLOCK) plan_kernel(const RobotDev* __restrict_
 #endif
   }
   __syncthreads();
+  TR();
   if (uni(g_L.S.status == 0 && g_L.S.phase == 0)) {
     // first launch: init_planner's validity of start and goal (birrt_star.cpp:350-362), one collision tile
     if (threadIdx.x < 2 * NJ) {
@@ -5898,6 +5899,7 @@ __global__ void __launch_bounds__(BLOCK) plan_kernel(const RobotDev* __restrict_
       g_L.S.phase = 2;
     }
     __syncthreads();
+    TR();
   }
   if (uni(g_L.S.status == 0 && g_L.S.phase == 0) && threadIdx.x < 2) {
     // first launch: the two roots (init_planner, birrt_star.cpp:386-443) from the query's start / goal
