@@ -981,6 +981,7 @@ static QueryDev make_qdev(QueryBuffers& b, size_t cap, long long rows) {
   d.nscouts = 0;
   d.pre_delay = 0;
   d.pre_commit = 0;
+  d.pre_refresh = 0;
   for (int s = 0; s < MAX_SCOUTS; ++s) {
     d.scbs[s] = nullptr; d.sjbs[s] = nullptr; d.svias[s] = nullptr; d.sworkers_s[s] = 1;
   }
@@ -1113,6 +1114,11 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
   if (const char* e = std::getenv("SMP_PRE_DELAY")) pre_delay = std::atoi(e);
   int early_ask = 0;  // SMP_EARLY_ASK=1: after the first solution, iteration k + 2 is asked for before k's rewires (DESIGN.md "Early asks")
   if (const char* e = std::getenv("SMP_EARLY_ASK")) early_ask = std::atoi(e);
+  // SMP_PRE_REFRESH: a pre-solution scout rechecks its nearest on the leader's newer sizes after its expand job (bit 0)
+  // and / or before it publishes (bit 1), starting the pass over (at most twice) when a newer node is nearer
+  // (DESIGN.md "Pre-solution refresh"; bit 0 alone measured best)
+  int pre_refresh = 1;
+  if (const char* e = std::getenv("SMP_PRE_REFRESH")) pre_refresh = std::atoi(e);
   int conn_check = 0;  // SMP_CONN_CHECK=1: connect's edges checked by the scouts with their SC_CONN scans (experiments)
   if (const char* e = std::getenv("SMP_CONN_CHECK")) conn_check = std::atoi(e);
   int pre_commit = 1;  // SMP_PRE_COMMIT=0: every iteration runs the full path (experiments)
@@ -1213,6 +1219,7 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
       qdev[i].pre_delay = pre_delay;
       qdev[i].pre_commit = pre_commit;
       qdev[i].early_ask = early_ask;
+      qdev[i].pre_refresh = pre_refresh;
       qdev[i].conn_check = conn_check;
       qdev[i].sampler_jb = p->qb[i].jb.p;
       for (int s = 0; s < ns; ++s) {

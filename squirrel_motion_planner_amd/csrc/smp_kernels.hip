@@ -5203,6 +5203,47 @@ __device__ void scout_pre_publish(const Ctx& C, int par, unsigned tag, bool vali
   __syncthreads();
 }
 
+// Before the first solution the leader appends nodes while a scout pass runs; one of them nearer to the sample than
+// the record's nearest node would make the leader redo the iteration.  True (all threads) when the leader's latest
+// drained size of tree t (g_L.cnt, with tree B's in g_L.found) holds such a node: the pass then starts over on those
+// sizes, with the record's fields and the snapshot sizes reset (DESIGN.md "Pre-solution refresh").
+__device__ __forceinline__ bool pre_newer(const Ctx& C, int t, int X, int XB) {
+  QState& S = g_L.S;
+  ScoutRec& R = g_L.sr;
+  if (threadIdx.x == 0) {
+    const unsigned long long sz = ld_agent(&C.Q.scb->cur_sz);
+    const int n0 = (int)((sz >> 20) & 0xfffff), n1 = (int)(sz & 0xfffff);
+    g_L.cnt = max(X, t == 0 ? n0 : n1);
+    g_L.found = max(XB, t == 0 ? n1 : n0);
+  }
+  __syncthreads();
+  const int Xn = uni(g_L.cnt), XBn = uni(g_L.found);
+  __syncthreads();
+  if (Xn <= X) return false;
+  // the nodes [X, Xn) were stored by the leader after this CU may have cached their lines (a line holds 16 nodes of a
+  // column): drop stale copies before any load of them, as before a pass (scout_main)
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  drain();
+  __syncthreads();
+  bool again = Xn - X > 64;
+  if (!again) {
+    double dp;
+    tail_scan(C, t, g_L.xr, X, Xn, &dp);
+    again = dp < R.nn.d;  // (both uniform: LDS values read after tail_scan's barriers)
+  }
+  if (!again) return false;
+  if (threadIdx.x == 0) {
+    S.n[t] = Xn;
+    S.n[1 - t] = XBn;
+    S.prof[26]++;
+    R.cn.ok = 0;
+    R.pre.ok = 0;
+    R.nn.ok = 0; R.ex.ok = 0; R.nr.ok = 0; R.n_choose = 0; R.n_rewire = 0; R.cc.ok = 0; R.cc.nfirst = -1;
+  }
+  __syncthreads();
+  return true;
+}
+
 // The scout's pass for iteration `it` of the leader, which expands tree t from a snapshot of its first X nodes:
 // the leader's steps up to its rewire collision job (iteration / choose_parent / rewire, same functions on the
 // scout's own LDS, job board, helpers and via-node scratch), recording the results the leader keys on; nothing is
@@ -5267,6 +5308,8 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
     sc_end(C, par, tag, opt);
     return;
   }
+  int rp = 0;  // passes redone on newer tree sizes (pre_refresh)
+redo:
   // nearest + expand edge (iteration())
   if (opt && sc_moved(C)) return;
   int nid;
@@ -5341,6 +5384,12 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
     g_L.ext_bp = 0;
   }
   __syncthreads();
+  if (!opt && (C.Q.pre_refresh & 1) && rp < 2 && pre_newer(C, t, X, XB)) {
+    X = uni(g_L.cnt);
+    XB = uni(g_L.found);
+    rp++;
+    goto redo;
+  }
   if (opt) {
     sc_copy_out(sb, par, &R.e[0], sizeof(ScoutEdge));
     sc_copy_out(sb, par, &R.ex, sizeof(ScoutExpand));
@@ -5378,6 +5427,12 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
     }
     __syncthreads();
     scout_pre_connect(C, par, tb);
+  }
+  if (!opt && (C.Q.pre_refresh & 2) && rp < 2 && pre_newer(C, t, X, XB)) {
+    X = uni(g_L.cnt);
+    XB = uni(g_L.found);
+    rp++;
+    goto redo;
   }
   if (!opt) {
     scout_pre_publish(C, par, tag, true);

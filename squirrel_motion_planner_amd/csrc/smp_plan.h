@@ -303,6 +303,7 @@ struct QueryDev {
   int pre_commit;              // 1: pre-solution iterations are committed from complete scout records
   int early_ask;               // 1: after the first solution, iteration k + 2 is asked for as soon as its scout is free
   int conn_check;              // 1: the scout's SC_CONN record carries the validity of connect's edges (scout_connect)
+  int pre_refresh;             // bits 0/1: a pre-solution scout restarts its pass when a newer node is nearer
   ScoutBoard* scbs[MAX_SCOUTS];
   JobBoard* sjbs[MAX_SCOUTS];
   ViaNode* svias[MAX_SCOUTS];

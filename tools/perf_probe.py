@@ -48,6 +48,8 @@ for iters in [int(v) for v in (sys.argv[1:] or ["2000", "10000", "50000"])]:
         # appended since the record's snapshot is nearer / connect redone in full
         print("   pre_commit outcomes: committed %d, no record %d, newer nearest %d, connect redone %d" % tuple(
             int(v) for v in raw[28:32]), flush=True)
+        if sp[26] > 0:  # SMP_PRE_REFRESH=1: scout passes started over on newer tree sizes
+            print("   scout passes redone on newer sizes: %d" % int(sp[26]), flush=True)
     nj = max(raw[15] * 1e8, 1)
     print("   jobs %d: publish %.1f us, own %.1f us, wait %.1f us per job" % (
         raw[15] * 1e8, raw[12] * 1e6 / nj, raw[13] * 1e6 / nj, raw[14] * 1e6 / nj), flush=True)
