@@ -3284,24 +3284,33 @@ __device__ void scout_slots() {
               !(g_L.asked_pre[j & (SCOUT_SLOTS - 1)] && S.have_sol && j >= S.first_iter + 3);
   g_L.sp_stage = -1;
 }
+// Wave 0, before scout_asks: the leader's iteration for every scout (and, before the first solution, the tree sizes
+// for the late snapshots of the scouts on this XCD) -- lane s stores scout s's, so the boards' stores issue together
+// instead of one dependent chain per scout in thread 0.
+__device__ __forceinline__ void scout_cur_lanes(const Ctx& C) {
+  const QState& S = g_L.S;
+  const long long j = S.iter;
+  const int s = (int)lane_id();
+  if (s >= C.Q.nscouts) return;
+  const bool pre = !(S.tree_opt && S.have_sol);
+  const int nsc = pre ? C.Q.nscouts : min(C.Q.nscouts, 2);  // scouts 2 and up retire after the first solution
+  ScoutBoard* sb = C.Q.scbs[s];
+  // from first_iter + 3 on no record asked before the first solution is looked up (scout_slots): scouts 2 and up
+  // stop (with their helpers) instead of polling beside the leader for the rest of the launch
+  if (!pre && j == S.first_iter + 3 && s >= 2) st_agent(&sb->stop, 1);
+  if (s >= nsc) return;
+  st_agent(&sb->cur, (unsigned long long)j);
+  // only to a scout on this XCD: the sizes hand over nodes stored without an agent release (a scout on another XCD
+  // takes its request's sizes, whose nodes scout_ask released)
+  if (pre && S.n[0] < (1 << 20) && S.n[1] < (1 << 20) && g_L.sc_same[s] == 1)
+    st_agent(&sb->cur_sz, ((unsigned long long)(j & 0xffffff) << 40) | ((unsigned long long)S.n[0] << 20) |
+                              (unsigned long long)S.n[1]);
+}
+// Thread 0: the requests for the coming iterations not yet asked for.
 __device__ void scout_asks(const Ctx& C, int t) {
   const QState& S = g_L.S;
   const long long j = S.iter;
   const bool pre = !(S.tree_opt && S.have_sol);
-  const bool sz = pre && S.n[0] < (1 << 20) && S.n[1] < (1 << 20);
-  const unsigned long long csz = ((unsigned long long)(j & 0xffffff) << 40) | ((unsigned long long)S.n[0] << 20) |
-                                 (unsigned long long)S.n[1];
-  const int nsc = pre ? C.Q.nscouts : min(C.Q.nscouts, 2);  // scouts 2 and up retire after the first solution
-  // from first_iter + 3 on no record asked before the first solution is looked up (scout_slots): scouts 2 and up
-  // stop (with their helpers) instead of polling beside the leader for the rest of the launch
-  if (!pre && j == S.first_iter + 3)
-    for (int s = 2; s < C.Q.nscouts; ++s) st_agent(&C.Q.scbs[s]->stop, 1);
-  for (int s = 0; s < nsc; ++s) {
-    st_agent(&C.Q.scbs[s]->cur, (unsigned long long)j);
-    // only to a scout on this XCD: the sizes hand over nodes stored without an agent release (a scout on another XCD
-    // takes its request's sizes, whose nodes scout_ask released)
-    if (sz && g_L.sc_same[s] == 1) st_agent(&C.Q.scbs[s]->cur_sz, csz);
-  }
   bool fenced = false;
   // before the first solution every scout has a request out (the trees only grow: records stay exact up to the
   // appended nodes); iteration j + a expands tree t for odd a, the other one for even a
@@ -3966,16 +3975,26 @@ __device__ __forceinline__ void sample_read(const Ctx& C) {
   // together; then thread 0's stores of the iteration
   drain();
   const bool stale_granule = __syncthreads_or(!pre_ok) != 0;  // also the round's barrier
+  TR();
   const bool prer_ok = prerec && !stale_granule;
-  if (threadIdx.x == 0) {
-    g_L.prer_ok = prer_ok;
-    if (prer_ok) g_L.sc_seen |= 1u << (sw - 1);
-    sample_publish(C);
+  if (threadIdx.x < 64) {
+    if (threadIdx.x == 0) {
+      g_L.prer_ok = prer_ok;
+      if (prer_ok) g_L.sc_seen |= 1u << (sw - 1);
+      sample_publish(C);
+    }
+    TR();
     if (C.Q.nscouts > 0) {
-      scout_asks(C, 1 - g_L.S.A);
-      scout_ask_early(C, g_L.sp_go[0]);  // record j's stage as this round found it
+      scout_cur_lanes(C);
+      TR();
+      if (threadIdx.x == 0) {
+        scout_asks(C, 1 - g_L.S.A);
+        TR();
+        scout_ask_early(C, g_L.sp_go[0]);  // record j's stage as this round found it
+      }
     }
   }
+  TR();
   const int st = uni(g_L.sp_go[0]);
   __syncthreads();
   if (pre && !prerec && st >= 0) spec_copy(sb, par, -1, st);
