@@ -3202,12 +3202,14 @@ __device__ void spec_copy(const ScoutBoard* sb, int par, int have, int st) {
 __device__ void scout_ask(const Ctx& C, long long k, int tree, bool pre, bool& fenced, int x_snap = -1) {
   const QState& S = g_L.S;
   const int ns = C.Q.nscouts;
-  int which = 1 + (int)(pre ? k % ns : (ns >= 2 ? (k & 1) : 0));
+  // (32-bit remainder: a 64-bit one is a long software division on the leader's path; which scout takes a record only
+  // has to be the one asked, so the wrap at 2^32 iterations is harmless)
+  int which = 1 + (int)(pre ? (unsigned)k % (unsigned)ns : (ns >= 2 ? (unsigned)(k & 1) : 0u));
   if ((g_L.sc_dead >> (which - 1)) & 1u) {  // a scout that never delivered: the next live one before the first
     if (!pre) return;                         // solution, none after it (the iteration takes the full path)
     int w = -1;
     for (int d = 1; d < ns && w < 0; ++d) {
-      const int c = (int)((k + d) % ns);
+      const int c = (int)((unsigned)(k + d) % (unsigned)ns);
       if (!((g_L.sc_dead >> c) & 1u)) w = c;
     }
     if (w < 0) return;
@@ -3977,6 +3979,9 @@ __device__ __forceinline__ void sample_read(const Ctx& C) {
   const bool stale_granule = __syncthreads_or(!pre_ok) != 0;  // also the round's barrier
   TR();
   const bool prer_ok = prerec && !stale_granule;
+  // the iteration's stores, over two waves: wave 0 the sampler's and the scout boards' iteration (a lane per scout),
+  // thread 64 the new requests (only LDS fields of its own; the last iteration's tree stores a request hands over
+  // were drained by every wave above)
   if (threadIdx.x < 64) {
     if (threadIdx.x == 0) {
       g_L.prer_ok = prer_ok;
@@ -3984,15 +3989,11 @@ __device__ __forceinline__ void sample_read(const Ctx& C) {
       sample_publish(C);
     }
     TR();
-    if (C.Q.nscouts > 0) {
-      scout_cur_lanes(C);
-      TR();
-      if (threadIdx.x == 0) {
-        scout_asks(C, 1 - g_L.S.A);
-        TR();
-        scout_ask_early(C, g_L.sp_go[0]);  // record j's stage as this round found it
-      }
-    }
+    if (C.Q.nscouts > 0) scout_cur_lanes(C);
+    TR();
+  } else if (threadIdx.x == 64 && C.Q.nscouts > 0) {
+    scout_asks(C, 1 - g_L.S.A);
+    scout_ask_early(C, g_L.sp_go[0]);  // record j's stage as this round found it
   }
   TR();
   const int st = uni(g_L.sp_go[0]);
@@ -4825,10 +4826,9 @@ __device__ __forceinline__ void iteration(const Ctx& C) {
   if (threadIdx.x == 0) g_L.conn_rec = 0;
   TR();
 #define PHASE(k) if (threadIdx.x == 0) { _t1 = pclk(); g_L.S.prof[k] += _t1 - _t0; _t0 = _t1; }
-  if (threadIdx.x == 0) {
-    sample_version(C);
-    if (C.Q.nscouts > 0) scout_slots();
-  }
+  // two waves in parallel (disjoint LDS fields; each a serial chain of LDS reads)
+  if (threadIdx.x == 0) sample_version(C);
+  else if (threadIdx.x == 64 && C.Q.nscouts > 0) scout_slots();
   __syncthreads();
   TR();
   sample_read(C);
