@@ -4842,13 +4842,24 @@ __device__ __forceinline__ void iteration(const Ctx& C) {
   TR();
   PHASE(P_NN);
   if (threadIdx.x == 0) {
-    load_node(C, A, nid, &g_L.nn);
     // expandTree single step (birrt_star.cpp:2224-2256).  If the scout's record of this iteration already holds
     // its expand stage for the same sample, tree and nearest node, the step target and the interpolation data are
     // its (the same function of the same inputs); else computed here.
     const ScoutRec& R = g_L.sr;
-    bool rec = g_L.sp_on && g_L.sp_stage >= SC_EXPAND && R.ex.ok && R.nn.ok && R.nn.t == A && R.nn.id == nid &&
-               same8(R.nn.q, g_L.xr) && same8(R.e[0].s, g_L.nn.q) && same8(R.e[0].g, R.ex.ext);
+    const bool rid = g_L.sp_on && g_L.sp_stage >= SC_EXPAND && R.ex.ok && R.nn.ok && R.nn.t == A && R.nn.id == nid &&
+                     same8(R.nn.q, g_L.xr);
+    if (rid) {
+      // the record's nearest node is this one: its configuration is the record's edge start (configurations never
+      // change) and its costs the record's (a staged record is taken only on the tree's rewire count as this
+      // iteration found it, and only rewires change the costs of existing nodes) -- no dependent global load
+      for (int j = 0; j < NJ; ++j) g_L.nn.q[j] = R.e[0].s[j];
+      for (int k = 0; k < 3; ++k) g_L.nn.c[k] = R.nn.c[k];
+      g_L.nn.id = nid;
+      g_L.nn.parent = -1;  // (not used by the iteration)
+    } else {
+      load_node(C, A, nid, &g_L.nn);
+    }
+    bool rec = rid && same8(R.e[0].g, R.ex.ext);
     g_L.flag = rec;
     if (rec) {
       for (int j = 0; j < NJ; ++j) {
