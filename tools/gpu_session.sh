@@ -4,6 +4,7 @@ mkdir -p $OUT
 ( while true; do date +%s >> $OUT/heartbeat.txt; sleep 30; done ) &
 HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
-PMC_LIMIT=200 BENCH_LIMIT=300 KT_LIMIT=200 bash tools/profile_round.sh r05 c2 && echo "c2 rc=0" >> $OUT/status.txt &&
-PMC_LIMIT=200 BENCH_LIMIT=300 KT_LIMIT=200 bash tools/profile_round.sh r05 c3 --workload c3 --queries-per-gpu 8 && echo "c3 rc=0" >> $OUT/status.txt &&
-PMC_LIMIT=200 BENCH_LIMIT=300 KT_LIMIT=200 bash tools/profile_round.sh r05 c5 --workload c5 --queries-per-gpu 8 && echo "c5 rc=0" >> $OUT/status.txt
+timeout -k 10 700 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests > $OUT/r05_t_gpu_nnrec.txt 2>&1 &&
+timeout -k 10 300 python -u bench.py > $OUT/r05_bench_nnrec.json 2> $OUT/r05_bench_nnrec.err &&
+timeout -k 10 300 python -u bench.py > $OUT/r05_bench_nnrec2.json 2> $OUT/r05_bench_nnrec2.err &&
+timeout -k 10 200 python -u tools/perf_probe.py 4000 > $OUT/r05_perf_nnrec.txt 2>&1
