@@ -4,7 +4,6 @@ mkdir -p $OUT
 ( while true; do date +%s >> $OUT/heartbeat.txt; sleep 30; done ) &
 HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
-timeout -k 10 700 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests > $OUT/r05_t_gpu_nnrec.txt 2>&1 &&
-timeout -k 10 300 python -u bench.py > $OUT/r05_bench_nnrec.json 2> $OUT/r05_bench_nnrec.err &&
-timeout -k 10 300 python -u bench.py > $OUT/r05_bench_nnrec2.json 2> $OUT/r05_bench_nnrec2.err &&
-timeout -k 10 200 python -u tools/perf_probe.py 4000 > $OUT/r05_perf_nnrec.txt 2>&1
+timeout -k 10 400 python -u bench.py --workload c3 > $OUT/r05_bench_c3_final2.json 2> $OUT/r05_bench_c3_final2.err &&
+timeout -k 10 400 python -u bench.py --workload c5 > $OUT/r05_bench_c5_final2.json 2> $OUT/r05_bench_c5_final2.err &&
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $OUT/r05_smoke_final3.txt 2>&1
