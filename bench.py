@@ -432,7 +432,8 @@ def main():
                          "algorithmic_bytes_rank0": alg_bytes_rank0},
         }
         if alone is not None:
-            out.update(D.scaling_fields(checked / elapsed, world, (alone[1]["checked"], alone[0])))
+            rpg = int(os.environ.get("SMP_SLOT_SHARE", "1")) if backend == "gloo" else 1
+            out.update(D.scaling_fields(checked / elapsed, world, (alone[1]["checked"], alone[0]), ranks_per_gpu=rpg))
             out["single_gpu_same_workload"]["how"] = (
                 "rank 0 planned its own per-GPU share (the same %d queries, seeds and budgets) again alone, the other "
                 "ranks waiting at a barrier" % len(mine))

@@ -144,6 +144,7 @@ struct smp_planner {
   int num_cus = 256;
   int num_xcd = 8;                 // XCDs (hipDeviceAttributeNumberOfXccs): the per-XCD helper budget of provision()
   unsigned* h_ttff = nullptr;      // host-mapped first-solution flags, one per query (QueryDev::ttff)
+  unsigned* h_abort = nullptr;     // host-mapped abort word of the planner's launches (QueryDev::abort)
   QState* h_st = nullptr;          // pinned host copies of the queries' loop states (asynchronous uploads)
   int n_st = 0;
   int n_ttff = 0;
@@ -465,6 +466,7 @@ void smp_planner_destroy(smp_planner* p) {
   if (p->ev1) (void)hipEventDestroy(p->ev1);
   if (p->stream) (void)hipStreamDestroy(p->stream);
   if (p->h_ttff) (void)hipHostFree(p->h_ttff);
+  if (p->h_abort) (void)hipHostFree(p->h_abort);
   if (p->h_st) (void)hipHostFree(p->h_st);
   delete p;
 }
@@ -999,6 +1001,7 @@ static QueryDev make_qdev(QueryBuffers& b, size_t cap, long long rows) {
   d.sampler = 0;
   d.trace = nullptr;
   d.ttff = nullptr;
+  d.abort = nullptr;
   d.lfin = nullptr;
   d.lquota = 0;
   // scans of trees of at least this many nodes are split over the helpers (DESIGN.md "Scans of large trees");
@@ -1263,6 +1266,14 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
     HIPCHK(hipHostGetDevicePointer((void**)&dflag, p->h_ttff, 0));
     for (int i = 0; i < nq; ++i) qdev[i].ttff = dflag + i;
   }
+  // the abort word (QueryDev::abort): cleared for this call (busy_check has seen every earlier launch drain)
+  if (!p->h_abort) HIPCHK(hipHostMalloc(&p->h_abort, sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent));
+  __atomic_store_n(p->h_abort, 0u, __ATOMIC_RELEASE);
+  {
+    unsigned* dabort = nullptr;
+    HIPCHK(hipHostGetDevicePointer((void**)&dabort, p->h_abort, 0));
+    for (int i = 0; i < nq; ++i) qdev[i].abort = dabort;
+  }
   std::vector<double> host_ttff(nq, -1.0);
   auto poll_ttff = [&]() {
     for (int i = 0; i < nq; ++i)
@@ -1298,6 +1309,9 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
   double tmax = 0;
   for (int i = 0; i < nq; ++i) if (qs[i].budget_kind == SMP_BUDGET_SECONDS) tmax = std::max(tmax, qs[i].budget);
   auto t_begin = std::chrono::steady_clock::now();
+  // a seconds budget bounds the host's wait for a launch at 4x the budget + this slack (SMP_WAIT_SLACK_S: tests)
+  double wait_slack = 60.0;
+  if (const char* e = std::getenv("SMP_WAIT_SLACK_S")) wait_slack = std::atof(e);
   // a single query runs its whole budget in one launch (the loop state is resumable, but a relaunch costs the host
   // round trip, the board reset and the scouts' restart: C2, 5 launches of 256 .. 4096 iterations, ~1 ms each);
   // several queries start at 256 iterations and double, so that finished ones free their CUs early (rebalance)
@@ -1315,7 +1329,7 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
     if (tmax == 0 && launches > max_iters / 256 + 64 + 2 * nq +
                                     (slice_ms > 0 ? (long long)(total_ms / slice_ms) * 2 : 0))
       return SMP_ERR_HIP;
-    if (tmax > 0 && std::chrono::duration<double>(std::chrono::steady_clock::now() - t_begin).count() > tmax * 4 + 60)
+    if (tmax > 0 && std::chrono::duration<double>(std::chrono::steady_clock::now() - t_begin).count() > tmax * 4 + wait_slack)
       return SMP_ERR_HIP;
     const int na = (int)act.size();
     HIPCHK(hipMemsetAsync(p->d_lfin.p, 0, sizeof(unsigned), p->stream));
@@ -1351,8 +1365,11 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
         for (int i : act) all = all && host_ttff[i] >= 0;
         if (all) std::this_thread::sleep_for(std::chrono::microseconds(50));
         else std::this_thread::yield();
-        if (tmax > 0 && std::chrono::duration<double>(std::chrono::steady_clock::now() - t_begin).count() > tmax * 4 + 60) {
-          p->busy = true;  // the launch still runs on this planner's buffers
+        if (tmax > 0 && std::chrono::duration<double>(std::chrono::steady_clock::now() - t_begin).count() > tmax * 4 + wait_slack) {
+          // the launch still runs on this planner's buffers: ask it to end (its leaders poll the abort word every
+          // ABORT_EVERY iterations) and refuse calls until it has drained (busy_check)
+          __atomic_store_n(p->h_abort, 1u, __ATOMIC_RELEASE);
+          p->busy = true;
           return SMP_ERR_HIP;
         }
       }

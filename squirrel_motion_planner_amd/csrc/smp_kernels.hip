@@ -6038,11 +6038,13 @@ __global__ void __launch_bounds__(BLOCK) plan_kernel(const RobotDev* __restrict_
   const unsigned long long t_launch = wall_clock64();
   for (int k = 0; k < iters; ++k) {
     if (uni(g_L.S.status != 0 || g_L.S.phase != 1)) break;
-    if ((C.Q.lquota > 0 || C.Q.lticks > 0) && (k & 7) == 7) {
-      // enough of the launch's queries finished, or its time slice is over: end it (resumable)
+    if (((C.Q.lquota > 0 || C.Q.lticks > 0) && (k & 7) == 7) || (C.Q.abort && (k & (ABORT_EVERY - 1)) == ABORT_EVERY - 1)) {
+      // enough of the launch's queries finished, its time slice is over, or the host abandoned the call: end it
+      // (resumable; the stop words below send the scouts and helpers home)
       if (threadIdx.x == 0)
         g_L.go_end = (C.Q.lquota > 0 && ld_agent(C.Q.lfin) >= (unsigned)C.Q.lquota) ||
-                     (C.Q.lticks > 0 && (long long)(wall_clock64() - t_launch) > C.Q.lticks);
+                     (C.Q.lticks > 0 && (long long)(wall_clock64() - t_launch) > C.Q.lticks) ||
+                     (C.Q.abort && __hip_atomic_load(C.Q.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u);
       __syncthreads();
       if (uni(g_L.go_end)) break;
     }

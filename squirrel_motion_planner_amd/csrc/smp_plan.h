@@ -135,8 +135,11 @@ struct JobBoard {
   unsigned long long res[JOB_TILES];
   int pad2[32 - (2 * JOB_TILES) % 32];
   // leader -> helpers: a scan job (DESIGN.md "Scans of large trees"), in its own granules beside `pay`, so that a scan may
-  // run while a collision job holds `pay`: word 0 = header (scan bit << 18 | near << 19 | tree << 20), words 1-16 the
-  // query configuration's halves, 17 range start, 18 range end, 19 excluded id, 20-21 radius halves, 22 participants
+  // run while a collision job holds `pay`: word 0 = header (scan bit << 18 | near << 19 | tree << 20 | near == 2 << 21,
+  // bit 21 marking a fused nearest + near set of one configuration, slice_near<true>), words 1-16 the query
+  // configuration's halves, 17 range start, 18 range end, 19 excluded id, 20-21 radius halves, 22 participants.  A scan
+  // job thus fills words 0-22; SCAN_WORDS = 33 is the count an idle helper's first poll covers (the scan header's
+  // edge-count field 1 = one edge's 32 granules + the header, as a collision job of one edge), words 23-32 unused.
   unsigned long long spay[64];
   // run-ahead sampler (DESIGN.md "Sampler").  Leader -> sampler: its current iteration and the informed-
   // sampling parameters, versioned (payload stores drained before the version store).
@@ -291,6 +294,7 @@ struct ScoutBoard {
   unsigned long long pre_g[SCOUT_SLOTS][PRE_GRANULES];  // PreRec granules, by record slot
 };
 
+constexpr int ABORT_EVERY = 64;  // iterations between a leader's polls of the host's abort word (QueryDev::abort)
 struct QueryDev {
   QState* st;
   JobBoard* jb;                // null: no helpers
@@ -322,6 +326,10 @@ struct QueryDev {
   long long lticks;            // > 0: the launch ends this many device-clock ticks after it started (resumable), so
                                // that the host re-provisions (DESIGN.md "Many queries")
   unsigned* ttff;              // host-mapped word set to 1 when the first feasible path is committed (null: none)
+  // host-mapped word the host sets when it abandons a planning call (its wait timed out): every leader polls it every
+  // ABORT_EVERY iterations and ends the launch (its stop words send its scouts and helpers home), so an abandoned
+  // launch drains instead of holding the CUs to the end of its budget (null: none)
+  const unsigned* abort;
   int scan_min;                // nodes in a scan's range from which it is split over the helpers (0: never)
   int scan_pnn, scan_pnear;    // participants (this workgroup + helpers) of a split nearest / near scan, <= SCAN_P
   int scan_nshift;             // a split near scan takes one participant per 2^scan_nshift nodes (at least 8)

@@ -121,13 +121,20 @@ def single_rank_reference(run, rank, src=0):
     return out
 
 
-def scaling_fields(value_all, world, alone):
+def scaling_fields(value_all, world, alone, ranks_per_gpu=1):
     """The line's scaling fields: `alone` = (configurations checked, seconds) of one GPU planning the same per-GPU
     share alone; scaling_efficiency = whole-job rate / (world x that single-GPU rate) (weak scaling: the per-GPU work
-    is the same)."""
+    is the same).  With ranks_per_gpu > 1 (a rehearsal: more ranks than GPUs, each planner provisioned with its share of
+    one device, SMP_SLOT_SHARE) rank 0's "alone" run still held only its share of the GPU, so the quotient is not a
+    multi-GPU efficiency: the line carries the rehearsal's fields and scaling_efficiency None."""
     checked, seconds = alone
     single = checked / seconds if seconds > 0 else None
-    return {"single_gpu_same_workload": {"value": single, "unit": "configs/s", "configs_checked": checked,
-                                         "seconds": seconds},
-            "scaling_efficiency": value_all / (world * single) if single else None}
+    out = {"single_gpu_same_workload": {"value": single, "unit": "configs/s", "configs_checked": checked,
+                                        "seconds": seconds},
+           "scaling_efficiency": value_all / (world * single) if single and ranks_per_gpu == 1 else None}
+    if ranks_per_gpu > 1:
+        out["ranks_per_gpu"] = ranks_per_gpu
+        out["rehearsal"] = ("ranks share %d per GPU; single_gpu_same_workload ran at 1/%d of the device's slots, so no "
+                            "scaling efficiency is derived" % (ranks_per_gpu, ranks_per_gpu))
+    return out
 

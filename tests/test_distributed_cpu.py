@@ -160,3 +160,13 @@ def test_scene_broadcast_and_sharding_world2(tmp_path):
     for r in range(world):
         red = np.load(os.path.join(str(tmp_path), "red%d.npy" % r))
         assert red.tolist() == [3.0, 30.0, 2.0, 20.0]
+
+
+def test_rehearsal_scaling_fields_carry_no_efficiency():
+    """Ranks sharing one GPU (ranks_per_gpu > 1): the line is labelled a rehearsal and derives no efficiency."""
+    from squirrel_motion_planner_amd import distributed as D
+    f = D.scaling_fields(10.0, 2, (400, 100.0), ranks_per_gpu=2)
+    assert f["scaling_efficiency"] is None and f["ranks_per_gpu"] == 2 and "rehearsal" in f
+    assert f["single_gpu_same_workload"]["value"] == 4.0
+    g = D.scaling_fields(10.0, 2, (400, 100.0))
+    assert g["scaling_efficiency"] == 10.0 / (2 * 4.0) and "rehearsal" not in g

@@ -98,3 +98,34 @@ def test_oversubscribed_helpers_are_clamped(c2):
     for k in ("iterations", "configs_checked", "nodes_start", "nodes_goal", "cost_best"):
         assert ro[k] == ra[k], k
     assert ro["time_total"] < 2.0 * ra["time_total"] + 0.01, (ro["time_total"], ra["time_total"])
+
+
+def test_abandoned_launch_drains_on_the_abort_word(c2, monkeypatch):
+    """A call whose wait for its launch times out returns SMP_ERR_HIP and marks the planner busy (its buffers are still in
+    use); it also sets the host-mapped abort word that every leader polls every ABORT_EVERY iterations, so the launch
+    ends within a few milliseconds instead of running to the end of its budget.  Here the wait is cut to 0.1 s of a 5 s
+    budget (SMP_WAIT_SLACK_S = -19.9: 4 x 5 s - 19.9 s): the planner is usable again well before the budget's end, and
+    plans as before."""
+    sc, scene = c2
+    gp = GpuPlanner(Robot(), path_optimality_threshold=-math.inf)
+    gp.set_scene(scene)
+    ref = gp.plan(GpuPlanner.make_query(sc.start, sc.goal, sc.env_x, sc.env_y, iterations=300, seed=2))
+    monkeypatch.setenv("SMP_WAIT_SLACK_S", "-19.9")
+    t = time.perf_counter()
+    with pytest.raises(L.SmpError) as e:
+        gp.plan(GpuPlanner.make_query(sc.start, sc.goal, sc.env_x, sc.env_y, seconds=5.0, seed=1))
+    assert e.value.status == L.SMP_ERR_HIP
+    monkeypatch.delenv("SMP_WAIT_SLACK_S")
+    r = None
+    while time.perf_counter() - t < 4.0:
+        try:
+            r = gp.plan(GpuPlanner.make_query(sc.start, sc.goal, sc.env_x, sc.env_y, iterations=300, seed=2))
+            break
+        except L.SmpError as busy:
+            assert busy.status == L.SMP_ERR_HIP
+            time.sleep(0.01)
+    drained = time.perf_counter() - t
+    assert r is not None and drained < 1.0, drained
+    for k in ("status", "iterations", "configs_checked", "nodes_start", "nodes_goal"):
+        assert r[k] == ref[k], k
+    assert np.array_equal(r["path"], ref["path"])

@@ -619,12 +619,15 @@ def test_large_tree_run_matches_golden(robot):
     assert np.array_equal(r["path"], g["path"])
 
 
-@pytest.mark.parametrize("n1,n2", [(3000, 3600), (20000, 20300)])
+@pytest.mark.parametrize("n1,n2", [(3000, 3600), (20000, 20300), (300000, 300200)])
 def test_oracle_continues_the_gpu_state(gp, orobot, n1, n2):
     """The oracle continued from the GPU planner's state after n1 iterations (GpuPlanner.export_state ->
     Oracle.resume: both trees with their child order and in-edges, the loop scalars) plans exactly the GPU's own run of
     n2 iterations: the GPU's state is the reference loop's state at n1, and the large-tree CPU timing
-    (tools/large_tree_report.py) resumes the CPU from the GPU's trees."""
+    (bench.py cpu_window) resumes the CPU from the GPU's trees.  The 3e5 case (trees of ~160k / ~140k nodes) runs the
+    distributed scans' fp32-prefiltered slices (DESIGN.md "fp32 prefilter") where they are built for: every nearest
+    (first strict minimum, BS:4076-4133) and near set (radius test, BS:4272-4324) of its last 200 iterations must equal
+    the oracle's fp64 scans for the trees, costs and path to match."""
     sc, gscene, osc = scene_pair("c2")
     gp.set_scene(gscene)
     gp.set_disabled_map_links([])

@@ -3,7 +3,13 @@
 4272-4324): integer ids must match exactly.  Trees are synthetic: uniform and clustered configurations, costs
 with many ties, constant / ascending / descending costs, and nodes placed on the near radius.  Every case runs in the
 four forms the planner uses: the workgroup's own scans (nearest, near_set), a distributed scan's slice functions over the
-whole range (slice_nn, slice_near), and the fused nearest + near set of connect (near_set<20, true>, slice_near<true>)."""
+whole range (slice_nn, slice_near), and the fused nearest + near set of connect (near_set<20, true>, slice_near<true>).
+
+What the planner runs: the "local" forms below 2048 nodes (fp64 register path); from 2048 nodes the local scans and every
+slice of a distributed scan go through the inlined fp32-prefilter forms (slice_inl / fused_slice_inl, and "local" /
+"fused" at n >= 2048, which call them).  The "slice" / "fused_slice" modes run the fp64 slice functions slice_nn /
+slice_near, which the planner keeps only as the fallback of a histogram that cannot split its costs; they stay here as a
+cross-check of that fallback."""
 
 MODES = {"local": {}, "slice": {"slices": True}, "fused": {"fused": True}, "fused_slice": {"slices": True, "fused": True},
          "slice_inl": {"slices": True, "inline": True}, "fused_slice_inl": {"slices": True, "fused": True, "inline": True}}
@@ -107,3 +113,65 @@ def test_tree_scans_three_chunks(kind, mode):
         nn, kk, lo, hi = ref_scans(q, cost, queries[k], 4.0, excl[k])
         assert got["nearest"][k] == nn and got["k"][k] == kk
         assert list(got["lo"][k]) == list(lo) and list(got["hi"][k]) == list(hi)
+
+
+@pytest.mark.parametrize("mode", ["local", "fused", "slice_inl", "fused_slice_inl"])
+@pytest.mark.parametrize("n", [2048, 5000])
+def test_fp32_prefilter_near_ties(n, mode):
+    """Nearest-node ties and near-ties that the fp32 copy cannot separate (nn32_finish's candidate threshold decides
+    which threads rescan in fp64): exact duplicates of one configuration at ids spread over threads and waves (the first
+    strict minimum is the lowest id), nodes within 1e-9 .. 1e-7 of the query (equal in fp32, ordered in fp64), a second
+    cluster at the same fp32 distance, and nodes on the radius within the fp32 error band.  Run in the fp32 forms the
+    planner uses (local scans of 2048+ nodes, helper / publisher slices)."""
+    from squirrel_motion_planner_amd import probes
+    rng = np.random.default_rng(n + len(mode))
+    q = rng.uniform(-3, 3, (n, 8))
+    cost = rng.uniform(0, 10, n)
+    cost[0] = 0.0
+    x = rng.uniform(-2, 2, 8)
+    base = x + np.array([0.3, -0.2, 0.1, 0.05, 0.0, 0.0, 0.0, 0.0])
+    # duplicates of one node (equal fp64 distance) at ids across threads / waves / the slice's node stride
+    dup = [n - 1, 1500, 777, 513, 64, 65]
+    for i in dup:
+        q[i] = base
+    # nodes within 1e-9 .. 1e-7 of the query in one joint: identical in fp32, different in fp64
+    tiny = [(901, 1e-7), (902, -3e-8), (1903 % n, 1e-9), (17, 5e-8)]
+    queries, excl = [], []
+    for k, (i, d) in enumerate(tiny):
+        e = np.zeros(8)
+        e[k % 8] = d
+        q[i] = x + e
+    queries.append(x.copy())
+    excl.append(-1)
+    # query 1: the duplicates are the nearest (no node closer): first strict minimum = lowest duplicate id
+    queries.append(base + np.array([1e-8, 0, 0, 0, 0, 0, 0, 0]))
+    excl.append(-1)
+    # query 2: two clusters at fp32-equal distances (mirror images), the fp64 distances differ in the last bits
+    x2 = rng.uniform(-1, 1, 8)
+    for t, i in enumerate((300, 1200, 2046)):
+        e = np.zeros(8)
+        e[3] = 0.25 + (t - 1) * 1e-12
+        q[i] = x2 + (e if t % 2 == 0 else -e)
+    queries.append(x2)
+    excl.append(1200)
+    # query 3: nodes on the radius within the fp32 error band, costs tied
+    x3 = rng.uniform(-1, 1, 8)
+    r = 4.0
+    for t, f in enumerate((1.0, 1.0 - 1e-9, 1.0 + 1e-9, 1.0 - 1e-7, 1.0 + 1e-7, 1.0 - 3e-8)):
+        e = np.zeros(8)
+        e[(t + 2) % 8] = r * f
+        q[100 + 37 * t] = x3 + e
+        cost[100 + 37 * t] = 4.5
+    queries.append(x3)
+    excl.append(-1)
+    queries = np.array(queries)
+    got = probes.tree_scan(q, cost, queries, excl, r, **MODES[mode])
+    for k in range(len(queries)):
+        nn, kk, lo, hi = ref_scans(q, cost, queries[k], r, excl[k])
+        assert got["nearest"][k] == nn, (k, got["nearest"][k], nn)
+        assert got["k"][k] == kk
+        t = len(lo)
+        assert list(got["lo"][k][:t]) == list(lo), (k, got["lo"][k], lo)
+        assert list(got["hi"][k][:t]) == list(hi), (k, got["hi"][k], hi)
+    nn1 = ref_scans(q, cost, queries[1], r, -1)[0]
+    assert nn1 == min(dup)

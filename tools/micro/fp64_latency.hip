@@ -1,16 +1,18 @@
-// Microbenchmark (tooling, not product): cycles per fp64 instruction on gfx950, dependent chain vs 4/8
+// Microbenchmark (tooling, not product): cycles per fp64 (and fp32) instruction on gfx950, dependent chain vs 4/8
 // independent chains, one wave and 2 waves per SIMD.  hipcc --offload-arch=gfx950 -O3 fp64_latency.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
 
-template <int CH, int OP>
-__global__ void k(double* out, long long* cyc, double a, double b, int n) {
-  double x[CH];
+template <typename T, int CH, int OP>
+__global__ void k(T* out, long long* cyc, T a, T b, int n) {
+  T x[CH];
 #pragma unroll
   for (int c = 0; c < CH; ++c) x[c] = a + threadIdx.x + c;
   __syncthreads();
   long long t0 = __builtin_amdgcn_s_memtime();
-  for (int i = 0; i < n; ++i) {
+  for (int i = 0; i < n; i += 32) {  // 32 steps per loop trip: the loop's branch is amortised
+#pragma unroll
+    for (int u = 0; u < 32; ++u)
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
       if (OP == 0) x[c] = x[c] * b;
@@ -22,23 +24,23 @@ __global__ void k(double* out, long long* cyc, double a, double b, int n) {
     }
   }
   long long t1 = __builtin_amdgcn_s_memtime();
-  double s = 0;
+  T s = 0;
 #pragma unroll
   for (int c = 0; c < CH; ++c) s += x[c];
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
   if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
 }
 
-template <int CH, int OP>
+template <int CH, int OP, typename T = double>
 void run(const char* name, int threads) {
-  double* out; long long* cyc;
-  hipMalloc(&out, 4096 * sizeof(double)); hipMalloc(&cyc, 64 * sizeof(long long));
+  T* out; long long* cyc;
+  hipMalloc(&out, 4096 * sizeof(T)); hipMalloc(&cyc, 64 * sizeof(long long));
   const int n = 4096;
-  hipLaunchKernelGGL((k<CH, OP>), dim3(1), dim3(threads), 0, 0, out, cyc, 1.0000001, 0.9999999, n);
+  hipLaunchKernelGGL((k<T, CH, OP>), dim3(1), dim3(threads), 0, 0, out, cyc, (T)1.0000001, (T)0.9999999, n);
   hipDeviceSynchronize();
   long long c = 0;
   hipMemcpy(&c, cyc, sizeof(c), hipMemcpyDeviceToHost);
-  printf("%-8s chains %d threads %4d: %.2f cycles per instruction per wave (per chain step %.2f)\n", name, CH, threads,
+  printf("%-3s %-8s chains %d threads %4d: %.2f cycles per instruction per wave (per chain step %.2f)\n", sizeof(T) == 8 ? "f64" : "f32", name, CH, threads,
          (double)c / (n * CH), (double)c / n);
   hipFree(out); hipFree(cyc);
 }
@@ -51,6 +53,10 @@ int main() {
     run<1, 3>("floor", th); run<8, 3>("floor", th);
     run<1, 4>("div", th); run<8, 4>("div", th);
     run<1, 5>("sqrt", th); run<8, 5>("sqrt", th);
+    run<1, 0, float>("mul", th); run<8, 0, float>("mul", th);
+    run<1, 1, float>("add", th); run<8, 1, float>("add", th);
+    run<1, 2, float>("fma", th); run<8, 2, float>("fma", th);
+    run<1, 4, float>("div", th); run<1, 5, float>("sqrt", th);
   }
   return 0;
 }
