@@ -537,6 +537,46 @@ __device__ __forceinline__ void tree_cols(gcdptr tq, int cap, gcdptr* c) {
 __device__ __forceinline__ bool wave_group_live(int first, int end) {
   return __builtin_amdgcn_readfirstlane((int)(first < end)) != 0;
 }
+// Element i of a column with a scalar base: the byte offset is formed in 32 bits (cap <= 2^27 nodes), so the load issues as
+// global_load with the base in SGPRs and one offset VGPR shared by every column of the node (no 64-bit vector address
+// arithmetic per column).  The scans issue a group's loads unconditionally (indices clamped to the range) and decide
+// validity afterwards: a load inside a per-batch branch whose other arm supplies a default value makes the compiler
+// wait for the load (s_waitcnt vmcnt(0)) at the branch's join, so each batch would cost its own memory round trip.
+__device__ __forceinline__ double ld_col(gcdptr col, unsigned i) {
+  return *(gcdptr)((const char __attribute__((address_space(1)))*)col + i * 8u);
+}
+typedef const float __attribute__((address_space(1)))* gcfptr;
+__device__ __forceinline__ float ld_col(gcfptr col, unsigned i) {  // as ld_col(gcdptr, ..)
+  return *(gcfptr)((const char __attribute__((address_space(1)))*)col + i * 4u);
+}
+// One round of a scan's loads: NPT nodes per thread, b0 + u * BLOCK (u < NPT), of which the first K (a wave-uniform count)
+// are loaded -- all at once, indices clamped to the range -- and the rest take `fill` (their results are masked out).
+template <int K, int NPT, typename P, typename T>
+__device__ __forceinline__ void load_round_k(T (*a)[NJ], const P* cols, int b0, int i1, const T* fill) {
+#pragma unroll
+  for (int u = 0; u < NPT; ++u) {
+    if (u < K) {
+      const unsigned ii = (unsigned)min(b0 + u * BLOCK, i1 - 1);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) a[u][j] = ld_col(cols[j], ii);
+    } else {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) a[u][j] = fill[j];
+    }
+  }
+}
+// The live nodes of a round are a prefix of the u (b0 - lane + u * BLOCK < i1): the round loads 1, 2, 4 or NPT of them by a
+// wave-uniform switch, so one memory round trip covers it and a small tree's round does not load NPT nodes per thread.
+template <int NPT, typename P, typename T>
+__device__ __forceinline__ void load_round(T (*a)[NJ], const P* cols, int b0, int i1, const T* fill) {
+  static_assert(NPT == 8, "rounds of 8 nodes per thread");
+  const int first = b0 - lane_id();
+  const int nl = uni(min(NPT, (i1 - first + BLOCK - 1) / BLOCK));
+  if (nl > 4) load_round_k<8, NPT>(a, cols, b0, i1, fill);
+  else if (nl > 2) load_round_k<4, NPT>(a, cols, b0, i1, fill);
+  else if (nl > 1) load_round_k<2, NPT>(a, cols, b0, i1, fill);
+  else load_round_k<1, NPT>(a, cols, b0, i1, fill);
+}
 
 // Stores into the tree arrays that the scout reads (q, cost, parent).  Plain stores: the lines stay in this XCD's
 // L2, where a scout on the same XCD (the usual placement, plan_kernel) and the leader's own scans find them;
@@ -575,7 +615,7 @@ __device__ int g_dbg[8];
 #define load_node(C, t, id, o) load_node_at(C, t, id, o, __LINE__)
 __device__ __forceinline__ void load_node_at(const Ctx& C, int t, int id, NodeRef* o, int line) {
   const TreeDev& T = C.Q.tr[t];
-  int cap = C.Q.st->cap;
+  const int cap = g_L.S.cap;  // (the leader and scouts stage their QState in LDS: no dependent global load for it)
   BCHK(id, cap, line, t);
   (void)line;
   for (int j = 0; j < NJ; ++j) o->q[j] = T.q[(size_t)j * cap + id];
@@ -665,17 +705,7 @@ __device__ __forceinline__ int nearest_scan(const Ctx& C, int t, const double* q
   constexpr int NPT = 8;
   for (int i0 = i_begin + threadIdx.x; i0 < n; i0 += NPT * BLOCK) {
     double a[NPT][NJ];
-#pragma unroll
-    for (int u = 0; u < NPT; ++u) {
-      if (wave_group_live(i0 - lane_id() + u * BLOCK, n)) {
-        const unsigned ii = (unsigned)min(i0 + u * BLOCK, n - 1);
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) a[u][j] = tqc[j][ii];
-      } else {
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) a[u][j] = qq[j];
-      }
-    }
+    load_round<NPT>(a, tqc, i0, n, qq);
     double s[NPT];
 #pragma unroll
     for (int u = 0; u < NPT; ++u) s[u] = 0.0;
@@ -1100,17 +1130,7 @@ __device__ __forceinline__ void slice_nn_body(gcdptr tq, int cap, int i0, int i1
   constexpr int NPT = 8;
   for (int b0 = i0 + (int)threadIdx.x; b0 < i1; b0 += NPT * BLOCK) {
     double a[NPT][NJ];
-#pragma unroll
-    for (int u = 0; u < NPT; ++u) {
-      if (wave_group_live(b0 - lane_id() + u * BLOCK, i1)) {
-        const unsigned ii = (unsigned)min(b0 + u * BLOCK, i1 - 1);
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) a[u][j] = tqc[j][ii];
-      } else {
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) a[u][j] = qq[j];
-      }
-    }
+    load_round<NPT>(a, tqc, b0, i1, qq);
     double s[NPT];
 #pragma unroll
     for (int u = 0; u < NPT; ++u) s[u] = 0.0;
@@ -1137,7 +1157,6 @@ __device__ __forceinline__ void slice_nn_body(gcdptr tq, int cap, int i0, int i1
 // the minimum only if its s32 is within 2 E(2 m) of the smallest s32 m; each thread keeps its smallest and second
 // smallest s32, so the candidates are the threads' smallest nodes, and a thread whose second smallest is also within
 // the margin rescans its nodes in fp64 -- the first strict minimum in fp64, as the reference, decides.
-typedef const float __attribute__((address_space(1)))* gcfptr;
 __device__ __forceinline__ gcfptr uni_gf(const float* p) {
   const unsigned long long v = reinterpret_cast<unsigned long long>(p);
   const unsigned lo = __builtin_amdgcn_readfirstlane((int)(unsigned)v);
@@ -1150,6 +1169,15 @@ __device__ __forceinline__ void tree_cols_f(const float* tqf, int cap, gcfptr* c
   for (int j = 0; j < NJ; ++j) c[j] = b + (size_t)j * (unsigned)cap;
 }
 constexpr double F32_U = 0x1p-24;
+// The float nearest x from below / above (conservative thresholds).
+__device__ __forceinline__ float f32_down(double x) {
+  const float f = (float)x;
+  return (double)f > x ? nextafterf(f, -__builtin_inff()) : f;
+}
+__device__ __forceinline__ float f32_up(double x) {
+  const float f = (float)x;
+  return (double)f < x ? nextafterf(f, __builtin_inff()) : f;
+}
 __device__ __forceinline__ double s32_err(double s, double c) {
   return 4.0 * (5.6568543 * c * sqrt(s) + 8.0 * c * c + 9.0 * F32_U * s);
 }
@@ -1226,17 +1254,7 @@ __device__ __forceinline__ void slice_nn_body32(gcdptr tq, const float* tqf, int
   constexpr int NPT = 8;
   for (int b0 = i0 + (int)threadIdx.x; b0 < i1; b0 += NPT * BLOCK) {
     float a[NPT][NJ];
-#pragma unroll
-    for (int u = 0; u < NPT; ++u) {
-      if (wave_group_live(b0 - lane_id() + u * BLOCK, i1)) {
-        const unsigned ii = (unsigned)min(b0 + u * BLOCK, i1 - 1);
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) a[u][j] = tfc[j][ii];
-      } else {
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) a[u][j] = qf[j];
-      }
-    }
+    load_round<NPT>(a, tfc, b0, i1, qf);
 #pragma unroll
     for (int u = 0; u < NPT; ++u) {
       float xm;
@@ -1375,10 +1393,21 @@ __device__ __forceinline__ void slice_near_body(gcdptr tq, gcdptr tc, int cap, i
 // runs slice_near_body.  All threads.
 // F32: the radius test and the nearest node from the tree's fp32 copy tqf (the prefilter above), fp64 where it cannot
 // decide.
+// pf (probe kernels only; null in the planner): thread 0's shader-clock ticks per step, accumulated into pf[0..6] (scan and
+// radius test, chunk min / max, histogram or direct gather, bin prefix, gather, rank, nearest finish), pf[7] / pf[8] the
+// chunks taking the direct / histogram path.
+#define SNH_CLOCK(k)                                                                                              \
+  if (pf && threadIdx.x == 0) {                                                                                   \
+    const unsigned long long _t = __builtin_amdgcn_s_memtime();                                                   \
+    pf[k] += _t - _tp;                                                                                            \
+    _tp = _t;                                                                                                     \
+  }
 template <bool NN, bool F32 = false>
 __device__ __forceinline__ bool slice_near_hist(gcdptr tq, gcdptr tc, int cap, int i0, int i1, const double* q, int excl,
-                                                double r, ScanLds& X, const float* tqf = nullptr) {
+                                                double r, ScanLds& X, const float* tqf = nullptr,
+                                                unsigned long long* pf = nullptr) {
   constexpr int K = SCAN_K, NW = BLOCK / 64, CH = NEAR_NBK * BLOCK;
+  unsigned long long _tp = pf && threadIdx.x == 0 ? __builtin_amdgcn_s_memtime() : 0;
   double nb = 10000.0, nb_s = 1e300;  // NN: this thread's nearest candidate
   int nbi = 0x7fffffff;
   float b1 = __builtin_inff(), b2 = __builtin_inff(), cm = 0.0f;  // NN with F32: nn32_track's state
@@ -1396,6 +1425,12 @@ __device__ __forceinline__ bool slice_near_hist(gcdptr tq, gcdptr tc, int cap, i
   for (int j = 0; j < NJ; ++j) { qq[j] = q[j]; qf[j] = (float)q[j]; qm = fmaxf(qm, fabsf(qf[j])); }
   // F32: E(2 r2hi) = c K1 + 32 c^2 + K2 for a node's c (s32_err at s = 2 r2hi)
   const double K1 = 4.0 * 5.6568543 * sqrt(2.0 * r2hi), K2 = 4.0 * 9.0 * F32_U * 2.0 * r2hi;
+  // ... evaluated per node in fp32: E(m) <= m (kM + kM2 m) + K2 with m = max(|x_j|, |q_j|) and the constants rounded up; the
+  // thresholds r2lo - K2 and r2hi + K2 carry a slack of 4 fp32 ulps of r^2, which covers the roundings of the fp32 threshold
+  // expressions, so s32 < kA - m (kM + kM2 m) implies s32 + E < r2lo and s32 > kB + m (kM + kM2 m) implies s32 - E > r2hi
+  const double slack = r2hi * 0x1p-21;
+  const float kA = f32_down(r2lo - K2 - slack), kB = f32_up(r2hi + K2 + slack);
+  const float kM = f32_up(6.0 * F32_U * K1), kM2 = f32_up(32.0 * 36.0 * F32_U * F32_U);
   int tot_all = 0;  // near nodes of the chunks before this one (block-uniform)
   if (threadIdx.x == 0) X.take = 0;
   __syncthreads();
@@ -1410,17 +1445,13 @@ __device__ __forceinline__ bool slice_near_hist(gcdptr tq, gcdptr tc, int cap, i
       if (F32 && c0 + g * BLOCK + wave * 64 < i1) {
         float xf[4][NJ];
 #pragma unroll
-        for (int b = 0; b < 4; ++b) {
+        for (int b = 0; b < 4; ++b) {  // every load of the group at once (clamped indices; see ld_col)
           const int i = c0 + (g + b) * BLOCK + wave * 64 + lane;
-          if (wave_group_live(c0 + (g + b) * BLOCK + wave * 64, i1)) {
-            const unsigned ii = (unsigned)min(i, i1 - 1);
+          const unsigned ii = (unsigned)min(i, i1 - 1);
 #pragma unroll
-            for (int j = 0; j < NJ; ++j) xf[b][j] = tfc[j][ii];
-            key[g + b] = i < i1 ? (unsigned long long)__double_as_longlong(tc[ii]) : 0ull;
-          } else {
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) xf[b][j] = qf[j];
-          }
+          for (int j = 0; j < NJ; ++j) xf[b][j] = ld_col(tfc[j], ii);
+          const unsigned long long kb = (unsigned long long)__double_as_longlong(ld_col(tc, ii));
+          key[g + b] = i < i1 ? kb : 0ull;
         }
         bool nr[4], und[4];
         bool any_und = false;
@@ -1430,9 +1461,9 @@ __device__ __forceinline__ bool slice_near_hist(gcdptr tq, gcdptr tc, int cap, i
           const bool valid = i < i1 && i != excl;
           float xm;
           const float sv = s32_of(qf, xf[b], xm);
-          const double c = 6.0 * F32_U * (double)fmaxf(xm, qm), E = c * K1 + 32.0 * c * c + K2, sd = (double)sv;
-          nr[b] = valid && sd + E < r2lo;
-          und[b] = valid && !nr[b] && !(sd - E > r2hi);
+          const float m = fmaxf(xm, qm), em = m * (kM + kM2 * m);
+          nr[b] = valid && sv < kA - em;
+          und[b] = valid && !nr[b] && !(sv > kB + em);
           if (NN) nn32_track(i < i1, sv, i, xm, b1, b2, bi1, cm);
           any_und |= und[b];
         }
@@ -1465,17 +1496,13 @@ __device__ __forceinline__ bool slice_near_hist(gcdptr tq, gcdptr tc, int cap, i
       } else if (!F32 && c0 + g * BLOCK + wave * 64 < i1) {
         double x[4][NJ];
 #pragma unroll
-        for (int b = 0; b < 4; ++b) {
+        for (int b = 0; b < 4; ++b) {  // every load of the group at once (clamped indices; see ld_col)
           const int i = c0 + (g + b) * BLOCK + wave * 64 + lane;
-          if (wave_group_live(c0 + (g + b) * BLOCK + wave * 64, i1)) {
-            const unsigned ii = (unsigned)min(i, i1 - 1);
+          const unsigned ii = (unsigned)min(i, i1 - 1);
 #pragma unroll
-            for (int j = 0; j < NJ; ++j) x[b][j] = tqc[j][ii];
-            key[g + b] = i < i1 ? (unsigned long long)__double_as_longlong(tc[ii]) : 0ull;
-          } else {
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) x[b][j] = qq[j];
-          }
+          for (int j = 0; j < NJ; ++j) x[b][j] = ld_col(tqc[j], ii);
+          const unsigned long long kb = (unsigned long long)__double_as_longlong(ld_col(tc, ii));
+          key[g + b] = i < i1 ? kb : 0ull;
         }
         bool nr[4], amb[4];
         bool any_amb = false;
@@ -1509,11 +1536,13 @@ __device__ __forceinline__ bool slice_near_hist(gcdptr tq, gcdptr tc, int cap, i
         }
       }
     }
+    SNH_CLOCK(0);
     kmin = __ockl_wfred_min_u64(kmin);
     kmax = __ockl_wfred_max_u64(kmax);
     if (lane == 0) { X.hmin[wave] = kmin; X.hmax[wave] = kmax; X.wtot[wave] = wc; }
     if (threadIdx.x < NEAR_BINS) X.hist[threadIdx.x] = 0;
     __syncthreads();
+    SNH_CLOCK(1);
     int tot = 0;
     kmin = ~0ull; kmax = 0;
 #pragma unroll
@@ -1573,6 +1602,8 @@ __device__ __forceinline__ bool slice_near_hist(gcdptr tq, gcdptr tc, int cap, i
       __syncthreads();
       if (threadIdx.x == 0) X.take = take_c;
       __syncthreads();
+      SNH_CLOCK(2);
+      if (pf && threadIdx.x == 0) pf[7]++;
       continue;
     }
     const double cmin = __longlong_as_double((long long)kmin), cmax = __longlong_as_double((long long)kmax);
@@ -1586,6 +1617,8 @@ __device__ __forceinline__ bool slice_near_hist(gcdptr tq, gcdptr tc, int cap, i
         atomicAdd(&X.hist[bin], 1u);
       }
     __syncthreads();
+    SNH_CLOCK(2);
+    if (pf && threadIdx.x == 0) pf[8]++;
     if (wave == 0) {
       // lane l owns bins 4l .. 4l+3: inclusive cumulative counts (near_set)
       const unsigned h0 = X.hist[4 * lane], h1 = X.hist[4 * lane + 1];
@@ -1624,50 +1657,34 @@ __device__ __forceinline__ bool slice_near_hist(gcdptr tq, gcdptr tc, int cap, i
       X.ci[1][threadIdx.x - 64] = X.hi[threadIdx.x - 64];
     }
     __syncthreads();
+    SNH_CLOCK(3);
     if (!uni(X.fast)) {
       __syncthreads();
       return false;
     }
     const int blo = X.hblo, bhi = X.hbhi;
-    int nw_lo = 0, nw_hi = 0;
-#pragma unroll
-    for (int g = 0; g < NEAR_NBK; ++g) {
-      if (c0 + g * BLOCK + wave * 64 < i1) {
-        const bool nr = nmask >> g & 1;
-        const int bin = bins[g >> 2] >> (8 * (g & 3)) & 255;
-        nw_lo += __popcll(__ballot(nr && bin <= blo));
-        nw_hi += __popcll(__ballot(nr && bin >= bhi));
-      }
-    }
-    int base_lo = 0, base_hi = 0;
-    if (lane == 0 && nw_lo) base_lo = atomicAdd(&X.hcnt[0], nw_lo);
-    if (lane == 1 && nw_hi) base_hi = atomicAdd(&X.hcnt[1], nw_hi);
-    base_lo = __shfl(base_lo, 0);
-    base_hi = __shfl(base_hi, 1);
-    const unsigned long long below = (1ull << lane) - 1;
+    // gather in one pass: a candidate takes its buffer slot with an LDS atomic (the buffers' order does not matter: the
+    // rank below counts (key, id) pairs, which are distinct)
 #pragma unroll
     for (int g = 0; g < NEAR_NBK; ++g) {
       if (c0 + g * BLOCK + wave * 64 < i1) {
         const bool nr = nmask >> g & 1;
         const int bin = bins[g >> 2] >> (8 * (g & 3)) & 255;
         const int i = c0 + g * BLOCK + wave * 64 + lane;
-        const bool pl = nr && bin <= blo, ph = nr && bin >= bhi;
-        const unsigned long long ml = __ballot(pl), mh = __ballot(ph);
-        if (pl) {
-          const int slot = base_lo + __popcll(ml & below);
+        if (nr && bin <= blo) {
+          const int slot = atomicAdd(&X.hcnt[0], 1);
           X.ck[0][slot] = key[g];
           X.ci[0][slot] = i;
         }
-        if (ph) {
-          const int slot = base_hi + __popcll(mh & below);
+        if (nr && bin >= bhi) {
+          const int slot = atomicAdd(&X.hcnt[1], 1);
           X.ck[1][slot] = key[g];
           X.ci[1][slot] = i;
         }
-        base_lo += __popcll(ml);
-        base_hi += __popcll(mh);
       }
     }
     __syncthreads();
+    SNH_CLOCK(4);
     const int take = min(K, tot_all + tot);
     {
       // rank: threads [0, 256) the low buffer, [256, 512) the high buffer; L lanes per entry; the low list ascending,
@@ -1700,13 +1717,16 @@ __device__ __forceinline__ bool slice_near_hist(gcdptr tq, gcdptr tc, int cap, i
     __syncthreads();
     if (threadIdx.x == 0) X.take = take;
     __syncthreads();
+    SNH_CLOCK(5);
   }
   if (threadIdx.x == 0) X.cnt = tot_all;
   __syncthreads();
   if (NN && F32) nn32_finish(tqc, i0, i1, qq, qm, b1, b2, bi1, cm, X);
   else if (NN) slice_nn_reduce(nb, nbi, X);
+  SNH_CLOCK(6);
   return true;
 }
+#undef SNH_CLOCK
 
 template <bool NN>
 __device__ __noinline__ void slice_near(gcdptr tq, gcdptr tc, int cap, int i0, int i1, const double* q, int excl,
@@ -1724,8 +1744,9 @@ __device__ __noinline__ void slice_near_slow(gcdptr tq, gcdptr tc, int cap, int 
 // of scratch stores and loads per call through the CU's load pipeline, and most of a large tree's write traffic).
 template <bool NN, bool F32 = false>
 __device__ __forceinline__ void slice_near_inl(gcdptr tq, gcdptr tc, int cap, int i0, int i1, const double* q, int excl,
-                                               double r, ScanLds& X, const float* tqf = nullptr) {
-  if (uni(slice_near_hist<NN, F32>(tq, tc, cap, i0, i1, q, excl, r, X, tqf))) return;
+                                               double r, ScanLds& X, const float* tqf = nullptr,
+                                               unsigned long long* pf = nullptr) {
+  if (uni(slice_near_hist<NN, F32>(tq, tc, cap, i0, i1, q, excl, r, X, tqf, pf))) return;
   slice_near_slow<NN>(tq, tc, cap, i0, i1, q, excl, r, X);
 }
 
@@ -1906,17 +1927,13 @@ __device__ void near_set(const Ctx& C, int t, const double* q, int excl, bool sp
       if (c0 + g * BLOCK + wave * 64 < n) {
         double x[4][NJ];
 #pragma unroll
-        for (int b = 0; b < 4; ++b) {
+        for (int b = 0; b < 4; ++b) {  // every load of the group at once (clamped indices; see ld_col)
           const int i = c0 + (g + b) * BLOCK + wave * 64 + lane;
-          if (wave_group_live(c0 + (g + b) * BLOCK + wave * 64, n)) {
-            const unsigned ii = (unsigned)min(i, n - 1);
+          const unsigned ii = (unsigned)min(i, n - 1);
 #pragma unroll
-            for (int j = 0; j < NJ; ++j) x[b][j] = tqc[j][ii];
-            key[g + b] = i < n ? (unsigned long long)__double_as_longlong(tc[ii]) : 0ull;
-          } else {
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) x[b][j] = qq[j];
-          }
+          for (int j = 0; j < NJ; ++j) x[b][j] = ld_col(tqc[j], ii);
+          const unsigned long long kb = (unsigned long long)__double_as_longlong(ld_col(tc, ii));
+          key[g + b] = i < n ? kb : 0ull;
         }
         bool nr[4], amb[4];
         bool any_amb = false;
@@ -2076,43 +2093,23 @@ __device__ void near_set(const Ctx& C, int t, const double* q, int excl, bool sp
       return;
     }
     const int blo = g_L.nh.blo, bhi = g_L.nh.bhi;
-    // gather: count the wave's entries per list, one atomic per list, then write
-    int nw_lo = 0, nw_hi = 0;
-#pragma unroll
-    for (int g = 0; g < NEAR_NBK; ++g) {
-      if (c0 + g * BLOCK + wave * 64 < n) {
-        const bool nr = nmask >> g & 1;
-        const int bin = bins[g >> 2] >> (8 * (g & 3)) & 255;
-        nw_lo += __popcll(__ballot(nr && bin <= blo));
-        nw_hi += __popcll(__ballot(nr && bin >= bhi));
-      }
-    }
-    int base_lo = 0, base_hi = 0;
-    if (lane == 0 && nw_lo) base_lo = atomicAdd(&g_L.nh.cnt[0], nw_lo);
-    if (lane == 1 && nw_hi) base_hi = atomicAdd(&g_L.nh.cnt[1], nw_hi);
-    base_lo = __shfl(base_lo, 0);
-    base_hi = __shfl(base_hi, 1);
-    const unsigned long long below = (1ull << lane) - 1;
+    // gather in one pass: a candidate takes its buffer slot with an LDS atomic (order-free: the rank counts (key, id))
 #pragma unroll
     for (int g = 0; g < NEAR_NBK; ++g) {
       if (c0 + g * BLOCK + wave * 64 < n) {
         const bool nr = nmask >> g & 1;
         const int bin = bins[g >> 2] >> (8 * (g & 3)) & 255;
         const int i = c0 + g * BLOCK + wave * 64 + lane;
-        const bool pl = nr && bin <= blo, ph = nr && bin >= bhi;
-        const unsigned long long ml = __ballot(pl), mh = __ballot(ph);
-        if (pl) {
-          const int slot = base_lo + __popcll(ml & below);
+        if (nr && bin <= blo) {
+          const int slot = atomicAdd(&g_L.nh.cnt[0], 1);
           g_L.nh.ck[0][slot] = key[g];
           g_L.nh.ci[0][slot] = i;
         }
-        if (ph) {
-          const int slot = base_hi + __popcll(mh & below);
+        if (nr && bin >= bhi) {
+          const int slot = atomicAdd(&g_L.nh.cnt[1], 1);
           g_L.nh.ck[1][slot] = key[g];
           g_L.nh.ci[1][slot] = i;
         }
-        base_lo += __popcll(ml);
-        base_hi += __popcll(mh);
       }
     }
     __syncthreads();
@@ -6170,8 +6167,8 @@ __device__ __forceinline__ void near_probe_body(const double* tqv, const double*
     unsigned long long t1 = wall_clock64();
     for (int rep = 0; rep < reps; ++rep) {
       if constexpr (INL) {
-        if (mode == 4) slice_near_inl<false, true>(tq, tc, cap, 0, n, g_L.xr, excl[k], r, g_L.sc.s, tqf);
-        else slice_near_inl<true, true>(tq, tc, cap, 0, n, g_L.xr, excl[k], r, g_L.sc.s, tqf);
+        if (mode == 4) slice_near_inl<false, true>(tq, tc, cap, 0, n, g_L.xr, excl[k], r, g_L.sc.s, tqf, &g_L.S.prof[20]);
+        else slice_near_inl<true, true>(tq, tc, cap, 0, n, g_L.xr, excl[k], r, g_L.sc.s, tqf, &g_L.S.prof[20]);
       } else {
         if (mode == 1) slice_near<false>(tq, tc, cap, 0, n, g_L.xr, excl[k], r, g_L.sc.s);
         else if (mode == 3) slice_near<true>(tq, tc, cap, 0, n, g_L.xr, excl[k], r, g_L.sc.s);

@@ -13,7 +13,6 @@ step() {  # step NAME LIMIT CMD...
   echo "step $name rc $rc" | tee -a $OUT/steps.txt
   [ $rc -le 1 ] || exit $rc
 }
-step s4_micro 60 ./tools/micro/fp64_latency
-SMP_LIB=$PWD/squirrel_motion_planner_amd/lib/libsmp_gpu_jps8.so SMP_JOB_PROF=1 step s7_jps8 200 python -u tools/perf_probe.py 4000
-SMP_LIB=$PWD/squirrel_motion_planner_amd/lib/libsmp_gpu_jpp64.so SMP_JOB_PROF=1 step s8_jpp64 200 python -u tools/perf_probe.py 4000
-SMP_LIB=$PWD/squirrel_motion_planner_amd/lib/libsmp_gpu_jp.so SMP_JOB_PROF=1 SMP_HELPERS=100 step s9_jph100 200 python -u tools/perf_probe.py 4000
+step s1_tests 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py -k "planner_parity or distributed_scans or bench_workload or oracle_continues"
+step s2_perf 200 python -u tools/perf_probe.py 4000 30000
+SMP_LIB=$PWD/squirrel_motion_planner_amd/lib/libsmp_gpu_trace.so step s12_trace 200 python -u tools/trace_probe.py 3100
