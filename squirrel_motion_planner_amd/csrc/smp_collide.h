@@ -706,8 +706,8 @@ struct TileOrder {
 //      loads of all of them issued together; the rare spheres near an occupied box are swept by the whole
 //      wave; then lanes over the flat list of sphere pairs of the enabled link pairs, the wave's
 //      configurations interleaved per pair.  No block barrier inside stage C.
-// gfx950 fp64 has ~40 cycles of dependent latency (tools/micro/fp64_latency.hip), so every stage is laid
-// out as many short independent chains per lane rather than one long chain.
+// Every stage is laid out as many short independent chains per lane rather than one long chain (a dependent fp64
+// mul / add is ~5 cycles on gfx950, an LDS round trip 50-100: tools/micro/fp64_latency.hip).
 template <int CT>
 __device__ __forceinline__ void collide_tile(const RobotDev* __restrict__ rb, const SceneDev& sc_in,
                                              const MapCfg* __restrict__ mc, int nc, const double (*q_lds)[NJ],

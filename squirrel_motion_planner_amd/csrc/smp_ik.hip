@@ -5,8 +5,9 @@
 // control_laws.cpp:5273-5301), the manipulability measure (control_laws.cpp:6050-6089), the variable damping
 // (control_laws.cpp:5557-5569), the damped pseudo-inverse applied to the error (control_laws.cpp:3455-3497), the
 // joint update with the joint-limit check (control_laws.cpp:3504-3550), forward kinematics and the clamped error
-// (control_laws.cpp:2167-2245).  An iteration is a dependent chain of small steps, and gfx950 fp64 has ~40 cycles
-// of dependent latency, so a run stays on one wavefront and each step is laid out to be short and wide:
+// (control_laws.cpp:2167-2245).  An iteration is a dependent chain of small steps (a dependent fp64 mul / add costs ~5
+// cycles on gfx950, a division ~70, an LDS round trip ~50-100: tools/micro/fp64_latency.hip), so a run stays on one
+// wavefront and each step is laid out to be short and wide:
 //   J    lanes 0-7: Jacobian column c (the joint rotations come from the previous FK) and, in the same
 //        instruction stream, the quaternion and error component min(c, 5) of the previous FK (the goal terms in
 //        registers for the whole run);

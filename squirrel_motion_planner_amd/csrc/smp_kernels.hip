@@ -862,8 +862,8 @@ __device__ __forceinline__ int nearest_leader(const Ctx& C, int t, const double*
 }
 
 // (cost,id) lexicographic order of the near list (std::sort order made total).  Costs are
-// non-negative doubles, whose bit patterns order like the values, so keys compare as integers (fp64 compares
-// carry ~40 cycles of dependent latency on gfx950).
+// non-negative doubles, whose bit patterns order like the values, so keys compare as integers (64-bit integer
+// compares stay in the scalar / VALU integer pipe and need no fp64 compare-to-mask step).
 __device__ __forceinline__ bool ki_less(unsigned long long ka, int ia, unsigned long long kb, int ib) {
   return ka < kb || (ka == kb && ia < ib);
 }
@@ -2849,14 +2849,22 @@ __device__ void scan_run(const Ctx& C, int near, int t, const double* q, int i0,
 #endif
 }
 
+// The (distance key, id) minimum of the P slices' nearest results (each wave computes it: lane w reads slice w; a serial
+// loop would wait on one LDS read per slice).
+__device__ __forceinline__ void merge_nearest(const MergeLds& M, int P, unsigned long long& bk, int& bi) {
+  const int w = lane_id();
+  const unsigned long long k = w < P ? M.nk[w] : ~0ull;
+  const int i = w < P ? M.ni[w] : 0x7fffffff;
+  bk = __ockl_wfred_min_u64(k);
+  bi = __ockl_wfred_min_i32(k == bk ? i : 0x7fffffff);
+}
 __device__ int nearest_dist(const Ctx& C, int t, const double* q, int i0, int n, double* d_out) {
   const int P = scan_parts(C, 0, n - i0);
   scan_run(C, 0, t, q, i0, n, -1, 0.0, P);
   const MergeLds& M = g_L.sc.m;
-  unsigned long long bk = M.nk[0];
-  int bi = M.ni[0];
-  for (int w = 1; w < P; ++w)
-    if (M.nk[w] < bk || (M.nk[w] == bk && M.ni[w] < bi)) { bk = M.nk[w]; bi = M.ni[w]; }
+  unsigned long long bk;
+  int bi;
+  merge_nearest(M, P, bk, bi);
   __syncthreads();
 #ifdef SMP_SCAN_PROF
   if (threadIdx.x == 0) SCANPROF_ADD(4, wall_clock64() - g_L.spc_t);
@@ -2875,20 +2883,20 @@ __device__ void near_set_dist(const Ctx& C, int t, const double* q, int excl, bo
   scan_run(C, nn ? 2 : 1, t, q, 0, n, excl, g_L.S.near_r, P);
   TR();
   const MergeLds& M = g_L.sc.m;
-  int tot = 0;
-  for (int w = 0; w < P; ++w) tot += M.cnt[w];
-  tot = uni(tot);
-  const int take = min(SCAN_K, tot);
   static_assert(SCAN_PNEAR <= 64, "one lane per list");
+  int tot = 0, take = 0;
   if (threadIdx.x < 128) {
-    // per round: the extreme head by two 32-bit wave reductions (high word, then the low word among the lanes holding
-    // that high word: DPP min / max steps on 32 bits, cheaper than one 64-bit reduction), the id reduction only when
-    // two heads hold equal keys; each lane has its list's next entry loaded ahead, so a winning lane's new head is in
-    // registers when the next round starts
     const int side = (int)threadIdx.x >> 6, w = lane_id();
+    tot = __ockl_wfred_add_i32(w < P ? M.cnt[w] : 0);  // (lane-parallel: a serial sum waits on one LDS read per list)
+    take = min(SCAN_K, tot);
     const int len = w < P ? M.len[w] : 0;
     const unsigned long long KN = side ? 0ull : ~0ull;
     const int IN = side ? -1 : 0x7fffffff;
+    // per round: the extreme head by two 32-bit wave reductions (high word, then the low word among the lanes holding
+    // that high word: DPP min / max steps on 32 bits, cheaper than one 64-bit reduction), the id reduction only when
+    // two heads hold equal keys; each lane has its list's next entry loaded ahead, so a winning lane's new head is in
+    // registers when the next round starts (a threshold merge -- candidates up to the extreme of the full lists' last
+    // entries, ranked by counting -- measured slower: 7.5 -> 10.8 us per merge at 1e5 iterations)
     int p = 0;
     unsigned long long k = len > 0 ? merge_key(M, side, w, 0) : KN;
     int id = len > 0 ? M.id[side][w][0] : IN;
@@ -2917,14 +2925,12 @@ __device__ void near_set_dist(const Ctx& C, int t, const double* q, int excl, bo
   TR();
   if (threadIdx.x == 0) {
     g_L.nk = tot; g_L.n_lo = take; g_L.n_hi = take; g_L.S.near_nodes += n;
-    if (nn) {  // the fused scan's nearest node: the (distance key, id) minimum of the slices
-      unsigned long long bk = M.nk[0];
-      int bi = M.ni[0];
-      for (int w = 1; w < P; ++w)
-        if (M.nk[w] < bk || (M.nk[w] == bk && M.ni[w] < bi)) { bk = M.nk[w]; bi = M.ni[w]; }
-      g_L.fnn_d = __longlong_as_double((long long)bk);
-      g_L.fnn_id = bi;
-    }
+  }
+  if (nn && threadIdx.x < 64) {  // the fused scan's nearest node: the (distance key, id) minimum of the slices
+    unsigned long long bk;
+    int bi;
+    merge_nearest(M, P, bk, bi);
+    if (threadIdx.x == 0) { g_L.fnn_d = __longlong_as_double((long long)bk); g_L.fnn_id = bi; }
   }
   __syncthreads();
 #ifdef SMP_SCAN_PROF

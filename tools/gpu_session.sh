@@ -13,6 +13,7 @@ step() {  # step NAME LIMIT CMD...
   echo "step $name rc $rc" | tee -a $OUT/steps.txt
   [ $rc -le 1 ] || exit $rc
 }
-step s1_tests 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py -k "planner_parity or distributed_scans or bench_workload or oracle_continues"
+step s1_tests 500 python -u -m pytest -x -q --timeout 400 --timeout-method thread tests/test_gpu_parity.py -k "distributed_scans or large_tree or oracle_continues or planner_parity"
+step b1_3e5 200 python -u bench.py --iterations 300000 --steps 1 --warmup 0 --no-cpu
 step s2_perf 200 python -u tools/perf_probe.py 4000 30000
-SMP_LIB=$PWD/squirrel_motion_planner_amd/lib/libsmp_gpu_trace.so step s12_trace 200 python -u tools/trace_probe.py 3100
+step s14_ttff 300 python -u tools/ttff_seeds.py 3 gpurun_out/r06_ttff_seeds_a.json

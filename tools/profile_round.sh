@@ -30,6 +30,9 @@ if [ -z "$SKIP_BENCH" ]; then
 fi
 if [ -z "$SKIP_KT" ]; then
   cd /tmp
-  timeout -k 10 ${KT_LIMIT:-400} rocprofv3 --kernel-trace --stats -d ${P}_prof_kt -o kt -- python3 $R/bench.py --no-cpu --steps 3 --warmup 1 "$@" > ${P}_kt.log 2>&1
+  # the traced run prints its own bench line (same steps / warmup as the bench): the kernel trace's mean plan_kernel
+  # dispatch and that line's ms_per_step come from one process, so kernel <= step is checkable within it
+  timeout -k 10 ${KT_LIMIT:-400} rocprofv3 --kernel-trace --stats -d ${P}_prof_kt -o kt -- python3 $R/bench.py --no-cpu --steps ${KT_STEPS:-20} --warmup ${KT_WARMUP:-5} "$@" > ${P}_kt.log 2>&1
   cd $R
+  grep '^{"metric"' ${P}_kt.log > ${P}_kt_bench.json || true
 fi
