@@ -170,6 +170,11 @@ __device__ __forceinline__ void chain_local(const RobotDev* __restrict__ rb, int
 
 __device__ __forceinline__ uint32_t shfl_u32(uint32_t v, int src) { return (uint32_t)__shfl((int)v, src); }
 
+// Inclusive prefix sum over the 64 lanes of a wavefront (all lanes active): ockl's DPP scan (row shifts and row
+// broadcasts, six VALU steps) instead of a shuffle tree, whose six ds_bpermute steps each wait an LDS round trip.
+extern "C" __device__ int __ockl_wfscan_add_i32(int, bool);
+__device__ __forceinline__ int wave_incl_scan(int v) { return __ockl_wfscan_add_i32(v, true); }
+
 // The scene's scalars in scalar registers.  A caller's SceneDev may live in private (scratch) memory -- the planner
 // keeps its context there -- and every use of a field would then be a scratch load, several of them dependent per
 // sphere centre (centre_cell) and per exact sweep (sphere_reach); read once here, they are wave-uniform SGPRs.
@@ -321,12 +326,8 @@ __device__ __forceinline__ int sweep_occupied(const SceneDev& sc, const double* 
     w = 0;
   }
   const int cnt = __popcll(w);
-  int inc = cnt;
-  for (int d = 1; d < 64; d <<= 1) {
-    const int v = __shfl_up(inc, d);
-    if (lane >= d) inc += v;
-  }
-  const int T = __shfl(inc, 63);
+  const int inc = wave_incl_scan(cnt);
+  const int T = __builtin_amdgcn_readlane(inc, 63);
   if (T > MAP_LIST) return 2;
   for (int pos = inc - cnt; w; ++pos) {
     const int bit = __builtin_ctzll(w);
@@ -385,11 +386,7 @@ __device__ __forceinline__ bool wave_map_staged(const RobotDev* __restrict__ rb,
       nb = sphere_bricks(sc, wc[s], rb->sph_r[s], lo, hi, b0, nbx);
       if (nb > 64) nb = 0;  // swept by wave_sphere_map (its per-cell loads)
     }
-    int inc = nb;
-    for (int d = 1; d < 64; d <<= 1) {
-      const int v = __shfl_up(inc, d);
-      if (lane >= d) inc += v;
-    }
+    const int inc = wave_incl_scan(nb);
     const bool staged = nb > 0 && base + inc <= CAP;
     const int start = base + inc - nb;
     if (s < nsph) off[s] = staged ? (OffT)start : NONE;
@@ -397,7 +394,7 @@ __device__ __forceinline__ bool wave_map_staged(const RobotDev* __restrict__ rb,
       for (int b = 0; b < nb; ++b) owner[start + b] = (uint8_t)s;
     spill[g] = __ballot(is_c && !staged);
     const uint64_t sm = __ballot(staged);
-    if (sm) base += __shfl(inc, 63 - __builtin_clzll(sm));
+    if (sm) base += __builtin_amdgcn_readlane(inc, 63 - __builtin_clzll(sm));
   }
   wave_sync();
   // one round: every staged word loaded (two slots per lane), then stored
@@ -624,10 +621,12 @@ __device__ __forceinline__ bool wave_prim_map(const SceneDev& sc, int ty, const 
     if (__ballot(rel == 2)) return true;
     // the undecided bricks, a lane per cell
     for (uint64_t um = __ballot(rel == 1); um;) {
-      const int src = __builtin_ctzll(um);
+      const int src = __builtin_ctzll(um);  // (wave-uniform: the brick's words and indices by v_readlane)
       um &= um - 1;
-      const uint32_t wlo = shfl_u32((uint32_t)w, src), whi = shfl_u32((uint32_t)(w >> 32), src);
-      const int sbi = __shfl(bi, src), sbj = __shfl(bj, src), sbk = __shfl(bk, src);
+      const uint32_t wlo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)w, src);
+      const uint32_t whi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(w >> 32), src);
+      const int sbi = __builtin_amdgcn_readlane(bi, src), sbj = __builtin_amdgcn_readlane(bj, src);
+      const int sbk = __builtin_amdgcn_readlane(bk, src);
       const bool set = ((lane < 32 ? wlo >> lane : whi >> (lane - 32)) & 1u) != 0;
       const bool hit = set && prim_cell(ty, h, pw, sc, 4 * sbi + (lane & 3), 4 * sbj + ((lane >> 2) & 3), 4 * sbk + (lane >> 4));
       if (__ballot(hit)) return true;

@@ -867,6 +867,9 @@ __device__ __forceinline__ int nearest_leader(const Ctx& C, int t, const double*
 __device__ __forceinline__ bool ki_less(unsigned long long ka, int ia, unsigned long long kb, int ib) {
   return ka < kb || (ka == kb && ia < ib);
 }
+// Lane i ^ 1 / i ^ 2 of a quad (DPP quad_perm, no LDS round trip; the whole quad active).
+__device__ __forceinline__ int quad_xor1(int v) { return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false); }
+__device__ __forceinline__ int quad_xor2(int v) { return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false); }
 // Wave-uniform lane read (v_readlane: scalar result, no LDS round trip).
 __device__ __forceinline__ unsigned long long readlane_u64(unsigned long long v, int l) {
   const unsigned lo = __builtin_amdgcn_readlane((int)(unsigned)v, l);
@@ -1590,8 +1593,8 @@ __device__ __forceinline__ bool slice_near_hist(gcdptr tq, gcdptr tc, int cap, i
           ci = X.ci[0][c];
           for (int j = sl; j < tot; j += 4) rank += ki_less(X.ck[0][j], X.ci[0][j], ck, ci);
         }
-        rank += __shfl_xor(rank, 1);
-        rank += __shfl_xor(rank, 2);
+        rank += quad_xor1(rank);
+        rank += quad_xor2(rank);
         if (c < tot && sl == 0) {
           if (rank < take_c) { X.lk[rank] = ck; X.li[rank] = ci; }
           const int h = tot - 1 - rank;
@@ -1623,23 +1626,19 @@ __device__ __forceinline__ bool slice_near_hist(gcdptr tq, gcdptr tc, int cap, i
       // lane l owns bins 4l .. 4l+3: inclusive cumulative counts (near_set)
       const unsigned h0 = X.hist[4 * lane], h1 = X.hist[4 * lane + 1];
       const unsigned h2 = X.hist[4 * lane + 2], h3 = X.hist[4 * lane + 3];
-      int inc = h0 + h1 + h2 + h3;
-      for (int off = 1; off < 64; off <<= 1) {
-        const int o = __shfl_up(inc, off);
-        if (lane >= off) inc += o;
-      }
+      const int inc = wave_incl_scan(h0 + h1 + h2 + h3);
       const int c3 = inc, c2 = c3 - (int)h3, c1 = c2 - (int)h2, c0b = c1 - (int)h1;
       const int e0 = c0b - (int)h0;
       const int flo = c0b >= take_c ? 0 : c1 >= take_c ? 1 : c2 >= take_c ? 2 : c3 >= take_c ? 3 : 4;
       const int Llo = __builtin_ctzll(__ballot(flo < 4));
-      const int blo = 4 * Llo + __shfl(flo, Llo);
-      const int cnt_lo = __shfl(flo == 0 ? c0b : flo == 1 ? c1 : flo == 2 ? c2 : c3, Llo);
+      const int blo = 4 * Llo + __builtin_amdgcn_readlane(flo, Llo);
+      const int cnt_lo = __builtin_amdgcn_readlane(flo == 0 ? c0b : flo == 1 ? c1 : flo == 2 ? c2 : c3, Llo);
       const int lim = tot - take_c;
       const int fhi = c2 <= lim ? 3 : c1 <= lim ? 2 : c0b <= lim ? 1 : e0 <= lim ? 0 : -1;
       const int Lhi = 63 - __builtin_clzll(__ballot(fhi >= 0));
-      const int fh = __shfl(fhi, Lhi);
+      const int fh = __builtin_amdgcn_readlane(fhi, Lhi);
       const int bhi = 4 * Lhi + fh;
-      const int cnt_hi = tot - __shfl(fhi == 3 ? c2 : fhi == 2 ? c1 : fhi == 1 ? c0b : e0, Lhi);
+      const int cnt_hi = tot - __builtin_amdgcn_readlane(fhi == 3 ? c2 : fhi == 2 ? c1 : fhi == 1 ? c0b : e0, Lhi);
       if (lane == 0) {
         X.hblo = blo;
         X.hbhi = bhi;
@@ -1706,8 +1705,8 @@ __device__ __forceinline__ bool slice_near_hist(gcdptr tq, gcdptr tc, int cap, i
           rank += e == 0 ? ki_less(ok, oi, ck, ci) : ki_less(ck, ci, ok, oi);
         }
       }
-      rank += __shfl_xor(rank, 1);
-      if (L == 4) rank += __shfl_xor(rank, 2);
+      rank += quad_xor1(rank);
+      if (L == 4) rank += quad_xor2(rank);
       if (c < m && sl == 0 && rank < take) {
         if (e == 0) { X.lk[rank] = ck; X.li[rank] = ci; }
         else { X.hk[rank] = ck; X.hi[rank] = ci; }
@@ -2018,8 +2017,8 @@ __device__ void near_set(const Ctx& C, int t, const double* q, int excl, bool sp
           ci = g_L.nh.ci[0][c];
           for (int j = sl; j < tot; j += 4) rank += ki_less(g_L.nh.ck[0][j], g_L.nh.ci[0][j], ck, ci);
         }
-        rank += __shfl_xor(rank, 1);
-        rank += __shfl_xor(rank, 2);
+        rank += quad_xor1(rank);
+        rank += quad_xor2(rank);
         if (c < tot && sl == 0) {
           if (rank < take_c) { g_L.lo_c[rank] = __longlong_as_double((long long)ck); g_L.lo_i[rank] = ci; }
           const int h = tot - 1 - rank;
@@ -2049,25 +2048,21 @@ __device__ void near_set(const Ctx& C, int t, const double* q, int excl, bool sp
       // lane l owns bins 4l .. 4l+3: inclusive cumulative counts
       const unsigned h0 = g_L.nh.hist[4 * lane], h1 = g_L.nh.hist[4 * lane + 1];
       const unsigned h2 = g_L.nh.hist[4 * lane + 2], h3 = g_L.nh.hist[4 * lane + 3];
-      int inc = h0 + h1 + h2 + h3;
-      for (int off = 1; off < 64; off <<= 1) {
-        const int o = __shfl_up(inc, off);
-        if (lane >= off) inc += o;
-      }
+      const int inc = wave_incl_scan(h0 + h1 + h2 + h3);
       const int c3 = inc, c2 = c3 - (int)h3, c1 = c2 - (int)h2, c0b = c1 - (int)h1;  // inclusive
       const int e0 = c0b - (int)h0;                                                   // exclusive of bin 4l
       // b_lo: first bin with inclusive count >= take_c
       const int flo = c0b >= take_c ? 0 : c1 >= take_c ? 1 : c2 >= take_c ? 2 : c3 >= take_c ? 3 : 4;
       const int Llo = __builtin_ctzll(__ballot(flo < 4));
-      const int blo = 4 * Llo + __shfl(flo, Llo);
-      const int cnt_lo = __shfl(flo == 0 ? c0b : flo == 1 ? c1 : flo == 2 ? c2 : c3, Llo);
+      const int blo = 4 * Llo + __builtin_amdgcn_readlane(flo, Llo);
+      const int cnt_lo = __builtin_amdgcn_readlane(flo == 0 ? c0b : flo == 1 ? c1 : flo == 2 ? c2 : c3, Llo);
       // b_hi: last bin whose exclusive count is <= tot - take_c (suffix count >= take_c)
       const int lim = tot - take_c;
       const int fhi = c2 <= lim ? 3 : c1 <= lim ? 2 : c0b <= lim ? 1 : e0 <= lim ? 0 : -1;
       const int Lhi = 63 - __builtin_clzll(__ballot(fhi >= 0));
-      const int fh = __shfl(fhi, Lhi);
+      const int fh = __builtin_amdgcn_readlane(fhi, Lhi);
       const int bhi = 4 * Lhi + fh;
-      const int cnt_hi = tot - __shfl(fhi == 3 ? c2 : fhi == 2 ? c1 : fhi == 1 ? c0b : e0, Lhi);
+      const int cnt_hi = tot - __builtin_amdgcn_readlane(fhi == 3 ? c2 : fhi == 2 ? c1 : fhi == 1 ? c0b : e0, Lhi);
       if (lane == 0) {
         g_L.nh.blo = blo;
         g_L.nh.bhi = bhi;
@@ -2134,8 +2129,8 @@ __device__ void near_set(const Ctx& C, int t, const double* q, int excl, bool sp
           rank += e == 0 ? ki_less(ok, oi, ck, ci) : ki_less(ck, ci, ok, oi);
         }
       }
-      rank += __shfl_xor(rank, 1);
-      if (L == 4) rank += __shfl_xor(rank, 2);
+      rank += quad_xor1(rank);
+      if (L == 4) rank += quad_xor2(rank);
       if (c < m && sl == 0 && rank < take) {
         if (e == 0) { g_L.lo_c[rank] = __longlong_as_double((long long)ck); g_L.lo_i[rank] = ci; }
         else { g_L.hi_c[take - 1 - rank] = __longlong_as_double((long long)ck); g_L.hi_i[take - 1 - rank] = ci; }
@@ -2447,7 +2442,7 @@ __device__ __forceinline__ void edge_validity_job(const Ctx& C, int E, int pslot
         if ((int)(v >> 32) == seq) { J.rmask[t] = (unsigned)v; J.rdone[t] = 1; }
         else ++left;
       }
-      for (int off = 32; off > 0; off >>= 1) left += __shfl_xor(left, off);
+      left = __ockl_wfred_add_i32(left);  // (DPP reduction: a shuffle tree costs six LDS-latency bpermutes)
       if (threadIdx.x == 0) {
         const unsigned long long now = wall_clock64();
         if (left != last_left) { last_left = left; t_prog = now; }
@@ -2472,7 +2467,7 @@ __device__ __forceinline__ void edge_validity_job(const Ctx& C, int E, int pslot
         int cand = 1 << 30;
         for (int t = threadIdx.x; t < nt; t += 64)
           if (!J.rdone[t]) { cand = t; break; }
-        for (int off = 32; off > 0; off >>= 1) cand = min(cand, __shfl_xor(cand, off));
+        cand = __ockl_wfred_min_i32(cand);
         if (threadIdx.x == 0) J.steal = cand < nt ? cand : -1;
       }
       __syncthreads();
@@ -3558,7 +3553,7 @@ __device__ int count_edges(int E, bool stop_first) {
     const int ev = (stop_first && mfree) ? __builtin_ctzll(mfree) : 64;
     int chk = 0, val = 0;
     if (need && e <= ev) { chk = f >= np1 ? np1 : f + 1; val = f >= np1 ? np1 : f; }
-    for (int off = 32; off > 0; off >>= 1) { chk += __shfl_xor(chk, off); val += __shfl_xor(val, off); }
+    chk = __ockl_wfred_add_i32(chk); val = __ockl_wfred_add_i32(val);
     if (e == 0) {
       g_L.S.prof[g_L.count_slot] += chk;
       g_L.S.checked += chk;
@@ -4243,7 +4238,7 @@ __device__ void rewire(const Ctx& C, int t) {
       const int ec = mc ? __builtin_ctzll(mc) : 64;
       int chk = 0, val = 0;
       if (act && e <= ec) { chk = f >= np1 ? np1 : f + 1; val = f >= np1 ? np1 : f; }
-      for (int off = 32; off > 0; off >>= 1) { chk += __shfl_xor(chk, off); val += __shfl_xor(val, off); }
+      chk = __ockl_wfred_add_i32(chk); val = __ockl_wfred_add_i32(val);
       if (e == 0) {
         g_L.S.prof[g_L.count_slot] += chk;
         g_L.S.checked += chk;
@@ -4455,7 +4450,7 @@ __device__ void connect_graphs(const Ctx& C, int t) {
           const int ev = m ? __builtin_ctzll(m) : 64;
           int chk = 0, val = 0;
           if (act && e <= ev) { chk = f >= np1 ? np1 : f + 1; val = f >= np1 ? np1 : f; }
-          for (int off = 32; off > 0; off >>= 1) { chk += __shfl_xor(chk, off); val += __shfl_xor(val, off); }
+          chk = __ockl_wfred_add_i32(chk); val = __ockl_wfred_add_i32(val);
           if (e == 0) {
             g_L.S.prof[g_L.count_slot] += chk;
             g_L.S.checked += chk;
