@@ -867,6 +867,8 @@ __device__ __forceinline__ int nearest_leader(const Ctx& C, int t, const double*
 __device__ __forceinline__ bool ki_less(unsigned long long ka, int ia, unsigned long long kb, int ib) {
   return ka < kb || (ka == kb && ia < ib);
 }
+// Lane i | 1 (the odd lane of lane i's pair: DPP quad_perm [1, 1, 3, 3], no LDS round trip; the whole quad active).
+__device__ __forceinline__ int odd_lane_of_pair(int v) { return __builtin_amdgcn_mov_dpp(v, 0xF5, 0xF, 0xF, false); }
 // Lane i ^ 1 / i ^ 2 of a quad (DPP quad_perm, no LDS round trip; the whole quad active).
 __device__ __forceinline__ int quad_xor1(int v) { return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false); }
 __device__ __forceinline__ int quad_xor2(int v) { return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false); }
@@ -2187,8 +2189,15 @@ __device__ void edge_costs(const Ctx& C, int E) {
   __syncthreads();
   if (threadIdx.x < E * 3) {
     int e = threadIdx.x / 3, k = threadIdx.x - e * 3;
+    // the segment norms in order (the reference's sum), all MAX_PTS loads issued before the first add: a runtime-bound
+    // loop waited one LDS round trip per segment
+    double sg[MAX_PTS];
+#pragma unroll
+    for (int s = 0; s < MAX_PTS; ++s) sg[s] = s < np ? g_L.u.seg[e][s][k] : 0.0;
     double acc = 0.0;
-    for (int s = 0; s < np; ++s) acc += g_L.u.seg[e][s][k];
+#pragma unroll
+    for (int s = 0; s < MAX_PTS; ++s)
+      if (s < np) acc += sg[s];
     g_L.eg_acc[e][k] = acc;
     g_L.eg_cost[e][k] = g_L.eg_base[e][k] + acc;
   }
@@ -3963,7 +3972,7 @@ __device__ __forceinline__ void sample_read(const Ctx& C) {
     const int pk = (int)threadIdx.x - 2 * NJ;
     const bool ok = threadIdx.x >= RING_G ||
                     ((unsigned)(v >> 32) == want && (pk < 0 || (unsigned)v == ring_param(pk, S.have_sol, S.cbest)));
-    const unsigned hi = (unsigned)__shfl((int)(unsigned)v, (threadIdx.x | 1) & 63);
+    const unsigned hi = (unsigned)odd_lane_of_pair((int)(unsigned)v);
     if (threadIdx.x < 2 * NJ && !(threadIdx.x & 1))
       g_L.xr[threadIdx.x >> 1] = __longlong_as_double((long long)(((unsigned long long)hi << 32) | (unsigned)v));
     const bool all = __ballot(!ok) == 0;
@@ -4096,21 +4105,23 @@ __device__ void cost_update(const Ctx& C, int t, int v, const double* red) {
 
 // choose_node_parent_interpolation, unconstrained (birrt_star.cpp:4594-4738, 4916-4935).
 // Uses g_L.lo_* (near list prefix) and g_L.xn / g_L.nn; may update g_L.xn, g_L.en_*; returns via g_L.ext_bp.
+// choose_parent's candidate prefix (birrt_star.cpp:4594-4620): the near nodes in (cost, id) order up to the first whose
+// cost is not below x_new's, at most max_near -- wave 0, one lane per list entry, the prefix length by a ballot (a loop
+// on one thread waited one LDS round trip per entry).  Returns the count in every lane of wave 0 (0 without near nodes).
+__device__ __forceinline__ int choose_prefix() {
+  const int lane = lane_id();
+  const int m = g_L.nk > 0 ? min(g_L.n_lo, g_L.S.max_near) : 0;
+  const bool below = lane < m && g_L.lo_c[lane] < g_L.xn.c[0];
+  return min(m, (int)__builtin_ctzll(~__ballot(below)));  // (m <= 20: lane 63 is never `below`)
+}
 __device__ void choose_parent(const Ctx& C, int t) {
-  if (threadIdx.x == 0) {
-    g_L.ext_bp = 0;
-    g_L.found = -1;
-    g_L.cnt = 0;
-    if (g_L.nk > 0) {
-      g_L.xn.parent = g_L.nn.id;
-      // candidate prefix: stop at the first near node whose cost is not below x_new's
-      int m = min(g_L.n_lo, g_L.S.max_near);
-      int E = 0;
-      for (int i = 0; i < m; ++i) {
-        if (!(g_L.lo_c[i] < g_L.xn.c[0])) break;
-        E++;
-      }
+  if (threadIdx.x < 64) {
+    const int E = choose_prefix();  // candidate prefix: stop at the first near node whose cost is not below x_new's
+    if (threadIdx.x == 0) {
+      g_L.ext_bp = 0;
+      g_L.found = -1;
       g_L.cnt = E;
+      if (g_L.nk > 0) g_L.xn.parent = g_L.nn.id;
     }
   }
   __syncthreads();
@@ -5309,7 +5320,7 @@ __device__ void scout_iteration(const Ctx& C, long long it, int t, int X, int op
       if (threadIdx.x < 2 * NJ) v = ld_agent(&lb->ring[it % SMP_RING].g[threadIdx.x]);
       const bool cur = threadIdx.x >= 2 * NJ || (unsigned)(v >> 32) == want;
       if (__ballot(!cur) == 0) {
-        const unsigned hi = (unsigned)__shfl((int)(unsigned)v, (threadIdx.x | 1) & 63);
+        const unsigned hi = (unsigned)odd_lane_of_pair((int)(unsigned)v);
         if (threadIdx.x < 2 * NJ && !(threadIdx.x & 1))
           g_L.xr[threadIdx.x >> 1] = __longlong_as_double((long long)(((unsigned long long)hi << 32) | (unsigned)v));
         ok = 1;
@@ -5496,17 +5507,12 @@ redo:
   TR();
   if (sc_moved(C)) return;
   // choose_parent's candidate edges (all needed ones checked: the job computes every tile)
-  if (threadIdx.x == 0) {
-    int E = 0;
-    if (g_L.nk > 0) {
-      const int m = min(g_L.n_lo, S.max_near);
-      for (int i = 0; i < m; ++i) {
-        if (!(g_L.lo_c[i] < g_L.xn.c[0])) break;
-        E++;
-      }
+  if (threadIdx.x < 64) {
+    const int E = choose_prefix();
+    if (threadIdx.x == 0) {
+      g_L.cnt = E;
+      g_L.found = -1;
     }
-    g_L.cnt = E;
-    g_L.found = -1;
   }
   __syncthreads();
   const int E = uni(g_L.cnt);
@@ -5532,10 +5538,13 @@ redo:
       for (int k = 0; k < 3; ++k) w.acc[k] = g_L.eg_acc[e][k];
       w.first = g_L.eg_need[e] ? g_L.eg_first[e] : -1;
     }
-    if (threadIdx.x == 0) {
-      R.n_choose = E;
-      for (int e = 0; e < E; ++e)
-        if (g_L.eg_need[e] && g_L.eg_first[e] > S.n_pts) { g_L.found = e; break; }
+    if (threadIdx.x < 64) {  // the first needed candidate that is free (ballot: E <= 20)
+      const bool fr = (int)threadIdx.x < E && g_L.eg_need[threadIdx.x] && g_L.eg_first[threadIdx.x] > S.n_pts;
+      const unsigned long long fm = __ballot(fr);
+      if (threadIdx.x == 0) {
+        R.n_choose = E;
+        if (fm) g_L.found = (int)__builtin_ctzll(fm);
+      }
     }
     __syncthreads();
   }

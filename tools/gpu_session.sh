@@ -13,10 +13,6 @@ step() {  # step NAME LIMIT CMD...
   echo "step $name rc $rc" | tee -a $OUT/steps.txt
   [ $rc -le 1 ] || exit $rc
 }
-step s1_tests 500 python -u -m pytest -x -q --timeout 400 --timeout-method thread tests/test_gpu_tree_scans.py tests/test_gpu_collisions.py tests/test_gpu_parity.py -k "tree_scans or fp32 or collision or tile or check or distributed_scans or planner_parity or bench_workload"
-step s2_perf 200 python -u tools/perf_probe.py 4000 30000
-step s6_tile 300 python -u tools/tile_probe.py
-step b1_3e5 200 python -u bench.py --iterations 300000 --steps 1 --warmup 0 --no-cpu
-cd /tmp && export TMPDIR=/tmp
-timeout -k 10 120 rocprofv3 -L > $OUT/s15_counters.txt 2>&1; echo "list rc $?" >> $OUT/steps.txt
-timeout -s KILL 120 rocprofv3 --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS -d $OUT/s16_pmc -o pmc -- python3 $GRAFT_REPO_ROOT/tools/perf_probe.py 4000 > $OUT/s16_pmc.log 2>&1; echo "pmc rc $?" >> $OUT/steps.txt
+step t_sub 500 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_pre_refresh.py -k "planner_parity or bench_workload or large_tree or refreshed or early_ask or distributed"
+step e0 120 python -u tools/perf_probe.py 4000 30000
+step e7 120 python -u tools/perf_probe.py 4000
