@@ -251,7 +251,10 @@ __global__ void sqrt_div_kernel(const double* a, const double* b, int n, double*
 constexpr int SCAN_K = 20;  // near-list ends a scan keeps (near_set<20>; max_near_nodes <= 20)
 constexpr int NEAR_BINS = 256;   // near_set register path: cost histogram bins
 constexpr int NEAR_BUF = 128;    // near_set register path: candidate buffer entries per end
-constexpr int NEAR_NBK = 16;     // near_set register path: 64-node batches per wave held in registers
+#ifndef SMP_NEAR_NBK
+#define SMP_NEAR_NBK 16
+#endif
+constexpr int NEAR_NBK = SMP_NEAR_NBK;  // near_set register path: 64-node batches per wave held in registers
 struct ScanLds {
   union {
     struct {  // slice_near_body (per-wave sorted lists)
@@ -259,7 +262,7 @@ struct ScanLds {
       int wli[BLOCK / 64][SCAN_K], whi[BLOCK / 64][SCAN_K];
     };
     struct {  // slice_near_hist (near_set's register path): cost histogram and the two candidate buffers
-      unsigned hist[NEAR_BINS];
+      alignas(16) unsigned hist[NEAR_BINS];
       unsigned long long ck[2][NEAR_BUF];
       int ci[2][NEAR_BUF];
     };
@@ -274,9 +277,13 @@ struct ScanLds {
   unsigned long long wk[BLOCK / 64];
   int wi[BLOCK / 64];
 };
+constexpr int MERGE_LS = SCAN_K | 1;  // words per participant list in MergeLds (odd: conflict-free lane-per-list reads)
 struct MergeLds {
-  unsigned kw[2][SCAN_PNEAR][SCAN_K][2];  // [0] lows ascending, [1] highs descending, per participant: key halves
-  int id[2][SCAN_PNEAR][SCAN_K];
+  // [0] lows ascending, [1] highs descending, per participant: key halves and ids.  A list takes MERGE_LS (odd) words:
+  // the tournament's lane w reads list w, and an odd stride puts the 32 lists' heads in 32 different LDS banks (a
+  // stride of 40 words -- the key halves interleaved -- put every 8th list in one bank: 16-way conflicts per read)
+  unsigned kl[2][SCAN_PNEAR][MERGE_LS], kh[2][SCAN_PNEAR][MERGE_LS];
+  int id[2][SCAN_PNEAR][MERGE_LS];
   int len[SCAN_P], cnt[SCAN_P], done[SCAN_P], bad[SCAN_P];
   unsigned hv[SCAN_P][3];             // collection: near header (count, take) / nearest (key halves, id)
   unsigned hn[SCAN_PNEAR][3];         // collection: a fused scan's nearest (key halves, id)
@@ -285,7 +292,7 @@ struct MergeLds {
   int ndone, go[2], steal;
 };
 __device__ __forceinline__ unsigned long long merge_key(const MergeLds& M, int s, int w, int e) {
-  return (unsigned long long)M.kw[s][w][e][1] << 32 | M.kw[s][w][e][0];
+  return (unsigned long long)M.kh[s][w][e] << 32 | M.kl[s][w][e];
 }
 // LDS of job mode (leader and helper kernel): the published job + one job tile.
 struct JobLds {
@@ -352,7 +359,7 @@ struct PlanLds {
         int wtot[BLOCK / 64];
       } nr;
       struct {  // near_set, register path: cost histogram and the two candidate buffers
-        unsigned hist[NEAR_BINS];
+        alignas(16) unsigned hist[NEAR_BINS];
         unsigned long long ck[2][NEAR_BUF];
         int ci[2][NEAR_BUF];
         unsigned long long wmin[BLOCK / 64], wmax[BLOCK / 64];
@@ -1626,8 +1633,8 @@ __device__ __forceinline__ bool slice_near_hist(gcdptr tq, gcdptr tc, int cap, i
     if (pf && threadIdx.x == 0) pf[8]++;
     if (wave == 0) {
       // lane l owns bins 4l .. 4l+3: inclusive cumulative counts (near_set)
-      const unsigned h0 = X.hist[4 * lane], h1 = X.hist[4 * lane + 1];
-      const unsigned h2 = X.hist[4 * lane + 2], h3 = X.hist[4 * lane + 3];
+      const uint4 hv = reinterpret_cast<const uint4*>(X.hist)[lane];  // (one 16-byte read: a stride of 4 words per lane
+      const unsigned h0 = hv.x, h1 = hv.y, h2 = hv.z, h3 = hv.w;        // read word by word met 4-way bank conflicts)
       const int inc = wave_incl_scan(h0 + h1 + h2 + h3);
       const int c3 = inc, c2 = c3 - (int)h3, c1 = c2 - (int)h2, c0b = c1 - (int)h1;
       const int e0 = c0b - (int)h0;
@@ -2048,8 +2055,8 @@ __device__ void near_set(const Ctx& C, int t, const double* q, int excl, bool sp
     NEAR_CLOCK(2);
     if (wave == 0) {
       // lane l owns bins 4l .. 4l+3: inclusive cumulative counts
-      const unsigned h0 = g_L.nh.hist[4 * lane], h1 = g_L.nh.hist[4 * lane + 1];
-      const unsigned h2 = g_L.nh.hist[4 * lane + 2], h3 = g_L.nh.hist[4 * lane + 3];
+      const uint4 hv = reinterpret_cast<const uint4*>(g_L.nh.hist)[lane];  // (one 16-byte read per lane)
+      const unsigned h0 = hv.x, h1 = hv.y, h2 = hv.z, h3 = hv.w;
       const int inc = wave_incl_scan(h0 + h1 + h2 + h3);
       const int c3 = inc, c2 = c3 - (int)h3, c1 = c2 - (int)h2, c0b = c1 - (int)h1;  // inclusive
       const int e0 = c0b - (int)h0;                                                   // exclusive of bin 4l
@@ -2676,8 +2683,8 @@ __device__ __forceinline__ void merge_put(MergeLds& M, const ScanLds& X, int nea
     if (threadIdx.x < SCAN_K) {
       const int e = threadIdx.x;
       if (e < take) {
-        M.kw[0][w][e][0] = (unsigned)X.lk[e]; M.kw[0][w][e][1] = (unsigned)(X.lk[e] >> 32); M.id[0][w][e] = X.li[e];
-        M.kw[1][w][e][0] = (unsigned)X.hk[e]; M.kw[1][w][e][1] = (unsigned)(X.hk[e] >> 32); M.id[1][w][e] = X.hi[e];
+        M.kl[0][w][e] = (unsigned)X.lk[e]; M.kh[0][w][e] = (unsigned)(X.lk[e] >> 32); M.id[0][w][e] = X.li[e];
+        M.kl[1][w][e] = (unsigned)X.hk[e]; M.kh[1][w][e] = (unsigned)(X.hk[e] >> 32); M.id[1][w][e] = X.hi[e];
       }
     }
     if (threadIdx.x == 0) { M.len[w] = take; M.cnt[w] = X.cnt; }
@@ -2775,7 +2782,8 @@ __device__ void scan_run(const Ctx& C, int near, int t, const double* q, int i0,
               const int j = i - 2, side = j >= 3 * SCAN_K ? 1 : 0, jj = j - side * 3 * SCAN_K, e = jj / 3, f = jj - 3 * e;
               if (e < min((int)M.hv[w][1], SCAN_K)) {
                 if (!((okm >> u) & 1u)) M.bad[w] = 1;
-                else if (f < 2) M.kw[side][w][e][f] = val[u];
+                else if (f == 0) M.kl[side][w][e] = val[u];
+                else if (f == 1) M.kh[side][w][e] = val[u];
                 else M.id[side][w][e] = (int)val[u];
               }
             }
