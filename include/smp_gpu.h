@@ -64,7 +64,9 @@ enum {
   SMP_ERR_START_INVALID = -2, /* start configuration in collision (birrt_star.cpp:353-357) */
   SMP_ERR_GOAL_INVALID = -3,  /* goal configuration in collision (birrt_star.cpp:358-362) */
   SMP_ERR_NO_SOLUTION = -4,   /* budget exhausted without a path (birrt_star.cpp:1405) */
-  SMP_ERR_HIP = -5,           /* HIP runtime error */
+  SMP_ERR_HIP = -5,           /* HIP runtime error, or a launch the call gave up waiting for (a seconds budget's
+                                 4x + 60 s): the planner then sets its abort word, which every leader polls each 64
+                                 iterations, and answers SMP_ERR_HIP to every call until that launch has drained */
   SMP_ERR_PARSE = -6,         /* model / octomap parse error */
   SMP_ERR_CAPACITY = -7,      /* tree capacity exceeded (raise smp_params.node_capacity) */
   SMP_ERR_NO_DEVICE = -8      /* no usable GPU: the library never falls back to the CPU */

@@ -13,8 +13,6 @@ step() {  # step NAME LIMIT CMD...
   echo "step $name rc $rc" | tee -a $OUT/steps.txt
   [ $rc -le 1 ] || exit $rc
 }
-step t_sub 500 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_tree_scans.py tests/test_gpu_parity.py -k "tree_scans or fp32 or distributed or large_tree or oracle_continues or planner_parity"
-SMP_LIB=$PWD/squirrel_motion_planner_amd/lib/libsmp_gpu_trace1e5.so step s13_trace1e5 300 python -u tools/trace_probe.py 100100
-step perf 200 python -u tools/perf_probe.py 4000 30000
-step b3e5 200 python -u bench.py --iterations 300000 --steps 1 --warmup 0 --no-cpu
-step nstep 200 python -u tools/near_step_probe.py 30000
+step t_all 900 python -u -m pytest -x -q --timeout 400 --timeout-method thread -m gpu tests
+step smoke 120 python -c "import __graft_entry__ as g; g.smoke()"
+step bench 400 python -u bench.py --steps 20 --warmup 5
