@@ -1444,8 +1444,11 @@ __device__ __forceinline__ bool slice_near_hist(gcdptr tq, gcdptr tc, int cap, i
   const float kA = f32_down(r2lo - K2 - slack), kB = f32_up(r2hi + K2 + slack);
   const float kM = f32_up(6.0 * F32_U * K1), kM2 = f32_up(32.0 * 36.0 * F32_U * F32_U);
   int tot_all = 0;  // near nodes of the chunks before this one (block-uniform)
-  if (threadIdx.x == 0) X.take = 0;
-  __syncthreads();
+  int prev = 0;     // both running lists hold this many entries (block-uniform; X.take once the scan is done)
+  // Three barriers per chunk: the chunk's min / max, its histogram, its gathered candidates.  Every wave derives the
+  // bins of the K-th entries from the histogram itself (no barrier after a one-wave prefix), the running lists enter the
+  // candidate buffers before the histogram's barrier, and the ranked lists need no barrier of their own: the next
+  // chunk reads them only after its first barrier, the caller after the last one.
   for (int c0 = i0; c0 < i1; c0 += CH) {
     unsigned long long key[NEAR_NBK];
     unsigned nmask = 0;
@@ -1569,7 +1572,6 @@ __device__ __forceinline__ bool slice_near_hist(gcdptr tq, gcdptr tc, int cap, i
       continue;
     }
     const int take_c = min(K, tot);
-    const int prev = X.take;  // both running lists hold this many entries
     if (uni(tot <= NEAR_BUF && prev == 0)) {
       // few near nodes and no running lists: every near node of the chunk into one buffer (wave w's at the wave prefix
       // of the counts), each ranked by counting -- rank r below K is the r-th lowest entry, m - 1 - r below K the
@@ -1611,9 +1613,7 @@ __device__ __forceinline__ bool slice_near_hist(gcdptr tq, gcdptr tc, int cap, i
         }
       }
       tot_all += tot;
-      __syncthreads();
-      if (threadIdx.x == 0) X.take = take_c;
-      __syncthreads();
+      prev = take_c;
       SNH_CLOCK(2);
       if (pf && threadIdx.x == 0) pf[7]++;
       continue;
@@ -1628,34 +1628,7 @@ __device__ __forceinline__ bool slice_near_hist(gcdptr tq, gcdptr tc, int cap, i
         bins[b >> 2] |= (unsigned)bin << (8 * (b & 3));
         atomicAdd(&X.hist[bin], 1u);
       }
-    __syncthreads();
-    SNH_CLOCK(2);
-    if (pf && threadIdx.x == 0) pf[8]++;
-    if (wave == 0) {
-      // lane l owns bins 4l .. 4l+3: inclusive cumulative counts (near_set)
-      const uint4 hv = reinterpret_cast<const uint4*>(X.hist)[lane];  // (one 16-byte read: a stride of 4 words per lane
-      const unsigned h0 = hv.x, h1 = hv.y, h2 = hv.z, h3 = hv.w;        // read word by word met 4-way bank conflicts)
-      const int inc = wave_incl_scan(h0 + h1 + h2 + h3);
-      const int c3 = inc, c2 = c3 - (int)h3, c1 = c2 - (int)h2, c0b = c1 - (int)h1;
-      const int e0 = c0b - (int)h0;
-      const int flo = c0b >= take_c ? 0 : c1 >= take_c ? 1 : c2 >= take_c ? 2 : c3 >= take_c ? 3 : 4;
-      const int Llo = __builtin_ctzll(__ballot(flo < 4));
-      const int blo = 4 * Llo + __builtin_amdgcn_readlane(flo, Llo);
-      const int cnt_lo = __builtin_amdgcn_readlane(flo == 0 ? c0b : flo == 1 ? c1 : flo == 2 ? c2 : c3, Llo);
-      const int lim = tot - take_c;
-      const int fhi = c2 <= lim ? 3 : c1 <= lim ? 2 : c0b <= lim ? 1 : e0 <= lim ? 0 : -1;
-      const int Lhi = 63 - __builtin_clzll(__ballot(fhi >= 0));
-      const int fh = __builtin_amdgcn_readlane(fhi, Lhi);
-      const int bhi = 4 * Lhi + fh;
-      const int cnt_hi = tot - __builtin_amdgcn_readlane(fhi == 3 ? c2 : fhi == 2 ? c1 : fhi == 1 ? c0b : e0, Lhi);
-      if (lane == 0) {
-        X.hblo = blo;
-        X.hbhi = bhi;
-        X.fast = cnt_lo + prev <= NEAR_BUF && cnt_hi + prev <= NEAR_BUF;
-        X.hcnt[0] = prev;  // the running lists take the first buffer slots
-        X.hcnt[1] = prev;
-      }
-    }
+    // the running lists take the first buffer slots (no wave reads the buffers until after the gather's barrier)
     if (threadIdx.x < prev) {
       X.ck[0][threadIdx.x] = X.lk[threadIdx.x];
       X.ci[0][threadIdx.x] = X.li[threadIdx.x];
@@ -1664,13 +1637,37 @@ __device__ __forceinline__ bool slice_near_hist(gcdptr tq, gcdptr tc, int cap, i
       X.ck[1][threadIdx.x - 64] = X.hk[threadIdx.x - 64];
       X.ci[1][threadIdx.x - 64] = X.hi[threadIdx.x - 64];
     }
+    if (threadIdx.x == 0) { X.hcnt[0] = prev; X.hcnt[1] = prev; }
     __syncthreads();
+    SNH_CLOCK(2);
+    if (pf && threadIdx.x == 0) pf[8]++;
+    int blo, bhi;
+    bool fast;
+    {
+      // lane l owns bins 4l .. 4l+3: inclusive cumulative counts (near_set)
+      const uint4 hv = reinterpret_cast<const uint4*>(X.hist)[lane];  // (one 16-byte read: a stride of 4 words per lane
+      const unsigned h0 = hv.x, h1 = hv.y, h2 = hv.z, h3 = hv.w;        // read word by word met 4-way bank conflicts)
+      const int inc = wave_incl_scan(h0 + h1 + h2 + h3);
+      const int c3 = inc, c2 = c3 - (int)h3, c1 = c2 - (int)h2, c0b = c1 - (int)h1;
+      const int e0 = c0b - (int)h0;
+      const int flo = c0b >= take_c ? 0 : c1 >= take_c ? 1 : c2 >= take_c ? 2 : c3 >= take_c ? 3 : 4;
+      const int Llo = __builtin_ctzll(__ballot(flo < 4));
+      const int blo_w = 4 * Llo + __builtin_amdgcn_readlane(flo, Llo);
+      const int cnt_lo = __builtin_amdgcn_readlane(flo == 0 ? c0b : flo == 1 ? c1 : flo == 2 ? c2 : c3, Llo);
+      const int lim = tot - take_c;
+      const int fhi = c2 <= lim ? 3 : c1 <= lim ? 2 : c0b <= lim ? 1 : e0 <= lim ? 0 : -1;
+      const int Lhi = 63 - __builtin_clzll(__ballot(fhi >= 0));
+      const int fh = __builtin_amdgcn_readlane(fhi, Lhi);
+      const int cnt_hi = tot - __builtin_amdgcn_readlane(fhi == 3 ? c2 : fhi == 2 ? c1 : fhi == 1 ? c0b : e0, Lhi);
+      blo = blo_w;
+      bhi = 4 * Lhi + fh;
+      fast = cnt_lo + prev <= NEAR_BUF && cnt_hi + prev <= NEAR_BUF;
+    }
     SNH_CLOCK(3);
-    if (!uni(X.fast)) {
+    if (!fast) {  // (wave-uniform, the same in every wave)
       __syncthreads();
       return false;
     }
-    const int blo = X.hblo, bhi = X.hbhi;
     // gather in one pass: a candidate takes its buffer slot with an LDS atomic (the buffers' order does not matter: the
     // rank below counts (key, id) pairs, which are distinct)
 #pragma unroll
@@ -1722,12 +1719,10 @@ __device__ __forceinline__ bool slice_near_hist(gcdptr tq, gcdptr tc, int cap, i
       }
     }
     tot_all += tot;
-    __syncthreads();
-    if (threadIdx.x == 0) X.take = take;
-    __syncthreads();
+    prev = take;
     SNH_CLOCK(5);
   }
-  if (threadIdx.x == 0) X.cnt = tot_all;
+  if (threadIdx.x == 0) { X.cnt = tot_all; X.take = prev; }
   __syncthreads();
   if (NN && F32) nn32_finish(tqc, i0, i1, qq, qm, b1, b2, bi1, cm, X);
   else if (NN) slice_nn_reduce(nb, nbi, X);
