@@ -2159,6 +2159,40 @@ __device__ __noinline__ void near_set_scan(const Ctx& C, int t, const double* q,
 }
 
 // --------------------------------------------------------------------------------------- edges
+// Bit j set: joint j is revolute (RobotDev::rev as one register).
+__device__ __forceinline__ unsigned rev_mask(const RobotDev* rb) {
+  unsigned m = 0;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) m |= (rb->rev[j] != 0 ? 1u : 0u) << j;
+  return m;
+}
+
+// A double from lane l (two v_readlane: a wave-uniform value in scalar registers).
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), l);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// Segment s of the interpolated edge st -> st + np * stp: its total / revolute / prismatic norms
+// (compute_edge_cost_interpolation's per-segment terms, birrt_star.cpp:4162-4242; the joint sums in joint order).
+__device__ __forceinline__ void seg_norms(unsigned rm, const double* st, const double* stp, int s, double& t, double& r,
+                                          double& p) {
+  t = 0.0; r = 0.0; p = 0.0;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const double a = st[j] + s * stp[j];
+    const double b = st[j] + (s + 1) * stp[j];
+    const double d = (b - a) * (b - a);
+    t += d * 1.0;
+    const bool rv = (rm >> j) & 1u;
+    r += rv ? d : 0.0;
+    p += rv ? 0.0 : d;
+  }
+  t = sqrt(t); r = sqrt(r); p = sqrt(p);
+}
+
 // connectNodesInterpolation + compute_edge_cost_interpolation (birrt_star.cpp:4380-4440, 4443-4526,
 // 4162-4242) for E <= MAXE edges eg_start -> eg_target, base costs eg_base.  Segment norms in parallel,
 // ordered sums per edge.  Fills eg_step, eg_end (the child configuration) and eg_cost.
@@ -2174,28 +2208,26 @@ __device__ void edge_costs(const Ctx& C, int E) {
     g_L.eg_end[e][j] = g_L.eg_start[e][j] + np * st;
   }
   __syncthreads();
+  const unsigned rm = rev_mask(rb);
   for (int it = threadIdx.x; it < E * np; it += BLOCK) {
-    int e = it / np, s = it - e * np;
-    double t = 0.0, r = 0.0, p = 0.0;
-    for (int j = 0; j < NJ; ++j) {
-      double a = g_L.eg_start[e][j] + s * g_L.eg_step[e][j];
-      double b = g_L.eg_start[e][j] + (s + 1) * g_L.eg_step[e][j];
-      double d = (b - a) * (b - a);
-      t += d * 1.0;
-      if (rb->rev[j]) r += d; else p += d;
-    }
-    g_L.u.seg[e][s][0] = sqrt(t);
-    g_L.u.seg[e][s][1] = sqrt(r);
-    g_L.u.seg[e][s][2] = sqrt(p);
+    const int e = it / np, s = it - e * np;
+    double st[NJ], stp[NJ], t, r, p;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) { st[j] = g_L.eg_start[e][j]; stp[j] = g_L.eg_step[e][j]; }
+    seg_norms(rm, st, stp, s, t, r, p);
+    g_L.u.seg[e][s][0] = t;
+    g_L.u.seg[e][s][1] = r;
+    g_L.u.seg[e][s][2] = p;
   }
   __syncthreads();
   if (threadIdx.x < E * 3) {
     int e = threadIdx.x / 3, k = threadIdx.x - e * 3;
-    // the segment norms in order (the reference's sum), all MAX_PTS loads issued before the first add: a runtime-bound
-    // loop waited one LDS round trip per segment
+    // the segment norms in order (the reference's sum), all MAX_PTS loads issued before the first add, unconditionally
+    // (a runtime-bound loop, or loads under `s < np`, waited one LDS round trip per segment; the words past np are
+    // read and not added)
     double sg[MAX_PTS];
 #pragma unroll
-    for (int s = 0; s < MAX_PTS; ++s) sg[s] = s < np ? g_L.u.seg[e][s][k] : 0.0;
+    for (int s = 0; s < MAX_PTS; ++s) sg[s] = g_L.u.seg[e][s][k];
     double acc = 0.0;
 #pragma unroll
     for (int s = 0; s < MAX_PTS; ++s)
@@ -3577,75 +3609,161 @@ __device__ int count_edges(int E, bool stop_first) {
   return uni(g_L.found);
 }
 
-// stepTowardsRandSample (birrt_star.cpp:5712-5868), single lane.
-__device__ bool step_towards(const RobotDev* rb, const double* nn, double* x, double f) {
+// stepTowardsRandSample (birrt_star.cpp:5712-5868), one lane (or every lane of a wave on the same values).  The
+// revolute / prismatic split is a select on the mask bit, not a branch: a sum takes +0.0 for the joints of the other
+// kind, which leaves it unchanged bit for bit (the sums are of squares, never -0.0), and a joint of a finished kind
+// keeps 0.0 as the reference's extension does.
+__device__ __forceinline__ bool step_towards_m(unsigned rm, const double* nn, double* x, double f) {
   double ed[NJ], srev = 0.0, spr = 0.0;
+#pragma unroll
   for (int j = 0; j < NJ; ++j) {
+    const bool rv = (rm >> j) & 1u;
     ed[j] = x[j] - nn[j];
-    double d = ed[j] * ed[j];
-    if (rb->rev[j]) srev += d; else spr += d;
+    const double d = ed[j] * ed[j];
+    srev += rv ? d : 0.0;
+    spr += rv ? 0.0 : d;
   }
-  double lrev = sqrt(srev), lpr = sqrt(spr);
-  bool rev_done = lrev < 0.001, pr_done = lpr < 0.001;
+  const double lrev = sqrt(srev), lpr = sqrt(spr);
+  const bool rev_done = lrev < 0.001, pr_done = lpr < 0.001;
   double ext[NJ];
   srev = 0.0; spr = 0.0;
+#pragma unroll
   for (int j = 0; j < NJ; ++j) {
-    ext[j] = 0.0;
-    if (!rb->rev[j]) {
-      if (!pr_done) { ed[j] = ed[j] / lpr; double c = f * ed[j]; ext[j] = nn[j] + c; spr += c * c; }
-    } else {
-      if (!rev_done) { ed[j] = ed[j] / lrev; double c = f * ed[j]; ext[j] = nn[j] + c; srev += c * c; }
-    }
+    const bool rv = (rm >> j) & 1u;
+    const bool done = rv ? rev_done : pr_done;
+    const double c = f * (ed[j] / (rv ? lrev : lpr));
+    ext[j] = done ? 0.0 : nn[j] + c;
+    const double cc = done ? 0.0 : c * c;
+    srev += rv ? cc : 0.0;
+    spr += rv ? 0.0 : cc;
   }
-  double elp = spr == 0.0 ? 1000.0 : sqrt(spr);
-  double elr = srev == 0.0 ? 1000.0 : sqrt(srev);
-  bool reached = true;
-  if (elr < lrev) { for (int j = 0; j < NJ; ++j) if (rb->rev[j]) x[j] = ext[j]; reached = false; }
-  if (elp < lpr) { for (int j = 0; j < NJ; ++j) if (!rb->rev[j]) x[j] = ext[j]; reached = false; }
-  return reached;
+  const double elp = spr == 0.0 ? 1000.0 : sqrt(spr);
+  const double elr = srev == 0.0 ? 1000.0 : sqrt(srev);
+  const bool tr = elr < lrev, tp = elp < lpr;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const bool rv = (rm >> j) & 1u;
+    if (rv ? tr : tp) x[j] = ext[j];
+  }
+  return !(tr || tp);
+}
+__device__ bool step_towards(const RobotDev* rb, const double* nn, double* x, double f) {
+  return step_towards_m(rev_mask(rb), nn, x, f);
 }
 
 // Stepping loop shared by choose_parent / connectGraphs: from `cur` towards `target` with
 // unconstraint_extend_step_factor, collecting via nodes (ids nn_t, nn_t+1, ...) until the target is
 // reached; the last edge becomes `sel` (id nn_t at that point).  No collision checks (reference behaviour).
+// Wave 0 alone, the chain's state in registers (every lane holds the same values; lane s of the first half forms
+// segment s of a step's edge cost as edge_costs does): no barrier per step.  On return g_L.cur, ox, reached, nn_t,
+// n_via and edge slot 0 hold what the last step left, as a step-by-step block loop would.
+__device__ __noinline__ void via_chain_w(const Ctx& C, const double* target) {
+  const int lane = lane_id(), s = lane & 31;
+  const int np = g_L.S.n_pts, via_cap = g_L.S.via_cap;
+  const double f = g_L.S.step;
+  double cur[NJ], cc[3], tg[NJ], ox[NJ], stp[NJ], end[NJ], acc[3], cost[3];
+  int cid = g_L.cur.id, cpar = g_L.cur.parent;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) { cur[j] = g_L.cur.q[j]; tg[j] = target[j]; }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) cc[k] = g_L.cur.c[k];
+  int nn_t = g_L.nn_t, n_via = g_L.n_via, nsteps = 0;
+  const unsigned rm = rev_mask(&g_rb);
+  bool reached, overflow = false;
+  double lst[NJ], lcc[3];  // the last step's edge start and base cost (edge slot 0)
+  for (;;) {
+    ++nsteps;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) ox[j] = tg[j];
+    reached = step_towards_m(rm, cur, ox, f);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      stp[j] = (ox[j] - cur[j]) / double(np);
+      end[j] = cur[j] + np * stp[j];
+    }
+    double t, r, p;
+    seg_norms(rm, cur, stp, s, t, r, p);
+    // the ordered sums (edge_costs' third stage): lanes 0..2 sum the segments through LDS (in order; one wave, so
+    // its LDS writes are seen by its later reads), and every lane takes the three sums by v_readlane
+    if (lane < np) { g_L.u.seg[0][lane][0] = t; g_L.u.seg[0][lane][1] = r; g_L.u.seg[0][lane][2] = p; }
+    double al = 0.0;
+    if (lane < 3) {
+      double sg[MAX_PTS];
+#pragma unroll
+      for (int i = 0; i < MAX_PTS; ++i) sg[i] = g_L.u.seg[0][i][lane];  // (unconditional: see edge_costs)
+#pragma unroll
+      for (int i = 0; i < MAX_PTS; ++i)
+        if (i < np) al += sg[i];
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) acc[k] = readlane_d(al, k);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) cost[k] = cc[k] + acc[k];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) lst[j] = cur[j];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) lcc[k] = cc[k];
+    if (reached) break;
+    const int id = nn_t++;
+    if (n_via >= via_cap) { overflow = true; reached = true; break; }
+    if (lane == 0) {
+      ViaNode& v = C.Q.via[n_via];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) { v.q[j] = end[j]; v.e_start[j] = cur[j]; v.e_target[j] = ox[j]; }
+#pragma unroll
+      for (int k = 0; k < 3; ++k) v.c[k] = cost[k];
+      v.id = id;
+      v.parent = cid;
+    }
+    ++n_via;
+    cpar = cid;
+    cid = id;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) cur[j] = end[j];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) cc[k] = cost[k];
+  }
+  if (lane == 0) {
+    QState& S = g_L.S;
+    S.prof[P_NVIA] += nsteps;
+    if (overflow) { S.status = -7; S.phase = 2; }
+    else {
+      NodeRef& g = g_L.sel;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) { g.q[j] = end[j]; g_L.sel_start[j] = cur[j]; g_L.sel_target[j] = ox[j]; }
+#pragma unroll
+      for (int k = 0; k < 3; ++k) g.c[k] = cost[k];
+      g.id = nn_t;
+      g.parent = cid;
+    }
+    g_L.reached = 1;
+    g_L.nn_t = nn_t;
+    g_L.n_via = n_via;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      g_L.cur.q[j] = cur[j];
+      g_L.ox[j] = ox[j];
+      g_L.eg_start[0][j] = lst[j];
+      g_L.eg_target[0][j] = ox[j];
+      g_L.eg_step[0][j] = stp[j];
+      g_L.eg_end[0][j] = end[j];
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      g_L.cur.c[k] = cc[k];
+      g_L.eg_base[0][k] = lcc[k];
+      g_L.eg_acc[0][k] = acc[k];
+      g_L.eg_cost[0][k] = cost[k];
+    }
+    g_L.cur.id = cid;
+    g_L.cur.parent = cpar;
+  }
+}
 __device__ void via_chain(const Ctx& C, const double* target) {
   TR();
   PROF_BEGIN();
-  for (;;) {
-    if (threadIdx.x == 0) g_L.S.prof[P_NVIA]++;
-    if (threadIdx.x == 0) {
-      for (int j = 0; j < NJ; ++j) g_L.ox[j] = target[j];
-      g_L.reached = step_towards((&g_rb), g_L.cur.q, g_L.ox, g_L.S.step) ? 1 : 0;
-      for (int j = 0; j < NJ; ++j) { g_L.eg_start[0][j] = g_L.cur.q[j]; g_L.eg_target[0][j] = g_L.ox[j]; }
-      for (int k = 0; k < 3; ++k) g_L.eg_base[0][k] = g_L.cur.c[k];
-    }
-    __syncthreads();
-    edge_costs(C, 1);
-    if (threadIdx.x == 0) {
-      NodeRef g;
-      for (int j = 0; j < NJ; ++j) g.q[j] = g_L.eg_end[0][j];
-      for (int k = 0; k < 3; ++k) g.c[k] = g_L.eg_cost[0][k];
-      g.parent = g_L.cur.id;
-      if (!g_L.reached) {
-        g.id = g_L.nn_t++;
-        if (g_L.n_via >= g_L.S.via_cap) { g_L.S.status = -7; g_L.S.phase = 2; g_L.reached = 1; }
-        else {
-          ViaNode& v = C.Q.via[g_L.n_via++];
-          for (int j = 0; j < NJ; ++j) { v.q[j] = g.q[j]; v.e_start[j] = g_L.cur.q[j]; v.e_target[j] = g_L.ox[j]; }
-          for (int k = 0; k < 3; ++k) v.c[k] = g.c[k];
-          v.id = g.id;
-          v.parent = g.parent;
-        }
-        g_L.cur = g;
-      } else {
-        g.id = g_L.nn_t;
-        g_L.sel = g;
-        for (int j = 0; j < NJ; ++j) { g_L.sel_start[j] = g_L.cur.q[j]; g_L.sel_target[j] = g_L.ox[j]; }
-      }
-    }
-    __syncthreads();
-    if (uni(g_L.reached)) break;
-  }
+  if (threadIdx.x < 64) via_chain_w(C, target);
+  __syncthreads();
   PROF_END(P_VIA);
   TR();
 }

@@ -13,7 +13,6 @@ step() {  # step NAME LIMIT CMD...
   echo "step $name rc $rc" | tee -a $OUT/steps.txt
   [ $rc -le 1 ] || exit $rc
 }
-step t_scan 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_tree_scans.py tests/test_gpu_parity.py
-step nsp 200 python -u tools/near_step_probe.py 30000
+step t_all 900 python -u -m pytest -x -q --timeout 400 --timeout-method thread -m gpu tests
 step pp 300 python -u tools/perf_probe.py 4000 30000
 step bench 300 python -u bench.py --steps 20 --warmup 5
