@@ -2175,9 +2175,9 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
   return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
-// Segment s of the interpolated edge st -> st + np * stp: its total / revolute / prismatic norms
+// Segment s of the interpolated edge st -> st + np * stp: the squared lengths behind its total / revolute / prismatic norms
 // (compute_edge_cost_interpolation's per-segment terms, birrt_star.cpp:4162-4242; the joint sums in joint order).
-__device__ __forceinline__ void seg_norms(unsigned rm, const double* st, const double* stp, int s, double& t, double& r,
+__device__ __forceinline__ void seg_terms(unsigned rm, const double* st, const double* stp, int s, double& t, double& r,
                                           double& p) {
   t = 0.0; r = 0.0; p = 0.0;
 #pragma unroll
@@ -2190,6 +2190,11 @@ __device__ __forceinline__ void seg_norms(unsigned rm, const double* st, const d
     r += rv ? d : 0.0;
     p += rv ? 0.0 : d;
   }
+}
+// ... and their square roots (the norms)
+__device__ __forceinline__ void seg_norms(unsigned rm, const double* st, const double* stp, int s, double& t, double& r,
+                                          double& p) {
+  seg_terms(rm, st, stp, s, t, r, p);
   t = sqrt(t); r = sqrt(r); p = sqrt(p);
 }
 
@@ -3172,6 +3177,9 @@ __device__ bool spec_stage(const Ctx& C, int s, unsigned long long wait) {
     __builtin_amdgcn_s_sleep(1);
   }
   if (threadIdx.x == 0) g_L.S.sc_wait += wall_clock64() - t0;
+#ifdef SMP_WAIT_PROF  // the leader's waits by stage into prof[28..31]: nn / expand, near / choose, rewire, connect
+  if (threadIdx.x == 0) g_L.S.prof[s <= SC_EXPAND ? 28 : s <= SC_CHOOSE ? 29 : s == SC_DONE ? 30 : 31] += wall_clock64() - t0;
+#endif
   TR();
   if (got < 0) {
     if (threadIdx.x == 0) g_L.sp_on = 0;
@@ -3651,6 +3659,53 @@ __device__ bool step_towards(const RobotDev* rb, const double* nn, double* x, do
   return step_towards_m(rev_mask(rb), nn, x, f);
 }
 
+// step_towards_m for a whole wave (every lane active, the same nn / x / f in every lane, the same result).  An fp64
+// division or square root costs a wave ~70 / ~90 cycles of issue however few lanes it serves, so the per-joint
+// divisions run once, lane l dividing joint l % 8's difference, and the revolute / prismatic square roots once, even
+// and odd lanes; every lane takes the results back by v_readlane.  nn_l / x_l are lane l's copies of nn[l % 8] and
+// x[l % 8] (kept beside the arrays: picking an array element by lane compiles to a private-memory round trip); x_l
+// is updated with x.  The operations and their order per value are step_towards_m's.
+__device__ __forceinline__ bool step_towards_w(unsigned rm, const double* nn, double* x, double f, int lane, double nn_l,
+                                               double& x_l) {
+  double ed[NJ], srev = 0.0, spr = 0.0;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const bool rv = (rm >> j) & 1u;
+    ed[j] = x[j] - nn[j];
+    const double d = ed[j] * ed[j];
+    srev += rv ? d : 0.0;
+    spr += rv ? 0.0 : d;
+  }
+  const double l2 = sqrt((lane & 1) ? spr : srev);
+  const double lrev = readlane_d(l2, 0), lpr = readlane_d(l2, 1);
+  const bool rev_done = lrev < 0.001, pr_done = lpr < 0.001;
+  const bool rvl = (rm >> (lane & 7)) & 1u;
+  const double ql = (x_l - nn_l) / (rvl ? lrev : lpr);
+  double ext[NJ];
+  srev = 0.0; spr = 0.0;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const bool rv = (rm >> j) & 1u;
+    const bool done = rv ? rev_done : pr_done;
+    const double c = f * readlane_d(ql, j);
+    ext[j] = done ? 0.0 : nn[j] + c;
+    const double cc = done ? 0.0 : c * c;
+    srev += rv ? cc : 0.0;
+    spr += rv ? 0.0 : cc;
+  }
+  const double e2 = sqrt((lane & 1) ? spr : srev);
+  const double elr = srev == 0.0 ? 1000.0 : readlane_d(e2, 0);
+  const double elp = spr == 0.0 ? 1000.0 : readlane_d(e2, 1);
+  const bool tr = elr < lrev, tp = elp < lpr;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const bool rv = (rm >> j) & 1u;
+    if (rv ? tr : tp) x[j] = ext[j];
+  }
+  if (rvl ? tr : tp) x_l = (rvl ? rev_done : pr_done) ? 0.0 : nn_l + f * ql;
+  return !(tr || tp);
+}
+
 // Stepping loop shared by choose_parent / connectGraphs: from `cur` towards `target` with
 // unconstraint_extend_step_factor, collecting via nodes (ids nn_t, nn_t+1, ...) until the target is
 // reached; the last edge becomes `sel` (id nn_t at that point).  No collision checks (reference behaviour).
@@ -3669,23 +3724,48 @@ __device__ __noinline__ void via_chain_w(const Ctx& C, const double* target) {
   for (int k = 0; k < 3; ++k) cc[k] = g_L.cur.c[k];
   int nn_t = g_L.nn_t, n_via = g_L.n_via, nsteps = 0;
   const unsigned rm = rev_mask(&g_rb);
+  double cur_l = g_L.cur.q[lane & 7], ox_l;  // lane l's copies of cur[l % 8] / ox[l % 8] (step_towards_w)
+  const double tg_l = target[lane & 7];
+  static_assert(NJ == 8, "lane copies of the joints");
+#ifdef SMP_VIA_PROF  // lane-0 clocks into prof[28..31]: entry, stepping, edge costs, calls
+  unsigned long long _v0 = wall_clock64(), _v1;
+#define VIA_CLK(k) { _v1 = wall_clock64(); if (lane == 0) g_L.S.prof[k] += _v1 - _v0; _v0 = _v1; }
+#else
+#define VIA_CLK(k)
+#endif
+  VIA_CLK(31);
   bool reached, overflow = false;
   double lst[NJ], lcc[3];  // the last step's edge start and base cost (edge slot 0)
   for (;;) {
     ++nsteps;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) ox[j] = tg[j];
-    reached = step_towards_m(rm, cur, ox, f);
+    ox_l = tg_l;
+    reached = step_towards_w(rm, cur, ox, f, lane, cur_l, ox_l);
+    // the step of the edge: lane l divides joint l % 8's difference (one division for the wave)
+    const double ql = (ox_l - cur_l) / double(np);
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-      stp[j] = (ox[j] - cur[j]) / double(np);
+      stp[j] = readlane_d(ql, j);
       end[j] = cur[j] + np * stp[j];
     }
-    double t, r, p;
-    seg_norms(rm, cur, stp, s, t, r, p);
+    VIA_CLK(28);
+    // the segment norms: with np <= 21, lane 21 k + s takes norm k (total, revolute, prismatic) of segment s, one
+    // square root for the wave; else lane s all three of segment s
+    if (np <= 21) {
+      const int k = lane / 21, sg = lane - 21 * k;
+      double t, r, p;
+      seg_terms(rm, cur, stp, sg, t, r, p);
+      const double v = sqrt(k == 0 ? t : k == 1 ? r : p);
+      if (sg < np && k < 3) g_L.u.seg[0][sg][k] = v;
+    } else {
+      double t, r, p;
+      seg_norms(rm, cur, stp, s, t, r, p);
+      if (lane < np) { g_L.u.seg[0][lane][0] = t; g_L.u.seg[0][lane][1] = r; g_L.u.seg[0][lane][2] = p; }
+    }
+    VIA_CLK(29);
     // the ordered sums (edge_costs' third stage): lanes 0..2 sum the segments through LDS (in order; one wave, so
     // its LDS writes are seen by its later reads), and every lane takes the three sums by v_readlane
-    if (lane < np) { g_L.u.seg[0][lane][0] = t; g_L.u.seg[0][lane][1] = r; g_L.u.seg[0][lane][2] = p; }
     double al = 0.0;
     if (lane < 3) {
       double sg[MAX_PTS];
@@ -3697,6 +3777,7 @@ __device__ __noinline__ void via_chain_w(const Ctx& C, const double* target) {
     }
 #pragma unroll
     for (int k = 0; k < 3; ++k) acc[k] = readlane_d(al, k);
+    VIA_CLK(30);
 #pragma unroll
     for (int k = 0; k < 3; ++k) cost[k] = cc[k] + acc[k];
 #pragma unroll
@@ -3718,11 +3799,13 @@ __device__ __noinline__ void via_chain_w(const Ctx& C, const double* target) {
     ++n_via;
     cpar = cid;
     cid = id;
+    cur_l = cur_l + np * ql;  // end[l % 8]
 #pragma unroll
     for (int j = 0; j < NJ; ++j) cur[j] = end[j];
 #pragma unroll
     for (int k = 0; k < 3; ++k) cc[k] = cost[k];
   }
+#undef VIA_CLK
   if (lane == 0) {
     QState& S = g_L.S;
     S.prof[P_NVIA] += nsteps;
@@ -4681,7 +4764,8 @@ __device__ bool conn_stage(const Ctx& C, int B) {
 // runs the iteration itself); a record whose connect part does not hold is completed by connect_graphs.
 // Outcome counters of pre_commit in prof[28..31] (committed / no usable record / a newer nearest node / connect
 // completed by connect_graphs); those slots belong to the profiling builds' own clocks otherwise.
-#if defined(SMP_DETAIL_PROF) || defined(SMP_JOB_PROF) || defined(SMP_NEAR_PROF) || defined(SMP_SAMPLE_PROF)
+#if defined(SMP_DETAIL_PROF) || defined(SMP_JOB_PROF) || defined(SMP_NEAR_PROF) || defined(SMP_SAMPLE_PROF) || \
+    defined(SMP_VIA_PROF) || defined(SMP_WAIT_PROF)
 #define PRE_COUNT(k)
 #else
 #define PRE_COUNT(k) if (threadIdx.x == 0) g_L.S.prof[28 + (k)]++

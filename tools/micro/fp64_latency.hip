@@ -5,11 +5,12 @@
 
 template <typename T, int CH, int OP>
 __global__ void k(T* out, long long* cyc, T a, T b, int n) {
+  // cyc[0]: s_memtime ticks, cyc[1]: s_memrealtime ticks (100 MHz) over the same loop
   T x[CH];
 #pragma unroll
   for (int c = 0; c < CH; ++c) x[c] = a + threadIdx.x + c;
   __syncthreads();
-  long long t0 = __builtin_amdgcn_s_memtime();
+  long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
   for (int i = 0; i < n; i += 32) {  // 32 steps per loop trip: the loop's branch is amortised
 #pragma unroll
     for (int u = 0; u < 32; ++u)
@@ -23,12 +24,12 @@ __global__ void k(T* out, long long* cyc, T a, T b, int n) {
       else if (OP == 5) x[c] = sqrt(x[c]) + b;
     }
   }
-  long long t1 = __builtin_amdgcn_s_memtime();
+  long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
   T s = 0;
 #pragma unroll
   for (int c = 0; c < CH; ++c) s += x[c];
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
-  if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+  if (threadIdx.x == 0) { cyc[0] = t1 - t0; cyc[1] = r1 - r0; }
 }
 
 template <int CH, int OP, typename T = double>
@@ -38,10 +39,12 @@ void run(const char* name, int threads) {
   const int n = 4096;
   hipLaunchKernelGGL((k<T, CH, OP>), dim3(1), dim3(threads), 0, 0, out, cyc, (T)1.0000001, (T)0.9999999, n);
   hipDeviceSynchronize();
-  long long c = 0;
-  hipMemcpy(&c, cyc, sizeof(c), hipMemcpyDeviceToHost);
-  printf("%-3s %-8s chains %d threads %4d: %.2f cycles per instruction per wave (per chain step %.2f)\n", sizeof(T) == 8 ? "f64" : "f32", name, CH, threads,
-         (double)c / (n * CH), (double)c / n);
+  long long cc[2] = {0, 0};
+  hipMemcpy(cc, cyc, sizeof(cc), hipMemcpyDeviceToHost);
+  const double c = (double)cc[0], ns = (double)cc[1] * 10.0;
+  printf("%-3s %-8s chains %d threads %4d: %.2f s_memtime ticks per instruction per wave (per chain step %.2f; %.2f ns, "
+         "s_memtime at %.0f MHz)\n", sizeof(T) == 8 ? "f64" : "f32", name, CH, threads, c / (n * CH), c / n, ns / n,
+         c / ns * 1e3);
   hipFree(out); hipFree(cyc);
 }
 

@@ -67,7 +67,15 @@ for iters in [int(v) for v in (sys.argv[1:] or ["2000", "10000", "50000"])]:
     if os.environ.get("SMP_DETAIL_PROF"):  # SMP_DETAIL_PROF build: serial-section clocks (ticks, slots 28-31)
         print("   serial sections (us/iter): rewire commit %.2f (cost_update %.2f), connect replay %.2f, insert_via %.2f"
               % tuple(raw[k] / 1e2 / iters for k in (28, 29, 30, 31)), flush=True)
-    if raw[31] > 0 and not os.environ.get("SMP_DETAIL_PROF"):  # SMP_NEAR_PROF build: wave-0 clocks of near_set
+    if os.environ.get("SMP_VIA_PROF"):  # SMP_VIA_PROF build: the leader's via_chain_w clocks (ticks, slots 28-31)
+        ns = max(r["phases"]["n_via_steps"], 1)
+        print("   via chains: %d steps; per step: stepping + edge step %.2f us, segment norms %.2f us, ordered sums %.2f us;"
+              " entry %.2f us in all" % (ns, raw[28] / 1e2 / ns, raw[29] / 1e2 / ns, raw[30] / 1e2 / ns,
+                                         raw[31] / 1e2), flush=True)
+    if os.environ.get("SMP_WAIT_PROF"):  # SMP_WAIT_PROF build: the leader's record waits by stage (ticks, 28-31)
+        print("   leader waits (us/iter): nn + expand %.2f, near + choose %.2f, rewire %.2f, connect %.2f" % tuple(
+            raw[k] / 1e2 / iters for k in (28, 29, 30, 31)), flush=True)
+    if raw[31] > 0 and not any(os.environ.get(v) for v in ("SMP_DETAIL_PROF", "SMP_VIA_PROF", "SMP_WAIT_PROF")):  # SMP_NEAR_PROF build: wave-0 clocks of near_set
         nc = raw[31] * 1e8
         print("   near_set (%d calls, wave 0): scan %.1f us (insert %.1f us), merge %.1f us per call" % (
             nc, raw[28] * 1e6 / nc, raw[29] * 1e6 / nc, raw[30] * 1e6 / nc), flush=True)
