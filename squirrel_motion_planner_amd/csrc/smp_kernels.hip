@@ -5558,20 +5558,36 @@ redo:
   if (opt && sc_moved(C)) return;
   int nid;
   [[clang::always_inline]] nid = nearest(C, t, g_L.xr);
-  if (threadIdx.x == 0) {
-    load_node(C, t, nid, &g_L.nn);
+  if (threadIdx.x < 64) {
+    // wave 0: the nearest node's row (lane 0's loads), its distance, and the step towards the sample (step_towards_w:
+    // one division and two square-root pairs for the wave instead of a single lane's eight and four)
+    const int lane = threadIdx.x;
+    if (lane == 0) load_node(C, t, nid, &g_L.nn);
+    wave_sync();
+    double nq[NJ], xe[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) { nq[j] = g_L.nn.q[j]; xe[j] = g_L.xr[j]; }
     double s = 0.0;
-    for (int j = 0; j < NJ; ++j) { double d = g_L.xr[j] - g_L.nn.q[j]; s += d * d; }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) { const double d = xe[j] - nq[j]; s += d * d; }
     const double d = sqrt(s);
-    for (int j = 0; j < NJ; ++j) R.nn.q[j] = g_L.xr[j];
-    R.nn.d = d < 10000.0 ? d : 10000.0;
-    for (int k = 0; k < 3; ++k) R.nn.c[k] = g_L.nn.c[k];
-    R.nn.id = nid; R.nn.X = X; R.nn.t = t; R.nn.ok = 1;
-    for (int j = 0; j < NJ; ++j) g_L.ext[j] = g_L.xr[j];
-    step_towards((&g_rb), g_L.nn.q, g_L.ext, S.step);
-    for (int j = 0; j < NJ; ++j) { g_L.eg_start[0][j] = g_L.nn.q[j]; g_L.eg_target[0][j] = g_L.ext[j]; }
-    for (int k = 0; k < 3; ++k) g_L.eg_base[0][k] = g_L.nn.c[k];
-    g_L.eg_need[0] = 1;
+    const double nn_l = g_L.nn.q[lane & 7];
+    double x_l = g_L.xr[lane & 7];
+    step_towards_w(rev_mask(&g_rb), nq, xe, S.step, lane, nn_l, x_l);
+    if (lane < NJ) {
+      R.nn.q[lane] = g_L.xr[lane];
+      g_L.ext[lane] = x_l;
+      g_L.eg_start[0][lane] = nn_l;
+      g_L.eg_target[0][lane] = x_l;
+    } else if (lane < NJ + 3) {
+      const int k = lane - NJ;
+      R.nn.c[k] = g_L.nn.c[k];
+      g_L.eg_base[0][k] = g_L.nn.c[k];
+    } else if (lane == NJ + 3) {
+      R.nn.d = d < 10000.0 ? d : 10000.0;
+      R.nn.id = nid; R.nn.X = X; R.nn.t = t; R.nn.ok = 1;
+      g_L.eg_need[0] = 1;
+    }
   }
   __syncthreads();
   if (opt) {

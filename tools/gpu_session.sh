@@ -15,5 +15,4 @@ step() {  # step NAME LIMIT CMD...
 }
 step t_all 900 python -u -m pytest -x -q --timeout 400 --timeout-method thread -m gpu tests
 step pp 300 python -u tools/perf_probe.py 4000 30000
-SMP_LIB=squirrel_motion_planner_amd/lib/libsmp_gpu_nospec.so step pp_nospec 300 python -u tools/perf_probe.py 4000 30000
 step bench 300 python -u bench.py --steps 20 --warmup 5
