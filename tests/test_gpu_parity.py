@@ -259,6 +259,21 @@ def test_planner_parity_scout_counts(orobot, robot, scouts):
     assert_same_run(gp2, r, o)
 
 
+@pytest.mark.parametrize("n_pts", [10, 21, 22, 32])
+def test_planner_parity_segment_counts(orobot, robot, n_pts):
+    """num_traj_segments_interp other than the default 20, across the first solution: 21 is the largest count whose
+    via-chain segment norms take one lane each per norm (via_chain_w's lane groups of 21), 22 and up take the
+    three-norms-per-lane path, 32 = MAX_PTS; the scouts' records, the helpers' tiles and the edge costs all change."""
+    gp2 = GpuPlanner(robot, num_traj_segments=n_pts, path_optimality_threshold=-np.inf)
+    sc, gscene, osc = scene_pair("c2")
+    gp2.set_scene(gscene)
+    r = gp2.plan(GpuPlanner.make_query(sc.start, sc.goal, sc.env_x, sc.env_y, iterations=1500, seed=7))
+    o = O.Oracle(orobot, osc).plan(sc.start, sc.goal, env_x=sc.env_x, env_y=sc.env_y, max_iter=1500, seed=7,
+                                   opt_thresh=-np.inf, n_pts=n_pts)
+    assert r["status"] == 0 and r["scout"] >= 1
+    assert_same_run(gp2, r, o)
+
+
 def test_planner_parity_yaml_profile(orobot, robot):
     gp2 = GpuPlanner(robot, near_threshold=1.5, step_factor=0.6)
     sc, r, o = run_both(gp2, orobot, "c2", 5, 200, near_threshold=1.5, step_factor=0.6)

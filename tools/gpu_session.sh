@@ -13,8 +13,4 @@ step() {  # step NAME LIMIT CMD...
   echo "step $name rc $rc" | tee -a $OUT/steps.txt
   [ $rc -le 1 ] || exit $rc
 }
-step t_all 900 python -u -m pytest -x -q --timeout 400 --timeout-method thread -m gpu tests
-step smoke 180 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
-step prof_c2 1000 bash tools/profile_round.sh r06 c2
-step ttff 400 python -u tools/ttff_seeds.py 3 gpurun_out/r06_ttff_seeds.json
-step c4 200 python tools/configs_report.py c4 gpurun_out/r06_c4_convergence.json --seconds 2
+step t_seg 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_gpu_parity.py -k segment_counts
