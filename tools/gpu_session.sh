@@ -13,4 +13,7 @@ step() {  # step NAME LIMIT CMD...
   echo "step $name rc $rc" | tee -a $OUT/steps.txt
   [ $rc -le 1 ] || exit $rc
 }
-step t_seg 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_gpu_parity.py -k segment_counts
+step pp_def 200 python -u tools/perf_probe.py 4000 30000
+SMP_TILE_CT=4 step pp_ct4 200 python -u tools/perf_probe.py 4000 30000
+SMP_TILE_CT=2 step pp_ct2 200 python -u tools/perf_probe.py 4000 30000
+SMP_HELPER_CAP=230 step pp_h230 200 python -u tools/perf_probe.py 4000 30000
