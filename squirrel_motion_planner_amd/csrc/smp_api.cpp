@@ -1109,7 +1109,10 @@ static int plan_batch_impl(smp_planner* p, const smp_query* qs, int nq, smp_resu
   if (const char* e = std::getenv("SMP_HELPER_CAP")) cap_s = std::max(1, std::atoi(e));
   int lead_div = 3;  // SMP_LEAD_DIV: the leader's share of the helpers (C2: 1/3 3.82, 1/5 3.75, 1/8 3.73 M configs/s)
   if (const char* e = std::getenv("SMP_LEAD_DIV")) lead_div = std::max(1, std::atoi(e));
-  int pre_h = 6;  // SMP_PRE_HELPERS: helpers of each pre-solution-only scout (its jobs: expand + connect edge, 6 tiles)
+  // SMP_PRE_HELPERS: helpers of each pre-solution-only scout (its jobs: expand + connect edge, 42 configurations).  12
+  // (round 6; ct 4 tiles instead of 8): time to first path median 1.68 -> 1.61 ms over the 20 seeds on one box, C2 equal
+  // (57.5 / 57.7 us per iteration); 16 1.61 ms but C2 69.0 against 68.4 us at 30000 iterations
+  int pre_h = 12;
   if (const char* e = std::getenv("SMP_PRE_HELPERS")) pre_h = std::max(0, std::atoi(e));
   // before the first solution a scout starts record k when the leader reaches k - pre_delay (DESIGN.md "Pre-solution
   // commits"); SMP_PRE_DELAY overrides it for experiments (0: at the request)

@@ -13,7 +13,7 @@ step() {  # step NAME LIMIT CMD...
   echo "step $name rc $rc" | tee -a $OUT/steps.txt
   [ $rc -le 1 ] || exit $rc
 }
-step pp_def 200 python -u tools/perf_probe.py 4000 30000
-SMP_TILE_CT=4 step pp_ct4 200 python -u tools/perf_probe.py 4000 30000
-SMP_TILE_CT=2 step pp_ct2 200 python -u tools/perf_probe.py 4000 30000
-SMP_HELPER_CAP=230 step pp_h230 200 python -u tools/perf_probe.py 4000 30000
+step t_all 900 python -u -m pytest -x -q --timeout 400 --timeout-method thread -m gpu tests
+step smoke 180 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
+step prof_c2 1000 bash tools/profile_round.sh r06 c2
+step ttff 400 python -u tools/ttff_seeds.py 3 gpurun_out/r06_ttff_seeds.json
