@@ -13,7 +13,6 @@ step() {  # step NAME LIMIT CMD...
   echo "step $name rc $rc" | tee -a $OUT/steps.txt
   [ $rc -le 1 ] || exit $rc
 }
-step t_all 900 python -u -m pytest -x -q --timeout 400 --timeout-method thread -m gpu tests
-step smoke 180 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
-step prof_c2 1000 bash tools/profile_round.sh r06 c2
-step ttff 400 python -u tools/ttff_seeds.py 3 gpurun_out/r06_ttff_seeds.json
+step prof_3e5 900 bash tools/profile_round.sh r06 c2_iter300000 --iterations 300000 --steps 1 --warmup 0
+step c3 400 python -u bench.py --workload c3
+step c5 600 python -u bench.py --workload c5
