@@ -13,6 +13,4 @@ step() {  # step NAME LIMIT CMD...
   echo "step $name rc $rc" | tee -a $OUT/steps.txt
   [ $rc -le 1 ] || exit $rc
 }
-step prof_3e5 900 bash tools/profile_round.sh r06 c2_iter300000 --iterations 300000 --steps 1 --warmup 0
-step c3 400 python -u bench.py --workload c3
-step c5 600 python -u bench.py --workload c5
+KT_LIMIT=600 BENCH_LIMIT=900 PMC_LIMIT=600 step prof_1e6 1150 bash tools/profile_round.sh r06 c2_iter1000000 --iterations 1000000 --steps 1 --warmup 0
